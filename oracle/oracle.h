@@ -1,0 +1,84 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY (see blake3_ref.c header). CPU restatement
+ * of the reference's content-identification path:
+ *   generate_cas_id   core/src/object/cas.rs:23-62
+ *   file_checksum     core/src/object/validation/hash.rs:11-25
+ *   dedup/link        core/src/object/file_identifier/mod.rs:98-350
+ */
+#ifndef SDCAS_ORACLE_H
+#define SDCAS_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define B3REF_BLOCK_LEN 64
+#define B3REF_CHUNK_LEN 1024
+#define B3REF_CHUNK_START 1
+#define B3REF_CHUNK_END 2
+#define B3REF_PARENT 4
+#define B3REF_ROOT 8
+
+typedef struct {
+  uint32_t cv[8];
+  uint64_t counter;
+  uint8_t buf[64];
+  uint8_t buf_len;
+  uint8_t blocks_done;
+} b3ref_chunk;
+
+typedef struct {
+  b3ref_chunk chunk;
+  uint32_t stack[54][8];
+  unsigned stack_len;
+} b3ref_hasher;
+
+void b3ref_hasher_init(b3ref_hasher *h);
+void b3ref_hasher_update(b3ref_hasher *h, const void *data, size_t n);
+void b3ref_hasher_finalize(const b3ref_hasher *h, uint8_t out[32]);
+void b3ref_hash(const void *data, size_t n, uint8_t out[32]);
+void b3ref_compress_cv(const uint32_t cv[8], const uint8_t block[64], uint8_t block_len,
+                       uint64_t counter, uint8_t flags, uint32_t out_cv[8]);
+void b3ref_parent_cv(const uint32_t left[8], const uint32_t right[8], int root, uint32_t out[8]);
+
+/* status for read_exact() hitting EOF (Rust io::ErrorKind::UnexpectedEof has no errno) */
+#define ORACLE_STATUS_UNEXPECTED_EOF 100001
+
+/* cas.rs:23-62 over a real file; returns 0 or a positive status, writes 16 hex + NUL */
+int oracle_generate_cas_id(const char *path, uint64_t size, char out_hex[17]);
+/* hash.rs:11-25 over a real file; returns 0 or a positive status, writes 64 hex + NUL */
+int oracle_file_checksum(const char *path, char out_hex[65]);
+
+/* u64 cas key = digest bytes 0..7 big-endian, so "%016llx" == to_hex()[..16] */
+uint64_t oracle_digest_key(const uint8_t digest[32]);
+uint64_t oracle_cas_key_of_message(const uint8_t *msg, size_t n);
+
+/* synthetic corpora (include/sdcas_synth.h): cas key of file (key, size) and
+ * full-content checksum of a synthetic file */
+uint64_t oracle_synth_cas_key(uint64_t content_key, uint64_t size);
+void oracle_synth_checksum(uint64_t content_key, uint64_t size, uint8_t out[32]);
+/* build the cas message of a synthetic file into out (capacity >= msg len) */
+size_t oracle_synth_cas_message(uint64_t content_key, uint64_t size, uint8_t *out);
+
+/* Dedup/link restatement of file_identifier/mod.rs:98-350 in its canonical,
+ * deterministic form. Files are the orphan
+ * file_paths in id order, processed in chunks of `chunk_size` (CHUNK_SIZE=100,
+ * mod.rs:34). status[i] != 0 drops the file (mod.rs:125-141); has_key[i] == 0
+ * is an empty file (cas_id None, mod.rs:78-86). existing_keys[e] are the cas
+ * keys of Objects already in the library, in DB order.
+ * out_link[i]: i            -> file i creates a new Object
+ *              j (<i)       -> file i links to the Object created by file j
+ *              -(e+1)       -> file i links to existing Object e
+ *              INT64_MIN    -> dropped (status != 0)
+ * Returns created count; *linked receives the linked count (mod.rs:349). */
+int64_t oracle_identifier_dedup(size_t n, const uint64_t *keys, const uint8_t *has_key,
+                                const int32_t *status, size_t chunk_size, size_t n_existing,
+                                const uint64_t *existing_keys, int64_t *out_link, int64_t *linked);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

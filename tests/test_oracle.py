@@ -1,0 +1,128 @@
+"""CPU tests: the oracle against the golden vectors (upstream BLAKE3 C,
+llvm_blake3 1.3.1 + 1.8.2) and SURVEY.md Appendix B; the dedup restatement
+against hand-derived cases of core/src/object/file_identifier/mod.rs."""
+import os
+
+import numpy as np
+import pytest
+
+from tests._oracle import (cas_windows, content, content_key, golden, mix64, spec_content,
+                           write_sparse_file)
+
+APPENDIX_B = {0: "71e0a99173564931", 1: "9b779f74b305adc3", 1016: "c0de16cef5f85601",
+              1017: "62fe3d833d2df619", 102400: "c66a52267c7e5ee9", 102401: "17f74805066119da",
+              1048576: "5aefa86eb26df03d"}
+
+
+def test_blake3_vectors(oracle):
+    for c in golden("blake3_vectors.json"):
+        data = content("pattern251", 0, c["len"])
+        assert oracle.hash(data.tobytes()) == c["hash"], c["len"]
+
+
+def test_cas_messages_match_golden(oracle):
+    for c in golden("cas_ids.json"):
+        if c["size"] > (1 << 22):
+            continue
+        kind, key = spec_content(c["content"])
+        parts = [np.frombuffer(c["size"].to_bytes(8, "little"), np.uint8)]
+        parts += [content(kind, o, n, key) for o, n in cas_windows(c["size"])]
+        msg = np.concatenate(parts)
+        assert msg.size == c["msg_len"]
+        assert f"{oracle.cas_key_of_message(msg):016x}" == c["cas_id"]
+
+
+def test_appendix_b(oracle):
+    cases = {c["size"]: c["cas_id"] for c in golden("cas_ids.json") if c["content"] == "pattern251"}
+    for size, want in APPENDIX_B.items():
+        assert cases[size] == want
+
+
+def test_generate_cas_id_real_files(oracle, tmp_path):
+    """cas.rs:23-62 through real file I/O (sparse files for the big ones)"""
+    for c in golden("cas_ids.json"):
+        kind, key = spec_content(c["content"])
+        p = tmp_path / f"f_{c['content'].replace(':', '_')}_{c['size']}"
+        write_sparse_file(p, kind, key, c["size"], cas_windows(c["size"]))
+        assert oracle.generate_cas_id(str(p), c["size"]) == c["cas_id"], c
+
+
+def test_file_checksum_real_files(oracle, tmp_path):
+    for c in golden("checksums.json"):
+        if c["size"] > (8 << 20):
+            continue
+        kind, key = spec_content(c["content"])
+        p = tmp_path / f"c_{c['size']}"
+        p.write_bytes(content(kind, 0, c["size"], key).tobytes())
+        assert oracle.file_checksum(str(p)) == c["checksum"], c
+
+
+def test_synth_checksum(oracle):
+    for c in golden("checksums.json"):
+        if c["content"].startswith("synth") and c["size"] < (4 << 20):
+            _, key = spec_content(c["content"])
+            assert oracle.synth_checksum(key, c["size"]) == c["checksum"]
+
+
+def test_synth_generator_spots():
+    for c in golden("synth_spots.json"):
+        assert content_key(c["seed"], c["cid"]) == c["key"]
+        assert content("synth", c["off"], 16, c["key"]).tobytes().hex() == c["bytes"]
+
+
+def test_synth_cas_key_matches_message(oracle):
+    rng = np.random.default_rng(1)
+    for size in [0, 1, 1016, 5000, 102400, 102401, 300000, 7 << 20]:
+        key = int(rng.integers(0, 2**63))
+        msg = oracle.synth_cas_message(key, size)
+        parts = [np.frombuffer(size.to_bytes(8, "little"), np.uint8)]
+        parts += [content("synth", o, n, key) for o, n in cas_windows(size)]
+        assert np.array_equal(msg, np.concatenate(parts))
+        assert oracle.synth_cas_key(key, size) == oracle.cas_key_of_message(msg)
+
+
+def test_short_file_unexpected_eof(oracle, tmp_path):
+    """a file that is shorter than the size the indexer recorded fails with
+    UnexpectedEof in read_exact (cas.rs:36,43,56)"""
+    p = tmp_path / "short"
+    p.write_bytes(b"x" * 20000)
+    with pytest.raises(OSError) as e:
+        oracle.generate_cas_id(str(p), 200000)
+    assert e.value.errno == 100001
+
+
+def test_missing_file_errno(oracle, tmp_path):
+    with pytest.raises(OSError) as e:
+        oracle.generate_cas_id(str(tmp_path / "nope"), 10)
+    assert e.value.errno == 2
+
+
+# ---- dedup restatement (file_identifier/mod.rs:98-350) ----------------------
+
+def test_dedup_semantics(oracle):
+    # chunk size 3: chunk0 = files 0,1,2; chunk1 = 3,4,5; chunk2 = 6
+    keys = np.array([10, 10, 11, 10, 12, 11, 99], np.uint64)
+    has = np.array([1, 1, 1, 1, 1, 1, 0], np.uint8)
+    out, created, linked = oracle.identifier_dedup(keys, has, chunk_size=3)
+    # chunk0: 10 and 10 are intra-chunk duplicates -> two Objects (mod.rs:246-254)
+    # chunk1: 10 links to the first Object with cas 10 (file 0); 11 links to file 2; 12 new
+    # chunk2: None cas_id -> new Object
+    assert out.tolist() == [0, 1, 2, 0, 4, 2, 6]
+    assert created == 5 and linked == 2
+
+
+def test_dedup_existing_and_errors(oracle):
+    keys = np.array([5, 6, 5, 7], np.uint64)
+    has = np.ones(4, np.uint8)
+    status = np.array([0, 0, 0, 2], np.int32)
+    out, created, linked = oracle.identifier_dedup(keys, has, status, chunk_size=100,
+                                                   existing_keys=[6, 6, 9])
+    # 6 links to the FIRST existing Object carrying it; file 3 failed -> dropped
+    # same chunk: both 5s are new Objects
+    assert out.tolist() == [0, -1, 2, np.iinfo(np.int64).min]
+    assert created == 2 and linked == 1
+
+
+def test_mix64_python_matches_header():
+    # sds_mix64(0) reference value computed from the header's definition
+    assert int(mix64(np.uint64(0))) == 0xE220A8397B1DCDAF
