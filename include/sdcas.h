@@ -1,0 +1,156 @@
+/*
+ * sdcas.h — C ABI of the MI355X content-identification engine (libsdcas.so).
+ *
+ * Drop-in boundary for sd-core's content identification. The
+ * Rust host keeps its signatures and binds these entry points (cgo-style
+ * `extern "C"`, plain pointers and sizes, no ownership transfer; binding shown
+ * in INTEGRATION.md):
+ *
+ *   sdcas_cas_ids        replaces per-file generate_cas_id(path, size)
+ *                        core/src/object/cas.rs:23-62, called from
+ *                        core/src/object/file_identifier/mod.rs:78-82 (the
+ *                        join_all of FileMetadata::new at mod.rs:105-147
+ *                        becomes one call per chunk), non_indexed.rs:181,
+ *                        location/manager/watcher/utils.rs:236-240
+ *   sdcas_checksums      replaces file_checksum(path)
+ *                        core/src/object/validation/hash.rs:11-25, called from
+ *                        validation/validator_job.rs:154 and watcher/utils.rs:496
+ *   sdcas_dedup          replaces the cas_id -> Object group-by/link of
+ *                        file_identifier/mod.rs:149-254 (HashSet at :149-154,
+ *                        existing-object lookup :181-188, linear find :214-224,
+ *                        new Objects :246-254)
+ *   sdcas_*_from_messages / sdcas_hash_messages / sdcas_dev_*
+ *                        the same engine on pre-assembled messages (host or
+ *                        device memory) for tests and benchmarks
+ *
+ * Conventions
+ *   - Return value: SDCAS_OK (0) or a negative SDCAS_E_* library failure (no
+ *     device, invalid arguments, out of memory, HIP error). On failure the
+ *     caller falls back to its CPU path for the whole batch.
+ *   - Per-item status (out_status): 0, a positive errno from the file I/O, or
+ *     SDCAS_STATUS_UNEXPECTED_EOF when read_exact() ran out of file
+ *     (cas.rs:36,43,56). The Rust side maps errno with
+ *     io::Error::from_raw_os_error, reproducing the per-file skip of
+ *     file_identifier/mod.rs:125-141.
+ *   - cas keys: u64 whose big-endian bytes are digest bytes 0..7, so
+ *     format!("{:016x}", key) == hasher.finalize().to_hex()[..16] (cas.rs:61).
+ *     Digests: 32 bytes in BLAKE3 output order; lowercase hex of them is
+ *     hash.rs:22-24's to_hex().
+ *   - Ownership: the caller owns every input and output array; the library
+ *     owns device memory, pinned staging and streams inside the context and
+ *     retains no caller pointer after a call returns.
+ *   - Threading: a context is used by one thread at a time (calls on one
+ *     context serialise internally); create one context per worker thread or
+ *     wrap calls in spawn_blocking (the C calls block).
+ */
+#ifndef SDCAS_H
+#define SDCAS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SDCAS_OK 0
+#define SDCAS_E_NO_DEVICE (-1)
+#define SDCAS_E_INVALID (-2)
+#define SDCAS_E_OOM (-3)
+#define SDCAS_E_HIP (-4)
+#define SDCAS_E_CAPACITY (-5)
+
+#define SDCAS_STATUS_UNEXPECTED_EOF 100001
+
+/* constants of core/src/object/cas.rs:10-15 and validation/hash.rs:9 */
+#define SDCAS_SAMPLE_COUNT 4
+#define SDCAS_SAMPLE_SIZE 10240
+#define SDCAS_HEADER_OR_FOOTER_SIZE 8192
+#define SDCAS_MINIMUM_FILE_SIZE 102400
+#define SDCAS_SAMPLED_MESSAGE_LEN 57352
+#define SDCAS_CHECKSUM_BLOCK_LEN 1048576
+/* file_identifier/mod.rs:34 */
+#define SDCAS_IDENTIFIER_CHUNK_SIZE 100
+
+typedef struct sdcas_ctx sdcas_ctx;
+
+typedef struct sdcas_options {
+  int32_t device;          /* HIP device ordinal (-1: current device) */
+  uint32_t io_threads;     /* reader threads for the path APIs (0: 8) */
+  uint64_t staging_bytes;  /* pinned host staging per batch (0: 256 MiB) */
+} sdcas_options;
+
+const char *sdcas_version(void);
+
+/* Create / destroy a context bound to one GPU. opts may be NULL. */
+int sdcas_init(const sdcas_options *opts, sdcas_ctx **out_ctx);
+void sdcas_destroy(sdcas_ctx *ctx);
+/* Text of the last library failure on this context ("" if none). */
+const char *sdcas_last_error(const sdcas_ctx *ctx);
+
+/* ---- the reference functions, batched --------------------------------- */
+
+/* cas_id of n files: generate_cas_id(paths[i], sizes[i]) (cas.rs:23-62).
+ * sizes[i] is fs::metadata().len() as the identifier passes it (mod.rs:78-79);
+ * it feeds the size prefix and the sample spacing, while file bytes come from
+ * the file as it is now. out_keys[i] is valid iff out_status[i] == 0. */
+int sdcas_cas_ids(sdcas_ctx *ctx, const char *const *paths, const uint64_t *sizes, size_t n,
+                  uint64_t *out_keys, int32_t *out_status);
+
+/* file_checksum of n files (hash.rs:11-25): BLAKE3 of the whole content.
+ * out32 receives 32*n bytes. */
+int sdcas_checksums(sdcas_ctx *ctx, const char *const *paths, size_t n, uint8_t *out32,
+                    int32_t *out_status);
+
+/* ---- pre-assembled messages in host memory ----------------------------- */
+
+/* BLAKE3 of n messages blob[offsets[i] .. offsets[i]+lens[i]) -> out32 (32*n B). */
+int sdcas_hash_messages(sdcas_ctx *ctx, const uint8_t *blob, const uint64_t *offsets,
+                        const uint64_t *lens, size_t n, uint8_t *out32);
+/* the same, keeping only the cas key of each message */
+int sdcas_cas_ids_from_messages(sdcas_ctx *ctx, const uint8_t *blob, const uint64_t *offsets,
+                                const uint64_t *lens, size_t n, uint64_t *out_keys);
+
+/* ---- device-resident batches (inputs already in HBM) ------------------- */
+
+/* Size the device workspace for batches of up to max_msgs messages and
+ * max_chunks total 1 KiB chunks (sum of max(1, ceil(len/1024))). Allocates;
+ * call outside timed regions. */
+int sdcas_dev_reserve(sdcas_ctx *ctx, size_t max_msgs, uint64_t max_chunks);
+/* Enqueue the hash of n device-resident messages on `stream` (a hipStream_t,
+ * NULL = the context's stream). Requirements: every offset 16-byte aligned,
+ * and the blob readable for at least 64 bytes past the end of every message.
+ * Either output may be NULL. Asynchronous; sdcas_dev_sync() reports a
+ * capacity overflow detected on the device. */
+int sdcas_dev_hash_messages(sdcas_ctx *ctx, const uint8_t *d_blob, const uint64_t *d_offsets,
+                            const uint64_t *d_lens, size_t n, uint8_t *d_out32, uint64_t *d_out_keys,
+                            void *stream);
+int sdcas_dev_sync(sdcas_ctx *ctx, void *stream);
+
+/* ---- dedup / link (file_identifier/mod.rs:149-254) --------------------- */
+
+/* Canonical group-by of the identifier step over n orphan file_paths in id
+ * order, processed in chunks of chunk_size (0 -> 100). has_key[i] == 0 marks
+ * a cas_id of None (empty file, mod.rs:78-86); status[i] != 0 drops the file
+ * (may be NULL). existing_keys are the cas keys of Objects already in the
+ * library, in DB order (may be NULL when n_existing == 0).
+ * out_link[i] = i        file i creates a new Object
+ *             = j < i    file i links to the Object created by file j
+ *             = -(e+1)   file i links to existing Object e
+ *             = INT64_MIN dropped
+ * *out_created / *out_linked receive the counts identifier_job_step returns
+ * (mod.rs:349). */
+int sdcas_dedup(sdcas_ctx *ctx, const uint64_t *keys, const uint8_t *has_key, const int32_t *status,
+                size_t n, size_t chunk_size, const uint64_t *existing_keys, size_t n_existing,
+                int64_t *out_link, int64_t *out_created, int64_t *out_linked);
+
+/* ---- helpers ------------------------------------------------------------ */
+
+void sdcas_key_to_hex(uint64_t key, char out[17]);
+void sdcas_digest_to_hex(const uint8_t digest[32], char out[65]);
+uint64_t sdcas_cas_message_len(uint64_t size);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SDCAS_H */

@@ -1,0 +1,93 @@
+"""ctypes binding of libsdcas.so (include/sdcas.h, include/sdcas_bench.h).
+
+The library is the product: every hash and every dedup result comes from its
+HIP kernels. Importing this module without the built library, or calling it
+without a GPU, raises — there is no CPU fallback.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsdcas.so")
+
+SDCAS_OK = 0
+SDCAS_E_NO_DEVICE = -1
+SDCAS_E_INVALID = -2
+SDCAS_E_OOM = -3
+SDCAS_E_HIP = -4
+SDCAS_E_CAPACITY = -5
+SDCAS_STATUS_UNEXPECTED_EOF = 100001
+
+# every entry point include/sdcas.h and include/sdcas_bench.h declare
+ABI_SYMBOLS = [
+    "sdcas_version", "sdcas_init", "sdcas_destroy", "sdcas_last_error", "sdcas_cas_ids",
+    "sdcas_checksums", "sdcas_hash_messages", "sdcas_cas_ids_from_messages", "sdcas_dev_reserve",
+    "sdcas_dev_hash_messages", "sdcas_dev_sync", "sdcas_dedup", "sdcas_key_to_hex",
+    "sdcas_digest_to_hex", "sdcas_cas_message_len",
+    # bench / test plumbing
+    "sdcas_dev_synth_cas_messages", "sdcas_dev_synth_content", "sdcas_dev_dedup", "sdcas_dev_profile",
+    "sdcas_dev_last_kernel_ms",
+]
+
+
+class SdcasError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"sdcas error {code}: {msg}")
+        self.code = code
+
+
+class Options(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("io_threads", ctypes.c_uint32),
+                ("staging_bytes", ctypes.c_uint64)]
+
+
+_lib = None
+
+_vp = ctypes.c_void_p
+_sz = ctypes.c_size_t
+_u64 = ctypes.c_uint64
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    # One HIP runtime per process: PyTorch-ROCm bundles its own
+    # libamdhip64.so.7 / libhsa-runtime64.so.1 (same SONAMEs as /opt/rocm's).
+    # If torch is importable it is loaded FIRST so that the dynamic linker
+    # binds libsdcas.so to torch's already-loaded runtime instead of opening
+    # a second HSA runtime on the same GPU (which leaves torch with "No HIP
+    # GPUs are available"). Without torch, /opt/rocm's runtime is used.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is not built: run `make -C spacedrive_amd/csrc` "
+                          "(or __graft_entry__.build()) — there is no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    L.sdcas_version.restype = ctypes.c_char_p
+    L.sdcas_init.argtypes = [ctypes.POINTER(Options), ctypes.POINTER(_vp)]
+    L.sdcas_destroy.argtypes = [_vp]
+    L.sdcas_last_error.argtypes = [_vp]
+    L.sdcas_last_error.restype = ctypes.c_char_p
+    L.sdcas_cas_ids.argtypes = [_vp, _vp, _vp, _sz, _vp, _vp]
+    L.sdcas_checksums.argtypes = [_vp, _vp, _sz, _vp, _vp]
+    L.sdcas_hash_messages.argtypes = [_vp, _vp, _vp, _vp, _sz, _vp]
+    L.sdcas_cas_ids_from_messages.argtypes = [_vp, _vp, _vp, _vp, _sz, _vp]
+    L.sdcas_dev_reserve.argtypes = [_vp, _sz, _u64]
+    L.sdcas_dev_hash_messages.argtypes = [_vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp]
+    L.sdcas_dev_sync.argtypes = [_vp, _vp]
+    L.sdcas_dedup.argtypes = [_vp, _vp, _vp, _vp, _sz, _sz, _vp, _sz, _vp, _vp, _vp]
+    L.sdcas_key_to_hex.argtypes = [_u64, ctypes.c_char_p]
+    L.sdcas_digest_to_hex.argtypes = [_vp, ctypes.c_char_p]
+    L.sdcas_cas_message_len.argtypes = [_u64]
+    L.sdcas_cas_message_len.restype = _u64
+    L.sdcas_dev_synth_cas_messages.argtypes = [_vp, _vp, _vp, _vp, _sz, _vp, _vp]
+    L.sdcas_dev_synth_content.argtypes = [_vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp]
+    L.sdcas_dev_dedup.argtypes = [_vp, _vp, _vp, _vp, _sz, _sz, _vp, _vp, _vp]
+    L.sdcas_dev_profile.argtypes = [_vp, ctypes.c_int]
+    L.sdcas_dev_last_kernel_ms.argtypes = [_vp, ctypes.POINTER(ctypes.c_float),
+                                           ctypes.POINTER(ctypes.c_float)]
+    _lib = L
+    return L

@@ -1,0 +1,57 @@
+// b3_batch.h — host-side interface of the batched multi-message BLAKE3 engine.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace sdcas {
+
+constexpr uint32_t kTile = 1024;  // chunk slots per workgroup tile (1 MiB of message bytes)
+constexpr uint32_t kWG = 512;     // threads per workgroup: 2 slots per lane
+
+// Device workspace owned by the library context (caller never sees it).
+struct BatchWorkspace {
+  uint64_t* S = nullptr;           // [cap_msgs] first slot of each message
+  uint32_t* tile_first = nullptr;  // [cap_tiles] message owning each tile's first slot
+  uint64_t* total = nullptr;       // [2] total slots, error word
+  uint32_t* nodes = nullptr;       // [cap_chunks * 8] maximal in-tile node CVs, by first slot
+  void* scan_tmp = nullptr;
+  size_t scan_tmp_bytes = 0;
+  uint32_t cap_msgs = 0;
+  uint64_t cap_chunks = 0;
+  int grid = 0;
+};
+
+size_t batch_scan_temp_bytes(uint32_t max_msgs);
+int batch_grid(int device);
+
+// Hash n messages (blob + offs[i], lens[i] bytes; offsets 16-byte aligned),
+// all pointers device pointers. Writes 32-byte digests to out32 and/or cas
+// keys (digest bytes 0..7 big-endian) to out_keys (either may be null).
+// Total chunks must not exceed ws.cap_chunks (checked by the caller).
+hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint64_t* offs, const uint64_t* lens,
+                      uint32_t n, uint8_t* out32, uint64_t* out_keys, hipStream_t st, hipEvent_t ev0 = nullptr,
+                      hipEvent_t ev1 = nullptr);
+
+// ---- big files (C > kTile chunks), hashed as 1 MiB pieces -------------------
+struct PieceDesc {
+  uint64_t off;        // byte offset of the piece in the blob (16-byte aligned)
+  uint64_t j0;         // first chunk index (multiple of kTile)
+  uint64_t node_base;  // file's first entry in the file-node list
+  uint32_t len;        // bytes (<= 1 MiB; < 1 MiB only for a file's last piece)
+  uint32_t pad;
+};
+struct FileDesc {
+  uint64_t C;          // file chunk count (> kTile)
+  uint64_t node_base;  // first entry in the file-node list (Q + popcount(C mod kTile) entries)
+  uint64_t out_index;  // digest slot in out32
+};
+inline uint64_t bigfile_node_count(uint64_t C) {
+  return C / kTile + (uint64_t)__builtin_popcountll(C % kTile);
+}
+hipError_t piece_hash(const uint8_t* blob, const PieceDesc* pieces, uint32_t npieces, uint32_t* file_nodes,
+                      hipStream_t st);
+hipError_t bigfile_finish(const FileDesc* files, uint32_t nfiles, const uint32_t* file_nodes, uint8_t* out32,
+                          hipStream_t st);
+
+}  // namespace sdcas

@@ -1,0 +1,530 @@
+// b3_batch.hip — batched multi-message BLAKE3 on gfx950.
+//
+// One launch hashes n independent messages (cas_id messages of
+// core/src/object/cas.rs:23-62, or whole files for
+// core/src/object/validation/hash.rs:11-25) that sit in HBM at 16-byte aligned
+// offsets of one blob.
+//
+// Layout: every 1 KiB chunk of every message gets one "slot" of a flat slot
+// space (message m owns slots [S[m], S[m] + C[m]), C = max(1, ceil(len/1024)),
+// S = exclusive scan of C). Slots are cut into TILEs of 1024; one workgroup
+// owns one tile at a time (grid-stride over tiles), so every lane of every
+// wave hashes a chunk — no per-message padding, no idle lanes except in the
+// very last tile.
+//
+//   k_tile_first   which message owns each tile's first slot (lane/message)
+//   k_leaf_tree    per tile: (1) each lane hashes its chunk (16 compressions,
+//                  blocks straight from HBM as 4 x dwordx4 per block, next
+//                  block prefetched); single-chunk messages finish here as
+//                  ROOT. (2) chunk CVs go to LDS and every BLAKE3 tree node
+//                  that is an aligned, complete power-of-two block lying
+//                  inside the tile is reduced level by level (PARENT
+//                  compressions over a compacted task list). (3) the maximal
+//                  such nodes are written to `nodes` at their first slot.
+//   k_finish       lane per multi-chunk message: walks its maximal nodes left
+//                  to right (the decomposition is a closed-form function of
+//                  (chunk index, chunk count, slot in tile)) and merges them
+//                  with the BLAKE3 subtree-stack rule; the last merge is ROOT.
+//
+// The tree a message gets is exactly BLAKE3's left-balanced tree: complete
+// aligned power-of-two subtrees are tree nodes, and the stack merge (merge
+// while the stack is longer than popcount(chunks so far), then fold
+// right-to-left) reassembles them in the crate's order.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <stdint.h>
+
+#include "b3_device.h"
+#include "b3_batch.h"
+
+namespace sdcas {
+
+using namespace b3d;
+
+constexpr int kMaxStack = 64;
+constexpr int kMaxStackBig = 64;
+
+__host__ __device__ inline uint64_t chunk_count(uint64_t len) { return len == 0 ? 1 : (len + CHUNK_LEN - 1) / CHUNK_LEN; }
+
+// Highest level k such that the node of 2^k chunks starting at chunk j is
+// (a) an aligned complete block of the message, (b) not the whole message and
+// (c) inside the tile that holds chunk j at slot `s`.
+__host__ __device__ inline uint32_t node_level(uint64_t j, uint64_t C, uint32_t s) {
+  uint32_t k = 0;
+  for (;;) {
+    uint64_t w = 2ull << k;
+    if ((j & (w - 1)) || j + w > C || w >= C || (uint64_t)s + w > kTile) break;
+    ++k;
+  }
+  return k;
+}
+
+// Is the level-k node at (j, s) consumed by a parent computed in the same tile?
+__host__ __device__ inline bool parent_in_tile(uint64_t j, uint64_t C, uint32_t s, uint32_t k) {
+  uint64_t w = 1ull << k;
+  if (!((j >> k) & 1)) return false;  // left children's parents start at s: not computed
+  return j + w <= C && 2 * w < C && s >= w && (uint64_t)s + w <= kTile;
+}
+
+struct ChunkCountOp {
+  __host__ __device__ uint64_t operator()(uint64_t len) const { return chunk_count(len); }
+};
+
+__global__ void k_tile_first(const uint64_t* __restrict__ lens, const uint64_t* __restrict__ S, uint32_t n,
+                             uint64_t cap_chunks, uint32_t* __restrict__ tile_first, uint64_t* __restrict__ total) {
+  uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= n) return;
+  uint64_t s0 = S[m], C = chunk_count(lens[m]);
+  if (m == n - 1) *total = s0 + C;
+  for (uint64_t t = (s0 + kTile - 1) / kTile; t * kTile < s0 + C && t * kTile < cap_chunks; ++t) tile_first[t] = m;
+}
+
+// Hash one chunk (`clen` bytes at p, 0 <= clen <= 1024) with chunk counter j.
+__device__ __forceinline__ void hash_chunk(const uint8_t* __restrict__ p, uint32_t clen, uint64_t j, bool root,
+                                           uint32_t (&cv)[8]) {
+  set_iv(cv);
+  const uint32_t nb = clen == 0 ? 1 : (clen + BLOCK_LEN - 1) / BLOCK_LEN;
+#pragma unroll 1
+  for (uint32_t b = 0; b < nb; ++b) {
+    const uint32_t blen = min(BLOCK_LEN, clen - b * BLOCK_LEN);
+    uint32_t m[16];
+    load_full_block(p + b * BLOCK_LEN, m);
+    if (blen < BLOCK_LEN) mask_tail(m, blen);
+    const uint32_t flags = (b == 0 ? CHUNK_START : 0u) | (b + 1 == nb ? (CHUNK_END | (root ? ROOT : 0u)) : 0u);
+    compress(cv, m, j, blen, flags);
+  }
+}
+
+__device__ __forceinline__ void store_digest(uint32_t m, const uint32_t (&d)[8], uint8_t* out32, uint64_t* out_keys) {
+  if (out32) {
+    uint4* o = reinterpret_cast<uint4*>(out32 + 32ull * m);
+    o[0] = make_uint4(d[0], d[1], d[2], d[3]);
+    o[1] = make_uint4(d[4], d[5], d[6], d[7]);
+  }
+  if (out_keys) out_keys[m] = cas_key(d);
+}
+
+__global__ void __launch_bounds__(kWG) k_leaf_tree(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ offs,
+                                                   const uint64_t* __restrict__ lens, uint32_t n,
+                                                   const uint64_t* __restrict__ S,
+                                                   const uint32_t* __restrict__ tile_first,
+                                                   const uint64_t* __restrict__ total_p, uint64_t cap_chunks,
+                                                   uint32_t* __restrict__ nodes, uint8_t* __restrict__ out32,
+                                                   uint64_t* __restrict__ out_keys) {
+  __shared__ uint32_t cvs[kTile][8];   // chunk / node chaining values, by slot
+  __shared__ uint32_t sj[kTile];       // chunk index within its message
+  __shared__ uint32_t sC[kTile];       // chunk count of its message (0: slot not in a tree)
+  __shared__ uint64_t sS[kTile + 1];   // S[] of the tile's messages
+  __shared__ uint16_t task[kTile / 2];
+  __shared__ uint32_t ntask[16];
+
+  const uint64_t total = *total_p;
+  if (total > cap_chunks) return;  // reported by sdcas_dev_sync
+  const uint64_t ntiles = (total + kTile - 1) / kTile;
+  const uint32_t tid = threadIdx.x;
+
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const uint32_t m0 = tile_first[tile];
+    const uint32_t m1 = (tile + 1 < ntiles) ? tile_first[tile + 1] : n - 1;
+    const uint32_t cnt = m1 - m0 + 1;  // <= kTile + 1
+    for (uint32_t i = tid; i < cnt; i += kWG) sS[i] = S[m0 + i];
+    if (tid < 16) ntask[tid] = 0;
+    __syncthreads();
+
+    // (1) leaves
+#pragma unroll 1
+    for (uint32_t s = tid; s < kTile; s += kWG) {
+      const uint64_t g = tile * kTile + s;
+      if (g >= total) {
+        sC[s] = 0;
+        continue;
+      }
+      uint32_t lo = 0, hi = cnt - 1;  // last message with S <= g
+      while (lo < hi) {
+        uint32_t mid = (lo + hi + 1) >> 1;
+        if (sS[mid] <= g) lo = mid;
+        else hi = mid - 1;
+      }
+      const uint32_t m = m0 + lo;
+      const uint64_t j = g - sS[lo];
+      const uint64_t len = lens[m];
+      const uint64_t C = chunk_count(len);
+      const uint32_t clen = len == 0 ? 0u : (uint32_t)min<uint64_t>(CHUNK_LEN, len - j * CHUNK_LEN);
+      const bool root = (C == 1);
+      uint32_t cv[8];
+      hash_chunk(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
+      if (root) {
+        store_digest(m, cv, out32, out_keys);
+        sC[s] = 0;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) cvs[s][i] = cv[i];
+        sj[s] = (uint32_t)j;
+        sC[s] = (uint32_t)C;
+      }
+    }
+    __syncthreads();
+
+    // (2) in-tile tree, level by level over a compacted task list
+    for (uint32_t k = 1; (1u << k) <= kTile; ++k) {
+      const uint32_t w = 1u << k;
+      for (uint32_t s = tid; s < kTile; s += kWG) {
+        const uint32_t C = sC[s];
+        if (!C) continue;
+        const uint32_t j = sj[s];
+        if (!(j & (w - 1)) && j + w <= C && w < C && s + w <= kTile) task[atomicAdd(&ntask[k], 1u)] = (uint16_t)s;
+      }
+      __syncthreads();
+      const uint32_t T = ntask[k];
+      if (T == 0) break;
+#pragma unroll 1
+      for (uint32_t t = tid; t < T; t += kWG) {
+        const uint32_t s = task[t];
+        uint32_t l[8], r[8], o[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          l[i] = cvs[s][i];
+          r[i] = cvs[s + (w >> 1)][i];
+        }
+        parent(l, r, false, o);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) cvs[s][i] = o[i];
+      }
+      __syncthreads();
+    }
+
+    // (3) maximal nodes -> HBM at their first slot
+    for (uint32_t s = tid; s < kTile; s += kWG) {
+      const uint32_t C = sC[s];
+      if (!C) continue;
+      const uint32_t j = sj[s];
+      const uint32_t k = node_level(j, C, s);
+      if (parent_in_tile(j, C, s, k)) continue;
+      uint4* o = reinterpret_cast<uint4*>(nodes + 8ull * (tile * kTile + s));
+      o[0] = make_uint4(cvs[s][0], cvs[s][1], cvs[s][2], cvs[s][3]);
+      o[1] = make_uint4(cvs[s][4], cvs[s][5], cvs[s][6], cvs[s][7]);
+    }
+    __syncthreads();
+  }
+}
+
+
+__global__ void __launch_bounds__(256) k_finish(const uint64_t* __restrict__ lens, uint32_t n,
+                                                const uint64_t* __restrict__ S, const uint64_t* __restrict__ total_p,
+                                                uint64_t cap_chunks, const uint32_t* __restrict__ nodes,
+                                                uint8_t* __restrict__ out32, uint64_t* __restrict__ out_keys) {
+  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= n || *total_p > cap_chunks) return;
+  const uint64_t C = chunk_count(lens[m]);
+  if (C == 1) return;
+  const uint64_t s0 = S[m];
+  uint32_t stack[kMaxStack][8];
+  int depth = 0;
+  uint64_t j = 0;
+  while (j < C) {
+    const uint64_t g = s0 + j;
+    const uint32_t k = node_level(j, C, (uint32_t)(g % kTile));
+    const uint4* p = reinterpret_cast<const uint4*>(nodes + 8ull * g);
+    uint4 a = p[0], b = p[1];
+    uint32_t cv[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    // subtrees completed by the first j chunks are merged before going on
+    const int keep = __popcll(j);
+    while (depth > keep) {
+      uint32_t o[8];
+      parent(stack[depth - 2], stack[depth - 1], false, o);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) stack[depth - 2][i] = o[i];
+      --depth;
+    }
+    j += 1ull << k;
+    if (j == C) {
+      for (int d = depth - 1; d >= 0; --d) {
+        uint32_t o[8];
+        parent(stack[d], cv, d == 0, o);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) cv[i] = o[i];
+      }
+      store_digest(m, cv, out32, out_keys);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) stack[depth][i] = cv[i];
+      ++depth;
+    }
+  }
+}
+
+// ---- big files: 1 MiB pieces -----------------------------------------------
+//
+// A file of C > kTile chunks is cut at 1 MiB boundaries of the FILE into
+// pieces; piece q holds chunks [1024q, 1024q + 1024) and the last piece the
+// r = C mod 1024 remaining chunks (if any). One workgroup hashes one piece:
+// its 1024 chunks fill exactly one tile, so a full piece reduces to its
+// level-10 subtree CV (a node of the file's tree, never the root since
+// C > 1024), and a tail piece to the binary decomposition of r (one node per
+// 1-bit of r). These nodes go to a per-file node list: full piece q at index
+// q, tail nodes after the Q full pieces in decreasing size. Pieces of one file
+// may arrive over many launches (streamed windows); k_bigfile_finish merges a
+// file's list once all of it is there.
+
+__global__ void __launch_bounds__(kWG) k_piece_tree(const uint8_t* __restrict__ blob,
+                                                    const PieceDesc* __restrict__ pieces, uint32_t npieces,
+                                                    uint32_t* __restrict__ file_nodes) {
+  __shared__ uint32_t cvs[kTile][8];
+  __shared__ uint16_t task[kTile / 2];
+  __shared__ uint32_t ntask[16];
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t pi = blockIdx.x; pi < npieces; pi += gridDim.x) {
+    const PieceDesc pd = pieces[pi];
+    const uint32_t nchunks = (pd.len + CHUNK_LEN - 1) / CHUNK_LEN;
+    if (tid < 16) ntask[tid] = 0;
+#pragma unroll 1
+    for (uint32_t s = tid; s < nchunks; s += kWG) {
+      const uint32_t clen = min(CHUNK_LEN, pd.len - s * CHUNK_LEN);
+      uint32_t cv[8];
+      hash_chunk(blob + pd.off + (uint64_t)s * CHUNK_LEN, clen, pd.j0 + s, false, cv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) cvs[s][i] = cv[i];
+    }
+    __syncthreads();
+    for (uint32_t k = 1; (1u << k) <= kTile; ++k) {
+      const uint32_t w = 1u << k;
+      for (uint32_t s = tid; s < nchunks; s += kWG)
+        if (!(s & (w - 1)) && s + w <= nchunks) task[atomicAdd(&ntask[k], 1u)] = (uint16_t)s;
+      __syncthreads();
+      const uint32_t T = ntask[k];
+      if (T == 0) break;
+#pragma unroll 1
+      for (uint32_t t = tid; t < T; t += kWG) {
+        const uint32_t s = task[t];
+        uint32_t l[8], r[8], o[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          l[i] = cvs[s][i];
+          r[i] = cvs[s + (w >> 1)][i];
+        }
+        parent(l, r, false, o);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) cvs[s][i] = o[i];
+      }
+      __syncthreads();
+    }
+    // maximal nodes: the binary decomposition of nchunks (one node for a full piece)
+    for (uint32_t s = tid; s < nchunks; s += kWG) {
+      const uint32_t rest = nchunks - s;
+      // s starts a maximal node iff s is the sum of the higher bits of nchunks
+      const uint32_t k = 31 - __clz(rest);  // node size = highest power of two <= rest
+      if ((s & ((1u << k) - 1)) || (s != (nchunks & ~((2u << k) - 1)))) continue;
+      const uint64_t idx = pd.node_base + (nchunks == kTile ? pd.j0 / kTile : pd.j0 / kTile + __popc(nchunks >> (k + 1)));
+      uint4* o = reinterpret_cast<uint4*>(file_nodes + 8ull * idx);
+      o[0] = make_uint4(cvs[s][0], cvs[s][1], cvs[s][2], cvs[s][3]);
+      o[1] = make_uint4(cvs[s][4], cvs[s][5], cvs[s][6], cvs[s][7]);
+    }
+    __syncthreads();
+  }
+}
+
+// one workgroup per big file: merge its node list (Q level-10 piece CVs, then
+// the tail decomposition) into the root. The Q piece CVs are reduced
+// 1024 at a time in LDS (complete aligned groups of pieces are tree nodes);
+// the maximal groups and the tail nodes are merged by lane 0 with the
+// subtree-stack rule, the last merge being ROOT.
+__global__ void __launch_bounds__(kWG) k_bigfile_finish(const FileDesc* __restrict__ files, uint32_t nfiles,
+                                                        const uint32_t* __restrict__ file_nodes,
+                                                        uint8_t* __restrict__ out32) {
+  __shared__ uint32_t cvs[kTile][8];
+  __shared__ uint16_t task[kTile / 2];
+  __shared__ uint32_t ntask[16];
+  __shared__ uint32_t stack[kMaxStackBig][8];
+  __shared__ uint32_t depth_s;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t fi = blockIdx.x;
+  if (fi >= nfiles) return;
+  const FileDesc fd = files[fi];
+  const uint64_t C = fd.C;
+  const uint64_t Q = C / kTile;
+  const uint32_t r = (uint32_t)(C % kTile);
+  if (tid == 0) depth_s = 0;
+  // lane 0 pushes node (chunk position j, cv) after merging what j completes
+  auto push = [&](uint64_t j, const uint32_t (&cv)[8]) {
+    uint32_t depth = depth_s;
+    const uint32_t keep = __popcll(j);
+    while (depth > keep) {
+      uint32_t a[8], b[8], o[8];
+      for (int i = 0; i < 8; ++i) { a[i] = stack[depth - 2][i]; b[i] = stack[depth - 1][i]; }
+      parent(a, b, false, o);
+      for (int i = 0; i < 8; ++i) stack[depth - 2][i] = o[i];
+      --depth;
+    }
+    for (int i = 0; i < 8; ++i) stack[depth][i] = cv[i];
+    depth_s = depth + 1;
+  };
+  for (uint64_t b0 = 0; b0 < Q; b0 += kTile) {
+    const uint32_t nb = (uint32_t)min<uint64_t>(kTile, Q - b0);
+    if (tid < 16) ntask[tid] = 0;
+    for (uint32_t s = tid; s < nb; s += kWG) {
+      const uint4* p = reinterpret_cast<const uint4*>(file_nodes + 8ull * (fd.node_base + b0 + s));
+      uint4 a = p[0], b = p[1];
+      cvs[s][0] = a.x; cvs[s][1] = a.y; cvs[s][2] = a.z; cvs[s][3] = a.w;
+      cvs[s][4] = b.x; cvs[s][5] = b.y; cvs[s][6] = b.z; cvs[s][7] = b.w;
+    }
+    __syncthreads();
+    // groups of 2^k pieces: aligned, complete, and not the whole file
+    for (uint32_t k = 1; (1u << k) <= kTile; ++k) {
+      const uint32_t w = 1u << k;
+      for (uint32_t s = tid; s < nb; s += kWG)
+        if (!(s & (w - 1)) && s + w <= nb && (uint64_t)w * kTile < C) task[atomicAdd(&ntask[k], 1u)] = (uint16_t)s;
+      __syncthreads();
+      const uint32_t T = ntask[k];
+      if (T == 0) break;
+#pragma unroll 1
+      for (uint32_t t = tid; t < T; t += kWG) {
+        const uint32_t s = task[t];
+        uint32_t l[8], rr[8], o[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          l[i] = cvs[s][i];
+          rr[i] = cvs[s + (w >> 1)][i];
+        }
+        parent(l, rr, false, o);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) cvs[s][i] = o[i];
+      }
+      __syncthreads();
+    }
+    if (tid == 0) {
+      // maximal groups in order: greedy largest computed group at each position
+      uint32_t s = 0;
+      while (s < nb) {
+        uint32_t k = 0;
+        while (true) {
+          const uint32_t w = 2u << k;
+          if ((s & (w - 1)) || s + w > nb || (uint64_t)w * kTile >= C) break;
+          ++k;
+        }
+        uint32_t cv[8];
+        for (int i = 0; i < 8; ++i) cv[i] = cvs[s][i];
+        const uint64_t j = (b0 + s) * kTile;
+        const uint64_t jn = j + ((uint64_t)kTile << k);
+        if (jn == C) {
+          // whole remainder done: fold (only when r == 0 and this is the last group)
+          uint32_t depth = depth_s;
+          const uint32_t keep = __popcll(j);
+          while (depth > keep) {
+            uint32_t a[8], bb[8], o[8];
+            for (int i = 0; i < 8; ++i) { a[i] = stack[depth - 2][i]; bb[i] = stack[depth - 1][i]; }
+            parent(a, bb, false, o);
+            for (int i = 0; i < 8; ++i) stack[depth - 2][i] = o[i];
+            --depth;
+          }
+          for (int d = (int)depth - 1; d >= 0; --d) {
+            uint32_t a[8], o[8];
+            for (int i = 0; i < 8; ++i) a[i] = stack[d][i];
+            parent(a, cv, d == 0, o);
+            for (int i = 0; i < 8; ++i) cv[i] = o[i];
+          }
+          uint4* o = reinterpret_cast<uint4*>(out32 + 32ull * fd.out_index);
+          o[0] = make_uint4(cv[0], cv[1], cv[2], cv[3]);
+          o[1] = make_uint4(cv[4], cv[5], cv[6], cv[7]);
+          depth_s = 0;
+        } else {
+          push(j, cv);
+        }
+        s += 1u << k;
+      }
+    }
+    __syncthreads();
+  }
+  if (r && tid == 0) {
+    // tail nodes, decreasing sizes, at file_nodes[node_base + Q + t]
+    uint64_t j = Q * kTile;
+    uint32_t t = 0;
+    for (int k = 9; k >= 0; --k) {
+      if (!((r >> k) & 1)) continue;
+      const uint4* p = reinterpret_cast<const uint4*>(file_nodes + 8ull * (fd.node_base + Q + t));
+      uint4 a = p[0], b = p[1];
+      uint32_t cv[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      const uint64_t jn = j + (1ull << k);
+      if (jn == C) {
+        uint32_t depth = depth_s;
+        const uint32_t keep = __popcll(j);
+        while (depth > keep) {
+          uint32_t aa[8], bb[8], o[8];
+          for (int i = 0; i < 8; ++i) { aa[i] = stack[depth - 2][i]; bb[i] = stack[depth - 1][i]; }
+          parent(aa, bb, false, o);
+          for (int i = 0; i < 8; ++i) stack[depth - 2][i] = o[i];
+          --depth;
+        }
+        for (int d = (int)depth - 1; d >= 0; --d) {
+          uint32_t aa[8], o[8];
+          for (int i = 0; i < 8; ++i) aa[i] = stack[d][i];
+          parent(aa, cv, d == 0, o);
+          for (int i = 0; i < 8; ++i) cv[i] = o[i];
+        }
+        uint4* o = reinterpret_cast<uint4*>(out32 + 32ull * fd.out_index);
+        o[0] = make_uint4(cv[0], cv[1], cv[2], cv[3]);
+        o[1] = make_uint4(cv[4], cv[5], cv[6], cv[7]);
+      } else {
+        push(j, cv);
+      }
+      j = jn;
+      ++t;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+
+size_t batch_scan_temp_bytes(uint32_t max_msgs) {
+  size_t bytes = 0;
+  hipcub::TransformInputIterator<uint64_t, ChunkCountOp, const uint64_t*> it(nullptr, ChunkCountOp());
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, it, (uint64_t*)nullptr, (int)max_msgs);
+  return bytes;
+}
+
+int batch_grid(int device) {
+  static int cached[64] = {0};
+  if (device >= 0 && device < 64 && cached[device]) return cached[device];
+  int cus = 256, per = 1;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_leaf_tree, kWG, 0);
+  if (per < 1) per = 1;
+  int g = cus * per;
+  if (device >= 0 && device < 64) cached[device] = g;
+  return g;
+}
+
+hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint64_t* offs, const uint64_t* lens,
+                      uint32_t n, uint8_t* out32, uint64_t* out_keys, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
+  if (n == 0) return hipSuccess;
+  if (n > ws.cap_msgs) return hipErrorInvalidValue;
+  hipcub::TransformInputIterator<uint64_t, ChunkCountOp, const uint64_t*> it(lens, ChunkCountOp());
+  size_t tmp = ws.scan_tmp_bytes;
+  hipError_t e = hipcub::DeviceScan::ExclusiveSum(ws.scan_tmp, tmp, it, ws.S, (int)n, st);
+  if (e != hipSuccess) return e;
+  const uint32_t tb = 256;
+  hipLaunchKernelGGL(k_tile_first, dim3((n + tb - 1) / tb), dim3(tb), 0, st, lens, ws.S, n, ws.cap_chunks,
+                     ws.tile_first, ws.total);
+  if (ev0) (void)hipEventRecord(ev0, st);
+  hipLaunchKernelGGL(k_leaf_tree, dim3(ws.grid), dim3(kWG), 0, st, blob, offs, lens, n, ws.S, ws.tile_first,
+                     ws.total, ws.cap_chunks, ws.nodes, out32, out_keys);
+  if (ev1) (void)hipEventRecord(ev1, st);
+  hipLaunchKernelGGL(k_finish, dim3((n + tb - 1) / tb), dim3(tb), 0, st, lens, n, ws.S, ws.total, ws.cap_chunks,
+                     ws.nodes, out32, out_keys);
+  return hipGetLastError();
+}
+
+hipError_t piece_hash(const uint8_t* blob, const PieceDesc* pieces, uint32_t npieces, uint32_t* file_nodes,
+                      hipStream_t st) {
+  if (!npieces) return hipSuccess;
+  hipLaunchKernelGGL(k_piece_tree, dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
+  return hipGetLastError();
+}
+
+hipError_t bigfile_finish(const FileDesc* files, uint32_t nfiles, const uint32_t* file_nodes, uint8_t* out32,
+                          hipStream_t st) {
+  if (!nfiles) return hipSuccess;
+  hipLaunchKernelGGL(k_bigfile_finish, dim3(nfiles), dim3(kWG), 0, st, files, nfiles, file_nodes, out32);
+  return hipGetLastError();
+}
+
+}  // namespace sdcas

@@ -1,0 +1,127 @@
+// b3_device.h — BLAKE3 compression for gfx950, one message block per lane.
+//
+// Replaces the arithmetic of the third-party `blake3` 1.5.0 crate that
+// sd-core calls at core/src/object/cas.rs:24-61 and
+// core/src/object/validation/hash.rs:13-22 (Hasher::update/finalize).
+// Pure 32-bit integer ARX: every G step is v_add3_u32 + v_xor_b32 +
+// v_alignbit_b32, the seven rounds are fully unrolled with the message
+// permutation resolved at compile time, so a lane's compression is ~680 VALU
+// instructions with no data movement between lanes (the CPU crate's
+// `hash_many` transposes words into SIMD lanes; on CDNA every lane loads its
+// own block, so no transpose exists).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace b3d {
+
+constexpr uint32_t IV0 = 0x6A09E667u, IV1 = 0xBB67AE85u, IV2 = 0x3C6EF372u, IV3 = 0xA54FF53Au;
+constexpr uint32_t IV4 = 0x510E527Fu, IV5 = 0x9B05688Cu, IV6 = 0x1F83D9ABu, IV7 = 0x5BE0CD19u;
+
+enum : uint32_t { CHUNK_START = 1, CHUNK_END = 2, PARENT = 4, ROOT = 8 };
+constexpr uint32_t BLOCK_LEN = 64;
+constexpr uint32_t CHUNK_LEN = 1024;
+
+__device__ __forceinline__ uint32_t rotr(uint32_t x, uint32_t n) {
+  return __builtin_amdgcn_alignbit(x, x, n);
+}
+
+#define B3_G(a, b, c, d, x, y) \
+  do {                         \
+    a = a + b + (x);           \
+    d = rotr(d ^ a, 16);       \
+    c = c + d;                 \
+    b = rotr(b ^ c, 12);       \
+    a = a + b + (y);           \
+    d = rotr(d ^ a, 8);        \
+    c = c + d;                 \
+    b = rotr(b ^ c, 7);        \
+  } while (0)
+
+// one round; s0..s15 = this round's message schedule (compile-time)
+#define B3_ROUND(s0, s1, s2, s3, s4, s5, s6, s7, s8, s9, s10, s11, s12, s13, s14, s15) \
+  do {                                                                                \
+    B3_G(v0, v4, v8, v12, m[s0], m[s1]);                                              \
+    B3_G(v1, v5, v9, v13, m[s2], m[s3]);                                              \
+    B3_G(v2, v6, v10, v14, m[s4], m[s5]);                                             \
+    B3_G(v3, v7, v11, v15, m[s6], m[s7]);                                             \
+    B3_G(v0, v5, v10, v15, m[s8], m[s9]);                                             \
+    B3_G(v1, v6, v11, v12, m[s10], m[s11]);                                           \
+    B3_G(v2, v7, v8, v13, m[s12], m[s13]);                                            \
+    B3_G(v3, v4, v9, v14, m[s14], m[s15]);                                            \
+  } while (0)
+
+// cv <- first 8 words of compress(cv, m, counter, block_len, flags).
+// For a ROOT compression these 8 words are the 32 digest bytes (LE words),
+// because the root's output-block counter is 0 and every root on this path
+// (a single chunk, or a parent) has counter 0 as well.
+__device__ __forceinline__ void compress(uint32_t (&cv)[8], const uint32_t (&m)[16], uint64_t counter,
+                                         uint32_t block_len, uint32_t flags) {
+  uint32_t v0 = cv[0], v1 = cv[1], v2 = cv[2], v3 = cv[3];
+  uint32_t v4 = cv[4], v5 = cv[5], v6 = cv[6], v7 = cv[7];
+  uint32_t v8 = IV0, v9 = IV1, v10 = IV2, v11 = IV3;
+  uint32_t v12 = (uint32_t)counter, v13 = (uint32_t)(counter >> 32), v14 = block_len, v15 = flags;
+  B3_ROUND(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+  B3_ROUND(2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8);
+  B3_ROUND(3, 4, 10, 12, 13, 2, 7, 14, 6, 5, 9, 0, 11, 15, 8, 1);
+  B3_ROUND(10, 7, 12, 9, 14, 3, 13, 15, 4, 0, 11, 2, 5, 8, 1, 6);
+  B3_ROUND(12, 13, 9, 11, 15, 10, 14, 8, 7, 2, 5, 3, 0, 1, 6, 4);
+  B3_ROUND(9, 14, 11, 5, 8, 12, 15, 1, 13, 3, 0, 10, 2, 6, 4, 7);
+  B3_ROUND(11, 15, 5, 0, 1, 9, 8, 6, 14, 10, 2, 12, 3, 4, 7, 13);
+  cv[0] = v0 ^ v8;
+  cv[1] = v1 ^ v9;
+  cv[2] = v2 ^ v10;
+  cv[3] = v3 ^ v11;
+  cv[4] = v4 ^ v12;
+  cv[5] = v5 ^ v13;
+  cv[6] = v6 ^ v14;
+  cv[7] = v7 ^ v15;
+}
+
+__device__ __forceinline__ void set_iv(uint32_t (&cv)[8]) {
+  cv[0] = IV0; cv[1] = IV1; cv[2] = IV2; cv[3] = IV3;
+  cv[4] = IV4; cv[5] = IV5; cv[6] = IV6; cv[7] = IV7;
+}
+
+// parent node: message = left CV || right CV, counter 0, 64-byte block
+__device__ __forceinline__ void parent(const uint32_t (&l)[8], const uint32_t (&r)[8], bool root,
+                                       uint32_t (&out)[8]) {
+  uint32_t m[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    m[i] = l[i];
+    m[8 + i] = r[i];
+  }
+  set_iv(out);
+  compress(out, m, 0, BLOCK_LEN, PARENT | (root ? ROOT : 0u));
+}
+
+// 64 message bytes, 16-byte aligned, fully inside the message
+__device__ __forceinline__ void load_full_block(const uint8_t* p, uint32_t (&m)[16]) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  uint4 a = q[0], b = q[1], c = q[2], d = q[3];
+  m[0] = a.x; m[1] = a.y; m[2] = a.z; m[3] = a.w;
+  m[4] = b.x; m[5] = b.y; m[6] = b.z; m[7] = b.w;
+  m[8] = c.x; m[9] = c.y; m[10] = c.z; m[11] = c.w;
+  m[12] = d.x; m[13] = d.y; m[14] = d.z; m[15] = d.w;
+}
+
+// Zero the bytes of a just-loaded block that lie past `blen` (< 64): the last
+// block of a message is loaded as a full 64-byte block (the blob carries at
+// least 64 readable bytes after every message, see sdcas.h) and masked here,
+// so no lane ever branches into byte loads.
+__device__ __forceinline__ void mask_tail(uint32_t (&m)[16], uint32_t blen) {
+#pragma unroll
+  for (int w = 0; w < 16; ++w) {
+    const int r = (int)blen - 4 * w;
+    const uint32_t keep = r >= 4 ? 0xFFFFFFFFu : (r <= 0 ? 0u : ((1u << (8 * r)) - 1u));
+    m[w] &= keep;
+  }
+}
+
+// digest bytes 0..7 as a big-endian u64 (so "%016llx" == to_hex()[..16])
+__device__ __forceinline__ uint64_t cas_key(const uint32_t (&d)[8]) {
+  return ((uint64_t)__builtin_bswap32(d[0]) << 32) | (uint64_t)__builtin_bswap32(d[1]);
+}
+
+}  // namespace b3d

@@ -1,0 +1,865 @@
+// sdcas_api.hip — the C ABI of include/sdcas.h: context, staging, file I/O
+// and the batch calls that sd-core's Rust host binds.
+//
+// Host work here is exactly what the reference does around the hash
+// (core/src/object/cas.rs:23-62, core/src/object/validation/hash.rs:11-25):
+// the same reads at the same offsets, with the same error kinds — but into a
+// pinned staging buffer laid out as device messages, after which one H2D
+// copy and one kernel sequence hash the whole batch. There is no CPU hashing
+// path: every digest this library returns comes from the HIP kernels.
+#include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/sdcas.h"
+#include "../../include/sdcas_bench.h"
+#include "b3_batch.h"
+#include "dedup.h"
+#include "synth.h"
+
+using namespace sdcas;
+
+namespace {
+
+constexpr uint64_t kSample = SDCAS_SAMPLE_SIZE, kHF = SDCAS_HEADER_OR_FOOTER_SIZE;
+constexpr uint64_t kMin = SDCAS_MINIMUM_FILE_SIZE, kSampleCount = SDCAS_SAMPLE_COUNT;
+constexpr uint64_t kSlack = 64;  // readable bytes kept after every message
+
+inline uint64_t align16(uint64_t x) { return (x + 15) & ~15ull; }
+inline uint64_t chunks_of(uint64_t len) { return len == 0 ? 1 : (len + 1023) / 1024; }
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t cap = 0;  // elements
+  hipError_t ensure(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(n, 16);
+    hipError_t e = hipMalloc(&p, want * sizeof(T));
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+}  // namespace
+
+struct sdcas_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  std::mutex mu;
+  uint32_t io_threads = 8;
+  uint64_t staging_bytes = 256ull << 20;
+
+  BatchWorkspace ws;
+  DevBuf<uint64_t> ws_S, ws_total;
+  DevBuf<uint32_t> ws_tile_first, ws_nodes;
+  DevBuf<uint8_t> ws_scan;
+
+  // host-API device buffers
+  DevBuf<uint8_t> d_blob;
+  DevBuf<uint64_t> d_offs, d_lens, d_keys;
+  DevBuf<uint8_t> d_out32;
+  DevBuf<PieceDesc> d_pieces;
+  DevBuf<FileDesc> d_files;
+  DevBuf<uint32_t> d_file_nodes;
+  uint8_t* h_stage = nullptr;
+  size_t h_stage_cap = 0;
+
+  // dedup
+  DedupWorkspace dws;
+  DevBuf<uint64_t> dd_key_a, dd_key_b, dd_keys, dd_ekeys, dd_ekeys_sorted;
+  DevBuf<uint32_t> dd_idx_a, dd_idx_b, dd_head, dd_nvalid, dd_eidx;
+  DevBuf<uint8_t> dd_valid, dd_temp, dd_has;
+  DevBuf<int32_t> dd_status;
+  DevBuf<int64_t> dd_link;
+  DevBuf<unsigned long long> dd_counts;
+
+  // profiling
+  bool profile = false;
+  std::vector<hipEvent_t> ev_free;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_leaf, ev_all;
+
+  int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    err = buf;
+    return code;
+  }
+  int hip_fail(hipError_t e, const char* what) {
+    return fail(e == hipErrorOutOfMemory ? SDCAS_E_OOM : SDCAS_E_HIP, "%s: %s", what, hipGetErrorString(e));
+  }
+  hipEvent_t event() {
+    if (!ev_free.empty()) {
+      hipEvent_t e = ev_free.back();
+      ev_free.pop_back();
+      return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+  }
+};
+
+namespace {
+
+int reserve_ws(sdcas_ctx* c, size_t max_msgs, uint64_t max_chunks) {
+  hipError_t e;
+  if (max_msgs > 0xFFFFFFF0ull) return c->fail(SDCAS_E_CAPACITY, "batch of %zu messages exceeds 2^32", max_msgs);
+  const uint64_t tiles = max_chunks / kTile + 2;
+  if ((e = c->ws_S.ensure(max_msgs + 1))) return c->hip_fail(e, "workspace S");
+  if ((e = c->ws_total.ensure(2))) return c->hip_fail(e, "workspace total");
+  if ((e = c->ws_tile_first.ensure(tiles))) return c->hip_fail(e, "workspace tile_first");
+  if ((e = c->ws_nodes.ensure(8 * (tiles * kTile)))) return c->hip_fail(e, "workspace nodes");
+  size_t tb = batch_scan_temp_bytes((uint32_t)std::max<size_t>(max_msgs, 1));
+  if ((e = c->ws_scan.ensure(tb))) return c->hip_fail(e, "workspace scan");
+  c->ws.S = c->ws_S.p;
+  c->ws.total = c->ws_total.p;
+  c->ws.tile_first = c->ws_tile_first.p;
+  c->ws.nodes = c->ws_nodes.p;
+  c->ws.scan_tmp = c->ws_scan.p;
+  c->ws.scan_tmp_bytes = c->ws_scan.cap;
+  c->ws.cap_msgs = (uint32_t)(c->ws_S.cap - 1);
+  // every tile the leaf kernel may touch needs a tile_first entry and kTile node slots
+  c->ws.cap_chunks = std::min<uint64_t>((c->ws_tile_first.cap - 1) * kTile, c->ws_nodes.cap / 8 - kTile);
+  c->ws.grid = batch_grid(c->device);
+  return SDCAS_OK;
+}
+
+int ensure_stage(sdcas_ctx* c, size_t bytes) {
+  if (bytes <= c->h_stage_cap) return SDCAS_OK;
+  if (c->h_stage) (void)hipHostFree(c->h_stage);
+  c->h_stage = nullptr;
+  c->h_stage_cap = 0;
+  hipError_t e = hipHostMalloc(&c->h_stage, bytes, hipHostMallocDefault);
+  if (e) return c->hip_fail(e, "pinned staging");
+  c->h_stage_cap = bytes;
+  return SDCAS_OK;
+}
+
+// Enqueue the hash of n device messages (the one launch sequence every API
+// ends in), with optional HIP-event profiling of the leaf kernel.
+int launch_batch(sdcas_ctx* c, const uint8_t* blob, const uint64_t* offs, const uint64_t* lens, uint32_t n,
+                 uint8_t* out32, uint64_t* keys, hipStream_t st) {
+  hipError_t e;
+  if (c->profile) {
+    hipEvent_t a = c->event(), b = c->event(), la = c->event(), lb = c->event();
+    (void)hipEventRecord(a, st);
+    e = batch_hash(c->ws, blob, offs, lens, n, out32, keys, st, la, lb);
+    (void)hipEventRecord(b, st);
+    c->ev_all.push_back({a, b});
+    c->ev_leaf.push_back({la, lb});
+  } else {
+    e = batch_hash(c->ws, blob, offs, lens, n, out32, keys, st);
+  }
+  if (e) return c->hip_fail(e, "batch_hash");
+  return SDCAS_OK;
+}
+
+// Hash messages already packed in c->h_stage at 16-aligned offsets; results
+// to host arrays (out32 and/or keys, indexed from 0).
+int run_staged(sdcas_ctx* c, const std::vector<uint64_t>& offs, const std::vector<uint64_t>& lens,
+               uint64_t stage_bytes, uint64_t chunks, uint8_t* out32, uint64_t* keys) {
+  const uint32_t n = (uint32_t)offs.size();
+  if (!n) return SDCAS_OK;
+  int rc;
+  if ((rc = reserve_ws(c, std::max<size_t>(n, c->ws.cap_msgs), std::max<uint64_t>(chunks, c->ws.cap_chunks))))
+    return rc;
+  hipError_t e;
+  if ((e = c->d_blob.ensure(stage_bytes + kSlack))) return c->hip_fail(e, "device blob");
+  if ((e = c->d_offs.ensure(n)) || (e = c->d_lens.ensure(n))) return c->hip_fail(e, "device offsets");
+  if (out32 && (e = c->d_out32.ensure(32ull * n))) return c->hip_fail(e, "device digests");
+  if (keys && (e = c->d_keys.ensure(n))) return c->hip_fail(e, "device keys");
+  hipStream_t st = c->stream;
+  if ((e = hipMemcpyAsync(c->d_blob.p, c->h_stage, stage_bytes, hipMemcpyHostToDevice, st)) ||
+      (e = hipMemcpyAsync(c->d_offs.p, offs.data(), 8ull * n, hipMemcpyHostToDevice, st)) ||
+      (e = hipMemcpyAsync(c->d_lens.p, lens.data(), 8ull * n, hipMemcpyHostToDevice, st)))
+    return c->hip_fail(e, "H2D");
+  if ((rc = launch_batch(c, c->d_blob.p, c->d_offs.p, c->d_lens.p, n, out32 ? c->d_out32.p : nullptr,
+                         keys ? c->d_keys.p : nullptr, st)))
+    return rc;
+  if (out32 && (e = hipMemcpyAsync(out32, c->d_out32.p, 32ull * n, hipMemcpyDeviceToHost, st)))
+    return c->hip_fail(e, "D2H digests");
+  if (keys && (e = hipMemcpyAsync(keys, c->d_keys.p, 8ull * n, hipMemcpyDeviceToHost, st)))
+    return c->hip_fail(e, "D2H keys");
+  if ((e = hipStreamSynchronize(st))) return c->hip_fail(e, "sync");
+  return SDCAS_OK;
+}
+
+// Big messages (> 1 MiB) from host memory: stream 1 MiB pieces through the
+// staging buffer; `fill(dst, off, len)` provides message bytes [off, off+len)
+// and returns a status (0 ok). Digests go to out32[k] for message k.
+struct BigItem {
+  uint64_t len;
+  uint64_t out_index;
+};
+
+template <class Fill>
+int run_big(sdcas_ctx* c, const std::vector<BigItem>& items, uint8_t* out32_host, Fill fill, int32_t* status) {
+  if (items.empty()) return SDCAS_OK;
+  hipError_t e;
+  int rc;
+  const uint64_t piece_bytes = 1024ull * kTile;
+  const uint64_t window = std::max<uint64_t>(piece_bytes, (c->staging_bytes / piece_bytes) * piece_bytes);
+  if ((rc = ensure_stage(c, window + kSlack))) return rc;
+  if ((e = c->d_blob.ensure(window + kSlack))) return c->hip_fail(e, "device blob");
+  std::vector<FileDesc> files(items.size());
+  uint64_t nodes = 0;
+  for (size_t i = 0; i < items.size(); ++i) {
+    files[i].C = chunks_of(items[i].len);
+    files[i].node_base = nodes;
+    files[i].out_index = i;
+    nodes += bigfile_node_count(files[i].C);
+  }
+  if ((e = c->d_file_nodes.ensure(8 * nodes + 8))) return c->hip_fail(e, "file nodes");
+  if ((e = c->d_files.ensure(items.size()))) return c->hip_fail(e, "file descs");
+  if ((e = c->d_out32.ensure(32 * items.size()))) return c->hip_fail(e, "device digests");
+  const uint32_t max_pieces = (uint32_t)(window / piece_bytes);
+  if ((e = c->d_pieces.ensure(max_pieces))) return c->hip_fail(e, "piece descs");
+  hipStream_t st = c->stream;
+  std::vector<PieceDesc> pieces;
+  uint64_t used = 0;
+  auto flush = [&]() -> int {
+    if (pieces.empty()) return SDCAS_OK;
+    hipError_t ee;
+    if ((ee = hipMemcpyAsync(c->d_blob.p, c->h_stage, used, hipMemcpyHostToDevice, st)) ||
+        (ee = hipMemcpyAsync(c->d_pieces.p, pieces.data(), sizeof(PieceDesc) * pieces.size(),
+                             hipMemcpyHostToDevice, st)))
+      return c->hip_fail(ee, "H2D pieces");
+    if ((ee = piece_hash(c->d_blob.p, c->d_pieces.p, (uint32_t)pieces.size(), c->d_file_nodes.p, st)))
+      return c->hip_fail(ee, "piece_hash");
+    // the staging buffer is reused by the next window
+    if ((ee = hipStreamSynchronize(st))) return c->hip_fail(ee, "sync");
+    pieces.clear();
+    used = 0;
+    return SDCAS_OK;
+  };
+  for (size_t i = 0; i < items.size(); ++i) {
+    const uint64_t len = items[i].len;
+    for (uint64_t off = 0; off < len; off += piece_bytes) {
+      const uint32_t pl = (uint32_t)std::min<uint64_t>(piece_bytes, len - off);
+      if (used + pl > window && (rc = flush())) return rc;
+      int st_i = fill(i, c->h_stage + used, off, pl);
+      if (st_i) {
+        if (status) status[items[i].out_index] = st_i;
+        break;
+      }
+      PieceDesc pd{};
+      pd.off = used;
+      pd.j0 = off / 1024;
+      pd.node_base = files[i].node_base;
+      pd.len = pl;
+      pieces.push_back(pd);
+      used += align16(pl);
+    }
+  }
+  if ((rc = flush())) return rc;
+  if ((e = hipMemcpyAsync(c->d_files.p, files.data(), sizeof(FileDesc) * files.size(), hipMemcpyHostToDevice,
+                          st)))
+    return c->hip_fail(e, "H2D files");
+  if ((e = bigfile_finish(c->d_files.p, (uint32_t)files.size(), c->d_file_nodes.p, c->d_out32.p, st)))
+    return c->hip_fail(e, "bigfile_finish");
+  std::vector<uint8_t> tmp(32 * items.size());
+  if ((e = hipMemcpyAsync(tmp.data(), c->d_out32.p, tmp.size(), hipMemcpyDeviceToHost, st)) ||
+      (e = hipStreamSynchronize(st)))
+    return c->hip_fail(e, "D2H big digests");
+  for (size_t i = 0; i < items.size(); ++i) memcpy(out32_host + 32 * items[i].out_index, &tmp[32 * i], 32);
+  return SDCAS_OK;
+}
+
+// ---- file I/O with the reference's read pattern ---------------------------
+
+// read_exact at `off` (tokio AsyncReadExt::read_exact): fill n bytes or fail
+// with UnexpectedEof
+int pread_exact(int fd, uint8_t* dst, uint64_t n, uint64_t off) {
+  uint64_t got = 0;
+  while (got < n) {
+    ssize_t r = pread(fd, dst + got, n - got, (off_t)(off + got));
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      return errno;
+    }
+    if (r == 0) return SDCAS_STATUS_UNEXPECTED_EOF;
+    got += (uint64_t)r;
+  }
+  return 0;
+}
+
+// whole file into dst (capacity cap); returns status, *len = bytes read;
+// sets *overflow if the file holds more than cap bytes
+int read_whole(int fd, uint8_t* dst, uint64_t cap, uint64_t* len, bool* overflow) {
+  uint64_t got = 0;
+  *overflow = false;
+  for (;;) {
+    if (got == cap) {
+      uint8_t probe;
+      ssize_t r;
+      do r = pread(fd, &probe, 1, (off_t)got);
+      while (r < 0 && errno == EINTR);
+      if (r < 0) return errno;
+      if (r > 0) *overflow = true;
+      break;
+    }
+    ssize_t r = pread(fd, dst + got, cap - got, (off_t)got);
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      return errno;
+    }
+    if (r == 0) break;
+    got += (uint64_t)r;
+  }
+  *len = got;
+  return 0;
+}
+
+// cas.rs:23-62 message of one file into dst (capacity >= expected length).
+// Returns status; *len = message length. *retry_len != 0 asks the caller to
+// retry with a bigger slot (the file grew past `size` since it was indexed).
+int read_cas_message(const char* path, uint64_t size, uint8_t* dst, uint64_t cap, uint64_t* len,
+                     uint64_t* retry_len) {
+  *retry_len = 0;
+  int fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return errno;
+  for (int i = 0; i < 8; ++i) dst[i] = (uint8_t)(size >> (8 * i));  // cas.rs:25
+  int st = 0;
+  if (size <= kMin) {
+    // cas.rs:27-29: fs::read of the file as it is now
+    uint64_t got = 0;
+    bool over = false;
+    st = read_whole(fd, dst + 8, cap - 8, &got, &over);
+    if (!st && over) {
+      struct stat sb;
+      if (fstat(fd, &sb) == 0) *retry_len = 8 + (uint64_t)sb.st_size + 4096;
+      else st = errno;
+    }
+    *len = 8 + got;
+  } else {
+    // cas.rs:35-58: header, 4 samples at 8192 + k*seek_jump, footer at EOF-8192
+    uint8_t* p = dst + 8;
+    st = pread_exact(fd, p, kHF, 0);
+    p += kHF;
+    const uint64_t seek_jump = (size - kHF * 2) / kSampleCount;
+    for (uint64_t k = 0; !st && k < kSampleCount; ++k) {
+      st = pread_exact(fd, p, kSample, kHF + k * seek_jump);
+      p += kSample;
+    }
+    if (!st) {
+      struct stat sb;
+      if (fstat(fd, &sb) != 0) st = errno;
+      else if ((uint64_t)sb.st_size < kHF) st = EINVAL;  // seek(End(-8192)) before byte 0
+      else st = pread_exact(fd, p, kHF, (uint64_t)sb.st_size - kHF);
+    }
+    *len = SDCAS_SAMPLED_MESSAGE_LEN;
+  }
+  close(fd);
+  return st;
+}
+
+template <class F>
+void parallel_for(uint32_t threads, size_t n, F f) {
+  if (n == 0) return;
+  threads = (uint32_t)std::max<size_t>(1, std::min<size_t>(threads, n));
+  if (threads == 1) {
+    for (size_t i = 0; i < n; ++i) f(i);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  std::vector<std::thread> pool;
+  for (uint32_t t = 0; t < threads; ++t)
+    pool.emplace_back([&] {
+      for (size_t i; (i = next.fetch_add(1)) < n;) f(i);
+    });
+  for (auto& th : pool) th.join();
+}
+
+}  // namespace
+
+// ===========================================================================
+
+extern "C" {
+
+const char* sdcas_version(void) { return "sdcas-mi355x 0.1.0 (gfx950)"; }
+
+int sdcas_init(const sdcas_options* opts, sdcas_ctx** out) {
+  if (!out) return SDCAS_E_INVALID;
+  *out = nullptr;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return SDCAS_E_NO_DEVICE;
+  auto* c = new sdcas_ctx();
+  int dev = -1;
+  if (opts) {
+    dev = opts->device;
+    if (opts->io_threads) c->io_threads = opts->io_threads;
+    if (opts->staging_bytes) c->staging_bytes = std::max<uint64_t>(opts->staging_bytes, 1ull << 20);
+  }
+  if (dev < 0) (void)hipGetDevice(&dev);
+  if (dev >= count) {
+    delete c;
+    return SDCAS_E_NO_DEVICE;
+  }
+  c->device = dev;
+  if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return SDCAS_E_NO_DEVICE;
+  }
+  *out = c;
+  return SDCAS_OK;
+}
+
+void sdcas_destroy(sdcas_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (auto* b : {&c->ws_S, &c->ws_total, &c->d_offs, &c->d_lens, &c->d_keys, &c->dd_key_a, &c->dd_key_b,
+                  &c->dd_keys, &c->dd_ekeys, &c->dd_ekeys_sorted})
+    b->release();
+  for (auto* b : {&c->ws_tile_first, &c->ws_nodes, &c->d_file_nodes, &c->dd_idx_a, &c->dd_idx_b, &c->dd_head,
+                  &c->dd_nvalid, &c->dd_eidx})
+    b->release();
+  for (auto* b : {&c->ws_scan, &c->d_blob, &c->d_out32, &c->dd_valid, &c->dd_temp, &c->dd_has}) b->release();
+  c->d_pieces.release();
+  c->d_files.release();
+  c->dd_status.release();
+  c->dd_link.release();
+  c->dd_counts.release();
+  if (c->h_stage) (void)hipHostFree(c->h_stage);
+  for (auto e : c->ev_free) (void)hipEventDestroy(e);
+  for (auto& p : c->ev_leaf) (void)hipEventDestroy(p.first), (void)hipEventDestroy(p.second);
+  for (auto& p : c->ev_all) (void)hipEventDestroy(p.first), (void)hipEventDestroy(p.second);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* sdcas_last_error(const sdcas_ctx* c) { return c ? c->err.c_str() : "no context"; }
+
+uint64_t sdcas_cas_message_len(uint64_t size) { return size <= kMin ? size + 8 : SDCAS_SAMPLED_MESSAGE_LEN; }
+
+void sdcas_key_to_hex(uint64_t key, char out[17]) {
+  static const char* H = "0123456789abcdef";
+  for (int i = 0; i < 16; ++i) out[i] = H[(key >> (60 - 4 * i)) & 15];
+  out[16] = 0;
+}
+
+void sdcas_digest_to_hex(const uint8_t d[32], char out[65]) {
+  static const char* H = "0123456789abcdef";
+  for (int i = 0; i < 32; ++i) {
+    out[2 * i] = H[d[i] >> 4];
+    out[2 * i + 1] = H[d[i] & 15];
+  }
+  out[64] = 0;
+}
+
+int sdcas_dev_reserve(sdcas_ctx* c, size_t max_msgs, uint64_t max_chunks) {
+  if (!c) return SDCAS_E_INVALID;
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipSetDevice(c->device);
+  return reserve_ws(c, max_msgs, max_chunks);
+}
+
+int sdcas_dev_hash_messages(sdcas_ctx* c, const uint8_t* d_blob, const uint64_t* d_offsets, const uint64_t* d_lens,
+                            size_t n, uint8_t* d_out32, uint64_t* d_out_keys, void* stream) {
+  if (!c || (n && (!d_blob || !d_offsets || !d_lens))) return SDCAS_E_INVALID;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (n == 0) return SDCAS_OK;
+  if (n > c->ws.cap_msgs || !c->ws.S)
+    return c->fail(SDCAS_E_CAPACITY, "dev_hash_messages: %zu messages > reserved %u", n, c->ws.cap_msgs);
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  return launch_batch(c, d_blob, d_offsets, d_lens, (uint32_t)n, d_out32, d_out_keys, st);
+}
+
+int sdcas_dev_sync(sdcas_ctx* c, void* stream) {
+  if (!c) return SDCAS_E_INVALID;
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  hipError_t e = hipStreamSynchronize(st);
+  if (e) return c->hip_fail(e, "sync");
+  uint64_t total = 0;
+  if (c->ws.total && (e = hipMemcpy(&total, c->ws.total, 8, hipMemcpyDeviceToHost))) return c->hip_fail(e, "total");
+  if (total > c->ws.cap_chunks)
+    return c->fail(SDCAS_E_CAPACITY, "batch of %llu chunks exceeds reserved %llu", (unsigned long long)total,
+                   (unsigned long long)c->ws.cap_chunks);
+  return SDCAS_OK;
+}
+
+int sdcas_dev_profile(sdcas_ctx* c, int enable) {
+  if (!c) return SDCAS_E_INVALID;
+  c->profile = enable != 0;
+  for (auto* v : {&c->ev_all, &c->ev_leaf}) {
+    for (auto& p : *v) c->ev_free.push_back(p.first), c->ev_free.push_back(p.second);
+    v->clear();
+  }
+  return SDCAS_OK;
+}
+
+static float mean_ms(std::vector<std::pair<hipEvent_t, hipEvent_t>>& v) {
+  float sum = 0;
+  int cnt = 0;
+  for (auto& p : v) {
+    if (hipEventSynchronize(p.second) != hipSuccess) continue;
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, p.first, p.second) == hipSuccess) {
+      sum += ms;
+      ++cnt;
+    }
+  }
+  return cnt ? sum / cnt : 0.f;
+}
+
+int sdcas_dev_last_kernel_ms(sdcas_ctx* c, float* leaf_ms, float* total_ms) {
+  if (!c) return SDCAS_E_INVALID;
+  if (leaf_ms) *leaf_ms = mean_ms(c->ev_leaf);
+  if (total_ms) *total_ms = mean_ms(c->ev_all);
+  return SDCAS_OK;
+}
+
+int sdcas_hash_messages(sdcas_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* lens, size_t n,
+                        uint8_t* out32);
+static int hash_host_messages(sdcas_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* lens,
+                              size_t n, uint8_t* out32, uint64_t* keys) {
+  if (!c || (n && (!blob || !offsets || !lens))) return SDCAS_E_INVALID;
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipSetDevice(c->device);
+  const uint64_t big_cut = 1024ull * kTile;  // > 1 MiB: piece path
+  const uint64_t cap = c->staging_bytes;
+  int rc;
+  if ((rc = ensure_stage(c, cap + kSlack))) return rc;
+  std::vector<uint64_t> offs, ls;
+  std::vector<size_t> idx;
+  std::vector<BigItem> big;
+  uint64_t used = 0, chunks = 0;
+  std::vector<uint8_t> tmp32;
+  auto flush = [&]() -> int {
+    if (offs.empty()) return SDCAS_OK;
+    tmp32.resize(32 * offs.size());
+    std::vector<uint64_t> tk(keys ? offs.size() : 0);
+    int r = run_staged(c, offs, ls, used, chunks, out32 ? tmp32.data() : nullptr, keys ? tk.data() : nullptr);
+    if (r) return r;
+    for (size_t k = 0; k < idx.size(); ++k) {
+      if (out32) memcpy(out32 + 32 * idx[k], &tmp32[32 * k], 32);
+      if (keys) keys[idx[k]] = tk[k];
+    }
+    offs.clear(), ls.clear(), idx.clear();
+    used = chunks = 0;
+    return SDCAS_OK;
+  };
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t L = lens[i];
+    if (L > big_cut) {
+      big.push_back({L, i});
+      continue;
+    }
+    if (used + align16(L) > cap && (rc = flush())) return rc;
+    memcpy(c->h_stage + used, blob + offsets[i], L);
+    offs.push_back(used);
+    ls.push_back(L);
+    idx.push_back(i);
+    used += align16(L);
+    chunks += chunks_of(L);
+  }
+  if ((rc = flush())) return rc;
+  if (!big.empty()) {
+    std::vector<uint8_t> d32(32 * n);
+    rc = run_big(c, big, d32.data(),
+                 [&](size_t k, uint8_t* dst, uint64_t off, uint32_t len) {
+                   memcpy(dst, blob + offsets[big[k].out_index] + off, len);
+                   return 0;
+                 },
+                 nullptr);
+    if (rc) return rc;
+    for (auto& b : big) {
+      if (out32) memcpy(out32 + 32 * b.out_index, &d32[32 * b.out_index], 32);
+      if (keys) {
+        uint64_t k = 0;
+        for (int t = 0; t < 8; ++t) k = (k << 8) | d32[32 * b.out_index + t];
+        keys[b.out_index] = k;
+      }
+    }
+  }
+  return SDCAS_OK;
+}
+
+int sdcas_hash_messages(sdcas_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* lens, size_t n,
+                        uint8_t* out32) {
+  if (!out32 && n) return SDCAS_E_INVALID;
+  return hash_host_messages(c, blob, offsets, lens, n, out32, nullptr);
+}
+
+int sdcas_cas_ids_from_messages(sdcas_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* lens,
+                                size_t n, uint64_t* out_keys) {
+  if (!out_keys && n) return SDCAS_E_INVALID;
+  return hash_host_messages(c, blob, offsets, lens, n, nullptr, out_keys);
+}
+
+int sdcas_cas_ids(sdcas_ctx* c, const char* const* paths, const uint64_t* sizes, size_t n, uint64_t* out_keys,
+                  int32_t* out_status) {
+  if (!c || (n && (!paths || !sizes || !out_keys || !out_status))) return SDCAS_E_INVALID;
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipSetDevice(c->device);
+  const uint64_t cap = c->staging_bytes;
+  int rc;
+  if ((rc = ensure_stage(c, cap + kSlack))) return rc;
+  // slot sizes: the message the indexer's size predicts (cas.rs:27); a file
+  // that grew is retried in a later batch with its actual size
+  std::vector<uint64_t> want(n);
+  for (size_t i = 0; i < n; ++i) want[i] = sdcas_cas_message_len(sizes[i]);
+  std::vector<size_t> todo(n);
+  for (size_t i = 0; i < n; ++i) todo[i] = i;
+  for (int round = 0; round < 4 && !todo.empty(); ++round) {
+    std::vector<size_t> retry;
+    size_t p = 0;
+    while (p < todo.size()) {
+      // batch [p, q) fitting the staging buffer
+      std::vector<uint64_t> slot_off;
+      uint64_t used = 0;
+      size_t q = p;
+      while (q < todo.size()) {
+        const uint64_t need = align16(want[todo[q]]);
+        if (need > cap) {
+          // a single message beyond staging: only a whole-file cas message of
+          // a file grown past staging size; give it its own staging round
+          if ((rc = ensure_stage(c, need + kSlack))) return rc;
+        }
+        if (q > p && used + need > std::max<uint64_t>(cap, c->h_stage_cap - kSlack)) break;
+        slot_off.push_back(used);
+        used += need;
+        ++q;
+      }
+      const size_t m = q - p;
+      std::vector<uint64_t> mlen(m), retry_len(m);
+      std::vector<int32_t> st(m);
+      parallel_for(c->io_threads, m, [&](size_t k) {
+        const size_t i = todo[p + k];
+        st[k] = read_cas_message(paths[i], sizes[i], c->h_stage + slot_off[k], align16(want[i]), &mlen[k],
+                                 &retry_len[k]);
+      });
+      std::vector<uint64_t> offs, ls;
+      std::vector<size_t> idx;
+      uint64_t chunks = 0;
+      for (size_t k = 0; k < m; ++k) {
+        const size_t i = todo[p + k];
+        if (retry_len[k] && !st[k]) {
+          want[i] = retry_len[k];
+          retry.push_back(i);
+          continue;
+        }
+        out_status[i] = st[k];
+        if (st[k]) continue;
+        offs.push_back(slot_off[k]);
+        ls.push_back(mlen[k]);
+        idx.push_back(i);
+        chunks += chunks_of(mlen[k]);
+      }
+      std::vector<uint64_t> tk(offs.size());
+      if ((rc = run_staged(c, offs, ls, used, chunks, nullptr, tk.data()))) return rc;
+      for (size_t k = 0; k < idx.size(); ++k) out_keys[idx[k]] = tk[k];
+      p = q;
+    }
+    todo.swap(retry);
+  }
+  for (size_t i : todo) out_status[i] = EAGAIN;  // kept growing while being read
+  return SDCAS_OK;
+}
+
+int sdcas_checksums(sdcas_ctx* c, const char* const* paths, size_t n, uint8_t* out32, int32_t* out_status) {
+  if (!c || (n && (!paths || !out32 || !out_status))) return SDCAS_E_INVALID;
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipSetDevice(c->device);
+  const uint64_t cap = c->staging_bytes, big_cut = 1024ull * kTile;
+  int rc;
+  if ((rc = ensure_stage(c, cap + kSlack))) return rc;
+  // file lengths first (hash.rs reads to EOF; a regular file's EOF is its length)
+  std::vector<uint64_t> flen(n);
+  std::vector<int32_t> fst(n);
+  parallel_for(c->io_threads, n, [&](size_t i) {
+    struct stat sb;
+    if (stat(paths[i], &sb) != 0) fst[i] = errno;
+    else if (S_ISDIR(sb.st_mode)) fst[i] = EISDIR;
+    else flen[i] = (uint64_t)sb.st_size, fst[i] = 0;
+  });
+  std::vector<size_t> small;
+  std::vector<BigItem> big;
+  for (size_t i = 0; i < n; ++i) {
+    out_status[i] = fst[i];
+    if (fst[i]) continue;
+    if (flen[i] > big_cut) big.push_back({flen[i], i});
+    else small.push_back(i);
+  }
+  size_t p = 0;
+  while (p < small.size()) {
+    std::vector<uint64_t> slot;
+    uint64_t used = 0;
+    size_t q = p;
+    while (q < small.size() && (q == p || used + align16(flen[small[q]]) <= cap)) {
+      slot.push_back(used);
+      used += align16(flen[small[q]]);
+      ++q;
+    }
+    const size_t m = q - p;
+    std::vector<uint64_t> got(m);
+    std::vector<int32_t> st(m);
+    parallel_for(c->io_threads, m, [&](size_t k) {
+      const size_t i = small[p + k];
+      int fd = open(paths[i], O_RDONLY | O_CLOEXEC);
+      if (fd < 0) {
+        st[k] = errno;
+        return;
+      }
+      bool over = false;
+      st[k] = read_whole(fd, c->h_stage + slot[k], flen[i], &got[k], &over);
+      close(fd);
+    });
+    std::vector<uint64_t> offs, ls;
+    std::vector<size_t> idx;
+    uint64_t chunks = 0;
+    for (size_t k = 0; k < m; ++k) {
+      const size_t i = small[p + k];
+      out_status[i] = st[k];
+      if (st[k]) continue;
+      offs.push_back(slot[k]);
+      ls.push_back(got[k]);
+      idx.push_back(i);
+      chunks += chunks_of(got[k]);
+    }
+    std::vector<uint8_t> d32(32 * offs.size());
+    if ((rc = run_staged(c, offs, ls, used, chunks, d32.data(), nullptr))) return rc;
+    for (size_t k = 0; k < idx.size(); ++k) memcpy(out32 + 32 * idx[k], &d32[32 * k], 32);
+    p = q;
+  }
+  if (!big.empty()) {
+    std::vector<int> fds(big.size(), -1);
+    for (size_t k = 0; k < big.size(); ++k) fds[k] = open(paths[big[k].out_index], O_RDONLY | O_CLOEXEC);
+    std::vector<uint8_t> d32(32 * n);
+    rc = run_big(c, big, d32.data(),
+                 [&](size_t k, uint8_t* dst, uint64_t off, uint32_t len) -> int {
+                   if (fds[k] < 0) return errno ? errno : EIO;
+                   return pread_exact(fds[k], dst, len, off);  // hash.rs: 1 MiB reads to EOF
+                 },
+                 out_status);
+    for (int fd : fds)
+      if (fd >= 0) close(fd);
+    if (rc) return rc;
+    for (auto& b : big)
+      if (!out_status[b.out_index]) memcpy(out32 + 32 * b.out_index, &d32[32 * b.out_index], 32);
+  }
+  return SDCAS_OK;
+}
+
+// ---- dedup -----------------------------------------------------------------
+
+static int dedup_reserve(sdcas_ctx* c, size_t n, size_t ne) {
+  hipError_t e;
+  const size_t m = std::max<size_t>(n, ne);
+  if ((e = c->dd_key_a.ensure(m)) || (e = c->dd_key_b.ensure(m)) || (e = c->dd_idx_a.ensure(m)) ||
+      (e = c->dd_idx_b.ensure(m)) || (e = c->dd_head.ensure(m)) || (e = c->dd_valid.ensure(m)) ||
+      (e = c->dd_nvalid.ensure(1)) || (e = c->dd_counts.ensure(2)) || (e = c->dd_ekeys_sorted.ensure(ne + 1)) ||
+      (e = c->dd_eidx.ensure(ne + 1)))
+    return c->hip_fail(e, "dedup workspace");
+  size_t tb = DedupWorkspace::temp_bytes_for((uint32_t)std::max<size_t>(m, 1));
+  if ((e = c->dd_temp.ensure(tb))) return c->hip_fail(e, "dedup temp");
+  DedupWorkspace& w = c->dws;
+  w.key_a = c->dd_key_a.p;
+  w.key_b = c->dd_key_b.p;
+  w.idx_a = c->dd_idx_a.p;
+  w.idx_b = c->dd_idx_b.p;
+  w.head = c->dd_head.p;
+  w.valid = c->dd_valid.p;
+  w.nvalid = c->dd_nvalid.p;
+  w.temp = c->dd_temp.p;
+  w.temp_bytes = c->dd_temp.cap;
+  w.cap = (uint32_t)c->dd_key_a.cap;
+  return SDCAS_OK;
+}
+
+int sdcas_dedup(sdcas_ctx* c, const uint64_t* keys, const uint8_t* has_key, const int32_t* status, size_t n,
+                size_t chunk_size, const uint64_t* existing_keys, size_t n_existing, int64_t* out_link,
+                int64_t* out_created, int64_t* out_linked) {
+  if (!c || (n && (!keys || !has_key || !out_link)) || (n_existing && !existing_keys)) return SDCAS_E_INVALID;
+  if (n > 0xFFFFFFF0ull || n_existing > 0xFFFFFFF0ull) return SDCAS_E_CAPACITY;
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipSetDevice(c->device);
+  if (chunk_size == 0) chunk_size = SDCAS_IDENTIFIER_CHUNK_SIZE;
+  int rc;
+  if ((rc = dedup_reserve(c, n, n_existing))) return rc;
+  hipError_t e;
+  hipStream_t st = c->stream;
+  if ((e = c->dd_keys.ensure(n)) || (e = c->dd_has.ensure(n)) || (e = c->dd_link.ensure(n)) ||
+      (status && (e = c->dd_status.ensure(n))) || (e = c->dd_ekeys.ensure(n_existing + 1)))
+    return c->hip_fail(e, "dedup buffers");
+  if ((e = hipMemcpyAsync(c->dd_keys.p, keys, 8 * n, hipMemcpyHostToDevice, st)) ||
+      (e = hipMemcpyAsync(c->dd_has.p, has_key, n, hipMemcpyHostToDevice, st)) ||
+      (status && (e = hipMemcpyAsync(c->dd_status.p, status, 4 * n, hipMemcpyHostToDevice, st))) ||
+      (n_existing && (e = hipMemcpyAsync(c->dd_ekeys.p, existing_keys, 8 * n_existing, hipMemcpyHostToDevice, st))))
+    return c->hip_fail(e, "dedup H2D");
+  if (n_existing &&
+      (e = dedup_sort_existing(c->dws, c->dd_ekeys.p, (uint32_t)n_existing, c->dd_ekeys_sorted.p, c->dd_eidx.p, st)))
+    return c->hip_fail(e, "dedup existing sort");
+  if ((e = dedup_run(c->dws, c->dd_keys.p, c->dd_has.p, status ? c->dd_status.p : nullptr, (uint32_t)n,
+                     (uint32_t)chunk_size, c->dd_ekeys_sorted.p, c->dd_eidx.p, (uint32_t)n_existing, c->dd_link.p,
+                     c->dd_counts.p, st)))
+    return c->hip_fail(e, "dedup");
+  unsigned long long cnt[2] = {0, 0};
+  if (n && ((e = hipMemcpyAsync(out_link, c->dd_link.p, 8 * n, hipMemcpyDeviceToHost, st)) ||
+            (e = hipMemcpyAsync(cnt, c->dd_counts.p, sizeof cnt, hipMemcpyDeviceToHost, st))))
+    return c->hip_fail(e, "dedup D2H");
+  if ((e = hipStreamSynchronize(st))) return c->hip_fail(e, "dedup sync");
+  if (out_created) *out_created = (int64_t)cnt[0];
+  if (out_linked) *out_linked = (int64_t)cnt[1];
+  return SDCAS_OK;
+}
+
+int sdcas_dev_dedup(sdcas_ctx* c, const uint64_t* d_keys, const uint8_t* d_has_key, const int32_t* d_status,
+                    size_t n, size_t chunk_size, int64_t* d_out_link, uint64_t* d_counts, void* stream) {
+  if (!c || (n && (!d_keys || !d_has_key || !d_out_link))) return SDCAS_E_INVALID;
+  if (n > 0xFFFFFFF0ull) return SDCAS_E_CAPACITY;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (chunk_size == 0) chunk_size = SDCAS_IDENTIFIER_CHUNK_SIZE;
+  int rc;
+  if (n > c->dws.cap && (rc = dedup_reserve(c, n, 0))) return rc;
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  hipError_t e = dedup_run(c->dws, d_keys, d_has_key, d_status, (uint32_t)n, (uint32_t)chunk_size, nullptr, nullptr,
+                           0, d_out_link, (unsigned long long*)d_counts, st);
+  if (e) return c->hip_fail(e, "dev_dedup");
+  return SDCAS_OK;
+}
+
+// ---- synthetic corpora -------------------------------------------------------
+
+int sdcas_dev_synth_cas_messages(sdcas_ctx* c, const uint64_t* d_keys, const uint64_t* d_sizes,
+                                 const uint64_t* d_offs, size_t n, uint8_t* d_blob, void* stream) {
+  if (!c) return SDCAS_E_INVALID;
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  hipError_t e = synth_cas_messages(d_keys, d_sizes, d_offs, (uint32_t)n, d_blob, st);
+  return e ? c->hip_fail(e, "synth") : SDCAS_OK;
+}
+
+int sdcas_dev_synth_content(sdcas_ctx* c, const uint64_t* d_keys, const uint64_t* d_starts, const uint64_t* d_lens,
+                            const uint64_t* d_offs, size_t n, uint8_t* d_blob, void* stream) {
+  if (!c) return SDCAS_E_INVALID;
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  hipError_t e = synth_content(d_keys, d_starts, d_lens, d_offs, (uint32_t)n, d_blob, st);
+  return e ? c->hip_fail(e, "synth") : SDCAS_OK;
+}
+
+}  // extern "C"

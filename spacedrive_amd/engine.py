@@ -1,0 +1,221 @@
+"""Host-side mirror of sd-core's content-identification interface over the
+libsdcas.so C ABI.
+
+The reference functions keep their names, argument meaning and error
+behaviour:
+
+* ``generate_cas_id(path, size) -> str`` — core/src/object/cas.rs:23-62
+  (16 lowercase hex chars; io errors raise ``OSError``; a file shorter than
+  the windows ``size`` implies raises ``OSError(UnexpectedEof, "failed to
+  fill whole buffer")`` like tokio's read_exact);
+* ``file_checksum(path) -> str`` — core/src/object/validation/hash.rs:11-25
+  (64 lowercase hex chars);
+* ``identifier_dedup(...)`` — the cas_id -> Object link of
+  core/src/object/file_identifier/mod.rs:98-350 in canonical form.
+
+The batch forms (``generate_cas_ids``, ``file_checksums``,
+``hash_messages``) are what the identifier/validator jobs would call once per
+chunk instead of per file. Everything runs on the GPU; there is no CPU path.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import _native as N
+
+
+def _arr(a, dtype):
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+def _ptr(a):
+    return a.ctypes.data if a is not None and a.size else None
+
+
+def key_to_hex(key: int) -> str:
+    return f"{int(key):016x}"
+
+
+def digest_to_hex(d) -> str:
+    return bytes(np.asarray(d, dtype=np.uint8)).hex()
+
+
+def io_error(status: int, path=None) -> OSError:
+    if status == N.SDCAS_STATUS_UNEXPECTED_EOF:
+        e = OSError(status, "failed to fill whole buffer")
+    else:
+        e = OSError(status, os.strerror(status) if status < 4096 else f"status {status}")
+    if path is not None:
+        e.filename = str(path)
+    return e
+
+
+class Engine:
+    """One libsdcas context bound to one GPU."""
+
+    def __init__(self, device: int = 0, io_threads: int = 0, staging_bytes: int = 0):
+        self.L = N.load()
+        opts = N.Options(device, io_threads, staging_bytes)
+        ctx = ctypes.c_void_p()
+        rc = self.L.sdcas_init(ctypes.byref(opts), ctypes.byref(ctx))
+        if rc != N.SDCAS_OK:
+            raise N.SdcasError(rc, "sdcas_init failed (no HIP device?)")
+        self.ctx = ctx
+
+    # -- lifetime -------------------------------------------------------------
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.L.sdcas_destroy(self.ctx)
+            self.ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != N.SDCAS_OK:
+            msg = self.L.sdcas_last_error(self.ctx).decode(errors="replace")
+            raise N.SdcasError(rc, f"{what}: {msg}")
+
+    # -- reference functions, batched ------------------------------------------
+    def generate_cas_ids(self, paths, sizes):
+        """cas.rs:23-62 for many files -> (keys uint64[n], status int32[n])"""
+        n = len(paths)
+        bpaths = [os.fsencode(p) for p in paths]
+        parr = (ctypes.c_char_p * max(n, 1))(*bpaths)
+        sizes = _arr(sizes, np.uint64)
+        keys = np.zeros(n, np.uint64)
+        st = np.zeros(n, np.int32)
+        self._check(self.L.sdcas_cas_ids(self.ctx, parr, _ptr(sizes), n, _ptr(keys), _ptr(st)),
+                    "sdcas_cas_ids")
+        return keys, st
+
+    def file_checksums(self, paths):
+        """hash.rs:11-25 for many files -> (digests uint8[n, 32], status int32[n])"""
+        n = len(paths)
+        parr = (ctypes.c_char_p * max(n, 1))(*[os.fsencode(p) for p in paths])
+        out = np.zeros((n, 32), np.uint8)
+        st = np.zeros(n, np.int32)
+        self._check(self.L.sdcas_checksums(self.ctx, parr, n, _ptr(out), _ptr(st)), "sdcas_checksums")
+        return out, st
+
+    def generate_cas_id(self, path, size) -> str:
+        keys, st = self.generate_cas_ids([path], [size])
+        if st[0]:
+            raise io_error(int(st[0]), path)
+        return key_to_hex(keys[0])
+
+    def file_checksum(self, path) -> str:
+        out, st = self.file_checksums([path])
+        if st[0]:
+            raise io_error(int(st[0]), path)
+        return digest_to_hex(out[0])
+
+    # -- pre-assembled messages ---------------------------------------------------
+    @staticmethod
+    def pack(messages):
+        """list of bytes-like -> (blob, offsets, lens)"""
+        lens = np.array([len(m) for m in messages], np.uint64)
+        offs = np.zeros(len(messages), np.uint64)
+        if len(messages):
+            offs[1:] = np.cumsum(lens[:-1])
+        blob = np.frombuffer(b"".join(bytes(m) for m in messages), np.uint8) if len(messages) else \
+            np.zeros(0, np.uint8)
+        return blob, offs, lens
+
+    def hash_messages(self, blob, offsets, lens):
+        blob = _arr(blob, np.uint8)
+        offsets, lens = _arr(offsets, np.uint64), _arr(lens, np.uint64)
+        n = lens.size
+        out = np.zeros((n, 32), np.uint8)
+        self._check(self.L.sdcas_hash_messages(self.ctx, _ptr(blob) or 1, _ptr(offsets), _ptr(lens), n,
+                                               _ptr(out)), "sdcas_hash_messages")
+        return out
+
+    def cas_ids_from_messages(self, blob, offsets, lens):
+        blob = _arr(blob, np.uint8)
+        offsets, lens = _arr(offsets, np.uint64), _arr(lens, np.uint64)
+        n = lens.size
+        keys = np.zeros(n, np.uint64)
+        self._check(self.L.sdcas_cas_ids_from_messages(self.ctx, _ptr(blob) or 1, _ptr(offsets),
+                                                       _ptr(lens), n, _ptr(keys)),
+                    "sdcas_cas_ids_from_messages")
+        return keys
+
+    # -- dedup ------------------------------------------------------------------------
+    def identifier_dedup(self, keys, has_key, status=None, chunk_size=100, existing_keys=()):
+        keys = _arr(keys, np.uint64)
+        n = keys.size
+        has_key = _arr(has_key, np.uint8)
+        st = None if status is None else _arr(status, np.int32)
+        ex = _arr(existing_keys, np.uint64)
+        out = np.zeros(n, np.int64)
+        created, linked = ctypes.c_int64(0), ctypes.c_int64(0)
+        self._check(self.L.sdcas_dedup(self.ctx, _ptr(keys), _ptr(has_key), _ptr(st), n, chunk_size,
+                                       _ptr(ex), ex.size, _ptr(out), ctypes.byref(created),
+                                       ctypes.byref(linked)), "sdcas_dedup")
+        return out, created.value, linked.value
+
+    # -- device-resident (pointers are ints: device addresses, e.g. tensor.data_ptr())
+    def dev_reserve(self, max_msgs, max_chunks):
+        self._check(self.L.sdcas_dev_reserve(self.ctx, int(max_msgs), int(max_chunks)), "dev_reserve")
+
+    def dev_hash_messages(self, blob, offs, lens, n, out32=0, keys=0, stream=0):
+        self._check(self.L.sdcas_dev_hash_messages(self.ctx, blob, offs, lens, int(n), out32 or None,
+                                                   keys or None, stream or None), "dev_hash_messages")
+
+    def dev_sync(self, stream=0):
+        self._check(self.L.sdcas_dev_sync(self.ctx, stream or None), "dev_sync")
+
+    def dev_synth_cas_messages(self, keys, sizes, offs, n, blob, stream=0):
+        self._check(self.L.sdcas_dev_synth_cas_messages(self.ctx, keys, sizes, offs, int(n), blob,
+                                                        stream or None), "synth")
+
+    def dev_synth_content(self, keys, starts, lens, offs, n, blob, stream=0):
+        self._check(self.L.sdcas_dev_synth_content(self.ctx, keys, starts, lens, offs, int(n), blob,
+                                                   stream or None), "synth")
+
+    def dev_dedup(self, keys, has_key, status, n, chunk_size, out_link, counts, stream=0):
+        self._check(self.L.sdcas_dev_dedup(self.ctx, keys, has_key, status or None, int(n), chunk_size,
+                                           out_link, counts or None, stream or None), "dev_dedup")
+
+    def dev_profile(self, enable=True):
+        self._check(self.L.sdcas_dev_profile(self.ctx, 1 if enable else 0), "dev_profile")
+
+    def dev_kernel_ms(self):
+        a, b = ctypes.c_float(0), ctypes.c_float(0)
+        self._check(self.L.sdcas_dev_last_kernel_ms(self.ctx, ctypes.byref(a), ctypes.byref(b)), "ms")
+        return a.value, b.value
+
+
+_default = None
+
+
+def default_engine() -> Engine:
+    global _default
+    if _default is None:
+        _default = Engine()
+    return _default
+
+
+def generate_cas_id(path, size) -> str:
+    """core/src/object/cas.rs:23 — `pub async fn generate_cas_id(path, size) -> Result<String>`"""
+    return default_engine().generate_cas_id(path, size)
+
+
+def file_checksum(path) -> str:
+    """core/src/object/validation/hash.rs:11 — `pub async fn file_checksum(path) -> Result<String>`"""
+    return default_engine().file_checksum(path)
+
+
+__all__ = ["Engine", "generate_cas_id", "file_checksum", "key_to_hex", "digest_to_hex", "io_error",
+           "default_engine"]

@@ -1,0 +1,64 @@
+"""CPU tests of the boundary: libsdcas.so loads and exports every entry point
+include/*.h declares (no compute calls — there is no GPU here)."""
+import os
+import re
+import subprocess
+
+import pytest
+
+from spacedrive_amd import _native as N
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    names = set()
+    for h in ("sdcas.h", "sdcas_bench.h"):
+        src = open(os.path.join(ROOT, "include", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names |= set(re.findall(r"\b(sdcas_\w+)\s*\(", src))
+    return names
+
+
+def test_header_and_binding_agree():
+    assert declared_symbols() == set(N.ABI_SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol():
+    L = N.load()
+    for s in declared_symbols():
+        assert hasattr(L, s), s
+    out = subprocess.run(["nm", "-D", "--defined-only", N.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT (sdcas_\w+)", out))
+    assert declared_symbols() <= exported
+
+
+def test_library_is_gfx950():
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-n", N.LIB_PATH], capture_output=True,
+                         text=True)
+    blob = open(N.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_pure_helpers_without_gpu():
+    import ctypes
+    L = N.load()
+    buf = ctypes.create_string_buffer(17)
+    L.sdcas_key_to_hex(0x71E0A99173564931, buf)
+    assert buf.value == b"71e0a99173564931"
+    assert L.sdcas_cas_message_len(0) == 8
+    assert L.sdcas_cas_message_len(102400) == 102408
+    assert L.sdcas_cas_message_len(102401) == 57352
+    d = bytes(range(32))
+    out = ctypes.create_string_buffer(65)
+    L.sdcas_digest_to_hex(d, out)
+    assert out.value.decode() == d.hex()
+
+
+def test_init_fails_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from spacedrive_amd import Engine
+    with pytest.raises(N.SdcasError):
+        Engine()

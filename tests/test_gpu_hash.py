@@ -1,0 +1,213 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the golden
+fixtures (upstream BLAKE3 C, tests/golden) and the CPU oracle, bit-exact."""
+import os
+
+import numpy as np
+import pytest
+
+from tests._oracle import cas_windows, content, golden, spec_content, write_sparse_file
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from spacedrive_amd import Engine
+    e = Engine(staging_bytes=64 << 20)
+    yield e
+    e.close()
+
+
+def test_blake3_vectors(eng):
+    cases = golden("blake3_vectors.json")
+    msgs = [content("pattern251", 0, c["len"]).tobytes() for c in cases]
+    out = eng.hash_messages(*eng.pack(msgs))
+    for c, d in zip(cases, out):
+        assert bytes(d).hex() == c["hash"], c["len"]
+
+
+def test_blake3_vectors_one_by_one(eng):
+    # every message alone in its batch: single-tile layouts
+    for c in golden("blake3_vectors.json"):
+        m = content("pattern251", 0, c["len"]).tobytes()
+        assert bytes(eng.hash_messages(*eng.pack([m]))[0]).hex() == c["hash"], c["len"]
+
+
+def test_cas_messages_golden(eng):
+    cases = [c for c in golden("cas_ids.json")]
+    msgs = []
+    for c in cases:
+        kind, key = spec_content(c["content"])
+        parts = [c["size"].to_bytes(8, "little")] + [content(kind, o, n, key).tobytes()
+                                                       for o, n in cas_windows(c["size"])]
+        msgs.append(b"".join(parts))
+    keys = eng.cas_ids_from_messages(*eng.pack(msgs))
+    for c, k in zip(cases, keys):
+        assert f"{int(k):016x}" == c["cas_id"], c
+
+
+def test_generate_cas_id_files(eng, tmp_path):
+    cases = golden("cas_ids.json")
+    paths, sizes = [], []
+    for c in cases:
+        kind, key = spec_content(c["content"])
+        p = tmp_path / f"f_{c['content'].replace(':', '_')}_{c['size']}"
+        write_sparse_file(p, kind, key, c["size"], cas_windows(c["size"]))
+        paths.append(str(p))
+        sizes.append(c["size"])
+    keys, st = eng.generate_cas_ids(paths, sizes)
+    assert (st == 0).all()
+    for c, k in zip(cases, keys):
+        assert f"{int(k):016x}" == c["cas_id"], c
+    # the single-file mirror of cas.rs:23
+    assert eng.generate_cas_id(paths[3], sizes[3]) == cases[3]["cas_id"]
+
+
+def test_file_checksums_golden(eng, tmp_path):
+    cases = [c for c in golden("checksums.json") if c["size"] < (64 << 20)]
+    paths = []
+    for c in cases:
+        kind, key = spec_content(c["content"])
+        p = tmp_path / f"c_{c['content'].replace(':', '_')}_{c['size']}"
+        p.write_bytes(content(kind, 0, c["size"], key).tobytes())
+        paths.append(str(p))
+    out, st = eng.file_checksums(paths)
+    assert (st == 0).all()
+    for c, d in zip(cases, out):
+        assert bytes(d).hex() == c["checksum"], c
+    assert eng.file_checksum(paths[0]) == cases[0]["checksum"]
+
+
+def test_checksum_4gib_plus_1(eng):
+    """unaligned multi-Mi-chunk tree (4096 full pieces + 1 tail byte) through
+    the streamed big-message path, against upstream BLAKE3 C"""
+    c = [c for c in golden("checksums.json") if c["size"] == (4 << 30) + 1][0]
+    n = c["size"]
+    period = np.arange(251 * 4096, dtype=np.uint64) % np.uint64(251)
+    blob = np.resize(period.astype(np.uint8), n)
+    out = eng.hash_messages(blob, np.array([0], np.uint64), np.array([n], np.uint64))
+    assert bytes(out[0]).hex() == c["checksum"]
+
+
+def test_errors_per_item(eng, tmp_path):
+    import errno
+    from spacedrive_amd import _native as N
+    short = tmp_path / "short"
+    short.write_bytes(b"x" * 20000)
+    ok = tmp_path / "ok"
+    ok.write_bytes(b"hello")
+    keys, st = eng.generate_cas_ids([str(tmp_path / "missing"), str(short), str(ok)], [10, 200000, 5])
+    assert st[0] == errno.ENOENT
+    assert st[1] == N.SDCAS_STATUS_UNEXPECTED_EOF
+    assert st[2] == 0
+    with pytest.raises(OSError) as e:
+        eng.generate_cas_id(str(short), 200000)
+    assert "fill whole buffer" in str(e.value)
+    d, st = eng.file_checksums([str(tmp_path), str(ok)])
+    assert st[0] == errno.EISDIR and st[1] == 0
+
+
+def test_file_grew_since_indexing(eng, oracle, tmp_path):
+    """the indexer's size is stale: content comes from the file as it is now
+    (cas.rs:29 fs::read), the prefix from `size`"""
+    p = tmp_path / "grown"
+    p.write_bytes(content("pattern251", 0, 70000).tobytes())
+    assert eng.generate_cas_id(str(p), 5000) == oracle.generate_cas_id(str(p), 5000)
+    p2 = tmp_path / "grown_past_100k"
+    p2.write_bytes(content("pattern251", 0, 300000).tobytes())
+    assert eng.generate_cas_id(str(p2), 100000) == oracle.generate_cas_id(str(p2), 100000)
+
+
+def test_random_messages_vs_oracle(eng, oracle):
+    rng = np.random.default_rng(1234)
+    lens = np.concatenate([
+        rng.integers(0, 4096, 300), rng.integers(0, 200_000, 200), rng.integers(900_000, 1_200_000, 6),
+        np.array([0, 1, 1023, 1024, 1025, 1048576, 1048577, 2 * 1048576 + 5, 3 * 1048576])])
+    rng.shuffle(lens)
+    msgs = [rng.integers(0, 256, int(L), dtype=np.uint8).tobytes() for L in lens]
+    out = eng.hash_messages(*eng.pack(msgs))
+    for m, d in zip(msgs, out):
+        assert bytes(d).hex() == oracle.hash(m), len(m)
+
+
+def test_tile_straddles_vs_oracle(eng, oracle):
+    """message lengths chosen so that messages start at every offset inside a
+    1024-slot tile and straddle tile boundaries at every tree level"""
+    rng = np.random.default_rng(7)
+    lens = []
+    for c in [1, 2, 3, 5, 7, 8, 9, 15, 16, 17, 31, 32, 33, 63, 64, 65, 100, 101, 127, 128, 129, 255, 256,
+              257, 511, 512, 513, 700, 1000, 1023, 1024]:
+        lens += [c * 1024, c * 1024 - 1, c * 1024 + 1]
+    lens = np.array(lens * 3)
+    rng.shuffle(lens)
+    msgs = [rng.integers(0, 256, int(L), dtype=np.uint8).tobytes() for L in lens]
+    out = eng.hash_messages(*eng.pack(msgs))
+    for m, d in zip(msgs, out):
+        assert bytes(d).hex() == oracle.hash(m), len(m)
+
+
+def test_device_api_synthetic_c2_sample(eng, oracle):
+    """C2-shaped synthetic corpus generated in HBM, hashed by the device API;
+    a random sample of files is re-derived by the CPU oracle"""
+    import torch
+    from tests._oracle import content_key
+    n = 20000
+    seed = 0x5D0002
+    idx = np.arange(n, dtype=np.uint64)
+    sizes = np.array([1024 + int(x) % (102400 - 1024 + 1) for x in _c2_raw(seed, idx)], np.uint64)
+    keys = np.array([content_key(seed, i) for i in range(n)], np.uint64)
+    lens = sizes + 8
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum((lens[:-1] + 15) // 16 * 16)
+    total = int(offs[-1] + (lens[-1] + 15) // 16 * 16) + 64
+    dev = torch.device("cuda:0")
+    d_blob = torch.empty(total, dtype=torch.uint8, device=dev)
+    t = lambda a: torch.from_numpy(a.view(np.int64)).to(dev)
+    d_keys, d_sizes, d_offs, d_lens = t(keys), t(sizes), t(offs), t(lens)
+    d_out = torch.zeros(n, dtype=torch.int64, device=dev)
+    eng.dev_reserve(n, int(((lens + 1023) // 1024).sum()))
+    eng.dev_synth_cas_messages(d_keys.data_ptr(), d_sizes.data_ptr(), d_offs.data_ptr(), n, d_blob.data_ptr())
+    eng.dev_hash_messages(d_blob.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), n, 0, d_out.data_ptr())
+    eng.dev_sync()
+    got = d_out.cpu().numpy().view(np.uint64)
+    rng = np.random.default_rng(3)
+    for i in rng.choice(n, 300, replace=False):
+        assert int(got[i]) == oracle.synth_cas_key(int(keys[i]), int(sizes[i])), i
+    # the generated bytes themselves match the synthetic definition
+    i = 17
+    o = int(offs[i])
+    assert bytes(d_blob[o:o + int(lens[i])].cpu().numpy()) == bytes(
+        oracle.synth_cas_message(int(keys[i]), int(sizes[i])))
+
+
+def _c2_raw(seed, idx):
+    from tests._oracle import mix64
+    with np.errstate(over="ignore"):
+        x = np.uint64(seed) ^ np.uint64(0xC2C2C2C2) ^ (idx << np.uint64(20)) ^ (idx >> np.uint64(44))
+        return mix64(x)
+
+
+def test_dedup_vs_oracle(eng, oracle):
+    rng = np.random.default_rng(99)
+    n = 50000
+    pool = rng.integers(0, 2**64, 8000, dtype=np.uint64)
+    keys = pool[rng.zipf(1.3, n) % pool.size]
+    has = (rng.random(n) > 0.02).astype(np.uint8)
+    status = np.where(rng.random(n) < 0.01, 2, 0).astype(np.int32)
+    existing = np.concatenate([pool[rng.integers(0, pool.size, 300)], rng.integers(0, 2**64, 50, dtype=np.uint64)])
+    for cs in (100, 7, 1):
+        want, wc, wl = oracle.identifier_dedup(keys, has, status, cs, existing)
+        got, gc, gl = eng.identifier_dedup(keys, has, status, cs, existing)
+        assert np.array_equal(want, got), cs
+        assert (wc, wl) == (gc, gl)
+
+
+def test_dedup_small_cases(eng):
+    keys = np.array([10, 10, 11, 10, 12, 11, 99], np.uint64)
+    has = np.array([1, 1, 1, 1, 1, 1, 0], np.uint8)
+    out, created, linked = eng.identifier_dedup(keys, has, chunk_size=3)
+    assert out.tolist() == [0, 1, 2, 0, 4, 2, 6] and created == 5 and linked == 2
+    out, created, linked = eng.identifier_dedup(np.array([2**64 - 1, 2**64 - 1], np.uint64), [1, 1])
+    assert out.tolist() == [0, 1] and created == 2
+    out, created, linked = eng.identifier_dedup(np.zeros(0, np.uint64), np.zeros(0, np.uint8))
+    assert out.size == 0 and created == 0
