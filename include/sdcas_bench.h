@@ -34,6 +34,10 @@ int sdcas_dev_dedup(sdcas_ctx *ctx, const uint64_t *d_keys, const uint8_t *d_has
 int sdcas_dev_profile(sdcas_ctx *ctx, int enable);
 int sdcas_dev_last_kernel_ms(sdcas_ctx *ctx, float *leaf_ms, float *total_ms);
 
+/* Tuning: select the leaf/tree kernel variant (-1 = default). Returns the
+ * number of variants. */
+int sdcas_dev_set_leaf_variant(sdcas_ctx *ctx, int variant);
+
 #ifdef __cplusplus
 }
 #endif

@@ -78,6 +78,11 @@ int64_t oracle_identifier_dedup(size_t n, const uint64_t *keys, const uint8_t *h
                                 const int32_t *status, size_t chunk_size, size_t n_existing,
                                 const uint64_t *existing_keys, int64_t *out_link, int64_t *linked);
 
+/* bench.py cpu_baseline leg (cpu_bench.c): hash the cas messages of C2 files
+ * [0, count) already in memory; secs[0] one thread, secs[1] `threads` threads */
+int oracle_cpu_bench_c2(uint64_t seed, size_t count, int threads, int prefer_upstream, uint64_t *keys,
+                        uint64_t *bytes, double *secs, int *kind, char *version_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -26,7 +26,7 @@ ABI_SYMBOLS = [
     "sdcas_digest_to_hex", "sdcas_cas_message_len",
     # bench / test plumbing
     "sdcas_dev_synth_cas_messages", "sdcas_dev_synth_content", "sdcas_dev_dedup", "sdcas_dev_profile",
-    "sdcas_dev_last_kernel_ms",
+    "sdcas_dev_last_kernel_ms", "sdcas_dev_set_leaf_variant",
 ]
 
 
@@ -89,5 +89,6 @@ def load():
     L.sdcas_dev_profile.argtypes = [_vp, ctypes.c_int]
     L.sdcas_dev_last_kernel_ms.argtypes = [_vp, ctypes.POINTER(ctypes.c_float),
                                            ctypes.POINTER(ctypes.c_float)]
+    L.sdcas_dev_set_leaf_variant.argtypes = [_vp, ctypes.c_int]
     _lib = L
     return L

@@ -19,11 +19,12 @@ struct BatchWorkspace {
   size_t scan_tmp_bytes = 0;
   uint32_t cap_msgs = 0;
   uint64_t cap_chunks = 0;
-  int grid = 0;
+  int variant = -1;  // leaf kernel variant (-1: default / SDCAS_LEAF_VARIANT)
 };
 
 size_t batch_scan_temp_bytes(uint32_t max_msgs);
-int batch_grid(int device);
+int leaf_variant();
+int leaf_variant_count();
 
 // Hash n messages (blob + offs[i], lens[i] bytes; offsets 16-byte aligned),
 // all pointers device pointers. Writes 32-byte digests to out32 and/or cas

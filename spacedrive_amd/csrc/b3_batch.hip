@@ -95,6 +95,51 @@ __device__ __forceinline__ void hash_chunk(const uint8_t* __restrict__ p, uint32
   }
 }
 
+// Same, with the next block's loads issued before the current block is
+// compressed (software pipelining: one 64-byte block per lane in flight while
+// the VALU works). The load address is clamped to the chunk's last block, so
+// the final iteration re-reads it harmlessly instead of running off the end.
+__device__ __forceinline__ void hash_chunk_pf(const uint8_t* __restrict__ p, uint32_t clen, uint64_t j, bool root,
+                                              uint32_t (&cv)[8]) {
+  set_iv(cv);
+  const uint32_t nb = clen == 0 ? 1 : (clen + BLOCK_LEN - 1) / BLOCK_LEN;
+  uint32_t m[16];
+  load_full_block(p, m);
+#pragma unroll 1
+  for (uint32_t b = 0; b < nb; ++b) {
+    uint32_t nx[16];
+    load_full_block(p + min(b + 1, nb - 1) * BLOCK_LEN, nx);
+    const uint32_t blen = min(BLOCK_LEN, clen - b * BLOCK_LEN);
+    if (blen < BLOCK_LEN) mask_tail(m, blen);
+    const uint32_t flags = (b == 0 ? CHUNK_START : 0u) | (b + 1 == nb ? (CHUNK_END | (root ? ROOT : 0u)) : 0u);
+    compress(cv, m, j, blen, flags);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m[i] = nx[i];
+  }
+}
+
+// DIAGNOSTIC ONLY (wrong digests, never the default): PF=2 compresses
+// register-made blocks without touching memory (pure VALU rate); PF=3 streams
+// the chunk's blocks and folds them with XOR, no compression (pure load rate).
+__device__ __forceinline__ void hash_chunk_diag(const uint8_t* __restrict__ p, uint32_t clen, uint64_t j, bool root,
+                                                uint32_t (&cv)[8], int mode) {
+  set_iv(cv);
+  const uint32_t nb = clen == 0 ? 1 : (clen + BLOCK_LEN - 1) / BLOCK_LEN;
+#pragma unroll 1
+  for (uint32_t b = 0; b < nb; ++b) {
+    uint32_t m[16];
+    if (mode == 2) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) m[i] = (uint32_t)(uintptr_t)p + b * 64 + i;
+      compress(cv, m, j, 64, b == 0 ? CHUNK_START : 0u);
+    } else {
+      load_full_block(p + b * BLOCK_LEN, m);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) cv[i & 7] ^= m[i];
+    }
+  }
+}
+
 __device__ __forceinline__ void store_digest(uint32_t m, const uint32_t (&d)[8], uint8_t* out32, uint64_t* out_keys) {
   if (out32) {
     uint4* o = reinterpret_cast<uint4*>(out32 + 32ull * m);
@@ -104,7 +149,8 @@ __device__ __forceinline__ void store_digest(uint32_t m, const uint32_t (&d)[8],
   if (out_keys) out_keys[m] = cas_key(d);
 }
 
-__global__ void __launch_bounds__(kWG) k_leaf_tree(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ offs,
+template <int WG, int PF>
+__global__ void __launch_bounds__(WG) k_leaf_tree(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ offs,
                                                    const uint64_t* __restrict__ lens, uint32_t n,
                                                    const uint64_t* __restrict__ S,
                                                    const uint32_t* __restrict__ tile_first,
@@ -127,13 +173,13 @@ __global__ void __launch_bounds__(kWG) k_leaf_tree(const uint8_t* __restrict__ b
     const uint32_t m0 = tile_first[tile];
     const uint32_t m1 = (tile + 1 < ntiles) ? tile_first[tile + 1] : n - 1;
     const uint32_t cnt = m1 - m0 + 1;  // <= kTile + 1
-    for (uint32_t i = tid; i < cnt; i += kWG) sS[i] = S[m0 + i];
+    for (uint32_t i = tid; i < cnt; i += WG) sS[i] = S[m0 + i];
     if (tid < 16) ntask[tid] = 0;
     __syncthreads();
 
     // (1) leaves
 #pragma unroll 1
-    for (uint32_t s = tid; s < kTile; s += kWG) {
+    for (uint32_t s = tid; s < kTile; s += WG) {
       const uint64_t g = tile * kTile + s;
       if (g >= total) {
         sC[s] = 0;
@@ -152,7 +198,9 @@ __global__ void __launch_bounds__(kWG) k_leaf_tree(const uint8_t* __restrict__ b
       const uint32_t clen = len == 0 ? 0u : (uint32_t)min<uint64_t>(CHUNK_LEN, len - j * CHUNK_LEN);
       const bool root = (C == 1);
       uint32_t cv[8];
-      hash_chunk(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
+      if (PF >= 2) hash_chunk_diag(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv, PF);
+      else if (PF) hash_chunk_pf(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
+      else hash_chunk(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
       if (root) {
         store_digest(m, cv, out32, out_keys);
         sC[s] = 0;
@@ -168,7 +216,7 @@ __global__ void __launch_bounds__(kWG) k_leaf_tree(const uint8_t* __restrict__ b
     // (2) in-tile tree, level by level over a compacted task list
     for (uint32_t k = 1; (1u << k) <= kTile; ++k) {
       const uint32_t w = 1u << k;
-      for (uint32_t s = tid; s < kTile; s += kWG) {
+      for (uint32_t s = tid; s < kTile; s += WG) {
         const uint32_t C = sC[s];
         if (!C) continue;
         const uint32_t j = sj[s];
@@ -178,7 +226,7 @@ __global__ void __launch_bounds__(kWG) k_leaf_tree(const uint8_t* __restrict__ b
       const uint32_t T = ntask[k];
       if (T == 0) break;
 #pragma unroll 1
-      for (uint32_t t = tid; t < T; t += kWG) {
+      for (uint32_t t = tid; t < T; t += WG) {
         const uint32_t s = task[t];
         uint32_t l[8], r[8], o[8];
 #pragma unroll
@@ -194,7 +242,7 @@ __global__ void __launch_bounds__(kWG) k_leaf_tree(const uint8_t* __restrict__ b
     }
 
     // (3) maximal nodes -> HBM at their first slot
-    for (uint32_t s = tid; s < kTile; s += kWG) {
+    for (uint32_t s = tid; s < kTile; s += WG) {
       const uint32_t C = sC[s];
       if (!C) continue;
       const uint32_t j = sj[s];
@@ -481,15 +529,45 @@ size_t batch_scan_temp_bytes(uint32_t max_msgs) {
   return bytes;
 }
 
-int batch_grid(int device) {
-  static int cached[64] = {0};
-  if (device >= 0 && device < 64 && cached[device]) return cached[device];
+// leaf/tree kernel variants (workgroup size x block prefetch); the default is
+// what bench measurements picked, SDCAS_LEAF_VARIANT overrides for A/B runs
+struct LeafVariant {
+  const void* fn;
+  int wg;
+};
+static const LeafVariant kLeafVariants[] = {
+    {(const void*)k_leaf_tree<512, 0>, 512},
+    {(const void*)k_leaf_tree<512, 1>, 512},
+    {(const void*)k_leaf_tree<256, 1>, 256},
+    {(const void*)k_leaf_tree<1024, 1>, 1024},
+    // diagnostic (wrong results): 4 = no memory reads, 5 = no compression
+    {(const void*)k_leaf_tree<512, 2>, 512},
+    {(const void*)k_leaf_tree<512, 3>, 512},
+};
+constexpr int kNumLeafVariants = sizeof(kLeafVariants) / sizeof(kLeafVariants[0]);
+constexpr int kDefaultLeafVariant = 1;
+
+int leaf_variant_count() { return kNumLeafVariants; }
+
+int leaf_variant() {
+  static int v = -2;
+  if (v == -2) {
+    const char* e = getenv("SDCAS_LEAF_VARIANT");
+    v = e ? atoi(e) : kDefaultLeafVariant;
+    if (v < 0 || v >= kNumLeafVariants) v = kDefaultLeafVariant;
+  }
+  return v;
+}
+
+int batch_grid(int device, int variant) {
+  static int cached[64][8] = {{0}};
+  if (device >= 0 && device < 64 && cached[device][variant]) return cached[device][variant];
   int cus = 256, per = 1;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_leaf_tree, kWG, 0);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kLeafVariants[variant].fn, kLeafVariants[variant].wg, 0);
   if (per < 1) per = 1;
   int g = cus * per;
-  if (device >= 0 && device < 64) cached[device] = g;
+  if (device >= 0 && device < 64) cached[device][variant] = g;
   return g;
 }
 
@@ -505,8 +583,16 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
   hipLaunchKernelGGL(k_tile_first, dim3((n + tb - 1) / tb), dim3(tb), 0, st, lens, ws.S, n, ws.cap_chunks,
                      ws.tile_first, ws.total);
   if (ev0) (void)hipEventRecord(ev0, st);
-  hipLaunchKernelGGL(k_leaf_tree, dim3(ws.grid), dim3(kWG), 0, st, blob, offs, lens, n, ws.S, ws.tile_first,
-                     ws.total, ws.cap_chunks, ws.nodes, out32, out_keys);
+  {
+    const int v = ws.variant >= 0 && ws.variant < kNumLeafVariants ? ws.variant : leaf_variant();
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const int grid = batch_grid(dev, v);
+    void* args[] = {(void*)&blob, (void*)&offs, (void*)&lens, (void*)&n, (void*)&ws.S, (void*)&ws.tile_first,
+                    (void*)&ws.total, (void*)&ws.cap_chunks, (void*)&ws.nodes, (void*)&out32, (void*)&out_keys};
+    hipError_t le = hipLaunchKernel(kLeafVariants[v].fn, dim3(grid), dim3(kLeafVariants[v].wg), args, 0, st);
+    if (le != hipSuccess) return le;
+  }
   if (ev1) (void)hipEventRecord(ev1, st);
   hipLaunchKernelGGL(k_finish, dim3((n + tb - 1) / tb), dim3(tb), 0, st, lens, n, ws.S, ws.total, ws.cap_chunks,
                      ws.nodes, out32, out_keys);

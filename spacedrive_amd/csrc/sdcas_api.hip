@@ -145,7 +145,6 @@ int reserve_ws(sdcas_ctx* c, size_t max_msgs, uint64_t max_chunks) {
   c->ws.cap_msgs = (uint32_t)(c->ws_S.cap - 1);
   // every tile the leaf kernel may touch needs a tile_first entry and kTile node slots
   c->ws.cap_chunks = std::min<uint64_t>((c->ws_tile_first.cap - 1) * kTile, c->ws_nodes.cap / 8 - kTile);
-  c->ws.grid = batch_grid(c->device);
   return SDCAS_OK;
 }
 
@@ -842,6 +841,13 @@ int sdcas_dev_dedup(sdcas_ctx* c, const uint64_t* d_keys, const uint8_t* d_has_k
                            0, d_out_link, (unsigned long long*)d_counts, st);
   if (e) return c->hip_fail(e, "dev_dedup");
   return SDCAS_OK;
+}
+
+int sdcas_dev_set_leaf_variant(sdcas_ctx* c, int variant) {
+  if (!c) return SDCAS_E_INVALID;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->ws.variant = variant;
+  return leaf_variant_count();
 }
 
 // ---- synthetic corpora -------------------------------------------------------

@@ -191,6 +191,10 @@ class Engine:
     def dev_profile(self, enable=True):
         self._check(self.L.sdcas_dev_profile(self.ctx, 1 if enable else 0), "dev_profile")
 
+    def dev_set_leaf_variant(self, v):
+        """tuning knob: leaf/tree kernel variant (-1 = default); returns the variant count"""
+        return self.L.sdcas_dev_set_leaf_variant(self.ctx, int(v))
+
     def dev_kernel_ms(self):
         a, b = ctypes.c_float(0), ctypes.c_float(0)
         self._check(self.L.sdcas_dev_last_kernel_ms(self.ctx, ctypes.byref(a), ctypes.byref(b)), "ms")
