@@ -132,7 +132,7 @@ __device__ __forceinline__ void hash_chunk_diag(const uint8_t* __restrict__ p, u
 #pragma unroll
       for (int i = 0; i < 16; ++i) m[i] = (uint32_t)(uintptr_t)p + b * 64 + i;
       compress(cv, m, j, 64, b == 0 ? CHUNK_START : 0u);
-    } else {
+    } else if (mode == 3) {
       load_full_block(p + b * BLOCK_LEN, m);
 #pragma unroll
       for (int i = 0; i < 16; ++i) cv[i & 7] ^= m[i];
