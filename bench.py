@@ -68,7 +68,7 @@ def compressions(lens):
 
 def load_traffic(workload):
     """HBM bytes per launch of the leaf kernel from the committed rocprofv3
-    PMC pass (profiles/*pmc*.json, written by tools/pmc_traffic.py), if any."""
+    PMC pass (profiles/*pmc*.json, written by tools/pmc_summarize.py), if any."""
     import glob
     best = None
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
@@ -144,7 +144,9 @@ def main():
     sizes, keys = c2_files(SEED_C2, lo, lo + n)
     lens = sizes + np.uint64(8)
     offs = np.zeros(n, np.uint64)
-    padded = (lens + np.uint64(15)) // np.uint64(16) * np.uint64(16)
+    # messages start on 128-byte lines (the L2/HBM line): a chunk then spans
+    # 8 lines instead of 9 (the layout of device memory is ours to choose)
+    padded = (lens + np.uint64(127)) // np.uint64(128) * np.uint64(128)
     offs[1:] = np.cumsum(padded[:-1])
     total_bytes = int(offs[-1] + padded[-1]) + 64
     chunks = int(((lens + np.uint64(1023)) // np.uint64(1024)).sum())

@@ -149,7 +149,18 @@ __device__ __forceinline__ void store_digest(uint32_t m, const uint32_t (&d)[8],
   if (out_keys) out_keys[m] = cas_key(d);
 }
 
-template <int WG, int PF>
+// per-level task regions of the in-tile tree: level k (1..10) holds at most
+// 2 * (kTile >> k) tasks (regular level-k nodes are disjoint 2^k blocks, spine
+// steps consume disjoint maximal 2^(k-1) blocks), 2046 entries in all
+__host__ __device__ constexpr uint32_t task_base(uint32_t k) { return 2 * (kTile - (kTile >> (k - 1))); }
+constexpr uint32_t kTaskCap = 2 * (kTile - 1);
+constexpr uint16_t kNoMsg = 0xFFFF;
+
+__device__ __forceinline__ uint32_t enc_task(uint32_t l, uint32_t r, uint32_t msg, bool root) {
+  return l | (r << 10) | (msg << 20) | (root ? 0x80000000u : 0u);
+}
+
+template <int WG, int PF, int TR = 1, int STAGGER = 0>
 __global__ void __launch_bounds__(WG) k_leaf_tree(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ offs,
                                                    const uint64_t* __restrict__ lens, uint32_t n,
                                                    const uint64_t* __restrict__ S,
@@ -158,41 +169,93 @@ __global__ void __launch_bounds__(WG) k_leaf_tree(const uint8_t* __restrict__ bl
                                                    uint32_t* __restrict__ nodes, uint8_t* __restrict__ out32,
                                                    uint64_t* __restrict__ out_keys) {
   __shared__ uint32_t cvs[kTile][8];   // chunk / node chaining values, by slot
-  __shared__ uint32_t sj[kTile];       // chunk index within its message
-  __shared__ uint32_t sC[kTile];       // chunk count of its message (0: slot not in a tree)
   __shared__ uint64_t sS[kTile + 1];   // S[] of the tile's messages
-  __shared__ uint16_t task[kTile / 2];
-  __shared__ uint32_t ntask[16];
+  __shared__ uint16_t smsg[kTile];     // slot -> message index in the tile (kNoMsg: past the end)
+  __shared__ uint32_t task[kTaskCap];  // tree tasks by level (enc_task)
+  __shared__ uint32_t ntask[12];
 
   const uint64_t total = *total_p;
   if (total > cap_chunks) return;  // reported by sdcas_dev_sync
   const uint64_t ntiles = (total + kTile - 1) / kTile;
   const uint32_t tid = threadIdx.x;
+  if (STAGGER) {
+    // Co-resident workgroups run identical tiles in lockstep, so their
+    // barrier-bound tree phases coincide and leave the CU's SIMDs idle.
+    // Offset them once by a fraction of a tile (speed only).
+    const uint32_t phase = (blockIdx.x / (gridDim.x / STAGGER)) % STAGGER;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t wait = (uint64_t)phase * 25000 / STAGGER;  // 100 MHz ticks: ~250 us per tile
+    while (__builtin_amdgcn_s_memrealtime() - t0 < wait) __builtin_amdgcn_s_sleep(100);
+  }
 
   for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const uint64_t tbase = tile * kTile;
     const uint32_t m0 = tile_first[tile];
     const uint32_t m1 = (tile + 1 < ntiles) ? tile_first[tile + 1] : n - 1;
     const uint32_t cnt = m1 - m0 + 1;  // <= kTile + 1
     for (uint32_t i = tid; i < cnt; i += WG) sS[i] = S[m0 + i];
-    if (tid < 16) ntask[tid] = 0;
+    if (tid < 12) ntask[tid] = 0;
     __syncthreads();
 
-    // (1) leaves
+    // (1) slot -> message, and the tree schedule: every aligned complete
+    // power-of-two node inside the tile (level k task at its first slot), plus
+    // the spine of each message lying wholly in the tile — the right-to-left
+    // fold over its binary decomposition, one step per part, scheduled in the
+    // level after that part's node is complete; the last step is the ROOT.
 #pragma unroll 1
     for (uint32_t s = tid; s < kTile; s += WG) {
-      const uint64_t g = tile * kTile + s;
+      const uint64_t g = tbase + s;
       if (g >= total) {
-        sC[s] = 0;
+        smsg[s] = kNoMsg;
         continue;
       }
       uint32_t lo = 0, hi = cnt - 1;  // last message with S <= g
       while (lo < hi) {
-        uint32_t mid = (lo + hi + 1) >> 1;
+        const uint32_t mid = (lo + hi + 1) >> 1;
         if (sS[mid] <= g) lo = mid;
         else hi = mid - 1;
       }
-      const uint32_t m = m0 + lo;
+      smsg[s] = (uint16_t)lo;
+      if (!TR) continue;
       const uint64_t j = g - sS[lo];
+      const uint64_t C = chunk_count(lens[m0 + lo]);
+      if (C == 1) continue;
+      const uint32_t K = node_level(j, C, s);
+      for (uint32_t k = 1; k <= K; ++k)
+        task[task_base(k) + atomicAdd(&ntask[k], 1u)] = enc_task(s, s + (1u << (k - 1)), 0, false);
+    }
+#pragma unroll 1
+    for (uint32_t i = tid; TR && i < cnt; i += WG) {
+      const uint64_t S0 = sS[i];
+      if (S0 < tbase) continue;
+      const uint64_t C = chunk_count(lens[m0 + i]);
+      if (C == 1 || S0 + C > tbase + kTile) continue;
+      const uint32_t s0 = (uint32_t)(S0 - tbase), c = (uint32_t)C;
+      if (!(c & (c - 1))) {
+        const uint32_t k = 31 - __clz(c);
+        task[task_base(k) + atomicAdd(&ntask[k], 1u)] = enc_task(s0, s0 + (c >> 1), i, true);
+      } else {
+        uint32_t rem = c, part = rem & (0u - rem);
+        uint32_t pos = c - part, acc = pos;
+        rem -= part;
+        while (rem) {
+          part = rem & (0u - rem);
+          pos -= part;
+          const uint32_t k = 32 - __clz(part);  // log2(part) + 1
+          task[task_base(k) + atomicAdd(&ntask[k], 1u)] = enc_task(s0 + pos, s0 + acc, i, rem == part);
+          acc = pos;
+          rem -= part;
+        }
+      }
+    }
+
+    // (2) leaves
+#pragma unroll 1
+    for (uint32_t s = tid; s < kTile; s += WG) {
+      const uint32_t mi = smsg[s];
+      if (mi == kNoMsg) continue;
+      const uint32_t m = m0 + mi;
+      const uint64_t j = tbase + s - sS[mi];
       const uint64_t len = lens[m];
       const uint64_t C = chunk_count(len);
       const uint32_t clen = len == 0 ? 0u : (uint32_t)min<uint64_t>(CHUNK_LEN, len - j * CHUNK_LEN);
@@ -203,59 +266,58 @@ __global__ void __launch_bounds__(WG) k_leaf_tree(const uint8_t* __restrict__ bl
       else hash_chunk(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
       if (root) {
         store_digest(m, cv, out32, out_keys);
-        sC[s] = 0;
       } else {
 #pragma unroll
         for (int i = 0; i < 8; ++i) cvs[s][i] = cv[i];
-        sj[s] = (uint32_t)j;
-        sC[s] = (uint32_t)C;
       }
     }
     __syncthreads();
 
-    // (2) in-tile tree, level by level over a compacted task list
-    for (uint32_t k = 1; (1u << k) <= kTile; ++k) {
-      const uint32_t w = 1u << k;
-      for (uint32_t s = tid; s < kTile; s += WG) {
-        const uint32_t C = sC[s];
-        if (!C) continue;
-        const uint32_t j = sj[s];
-        if (!(j & (w - 1)) && j + w <= C && w < C && s + w <= kTile) task[atomicAdd(&ntask[k], 1u)] = (uint16_t)s;
-      }
-      __syncthreads();
+    // (3) the tree, level by level: every task of a level is independent
+    for (uint32_t k = 1; TR && k <= 10; ++k) {
       const uint32_t T = ntask[k];
-      if (T == 0) break;
+      if (T == 0) continue;
 #pragma unroll 1
       for (uint32_t t = tid; t < T; t += WG) {
-        const uint32_t s = task[t];
-        uint32_t l[8], r[8], o[8];
+        const uint32_t e = task[task_base(k) + t];
+        const uint32_t l = e & 1023u, r = (e >> 10) & 1023u;
+        const bool root = e >> 31;
+        uint32_t a[8], b[8], o[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          l[i] = cvs[s][i];
-          r[i] = cvs[s + (w >> 1)][i];
+        for (int q = 0; q < 8; ++q) {
+          a[q] = cvs[l][q];
+          b[q] = cvs[r][q];
         }
-        parent(l, r, false, o);
+        parent(a, b, root, o);
+        if (root) {
+          store_digest(m0 + ((e >> 20) & 2047u), o, out32, out_keys);
+        } else {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) cvs[s][i] = o[i];
+          for (int q = 0; q < 8; ++q) cvs[l][q] = o[q];
+        }
       }
       __syncthreads();
     }
 
-    // (3) maximal nodes -> HBM at their first slot
-    for (uint32_t s = tid; s < kTile; s += WG) {
-      const uint32_t C = sC[s];
-      if (!C) continue;
-      const uint32_t j = sj[s];
+    // (4) messages crossing a tile boundary: their maximal in-tile nodes go to
+    // HBM at their first slot, for k_finish
+#pragma unroll 1
+    for (uint32_t s = tid; TR && s < kTile; s += WG) {
+      const uint32_t mi = smsg[s];
+      if (mi == kNoMsg) continue;
+      const uint64_t S0 = sS[mi];
+      const uint64_t C = chunk_count(lens[m0 + mi]);
+      if (C == 1 || (S0 >= tbase && S0 + C <= tbase + kTile)) continue;  // single chunk / spine done in (3)
+      const uint64_t j = tbase + s - S0;
       const uint32_t k = node_level(j, C, s);
       if (parent_in_tile(j, C, s, k)) continue;
-      uint4* o = reinterpret_cast<uint4*>(nodes + 8ull * (tile * kTile + s));
+      uint4* o = reinterpret_cast<uint4*>(nodes + 8ull * (tbase + s));
       o[0] = make_uint4(cvs[s][0], cvs[s][1], cvs[s][2], cvs[s][3]);
       o[1] = make_uint4(cvs[s][4], cvs[s][5], cvs[s][6], cvs[s][7]);
     }
     __syncthreads();
   }
 }
-
 
 __global__ void __launch_bounds__(256) k_finish(const uint64_t* __restrict__ lens, uint32_t n,
                                                 const uint64_t* __restrict__ S, const uint64_t* __restrict__ total_p,
@@ -266,6 +328,7 @@ __global__ void __launch_bounds__(256) k_finish(const uint64_t* __restrict__ len
   const uint64_t C = chunk_count(lens[m]);
   if (C == 1) return;
   const uint64_t s0 = S[m];
+  if (s0 / kTile == (s0 + C - 1) / kTile) return;  // lies in one tile: folded by k_leaf_tree
   uint32_t stack[kMaxStack][8];
   int depth = 0;
   uint64_t j = 0;
@@ -543,6 +606,12 @@ static const LeafVariant kLeafVariants[] = {
     // diagnostic (wrong results): 4 = no memory reads, 5 = no compression
     {(const void*)k_leaf_tree<512, 2>, 512},
     {(const void*)k_leaf_tree<512, 3>, 512},
+    // 6, 7 diagnostic (wrong results): no in-tile tree; no tree and no loads
+    {(const void*)k_leaf_tree<512, 1, 0>, 512},
+    {(const void*)k_leaf_tree<512, 2, 0>, 512},
+    // 8, 9: workgroups staggered by 1/3 and 1/2 of a tile
+    {(const void*)k_leaf_tree<512, 1, 1, 3>, 512},
+    {(const void*)k_leaf_tree<512, 1, 1, 2>, 512},
 };
 constexpr int kNumLeafVariants = sizeof(kLeafVariants) / sizeof(kLeafVariants[0]);
 constexpr int kDefaultLeafVariant = 1;

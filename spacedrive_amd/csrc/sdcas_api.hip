@@ -37,7 +37,8 @@ constexpr uint64_t kSample = SDCAS_SAMPLE_SIZE, kHF = SDCAS_HEADER_OR_FOOTER_SIZ
 constexpr uint64_t kMin = SDCAS_MINIMUM_FILE_SIZE, kSampleCount = SDCAS_SAMPLE_COUNT;
 constexpr uint64_t kSlack = 64;  // readable bytes kept after every message
 
-inline uint64_t align16(uint64_t x) { return (x + 15) & ~15ull; }
+// staged messages start on 128-byte (L2/HBM line) boundaries
+inline uint64_t align16(uint64_t x) { return (x + 127) & ~127ull; }
 inline uint64_t chunks_of(uint64_t len) { return len == 0 ? 1 : (len + 1023) / 1024; }
 
 template <class T>

@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--variants", default="")
+    ap.add_argument("--align", type=int, default=128, help="message start alignment in HBM")
     a = ap.parse_args()
     import torch
     from spacedrive_amd import Engine
@@ -26,7 +27,8 @@ def main():
     n = a.files
     sizes, keys = bench.c2_files(bench.SEED_C2, 0, n)
     lens = sizes + np.uint64(8)
-    padded = (lens + np.uint64(15)) // np.uint64(16) * np.uint64(16)
+    A = np.uint64(a.align)
+    padded = (lens + A - np.uint64(1)) // A * A
     offs = np.zeros(n, np.uint64)
     offs[1:] = np.cumsum(padded[:-1])
     total = int(offs[-1] + padded[-1]) + 64

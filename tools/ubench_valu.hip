@@ -65,6 +65,9 @@ __global__ void __launch_bounds__(256) k_op(uint32_t* out, int iters) {
       if (OP == 5) { OP1("v_perm_b32 %0, %0, %0, %1") }
       if (OP == 6) { OP1("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96") }
       if (OP == 7) { OP1("v_pk_add_u16 %0, %0, %1") }
+      if (OP == 8) { OP1("v_xor_b32_sdwa %0, %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0") }
+      if (OP == 9) { OP1("v_lshrrev_b32 %0, 7, %0") }
+      if (OP == 10) { OP1("v_lshl_or_b32 %0, %0, 7, %1") }
     }
   }
   uint32_t x = 0;
@@ -73,7 +76,31 @@ __global__ void __launch_bounds__(256) k_op(uint32_t* out, int iters) {
   out[t] = x;
 }
 
+__global__ void k_rot16_check(const uint32_t* in, uint32_t* out, int n) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    uint32_t d = in[2 * i], a = in[2 * i + 1];
+    out[2 * i] = xor_rot16(d, a);
+    out[2 * i + 1] = rotr(d ^ a, 16);
+  }
+}
+
 int main(int argc, char** argv) {
+  {
+    const int n = 1 << 16;
+    uint32_t *din, *dout;
+    hipMalloc(&din, 8 * n);
+    hipMalloc(&dout, 8 * n);
+    uint32_t* h = (uint32_t*)malloc(8 * n);
+    uint64_t x = 12345;
+    for (int i = 0; i < 2 * n; ++i) { x = x * 6364136223846793005ull + 1442695040888963407ull; h[i] = (uint32_t)(x >> 32); }
+    hipMemcpy(din, h, 8 * n, hipMemcpyHostToDevice);
+    hipLaunchKernelGGL(k_rot16_check, dim3(n / 256), dim3(256), 0, 0, din, dout, n);
+    hipMemcpy(h, dout, 8 * n, hipMemcpyDeviceToHost);
+    int bad = 0;
+    for (int i = 0; i < n; ++i) bad += h[2 * i] != h[2 * i + 1];
+    printf("xor_rot16 check: %d / %d mismatches (e.g. %08x vs %08x)\n", bad, n, h[0], h[1]);
+  }
   int cus = 0;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
   const int iters = argc > 1 ? atoi(argv[1]) : 2000;
@@ -106,8 +133,8 @@ int main(int argc, char** argv) {
     }
   }
   const char* names[] = {"v_add_u32", "v_xor_b32", "v_alignbit_b32", "v_add3_u32", "v_xad_u32", "v_perm_b32",
-                         "v_bitop3_b32", "v_pk_add_u16"};
-  for (int op = 0; op < 8; ++op) {
+                         "v_bitop3_b32", "v_pk_add_u16", "v_xor_b32_sdwa", "v_lshrrev_b32", "v_lshl_or_b32"};
+  for (int op = 0; op < 11; ++op) {
     const int blocks = cus * 8;
     for (int rep = 0; rep < 2; ++rep) {
       hipEventRecord(e0);
@@ -119,6 +146,9 @@ int main(int argc, char** argv) {
       if (op == 5) hipLaunchKernelGGL(k_op<5>, dim3(blocks), dim3(256), 0, 0, out, iters);
       if (op == 6) hipLaunchKernelGGL(k_op<6>, dim3(blocks), dim3(256), 0, 0, out, iters);
       if (op == 7) hipLaunchKernelGGL(k_op<7>, dim3(blocks), dim3(256), 0, 0, out, iters);
+      if (op == 8) hipLaunchKernelGGL(k_op<8>, dim3(blocks), dim3(256), 0, 0, out, iters);
+      if (op == 9) hipLaunchKernelGGL(k_op<9>, dim3(blocks), dim3(256), 0, 0, out, iters);
+      if (op == 10) hipLaunchKernelGGL(k_op<10>, dim3(blocks), dim3(256), 0, 0, out, iters);
       hipEventRecord(e1);
       hipEventSynchronize(e1);
       float ms;
