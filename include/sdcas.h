@@ -144,6 +144,44 @@ int sdcas_dedup(sdcas_ctx *ctx, const uint64_t *keys, const uint8_t *has_key, co
                 size_t n, size_t chunk_size, const uint64_t *existing_keys, size_t n_existing,
                 int64_t *out_link, int64_t *out_created, int64_t *out_linked);
 
+/* ---- multi-GPU dedup stages (one process per GPU) -------
+ *
+ * sdcas_dedup's group-by split at its one exchange step, for a node whose
+ * orphan file_paths (and existing Objects) are sharded over ranks. The host
+ * runs, on every rank, with its own communicator (RCCL all-to-all over xGMI;
+ * spacedrive_amd/dist_dedup.py is the reference driver):
+ *   1. combine(files)    -> records grouped by owner rank + per-file slot
+ *      combine(existing) -> records grouped by owner rank (ids = DB order)
+ *   2. all-to-all both record sets (counts from out_starts)
+ *   3. resolve on the received records -> one int64 answer per file record
+ *   4. all-to-all the answers back (the reverse of step 2's file exchange)
+ *   5. apply -> out_link / counts with sdcas_dedup's encoding, except that
+ *      every file index is the GLOBAL orphan ordinal d_ids[i].
+ * All pointers except out_starts are device pointers; calls are enqueued on
+ * `stream` (NULL = the context's); combine synchronises once to return
+ * out_starts. The owner of a key is its top 12 bits (the 3-hex thumbnail
+ * shard prefix) split into `world` equal ranges.
+ *
+ * combine: d_ids[n] ascending; d_has_key / d_status may be NULL (all
+ *   present / all ok). Writes d_rec[2*u], d_rec[2*u+1] = (cas key, min id)
+ *   for each distinct key u (capacity 2*n u64), d_slot[i] = record of file i
+ *   (0xFFFFFFFF no cas_id, 0xFFFFFFFE dropped; may be NULL), and
+ *   out_starts[0..world] (host) = first record of each owner; out_starts[world]
+ *   is the record count.
+ * resolve: d_result[p] for received file record p = -(db+1) if existing
+ *   Object db carries the key (the first in DB order), else the lowest orphan
+ *   ordinal carrying it on any rank.
+ * apply: d_result indexed by this rank's records (in send order); d_counts
+ *   (2 x u64, zeroed by the caller) += (created, linked). */
+int sdcas_dev_dedup_combine(sdcas_ctx *ctx, const uint64_t *d_keys, const uint8_t *d_has_key,
+                            const int32_t *d_status, const uint64_t *d_ids, size_t n, uint32_t world,
+                            uint64_t *d_rec, uint32_t *d_slot, uint64_t *out_starts, void *stream);
+int sdcas_dev_dedup_resolve(sdcas_ctx *ctx, const uint64_t *d_frec, size_t nf, const uint64_t *d_erec,
+                            size_t ne, int64_t *d_result, void *stream);
+int sdcas_dev_dedup_apply(sdcas_ctx *ctx, const uint64_t *d_ids, const uint32_t *d_slot, size_t n,
+                          const int64_t *d_result, size_t chunk_size, int64_t *d_link, uint64_t *d_counts,
+                          void *stream);
+
 /* ---- helpers ------------------------------------------------------------ */
 
 void sdcas_key_to_hex(uint64_t key, char out[17]);

@@ -23,7 +23,8 @@ ABI_SYMBOLS = [
     "sdcas_version", "sdcas_init", "sdcas_destroy", "sdcas_last_error", "sdcas_cas_ids",
     "sdcas_checksums", "sdcas_hash_messages", "sdcas_cas_ids_from_messages", "sdcas_dev_reserve",
     "sdcas_dev_hash_messages", "sdcas_dev_sync", "sdcas_dedup", "sdcas_key_to_hex",
-    "sdcas_digest_to_hex", "sdcas_cas_message_len",
+    "sdcas_digest_to_hex", "sdcas_cas_message_len", "sdcas_dev_dedup_combine", "sdcas_dev_dedup_resolve",
+    "sdcas_dev_dedup_apply",
     # bench / test plumbing
     "sdcas_dev_synth_cas_messages", "sdcas_dev_synth_content", "sdcas_dev_dedup", "sdcas_dev_profile",
     "sdcas_dev_last_kernel_ms", "sdcas_dev_set_leaf_variant",
@@ -90,5 +91,8 @@ def load():
     L.sdcas_dev_last_kernel_ms.argtypes = [_vp, ctypes.POINTER(ctypes.c_float),
                                            ctypes.POINTER(ctypes.c_float)]
     L.sdcas_dev_set_leaf_variant.argtypes = [_vp, ctypes.c_int]
+    L.sdcas_dev_dedup_combine.argtypes = [_vp, _vp, _vp, _vp, _vp, _sz, ctypes.c_uint32, _vp, _vp, _vp, _vp]
+    L.sdcas_dev_dedup_resolve.argtypes = [_vp, _vp, _sz, _vp, _sz, _vp, _vp]
+    L.sdcas_dev_dedup_apply.argtypes = [_vp, _vp, _vp, _sz, _vp, _sz, _vp, _vp, _vp]
     _lib = L
     return L

@@ -1,0 +1,78 @@
+// dist_dedup.h — device stages of the multi-GPU cas_id -> Object group-by
+// (SURVEY.md §8e): combine (per rank) -> all-to-all -> resolve (per owner)
+// -> all-to-all back -> apply (per rank). The collectives are the caller's
+// (RCCL through torch.distributed in spacedrive_amd/dist_dedup.py); these
+// stages only touch this GPU's HBM.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace sdcas {
+
+// slot codes of files that own no combined record
+constexpr uint32_t kSlotNoKey = 0xFFFFFFFFu;    // cas_id None: the file creates its own Object
+constexpr uint32_t kSlotDropped = 0xFFFFFFFEu;  // I/O error: the file is dropped
+
+// owner rank of a cas key: the top 12 bits (the 3-hex thumbnail shard prefix,
+// object/media/thumbnail/shard.rs:10-13) split into `world` equal, contiguous
+// bucket ranges, so owner() is monotone in the key and a key-sorted record
+// array is already grouped by owner
+__host__ __device__ inline uint32_t dd_owner(uint64_t key, uint32_t world) {
+  return (uint32_t)(((key >> 52) * (uint64_t)world) >> 12);
+}
+
+struct DistWs {
+  template <class T>
+  struct Buf {
+    T* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+      if (n <= cap) return hipSuccess;
+      if (p) (void)hipFree(p);
+      p = nullptr;
+      cap = 0;
+      size_t want = n < 16 ? 16 : n;
+      hipError_t e = hipMalloc(&p, want * sizeof(T));
+      if (!e) cap = want;
+      return e;
+    }
+    void release() {
+      if (p) (void)hipFree(p);
+      p = nullptr;
+      cap = 0;
+    }
+  };
+  Buf<uint64_t> key_a, key_b, umin, ukey, emin;
+  Buf<uint32_t> idx_a, idx_b, scan, nvalid, starts;
+  Buf<uint8_t> valid, temp;
+  void release();
+};
+
+// Stage 1. keys/has_key/status/ids: [n] (has_key, status may be null = all
+// present / all ok); ids ascending (the rank's files in orphan order, or the
+// rank's existing Objects in DB order). Writes one (key, min id) record per
+// distinct key to rec[2*u..2*u+1], key-sorted (hence grouped by owner), the
+// record index of every file to slot[i] (or kSlotNoKey/kSlotDropped; slot may
+// be null), and starts[0..world] (record index where each owner's range
+// begins) to h_starts after a stream sync. Returns the record count in *h_u.
+hipError_t dd_combine(DistWs& w, const uint64_t* keys, const uint8_t* has_key, const int32_t* status,
+                      const uint64_t* ids, uint32_t n, uint32_t world, uint64_t* rec, uint32_t* slot,
+                      uint64_t* h_starts, uint64_t* h_u, hipStream_t st);
+
+// Stage 2 (owner). frec: nf received (key, min file id) records, erec: ne
+// received (key, min DB index) records of existing Objects. result[p] for
+// file record p = -(db+1) if an existing Object carries the key (the first in
+// DB order), else the global minimum file id carrying the key.
+hipError_t dd_resolve(DistWs& w, const uint64_t* frec, uint32_t nf, const uint64_t* erec, uint32_t ne,
+                      int64_t* result, hipStream_t st);
+
+// Stage 3. result: [U] per this rank's record (returned in send order).
+// link[i] (global ids): INT64_MIN dropped; ids[i] creates; -(db+1) existing;
+// rep id otherwise — a file in the chunk of the key's first file creates its
+// own Object (mod.rs:246-254), later chunks link to that file's Object.
+// counts[0..1] += (created, linked) (device, zeroed by the caller).
+hipError_t dd_apply(const uint64_t* ids, const uint32_t* slot, uint32_t n, const int64_t* result,
+                    uint64_t chunk_size, int64_t* link, unsigned long long* counts, hipStream_t st);
+
+}  // namespace sdcas

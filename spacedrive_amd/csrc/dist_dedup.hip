@@ -1,0 +1,281 @@
+// dist_dedup.hip — device stages of the multi-GPU identifier group-by.
+//
+// The reference links file_paths to Objects by cas_id inside one process,
+// 100 files at a time (core/src/object/file_identifier/mod.rs:149-254 over
+// the chunks of file_identifier_job.rs:296-319). In canonical form (SURVEY.md
+// §8a a7; dedup.hip) the whole job reduces to, per cas key X:
+//   existing(X) = first Object in DB order carrying X   (mod.rs:181-238)
+//   rep(X)      = lowest orphan ordinal carrying X      (mod.rs:246-254)
+// and a per-file rule. Both are associative minima, so each rank first
+// COMBINES its files to one (key, min ordinal) record per distinct key — a
+// Zipf heavy hitter then costs one record per rank, not millions (C5) — the
+// records travel to the key's owner rank (RCCL all-to-all, by the caller),
+// the owner RESOLVES each key against its slice of existing Objects, and the
+// answers travel back in send order for each rank to APPLY to its files.
+//
+// HBM-bound integer work: radix sorts of (key, index) pairs and streaming
+// passes; per-key minima by 64-bit atomicMin on a unique-key array.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include "dist_dedup.h"
+
+namespace sdcas {
+
+namespace {
+
+constexpr uint32_t TB = 256;
+inline uint32_t blocks(uint32_t n) { return (n + TB - 1) / TB; }
+
+__global__ void k_dd_prepare(const uint8_t* __restrict__ has_key, const int32_t* __restrict__ status, uint32_t n,
+                             uint8_t* __restrict__ valid, uint32_t* __restrict__ idx, uint32_t* __restrict__ slot) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const bool ok = status == nullptr || status[i] == 0;  // mod.rs:125-141: errored files are dropped
+  const bool has = has_key == nullptr || has_key[i];    // mod.rs:83-86: empty files have no cas_id
+  valid[i] = ok && has;
+  idx[i] = i;
+  if (slot) slot[i] = !ok ? kSlotDropped : kSlotNoKey;
+}
+
+// run-head flags of a key-sorted array (first nv entries are real)
+__global__ void k_dd_flags(const uint64_t* __restrict__ skey, const uint32_t* __restrict__ nv_p, uint32_t nv_host,
+                           uint32_t n, uint32_t* __restrict__ flag) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const uint32_t nv = nv_p ? *nv_p : nv_host;
+  flag[p] = (p < nv && (p == 0 || skey[p] != skey[p - 1])) ? 1u : 0u;
+}
+
+__global__ void k_dd_emit(const uint64_t* __restrict__ skey, const uint32_t* __restrict__ sidx,
+                          const uint32_t* __restrict__ scan, const uint32_t* __restrict__ nv_p,
+                          const uint64_t* __restrict__ ids, uint64_t* __restrict__ rec, uint32_t* __restrict__ slot) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= *nv_p) return;
+  const uint32_t u = scan[p] - 1;
+  const uint32_t i = sidx[p];
+  if (slot) slot[i] = u;
+  if (p == 0 || skey[p] != skey[p - 1]) {
+    // stable sort + ascending ids: the run's first entry carries the minimum
+    rec[2 * (uint64_t)u] = skey[p];
+    rec[2 * (uint64_t)u + 1] = ids[i];
+  }
+}
+
+__global__ void k_dd_starts(const uint64_t* __restrict__ rec, const uint32_t* __restrict__ scan,
+                            const uint32_t* __restrict__ nv_p, uint32_t world, uint32_t* __restrict__ starts) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r > world) return;
+  const uint32_t nv = *nv_p;
+  const uint32_t U = nv ? scan[nv - 1] : 0u;
+  uint32_t lo = 0, hi = U;  // first record whose owner is >= r
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (dd_owner(rec[2 * (uint64_t)mid], world) < r) lo = mid + 1;
+    else hi = mid;
+  }
+  starts[r] = r == world ? U : lo;
+}
+
+__global__ void k_dd_split(const uint64_t* __restrict__ rec, uint32_t n, uint64_t* __restrict__ key,
+                           uint32_t* __restrict__ pos) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  key[p] = rec[2 * (uint64_t)p];
+  pos[p] = p;
+}
+
+// per unique key: key (optional) and the minimum of the records' values
+__global__ void k_dd_unique_min(const uint64_t* __restrict__ skey, const uint32_t* __restrict__ spos,
+                                const uint32_t* __restrict__ scan, uint32_t n, const uint64_t* __restrict__ rec,
+                                uint64_t* __restrict__ ukey, unsigned long long* __restrict__ umin) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const uint32_t u = scan[p] - 1;
+  if (ukey && (p == 0 || skey[p] != skey[p - 1])) ukey[u] = skey[p];
+  atomicMin(&umin[u], (unsigned long long)rec[2 * (uint64_t)spos[p] + 1]);
+}
+
+__global__ void k_dd_count_of(const uint32_t* __restrict__ scan, uint32_t n, uint32_t* __restrict__ out) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *out = n ? scan[n - 1] : 0u;
+}
+
+__global__ void k_dd_resolve(const uint64_t* __restrict__ skey, const uint32_t* __restrict__ spos,
+                             const uint32_t* __restrict__ scan, uint32_t nf, const uint64_t* __restrict__ fmin,
+                             const uint64_t* __restrict__ ekey, const uint64_t* __restrict__ emin,
+                             const uint32_t* __restrict__ ne_p, int64_t* __restrict__ result) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= nf) return;
+  const uint64_t key = skey[p];
+  const uint32_t ne = ne_p ? *ne_p : 0u;
+  uint32_t lo = 0, hi = ne;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (ekey[mid] < key) lo = mid + 1;
+    else hi = mid;
+  }
+  int64_t r;
+  if (lo < ne && ekey[lo] == key) r = -(int64_t)emin[lo] - 1;  // mod.rs:202-238: first existing Object
+  else r = (int64_t)fmin[scan[p] - 1];                           // the key's first file
+  result[spos[p]] = r;
+}
+
+__global__ void k_dd_apply(const uint64_t* __restrict__ ids, const uint32_t* __restrict__ slot, uint32_t n,
+                           const int64_t* __restrict__ result, uint64_t cs, int64_t* __restrict__ link,
+                           unsigned long long* __restrict__ counts) {
+  __shared__ unsigned long long sc[2];
+  if (threadIdx.x < 2) sc[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long c = 0, l = 0;
+  if (i < n) {
+    const uint32_t s = slot[i];
+    const int64_t me = (int64_t)ids[i];
+    int64_t v;
+    if (s == kSlotDropped) {
+      v = INT64_MIN;
+    } else if (s == kSlotNoKey) {
+      v = me;  // mod.rs:246-254: a file without cas_id gets its own Object
+    } else {
+      const int64_t r = result[s];
+      if (r < 0) v = r;
+      else v = ((uint64_t)me / cs == (uint64_t)r / cs) ? me : r;  // created in the key's first chunk
+    }
+    link[i] = v;
+    if (v == me) c = 1;
+    else if (v != INT64_MIN) l = 1;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    c += __shfl_down(c, off);
+    l += __shfl_down(l, off);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&sc[0], c);
+    atomicAdd(&sc[1], l);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && counts) {
+    atomicAdd(&counts[0], sc[0]);
+    atomicAdd(&counts[1], sc[1]);
+  }
+}
+
+hipError_t ensure_temp(DistWs& w, uint32_t n) {
+  size_t a = 0, b = 0, c = 0;
+  (void)hipcub::DeviceSelect::Flagged(nullptr, a, (const uint64_t*)nullptr, (const uint8_t*)nullptr,
+                                      (uint64_t*)nullptr, (uint32_t*)nullptr, (int)n);
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                           (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
+  (void)hipcub::DeviceScan::InclusiveSum(nullptr, c, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
+  size_t m = a > b ? a : b;
+  m = m > c ? m : c;
+  return w.temp.ensure(m + 256);
+}
+
+hipError_t ensure_n(DistWs& w, uint32_t n) {
+  hipError_t e;
+  if ((e = w.key_a.ensure(n)) || (e = w.key_b.ensure(n)) || (e = w.idx_a.ensure(n)) || (e = w.idx_b.ensure(n)) ||
+      (e = w.scan.ensure(n)) || (e = w.valid.ensure(n)) || (e = w.nvalid.ensure(4)))
+    return e;
+  return ensure_temp(w, n);
+}
+
+// sort n (key, pos) pairs from key_a/idx_b into key_b/idx_a, flags + inclusive
+// sum of run heads into scan
+hipError_t sort_and_scan(DistWs& w, uint32_t n, const uint32_t* nv_p, hipStream_t st) {
+  hipError_t e;
+  size_t tmp = w.temp.cap;
+  if ((e = hipcub::DeviceRadixSort::SortPairs(w.temp.p, tmp, w.key_a.p, w.key_b.p, w.idx_b.p, w.idx_a.p, (int)n, 0,
+                                              64, st)))
+    return e;
+  hipLaunchKernelGGL(k_dd_flags, dim3(blocks(n)), dim3(TB), 0, st, w.key_b.p, nv_p, n, n, w.scan.p);
+  tmp = w.temp.cap;
+  return hipcub::DeviceScan::InclusiveSum(w.temp.p, tmp, w.scan.p, w.scan.p, (int)n, st);
+}
+
+}  // namespace
+
+void DistWs::release() {
+  key_a.release(); key_b.release(); umin.release(); ukey.release(); emin.release();
+  idx_a.release(); idx_b.release(); scan.release(); nvalid.release(); starts.release();
+  valid.release(); temp.release();
+}
+
+hipError_t dd_combine(DistWs& w, const uint64_t* keys, const uint8_t* has_key, const int32_t* status,
+                      const uint64_t* ids, uint32_t n, uint32_t world, uint64_t* rec, uint32_t* slot,
+                      uint64_t* h_starts, uint64_t* h_u, hipStream_t st) {
+  hipError_t e;
+  if ((e = w.starts.ensure(world + 1))) return e;
+  if (n == 0) {
+    for (uint32_t r = 0; r <= world; ++r) h_starts[r] = 0;
+    *h_u = 0;
+    return hipSuccess;
+  }
+  if ((e = ensure_n(w, n))) return e;
+  hipLaunchKernelGGL(k_dd_prepare, dim3(blocks(n)), dim3(TB), 0, st, has_key, status, n, w.valid.p, w.idx_a.p, slot);
+  // compact present (key, index) pairs to the front; the tail keeps UINT64_MAX
+  // fillers that the stable sort leaves behind every real entry
+  if ((e = hipMemsetAsync(w.key_a.p, 0xFF, sizeof(uint64_t) * n, st))) return e;
+  size_t tmp = w.temp.cap;
+  if ((e = hipcub::DeviceSelect::Flagged(w.temp.p, tmp, keys, w.valid.p, w.key_a.p, w.nvalid.p, (int)n, st))) return e;
+  tmp = w.temp.cap;
+  if ((e = hipcub::DeviceSelect::Flagged(w.temp.p, tmp, w.idx_a.p, w.valid.p, w.idx_b.p, w.nvalid.p, (int)n, st)))
+    return e;
+  if ((e = sort_and_scan(w, n, w.nvalid.p, st))) return e;
+  hipLaunchKernelGGL(k_dd_emit, dim3(blocks(n)), dim3(TB), 0, st, w.key_b.p, w.idx_a.p, w.scan.p, w.nvalid.p, ids, rec,
+                     slot);
+  hipLaunchKernelGGL(k_dd_starts, dim3(blocks(world + 1)), dim3(TB), 0, st, rec, w.scan.p, w.nvalid.p, world,
+                     w.starts.p);
+  uint32_t hs[1025];
+  uint32_t* hp = world + 1 <= 1025 ? hs : new uint32_t[world + 1];
+  e = hipMemcpyAsync(hp, w.starts.p, sizeof(uint32_t) * (world + 1), hipMemcpyDeviceToHost, st);
+  if (!e) e = hipStreamSynchronize(st);
+  if (!e) {
+    for (uint32_t r = 0; r <= world; ++r) h_starts[r] = hp[r];
+    *h_u = hp[world];
+  }
+  if (hp != hs) delete[] hp;
+  if (e) return e;
+  return hipGetLastError();
+}
+
+hipError_t dd_resolve(DistWs& w, const uint64_t* frec, uint32_t nf, const uint64_t* erec, uint32_t ne,
+                      int64_t* result, hipStream_t st) {
+  hipError_t e;
+  const uint32_t m = nf > ne ? nf : ne;
+  if (m == 0) return hipSuccess;
+  if ((e = ensure_n(w, m)) || (e = w.umin.ensure(m)) || (e = w.ukey.ensure(ne + 1))) return e;
+  uint64_t* fmin = w.umin.p;  // per unique file key
+  // existing Objects first: unique keys (ukey) + their minimum DB index (emin)
+  uint64_t* emin = nullptr;
+  if (ne) {
+    if ((e = w.emin.ensure(ne))) return e;
+    emin = w.emin.p;
+    if ((e = hipMemsetAsync(emin, 0xFF, sizeof(uint64_t) * ne, st))) return e;
+    hipLaunchKernelGGL(k_dd_split, dim3(blocks(ne)), dim3(TB), 0, st, erec, ne, w.key_a.p, w.idx_b.p);
+    if ((e = sort_and_scan(w, ne, nullptr, st))) return e;
+    hipLaunchKernelGGL(k_dd_unique_min, dim3(blocks(ne)), dim3(TB), 0, st, w.key_b.p, w.idx_a.p, w.scan.p, ne, erec,
+                       w.ukey.p, (unsigned long long*)emin);
+  }
+  hipLaunchKernelGGL(k_dd_count_of, dim3(1), dim3(64), 0, st, w.scan.p, ne, w.nvalid.p + 1);
+  if (nf) {
+    if ((e = hipMemsetAsync(fmin, 0xFF, sizeof(uint64_t) * nf, st))) return e;
+    hipLaunchKernelGGL(k_dd_split, dim3(blocks(nf)), dim3(TB), 0, st, frec, nf, w.key_a.p, w.idx_b.p);
+    if ((e = sort_and_scan(w, nf, nullptr, st))) return e;
+    hipLaunchKernelGGL(k_dd_unique_min, dim3(blocks(nf)), dim3(TB), 0, st, w.key_b.p, w.idx_a.p, w.scan.p, nf, frec,
+                       (uint64_t*)nullptr, (unsigned long long*)fmin);
+    hipLaunchKernelGGL(k_dd_resolve, dim3(blocks(nf)), dim3(TB), 0, st, w.key_b.p, w.idx_a.p, w.scan.p, nf, fmin,
+                       w.ukey.p, emin ? emin : fmin, w.nvalid.p + 1, result);
+  }
+  return hipGetLastError();
+}
+
+hipError_t dd_apply(const uint64_t* ids, const uint32_t* slot, uint32_t n, const int64_t* result, uint64_t chunk_size,
+                    int64_t* link, unsigned long long* counts, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_dd_apply, dim3(blocks(n)), dim3(TB), 0, st, ids, slot, n, result, chunk_size ? chunk_size : 100,
+                     link, counts);
+  return hipGetLastError();
+}
+
+}  // namespace sdcas

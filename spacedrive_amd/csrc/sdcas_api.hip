@@ -27,6 +27,7 @@
 #include "../../include/sdcas_bench.h"
 #include "b3_batch.h"
 #include "dedup.h"
+#include "dist_dedup.h"
 #include "synth.h"
 
 using namespace sdcas;
@@ -95,6 +96,9 @@ struct sdcas_ctx {
   DevBuf<int32_t> dd_status;
   DevBuf<int64_t> dd_link;
   DevBuf<unsigned long long> dd_counts;
+
+  // multi-GPU dedup stages
+  DistWs dist;
 
   // profiling
   bool profile = false;
@@ -445,6 +449,7 @@ void sdcas_destroy(sdcas_ctx* c) {
   c->dd_status.release();
   c->dd_link.release();
   c->dd_counts.release();
+  c->dist.release();
   if (c->h_stage) (void)hipHostFree(c->h_stage);
   for (auto e : c->ev_free) (void)hipEventDestroy(e);
   for (auto& p : c->ev_leaf) (void)hipEventDestroy(p.first), (void)hipEventDestroy(p.second);
@@ -867,6 +872,46 @@ int sdcas_dev_synth_content(sdcas_ctx* c, const uint64_t* d_keys, const uint64_t
   hipStream_t st = stream ? (hipStream_t)stream : c->stream;
   hipError_t e = synth_content(d_keys, d_starts, d_lens, d_offs, (uint32_t)n, d_blob, st);
   return e ? c->hip_fail(e, "synth") : SDCAS_OK;
+}
+
+// ---- multi-GPU dedup stages -----------------------------------
+
+int sdcas_dev_dedup_combine(sdcas_ctx* c, const uint64_t* d_keys, const uint8_t* d_has_key, const int32_t* d_status,
+                            const uint64_t* d_ids, size_t n, uint32_t world, uint64_t* d_rec, uint32_t* d_slot,
+                            uint64_t* out_starts, void* stream) {
+  if (!c || world == 0 || !out_starts || (n && (!d_keys || !d_ids || !d_rec))) return SDCAS_E_INVALID;
+  if (n > 0xFFFFFFF0ull) return c->fail(SDCAS_E_CAPACITY, "dedup_combine: %zu records exceed 2^32", n);
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipSetDevice(c->device);
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  uint64_t u = 0;
+  hipError_t e = dd_combine(c->dist, d_keys, d_has_key, d_status, d_ids, (uint32_t)n, world, d_rec, d_slot,
+                            out_starts, &u, st);
+  return e ? c->hip_fail(e, "dedup_combine") : SDCAS_OK;
+}
+
+int sdcas_dev_dedup_resolve(sdcas_ctx* c, const uint64_t* d_frec, size_t nf, const uint64_t* d_erec, size_t ne,
+                            int64_t* d_result, void* stream) {
+  if (!c || (nf && (!d_frec || !d_result)) || (ne && !d_erec)) return SDCAS_E_INVALID;
+  if (nf > 0xFFFFFFF0ull || ne > 0xFFFFFFF0ull) return c->fail(SDCAS_E_CAPACITY, "dedup_resolve: > 2^32 records");
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipSetDevice(c->device);
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  hipError_t e = dd_resolve(c->dist, d_frec, (uint32_t)nf, d_erec, (uint32_t)ne, d_result, st);
+  return e ? c->hip_fail(e, "dedup_resolve") : SDCAS_OK;
+}
+
+int sdcas_dev_dedup_apply(sdcas_ctx* c, const uint64_t* d_ids, const uint32_t* d_slot, size_t n,
+                          const int64_t* d_result, size_t chunk_size, int64_t* d_link, uint64_t* d_counts,
+                          void* stream) {
+  if (!c || (n && (!d_ids || !d_slot || !d_link))) return SDCAS_E_INVALID;
+  if (n > 0xFFFFFFF0ull) return c->fail(SDCAS_E_CAPACITY, "dedup_apply: %zu files exceed 2^32", n);
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipSetDevice(c->device);
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  hipError_t e = dd_apply(d_ids, d_slot, (uint32_t)n, d_result, chunk_size ? chunk_size : SDCAS_IDENTIFIER_CHUNK_SIZE,
+                          d_link, (unsigned long long*)d_counts, st);
+  return e ? c->hip_fail(e, "dedup_apply") : SDCAS_OK;
 }
 
 }  // extern "C"

@@ -1,0 +1,155 @@
+"""Multi-GPU identifier dedup: the cas_id -> Object group-by of
+core/src/object/file_identifier/mod.rs:149-254 over orphan file_paths sharded
+across the GPUs of a node, one process per GPU.
+
+The reference runs this group-by 100 files at a time in one process
+(file_identifier_job.rs:296-319). In canonical form it
+only needs two per-key minima — the first existing Object in DB order and the
+lowest orphan ordinal carrying the key — plus a per-file rule, so it shards:
+
+  1. combine   every rank reduces its files to one (key, min ordinal) record
+               per distinct key, key-sorted, hence grouped by owner rank
+               (owner = top 12 key bits split into `world` ranges); existing
+               Objects likewise to (key, min DB index)
+  2. exchange  RCCL all-to-all of both record sets (16 B records)
+  3. resolve   the owner answers each file record: -(db+1) or the key's
+               global first ordinal
+  4. exchange  the answers go back (8 B each, the reverse all-to-all)
+  5. apply     every rank links its files: dropped / own Object / existing
+               Object / the Object created by the key's first file
+
+The device stages (1, 3, 5) are libsdcas's HIP kernels
+(sdcas_dev_dedup_{combine,resolve,apply}); the exchanges are
+torch.distributed all_to_all_single (backend "nccl" = RCCL over xGMI). The
+`stages` object is pluggable only so that the collective protocol can be
+exercised with gloo on CPU by the test-suite's numpy stages
+(tests/_dist_stages.py); the product path is `DeviceStages`.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import _native as N
+
+
+class DeviceStages:
+    """The three device stages through the C ABI, on torch tensors in HBM.
+
+    Every stage runs on a stream of its own, ordered after the caller's
+    current stream and before anything the caller enqueues next (torch's
+    default stream is the legacy NULL stream, which libsdcas would read as
+    "the context's non-blocking stream", so it is never handed over as is).
+    """
+
+    def __init__(self, engine, device=None):
+        self.eng = engine
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        self.stream = torch.cuda.Stream(self.device)
+
+    def _enter(self):
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        return self.stream.cuda_stream
+
+    def _leave(self, *tensors):
+        for t in tensors:
+            if t is not None and t.is_cuda:
+                t.record_stream(self.stream)
+        torch.cuda.current_stream(self.device).wait_stream(self.stream)
+
+    def combine(self, keys, has_key, status, ids, world):
+        """-> (rec int64[U, 2], slot int32[n] or None, starts list[world+1])"""
+        n = int(ids.numel())
+        dev = ids.device
+        rec = torch.empty((max(n, 1), 2), dtype=torch.int64, device=dev)
+        slot = torch.empty(max(n, 1), dtype=torch.int32, device=dev) if has_key is not None or status is not None \
+            or keys is not None else None
+        starts = (ctypes.c_uint64 * (world + 1))()
+        p = lambda t: t.data_ptr() if t is not None and t.numel() else None
+        rc = self.eng.L.sdcas_dev_dedup_combine(self.eng.ctx, p(keys), p(has_key), p(status), p(ids), n,
+                                                world, p(rec), p(slot) if slot is not None else None, starts,
+                                                self._enter())
+        self._leave(keys, has_key, status, ids, rec, slot)
+        self.eng._check(rc, "sdcas_dev_dedup_combine")
+        st = [int(x) for x in starts]
+        return rec[: st[world]], (slot[:n] if slot is not None else None), st
+
+    def resolve(self, frec, erec):
+        nf, ne = int(frec.shape[0]), int(erec.shape[0])
+        result = torch.empty(max(nf, 1), dtype=torch.int64, device=frec.device)
+        p = lambda t: t.data_ptr() if t.numel() else None
+        rc = self.eng.L.sdcas_dev_dedup_resolve(self.eng.ctx, p(frec), nf, p(erec), ne, p(result),
+                                                self._enter())
+        self._leave(frec, erec, result)
+        self.eng._check(rc, "sdcas_dev_dedup_resolve")
+        return result[:nf]
+
+    def apply(self, ids, slot, result, chunk_size):
+        """-> (link int64[n], counts int64[2] = (created, linked)) on the device"""
+        n = int(ids.numel())
+        link = torch.empty(max(n, 1), dtype=torch.int64, device=ids.device)
+        counts = torch.zeros(2, dtype=torch.int64, device=ids.device)
+        p = lambda t: t.data_ptr() if t.numel() else None
+        rc = self.eng.L.sdcas_dev_dedup_apply(self.eng.ctx, p(ids), p(slot), n, p(result), int(chunk_size),
+                                              p(link), counts.data_ptr(), self._enter())
+        self._leave(ids, slot, result, link, counts)
+        self.eng._check(rc, "sdcas_dev_dedup_apply")
+        return link[:n], counts
+
+
+def _exchange(send, send_counts, group):
+    """all_to_all of rows grouped by destination rank -> (recv, recv_counts)"""
+    dev = send.device
+    sc = torch.tensor(send_counts, dtype=torch.int64, device=dev)
+    rc = torch.empty_like(sc)
+    dist.all_to_all_single(rc, sc, group=group)
+    recv_counts = [int(x) for x in rc.tolist()]
+    recv = send.new_empty((sum(recv_counts),) + tuple(send.shape[1:]))
+    dist.all_to_all_single(recv, send.contiguous(), recv_counts, list(send_counts), group=group)
+    return recv, recv_counts
+
+
+def identifier_dedup_distributed(stages, keys, has_key, status, ids, chunk_size=100,
+                                 existing_keys=None, existing_ids=None, group=None):
+    """This rank's share of the identifier group-by.
+
+    keys/has_key/status/ids: this rank's orphan file_paths (ids = their global
+    ordinals in orphan order, ascending; has_key 0 = cas_id None; status != 0
+    = I/O error). existing_keys/existing_ids: this rank's share of the
+    library's existing Objects (ids = global DB order). Every rank must call
+    this (it is collective). Returns (link int64[n], created, linked): link
+    uses sdcas_dedup's encoding with global ordinals (i = creates, j = links
+    to the Object created by file j, -(e+1) = existing Object e, INT64_MIN =
+    dropped); created/linked are the node-wide totals identifier_job_step
+    would return summed over the job (mod.rs:349).
+    """
+    world = dist.get_world_size(group)
+    rec, slot, starts = stages.combine(keys, has_key, status, ids, world)
+    counts = [starts[r + 1] - starts[r] for r in range(world)]
+    if existing_keys is not None and existing_keys.numel():
+        erec, _, estarts = stages.combine(existing_keys, None, None, existing_ids, world)
+        ecounts = [estarts[r + 1] - estarts[r] for r in range(world)]
+    else:
+        erec = rec.new_empty((0, 2))
+        ecounts = [0] * world
+    frecv, fcounts = _exchange(rec, counts, group)
+    erecv, _ = _exchange(erec, ecounts, group)
+    answer = stages.resolve(frecv, erecv)
+    back, _ = _exchange(answer, fcounts, group)
+    link, cnt = stages.apply(ids, slot, back, chunk_size)
+    dist.all_reduce(cnt, group=group)
+    c = cnt.tolist()
+    return link, int(c[0]), int(c[1])
+
+
+def owner_of(keys: np.ndarray, world: int) -> np.ndarray:
+    """owner rank of cas keys (dist_dedup.h dd_owner): top 12 bits in `world` ranges"""
+    k = np.asarray(keys, dtype=np.uint64)
+    return ((k >> np.uint64(52)) * np.uint64(world) >> np.uint64(12)).astype(np.int64)
+
+
+__all__ = ["DeviceStages", "identifier_dedup_distributed", "owner_of"]
+_ = N  # the C ABI is bound by spacedrive_amd._native.load()

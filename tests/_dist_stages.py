@@ -1,0 +1,166 @@
+"""Test infrastructure: numpy restatement of the three device stages of the
+multi-GPU dedup (spacedrive_amd/csrc/dist_dedup.hip), on CPU torch tensors.
+
+Used (a) to run spacedrive_amd.dist_dedup's collective protocol under gloo on
+CPU, where there is no GPU, and (b) as a second checker of the device stages.
+Never used by the product path. Semantics follow
+core/src/object/file_identifier/mod.rs:149-254 in the canonical form of
+SURVEY.md §8a a7 (see tests/_oracle.py:identifier_dedup for the chunked loop).
+"""
+import numpy as np
+import torch
+
+from spacedrive_amd.dist_dedup import owner_of
+
+NOKEY = np.uint32(0xFFFFFFFF)
+DROPPED = np.uint32(0xFFFFFFFE)
+
+
+def _u64(t):
+    return t.numpy().view(np.uint64) if t is not None else None
+
+
+def _t64(a):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint64).view(np.int64))
+
+
+def virtual_exchange(send_list, counts_list):
+    """all-to-all among R virtual ranks in one process: send_list[r] rows
+    grouped by destination with counts_list[r][d] rows for d. Returns per
+    destination (recv rows, recv counts from each source)."""
+    R = len(send_list)
+    out, out_counts = [], []
+    offs = [np.concatenate([[0], np.cumsum(c)]).astype(np.int64) for c in counts_list]
+    for d in range(R):
+        parts = [send_list[s][int(offs[s][d]):int(offs[s][d + 1])] for s in range(R)]
+        out.append(torch.cat(parts) if parts else send_list[0][:0])
+        out_counts.append([int(counts_list[s][d]) for s in range(R)])
+    return out, out_counts
+
+
+def dedup_virtual(stages_for, shards, chunk_size, existing_shards=None):
+    """Run the protocol of identifier_dedup_distributed for R virtual ranks in
+    one process (stages_for(r) gives rank r's stage object; shards[r] =
+    (keys, has_key, status, ids) tensors). Returns (per-rank links, created,
+    linked)."""
+    R = len(shards)
+    st = [stages_for(r) for r in range(R)]
+    recs, slots, counts = [], [], []
+    for r, (k, h, s, ids) in enumerate(shards):
+        rec, slot, starts = st[r].combine(k, h, s, ids, R)
+        recs.append(rec)
+        slots.append(slot)
+        counts.append([starts[d + 1] - starts[d] for d in range(R)])
+    erecs, ecounts = [], []
+    for r in range(R):
+        if existing_shards is not None and existing_shards[r][0].numel():
+            ek, eids = existing_shards[r]
+            rec, _, starts = st[r].combine(ek, None, None, eids, R)
+        else:
+            rec, starts = recs[r][:0], [0] * (R + 1)
+        erecs.append(rec)
+        ecounts.append([starts[d + 1] - starts[d] for d in range(R)])
+    frecv, fc = virtual_exchange(recs, counts)
+    erecv, _ = virtual_exchange(erecs, ecounts)
+    answers = [st[d].resolve(frecv[d], erecv[d]) for d in range(R)]
+    # reverse exchange: destination d sends answers back grouped by source
+    back, _ = virtual_exchange(answers, fc)
+    links, created, linked = [], 0, 0
+    for r, (k, h, s, ids) in enumerate(shards):
+        link, cnt = st[r].apply(ids, slots[r], back[r], chunk_size)
+        links.append(link)
+        c = cnt.cpu().tolist()
+        created += int(c[0])
+        linked += int(c[1])
+    return links, created, linked
+
+
+class NumpyStages:
+    """Same contract as spacedrive_amd.dist_dedup.DeviceStages, on CPU."""
+
+    def combine(self, keys, has_key, status, ids, world):
+        ids_np = _u64(ids)
+        n = ids_np.size
+        k = _u64(keys) if keys is not None else np.zeros(n, np.uint64)
+        ok = np.ones(n, bool) if status is None else status.numpy() == 0
+        has = np.ones(n, bool) if has_key is None else has_key.numpy() != 0
+        valid = ok & has
+        slot = np.where(ok, NOKEY, DROPPED).astype(np.uint32)
+        vi = np.nonzero(valid)[0]
+        order = vi[np.argsort(k[vi], kind="stable")]
+        sk = k[order]
+        head = np.ones(sk.size, bool)
+        head[1:] = sk[1:] != sk[:-1]
+        uid = np.cumsum(head) - 1
+        slot[order] = uid.astype(np.uint32)
+        rec = np.stack([sk[head], ids_np[order[head]]], 1) if sk.size else np.zeros((0, 2), np.uint64)
+        own = owner_of(rec[:, 0], world)
+        starts = [int(x) for x in np.searchsorted(own, np.arange(world + 1), side="left")]
+        starts[world] = int(rec.shape[0])
+        return _t64(rec).reshape(-1, 2), torch.from_numpy(slot.view(np.int32)), starts
+
+    def resolve(self, frec, erec):
+        f = _u64(frec).reshape(-1, 2)
+        e = _u64(erec).reshape(-1, 2)
+        emin = {}
+        for key, db in e:
+            if key not in emin or db < emin[key]:
+                emin[int(key)] = int(db)
+        fmin = {}
+        for key, i in f:
+            key, i = int(key), int(i)
+            if key not in fmin or i < fmin[key]:
+                fmin[key] = i
+        res = np.empty(f.shape[0], np.int64)
+        for p, (key, _) in enumerate(f):
+            key = int(key)
+            res[p] = -emin[key] - 1 if key in emin else fmin[key]
+        return torch.from_numpy(res)
+
+    def apply(self, ids, slot, result, chunk_size):
+        ids_np = _u64(ids).astype(np.int64)
+        s = slot.numpy().view(np.uint32)
+        r = result.numpy()
+        link = np.empty(ids_np.size, np.int64)
+        for i in range(ids_np.size):
+            me = int(ids_np[i])
+            if s[i] == DROPPED:
+                link[i] = np.iinfo(np.int64).min
+            elif s[i] == NOKEY:
+                link[i] = me
+            else:
+                v = int(r[s[i]])
+                link[i] = v if v < 0 else (me if me // chunk_size == v // chunk_size else v)
+        created = int((link == ids_np).sum())
+        linked = int(((link != ids_np) & (link != np.iinfo(np.int64).min)).sum())
+        return torch.from_numpy(link), torch.tensor([created, linked], dtype=torch.int64)
+
+
+def make_corpus(seed, n, pool=4000, zipf=1.3, p_none=0.02, p_err=0.01, n_existing=300):
+    """keys with Zipf duplicates, None cas_ids, I/O errors, existing Objects"""
+    rng = np.random.default_rng(seed)
+    pool_keys = rng.integers(0, 2**64, pool, dtype=np.uint64)
+    keys = pool_keys[rng.zipf(zipf, n) % pool]
+    has = (rng.random(n) > p_none).astype(np.uint8)
+    status = np.where(rng.random(n) < p_err, 5, 0).astype(np.int32)
+    existing = np.concatenate([pool_keys[rng.integers(0, pool, n_existing)],
+                               rng.integers(0, 2**64, n_existing // 6, dtype=np.uint64)])
+    return keys, has, status, existing
+
+
+def shard(keys, has, status, existing, R, device="cpu", contiguous=True):
+    """split the orphan list into R contiguous ranges (rank r holds ordinals
+    [lo_r, hi_r)), existing Objects round-robin by DB index"""
+    n = keys.size
+    cuts = [n * r // R for r in range(R + 1)]
+    out = []
+    for r in range(R):
+        lo, hi = cuts[r], cuts[r + 1]
+        t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(device)
+        out.append((t(keys[lo:hi].view(np.int64), None), t(has[lo:hi], None), t(status[lo:hi], None),
+                    t(np.arange(lo, hi, dtype=np.int64), None)))
+    ex = []
+    for r in range(R):
+        idx = np.arange(r, existing.size, R, dtype=np.int64)
+        ex.append((torch.from_numpy(existing[idx].view(np.int64)).to(device), torch.from_numpy(idx).to(device)))
+    return out, ex

@@ -1,0 +1,166 @@
+"""Multi-GPU dedup: the collective protocol of
+spacedrive_amd.dist_dedup against the chunked CPU oracle of
+file_identifier/mod.rs:149-254 (oracle_identifier_dedup).
+
+CPU: the real torch.distributed protocol under gloo (world 2 and 4, one
+process per rank) with the numpy stages (tests/_dist_stages.py), and the
+virtual-rank protocol with the numpy stages.
+GPU: the device stages (libsdcas HIP kernels) under the virtual-rank protocol
+for R = 1..8, and the real protocol over RCCL at world 1.
+"""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+
+from tests._dist_stages import NumpyStages, dedup_virtual, make_corpus, shard
+
+INT64_MIN = np.iinfo(np.int64).min
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _gloo_worker(rank, world, port, outdir, seed, n, chunk_size):
+    import torch.distributed as dist
+
+    from spacedrive_amd.dist_dedup import identifier_dedup_distributed
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        keys, has, status, existing = make_corpus(seed, n)
+        shards, ex = shard(keys, has, status, existing, world)
+        k, h, s, ids = shards[rank]
+        ek, eids = ex[rank]
+        link, created, linked = identifier_dedup_distributed(NumpyStages(), k, h, s, ids, chunk_size, ek, eids)
+        np.savez(os.path.join(outdir, f"r{rank}.npz"), link=link.numpy(), created=created, linked=linked)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,chunk_size", [(2, 100), (4, 7), (3, 1)])
+def test_gloo_protocol_vs_oracle(oracle, world, chunk_size):
+    import torch.multiprocessing as mp
+    seed, n = 1000 + world, 3000
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_gloo_worker, args=(world, _free_port(), d, seed, n, chunk_size), nprocs=world,
+                           join=True, start_method="spawn")
+        parts = [np.load(os.path.join(d, f"r{r}.npz")) for r in range(world)]
+    got = np.concatenate([p["link"] for p in parts])
+    keys, has, status, existing = make_corpus(seed, n)
+    want, wc, wl = oracle.identifier_dedup(keys, has, status, chunk_size, existing)
+    assert np.array_equal(got, want)
+    for p in parts:  # node-wide totals on every rank
+        assert (int(p["created"]), int(p["linked"])) == (wc, wl)
+
+
+@pytest.mark.parametrize("R", [1, 2, 5, 8])
+def test_virtual_protocol_numpy_vs_oracle(oracle, R):
+    keys, has, status, existing = make_corpus(7 + R, 2500)
+    shards, ex = shard(keys, has, status, existing, R)
+    links, c, l = dedup_virtual(lambda r: NumpyStages(), shards, 100, ex)
+    want, wc, wl = oracle.identifier_dedup(keys, has, status, 100, existing)
+    assert np.array_equal(np.concatenate([x.numpy() for x in links]), want)
+    assert (c, l) == (wc, wl)
+
+
+def test_owner_is_monotone_and_covers_ranks():
+    from spacedrive_amd.dist_dedup import owner_of
+    k = np.sort(np.random.default_rng(0).integers(0, 2**64, 10000, dtype=np.uint64))
+    for w in (1, 2, 3, 8, 16):
+        o = owner_of(k, w)
+        assert np.all(np.diff(o) >= 0) and o.min() == 0 and o.max() == w - 1
+    assert owner_of(np.array([2**64 - 1], np.uint64), 8)[0] == 7
+
+
+# ---- GPU: device stages ------------------------------------------------------
+
+@pytest.fixture(scope="module")
+def eng():
+    from spacedrive_amd import Engine
+    e = Engine()
+    yield e
+    e.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R,chunk_size", [(1, 100), (2, 100), (3, 7), (8, 100), (8, 1)])
+def test_device_stages_virtual_vs_oracle(eng, oracle, R, chunk_size):
+    from spacedrive_amd.dist_dedup import DeviceStages
+    keys, has, status, existing = make_corpus(50 + R, 40000, pool=6000)
+    shards, ex = shard(keys, has, status, existing, R, device="cuda")
+    st = DeviceStages(eng)
+    links, c, l = dedup_virtual(lambda r: st, shards, chunk_size, ex)
+    want, wc, wl = oracle.identifier_dedup(keys, has, status, chunk_size, existing)
+    got = np.concatenate([x.cpu().numpy() for x in links])
+    assert np.array_equal(got, want)
+    assert (c, l) == (wc, wl)
+
+
+@pytest.mark.gpu
+def test_device_stages_match_numpy_stages(eng):
+    """stage by stage, device vs numpy restatement (records, slots, answers)"""
+    from spacedrive_amd.dist_dedup import DeviceStages
+    keys, has, status, existing = make_corpus(5, 20000)
+    keys[:3] = np.uint64(2**64 - 1)  # the sort's filler value is a legal key
+    (k, h, s, ids), = shard(keys, has, status, existing, 1, device="cuda")[0]
+    st, ns = DeviceStages(eng), NumpyStages()
+    for world in (1, 4, 7):
+        rec_d, slot_d, starts_d = st.combine(k, h, s, ids, world)
+        rec_n, slot_n, starts_n = ns.combine(k.cpu(), h.cpu(), s.cpu(), ids.cpu(), world)
+        assert starts_d == starts_n
+        assert torch.equal(rec_d.cpu(), rec_n)
+        assert torch.equal(slot_d.cpu(), slot_n)
+    ek = torch.from_numpy(existing.view(np.int64)).cuda()
+    eids = torch.arange(existing.size, dtype=torch.int64, device="cuda")
+    erec_d, _, _ = st.combine(ek, None, None, eids, 1)
+    ans_d = st.resolve(rec_d, erec_d)
+    ans_n = ns.resolve(rec_d.cpu(), erec_d.cpu())
+    assert torch.equal(ans_d.cpu(), ans_n)
+
+
+@pytest.mark.gpu
+def test_device_stages_empty_and_degenerate(eng, oracle):
+    from spacedrive_amd.dist_dedup import DeviceStages
+    st = DeviceStages(eng)
+    # a rank with no files, a rank whose files all lack cas_ids or failed
+    keys = np.array([5, 5, 6, 5, 7, 7], np.uint64)
+    has = np.array([1, 0, 1, 1, 0, 1], np.uint8)
+    status = np.array([0, 0, 2, 0, 0, 0], np.int32)
+    shards, ex = shard(keys, has, status, np.zeros(0, np.uint64), 3, device="cuda")
+    shards = [shards[0], shards[1], shards[2]]
+    empty = shard(np.zeros(0, np.uint64), np.zeros(0, np.uint8), np.zeros(0, np.int32), np.zeros(0, np.uint64), 1,
+                  device="cuda")[0][0]
+    # ordinals stay global: splice an empty rank in front
+    links, c, l = dedup_virtual(lambda r: st, [empty] + shards, 2)
+    want, wc, wl = oracle.identifier_dedup(keys, has, status, 2, np.zeros(0, np.uint64))
+    assert np.array_equal(np.concatenate([x.cpu().numpy() for x in links]), want)
+    assert (c, l) == (wc, wl)
+
+
+@pytest.mark.gpu
+def test_rccl_world1(eng, oracle):
+    """the real collective path (backend nccl = RCCL) at world size 1"""
+    import torch.distributed as dist
+
+    from spacedrive_amd.dist_dedup import DeviceStages, identifier_dedup_distributed
+    keys, has, status, existing = make_corpus(77, 30000)
+    (k, h, s, ids), = shard(keys, has, status, existing, 1, device="cuda")[0]
+    ek = torch.from_numpy(existing.view(np.int64)).cuda()
+    eids = torch.arange(existing.size, dtype=torch.int64, device="cuda")
+    store = dist.HashStore()
+    dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        link, c, l = identifier_dedup_distributed(DeviceStages(eng), k, h, s, ids, 100, ek, eids)
+    finally:
+        dist.destroy_process_group()
+    want, wc, wl = oracle.identifier_dedup(keys, has, status, 100, existing)
+    assert np.array_equal(link.cpu().numpy(), want)
+    assert (c, l) == (wc, wl)
