@@ -2,23 +2,34 @@
 """bench.py — headline benchmark of the MI355X content-identification engine.
 
 Metric (BASELINE.json): cas_id files/s + BLAKE3 GB/s hashed, per node.
-Workload at N=1: config C2 — 1,000,000 synthetic files per GPU, size ~
-Uniform{1024..102400} (seed 0x5D0002), so every file takes the whole-file
-cas_id branch of core/src/object/cas.rs:27-29: message = le64(size) || file.
-Messages are generated in HBM before timing (include/sdcas_synth.h); one
-"step" = one batched cas_id pass over all of a GPU's files through the C ABI
-(sdcas_dev_hash_messages: chunk scan, tile map, leaf+tree kernel, finish
-kernel), keys left in HBM.
+
+Default workload (N=1 headline): config C2 — 1,000,000 synthetic files per
+GPU, size ~ Uniform{1024..102400} (seed 0x5D0002), so every file takes the
+whole-file cas_id branch of core/src/object/cas.rs:27-29: message =
+le64(size) || file. Messages are generated in HBM before timing
+(include/sdcas_synth.h); one "step" = one batched cas_id pass over all of a
+GPU's files through the C ABI (sdcas_dev_hash_messages: chunk scan, tile map,
+leaf+tree kernel, finish kernel), keys left in HBM.
+
+Other workloads (--workload; reported the same way):
+  c3  1.25M mixed files per GPU (75% whole-file log-uniform 1 B..100 KiB, 25%
+      sampled 100 KiB..64 GiB, 15% duplicates); step = cas_id pass + the
+      node-wide identifier dedup (spacedrive_amd.dist_dedup: combine, RCCL
+      all-to-all, resolve, all-to-all back, apply)
+  c5  6.25M files per GPU from the 50M Zipf-skewed corpus (60% duplicate
+      files); same step as c3 — the dedup shuffle under heavy hitters
 
 Multi-GPU (torchrun): files are sharded, rank r owns global files
-[r*n, (r+1)*n) — independent units, no collective on the data path
-(SURVEY.md §8e); value = all ranks' files / max-over-ranks time.
+[r*n, (r+1)*n) (c5: files r, r+8, r+16, ... so every GPU sees the corpus'
+mix) — independent units for hashing (no collective), one
+all-to-all exchange for the c3/c5 dedup; value = all ranks'
+files / max-over-ranks time.
 
 Extra fields: blake3_gbps, roofline (leaf/tree kernel, HIP events on its
 stream, vs HBM peak; plus the VALU roofline the kernel is actually bound by),
-cpu_baseline (rank 0, N=1: the reference's shape — one hashing thread, SIMD
-BLAKE3 — on a bounded sample, via the oracle; its keys double as a parity
-check of the GPU keys).
+cpu_baseline (rank 0, N=1, c2: the reference's shape — one hashing thread,
+SIMD BLAKE3 — over the whole C2 workload, via the oracle; its keys double as
+a parity check of every GPU key).
 """
 import argparse
 import ctypes
@@ -32,31 +43,55 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from spacedrive_amd import synth as S  # noqa: E402
+
 METRIC = "cas_id files/sec + BLAKE3 GB/s hashed (node) at 1/2/4/8 MI355X"
-SEED_C2 = 0x5D0002
+SEED_C2 = S.SEED_C2
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# VALU: 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz (MI355X_MICROARCH.md: SIMD-32,
-# a wave64 VALU op issues over 2 cycles) = 7.86e13 int32 ops/s
+# VALU: 256 CU x 4 SIMD-32 x 2.4 GHz (MI355X_MICROARCH.md: a wave64 VALU op
+# issues over 2 cycles) = 7.86e13 int32 lane-ops/s
 VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9
 OPS_PER_COMPRESSION = 680  # 7 rounds x 8 G x 12 (add3, xor, alignbit) + 8 feed-forward xor
+# tools/ubench_valu.hip on MI355X: the 3-operand VOP3 ops BLAKE3 needs
+# (v_alignbit_b32, v_add3_u32) issue at half the VOP2 rate, and a
+# register-only compression loop saturates at 58.5 G compressions/s
+VALU_ROOF_MEASURED = 58.5e9
 
-
-def mix64(x):
-    with np.errstate(over="ignore"):
-        z = x + np.uint64(0x9E3779B97F4A7C15)
-        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
-        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
-        return z ^ (z >> np.uint64(31))
+WORKLOADS = {
+    "c2": dict(files=1_000_000, dedup=False,
+               desc="C2: 1M files x Uniform{1..100 KiB}, whole-file cas_id (cas.rs:27-29)"),
+    "c3": dict(files=1_250_000, dedup=True,
+               desc="C3: 10M mixed files over 8 GPUs (1.25M/GPU): 75% whole-file 1 B..100 KiB, 25% sampled "
+                    "100 KiB..64 GiB (cas.rs:30-59), 15% duplicates; cas_id + identifier dedup via RCCL all-to-all"),
+    "c5": dict(files=6_250_000, dedup=True,
+               desc="C5: 50M-file Zipf(1.1) corpus over 8 GPUs (6.25M/GPU), 60% duplicate files, bounded-Pareto "
+                    "sizes 1 KiB..1 GiB; cas_id + identifier dedup via RCCL all-to-all"),
+}
 
 
 def c2_files(seed, lo, hi):
     """sizes and content keys of C2 files [lo, hi) (include/sdcas_synth.h)"""
-    i = np.arange(lo, hi, dtype=np.uint64)
-    with np.errstate(over="ignore"):
-        raw = mix64(np.uint64(seed) ^ np.uint64(0xC2C2C2C2) ^ (i << np.uint64(20)) ^ (i >> np.uint64(44)))
-        sizes = np.uint64(1024) + raw % np.uint64(102400 - 1024 + 1)
-        keys = mix64(np.uint64(seed) ^ (i * np.uint64(0xD1B54A32D192ED03)))
-    return sizes, keys
+    return S.c2_files(lo, hi, seed)
+
+
+C5_STRIDE = 8  # the C5 corpus spans 8 GPUs: GPU r's share is files r, r+8, r+16, ...
+
+
+def files_of(workload, rank, n):
+    """(sizes, content keys, global orphan ordinals) of this rank's files"""
+    if workload == "c2":
+        s, k = S.c2_files(rank * n, (rank + 1) * n)
+        return s, k, np.arange(rank * n, (rank + 1) * n, dtype=np.int64)
+    if workload == "c3":
+        s, k, _ = S.c3_files(rank * n, (rank + 1) * n)
+        return s, k, np.arange(rank * n, (rank + 1) * n, dtype=np.int64)
+    if workload == "c5":
+        # a strided share keeps each GPU's mix (40% first copies, 60% Zipf
+        # draws) equal to the whole corpus' at any N <= 8
+        ids = np.arange(n, dtype=np.int64) * C5_STRIDE + rank % C5_STRIDE + (rank // C5_STRIDE) * n * C5_STRIDE
+        cid = S.c5_content_ids_at(ids.astype(np.uint64))
+        return S.c5_sizes_of(cid), S.content_key(S.SEED_C5, cid), ids
+    raise ValueError(workload)
 
 
 def compressions(lens):
@@ -76,7 +111,7 @@ def load_traffic(workload):
             d = json.load(open(p))
         except Exception:
             continue
-        if d.get("workload") == workload and d.get("kernel", "").startswith("k_leaf_tree"):
+        if d.get("workload") == workload.upper() and d.get("kernel", "").startswith("k_leaf_tree"):
             best = d
     return best
 
@@ -112,16 +147,30 @@ def cpu_baseline(gpu_keys, sample, threads):
     return base, parity
 
 
+def sample_parity(gpu_keys, sizes, ckeys, count, seed=1):
+    """CPU oracle keys of `count` files spread over the batch (incl. sampled)"""
+    from tests._oracle import load_oracle
+    o = load_oracle()
+    rng = np.random.default_rng(seed)
+    idx = np.unique(np.concatenate([rng.integers(0, sizes.size, count),
+                                    np.nonzero(sizes > S.MIN_FILE)[0][:count // 4]]))
+    bad = sum(int(gpu_keys[i]) != o.synth_cas_key(int(ckeys[i]), int(sizes[i])) for i in idx)
+    return {"checked_files": int(idx.size), "mismatches": int(bad),
+            "oracle": "scalar BLAKE3 restatement over the synthetic cas message (oracle/cas_ref.c)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--files", type=int, default=1_000_000, help="files per GPU (C2: 1M)")
-    ap.add_argument("--cpu-sample", type=int, default=200_000)
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--files", type=int, default=0, help="files per GPU (default: the workload's)")
+    ap.add_argument("--cpu-sample", type=int, default=1_000_000)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    W = WORKLOADS[args.workload]
 
     import torch
     import torch.distributed as dist
@@ -130,26 +179,27 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = world > 1
-    if distributed:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
+    torch.cuda.set_device(local if distributed else 0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    if distributed:
+        dist.init_process_group("nccl", device_id=dev)
+    elif W["dedup"]:
+        # the dedup driver is collective code: a world of one over RCCL
+        dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=dev)
 
     from spacedrive_amd import Engine
+    from spacedrive_amd.dist_dedup import DeviceStages, identifier_dedup_distributed
 
-    n = args.files
-    lo = rank * n
-    sizes, keys = c2_files(SEED_C2, lo, lo + n)
-    lens = sizes + np.uint64(8)
+    n = args.files or W["files"]
+    sizes, keys, ids = files_of(args.workload, rank, n)
+    lens = S.cas_msg_len(sizes)
     offs = np.zeros(n, np.uint64)
     # messages start on 128-byte lines (the L2/HBM line): a chunk then spans
     # 8 lines instead of 9 (the layout of device memory is ours to choose)
     padded = (lens + np.uint64(127)) // np.uint64(128) * np.uint64(128)
     offs[1:] = np.cumsum(padded[:-1])
     total_bytes = int(offs[-1] + padded[-1]) + 64
-    chunks = int(((lens + np.uint64(1023)) // np.uint64(1024)).sum())
+    chunks = int(np.maximum(np.uint64(1), (lens + np.uint64(1023)) // np.uint64(1024)).sum())
     msg_bytes = int(lens.sum())
     comp = int(compressions(lens).sum())
 
@@ -164,12 +214,28 @@ def main():
     eng.dev_synth_cas_messages(d_keys.data_ptr(), d_sizes.data_ptr(), d_offs.data_ptr(), n, d_blob.data_ptr(), sp)
     torch.cuda.synchronize()
 
+    dd = None
+    if W["dedup"]:
+        d_has = (d_sizes != 0).to(torch.uint8)  # mod.rs:78-86: empty files have no cas_id
+        d_ids = torch.from_numpy(ids).to(dev)
+        stages = DeviceStages(eng, dev.index)
+        dd = {"ms": []}
+
     def step():
         eng.dev_hash_messages(d_blob.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), n, 0, d_out.data_ptr(), sp)
+        if dd is not None:
+            eng.dev_sync(sp)
+            t0 = time.perf_counter()
+            link, created, linked = identifier_dedup_distributed(stages, d_out, d_has, None, d_ids, 100)
+            torch.cuda.synchronize()
+            dd["ms"].append((time.perf_counter() - t0) * 1e3)
+            dd["last"] = (link, created, linked)
 
     for _ in range(args.warmup):
         step()
     eng.dev_sync(sp)
+    if dd is not None:
+        dd["ms"].clear()
     eng.dev_profile(True)
     if distributed:
         dist.barrier()
@@ -185,19 +251,17 @@ def main():
     eng.dev_profile(False)
     eng.dev_sync(sp)
     if distributed:
-        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        tt = torch.tensor([dt, leaf_ms, seq_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
-        lt = torch.tensor([leaf_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(lt, op=dist.ReduceOp.MAX)
-        leaf_ms = float(lt.item())
+        dt, leaf_ms, seq_ms = (float(x) for x in tt.tolist())
 
     files_total = n * world * args.steps
     value = files_total / dt
     gbps = msg_bytes * world * args.steps / dt / 1e9
     leaf_s = leaf_ms / 1e3
     achieved_gbs = msg_bytes / leaf_s / 1e9 if leaf_s > 0 else None
-    traffic = load_traffic("C2")
+    traffic = load_traffic(args.workload)
+    valu_rate = comp / leaf_s if leaf_s > 0 else None
     roof = {
         "bound": "hbm", "kernel": "k_leaf_tree (leaf chunks + in-tile tree)",
         "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -207,11 +271,14 @@ def main():
         "leaf_ms": leaf_ms, "sequence_ms": seq_ms,
         "valu": {
             "compressions_per_launch": comp,
-            "achieved_compressions_per_s": comp / leaf_s if leaf_s > 0 else None,
-            "peak_compressions_per_s": VALU_PEAK_OPS / OPS_PER_COMPRESSION,
-            "frac": (comp / leaf_s) / (VALU_PEAK_OPS / OPS_PER_COMPRESSION) if leaf_s > 0 else None,
-            "note": "BLAKE3 is integer ARX: ~680 VALU ops per 64-byte compression; the VALU roof "
-                    "(7.4 TB/s of message bytes) sits just under the HBM roof",
+            "achieved_compressions_per_s": valu_rate,
+            "peak_compressions_per_s_spec": VALU_PEAK_OPS / OPS_PER_COMPRESSION,
+            "frac_of_spec": valu_rate / (VALU_PEAK_OPS / OPS_PER_COMPRESSION) if valu_rate else None,
+            "roof_compressions_per_s_measured": VALU_ROOF_MEASURED,
+            "frac_of_measured_roof": valu_rate / VALU_ROOF_MEASURED if valu_rate else None,
+            "note": "BLAKE3 is integer ARX (no MFMA): the kernel is VALU-bound, not HBM-bound. spec peak = "
+                    "680 ops/compression at the full VALU lane rate; measured roof = register-only "
+                    "compression loop on gfx950 (VOP3 v_alignbit/v_add3 issue at half rate)",
         },
     }
     if traffic:
@@ -221,21 +288,41 @@ def main():
         "metric": METRIC, "value": value, "unit": "files/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u32",
-        "data": "synthetic: C2 corpus generated in HBM (splitmix64 content per file, seed 0x5D0002)",
-        "config": {"workload": "C2: 1M files x Uniform{1..100 KiB}, whole-file cas_id (cas.rs:27-29)",
-                   "files_per_gpu": n, "message_bytes_per_gpu": msg_bytes, "chunks_per_gpu": chunks,
-                   "parallelism": f"files sharded over {world} GPU(s), no collective"},
+        "data": f"synthetic: {args.workload.upper()} corpus generated in HBM (splitmix64 content per file, "
+                f"include/sdcas_synth.h, spacedrive_amd/synth.py)",
+        "config": {"workload": W["desc"], "files_per_gpu": n, "message_bytes_per_gpu": msg_bytes,
+                   "chunks_per_gpu": chunks,
+                   "parallelism": f"files sharded over {world} GPU(s)" +
+                                  (", dedup: one RCCL all-to-all exchange" if W["dedup"] else ", no collective")},
         "blake3_gbps": gbps, "roofline": roof,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        gk = d_out[: args.cpu_sample].cpu().numpy().view(np.uint64)
-        base, parity = cpu_baseline(gk, min(args.cpu_sample, n), args.cpu_threads)
-        out["cpu_baseline"] = base
-        out["parity"] = parity
+    if dd is not None:
+        ms = torch.tensor([float(np.mean(dd["ms"]))], dtype=torch.float64, device=dev)
+        if distributed:
+            dist.all_reduce(ms, op=dist.ReduceOp.MAX)
+        _, created, linked = dd["last"]
+        out["dedup"] = {"ms_per_step": float(ms.item()), "objects_created": created, "files_linked": linked,
+                        "records_per_gpu": n}
+    if rank == 0 and world == 1:
+        gk = d_out.cpu().numpy().view(np.uint64)
+        if args.workload == "c2" and not args.no_cpu_baseline:
+            base, parity = cpu_baseline(gk, min(args.cpu_sample, n), args.cpu_threads)
+            out["cpu_baseline"] = base
+            out["parity"] = parity
+        else:
+            out["parity"] = sample_parity(gk, sizes, keys, 2000)
+        if dd is not None and args.workload == "c3":
+            from tests._oracle import load_oracle
+            link = dd["last"][0].cpu().numpy()
+            # the oracle walks ordinals 0..n-1 in chunks of 100: a contiguous
+            # share only (c5's strided share is checked by tests/test_dist_dedup.py)
+            want, wc, wl = load_oracle().identifier_dedup(gk, (sizes != 0).astype(np.uint8), None, 100)
+            out["parity"]["dedup"] = {"files": n, "link_mismatches": int((link != want).sum()),
+                                      "counts_match": (wc, wl) == (dd["last"][1], dd["last"][2])}
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()
-    if distributed:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
