@@ -127,6 +127,28 @@ int sdcas_dev_hash_messages(sdcas_ctx *ctx, const uint8_t *d_blob, const uint64_
                             void *stream);
 int sdcas_dev_sync(sdcas_ctx *ctx, void *stream);
 
+/* ---- device-resident big messages, streamed in pieces ------------------
+ *
+ * file_checksum (hash.rs:11-25) of messages too large to be resident at once
+ * (config C4: 1-4 GiB files, 256 GB): the caller delivers each message's
+ * bytes in any order as segments already in HBM; every full 1 MiB piece
+ * reduces to its level-10 BLAKE3 subtree node on the device, and finish
+ * merges each message's nodes into its root.
+ *   begin:  nfiles message lengths (host array), each > 1 MiB (smaller
+ *           messages go through sdcas_dev_hash_messages).
+ *   update: nseg segments (host arrays): bytes [h_msg_off[k], +h_len[k]) of
+ *           message h_file[k], resident at device address h_dev_addr[k]
+ *           (16-byte aligned, readable 64 B past the end). h_msg_off is a
+ *           multiple of 1 MiB; h_len is too unless the segment ends the
+ *           message. Every byte of every message exactly once over the
+ *           session. Enqueued on `stream`; the segments must stay resident
+ *           until the stream has passed this call. Use one stream per session.
+ *   finish: 32-byte digests to d_out32 (device, 32*nfiles), on `stream`. */
+int sdcas_dev_stream_begin(sdcas_ctx *ctx, const uint64_t *lens, size_t nfiles);
+int sdcas_dev_stream_update(sdcas_ctx *ctx, size_t nseg, const uint64_t *h_file, const uint64_t *h_msg_off,
+                            const uint64_t *h_len, const uint64_t *h_dev_addr, void *stream);
+int sdcas_dev_stream_finish(sdcas_ctx *ctx, uint8_t *d_out32, void *stream);
+
 /* ---- dedup / link (file_identifier/mod.rs:149-254) --------------------- */
 
 /* Canonical group-by of the identifier step over n orphan file_paths in id

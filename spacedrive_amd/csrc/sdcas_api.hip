@@ -100,6 +100,13 @@ struct sdcas_ctx {
   // multi-GPU dedup stages
   DistWs dist;
 
+  // device-resident big-message stream (sdcas_dev_stream_*)
+  std::vector<FileDesc> sm_files;
+  DevBuf<FileDesc> sm_d_files;
+  DevBuf<uint32_t> sm_nodes;
+  DevBuf<PieceDesc> sm_pieces;
+  bool sm_active = false;
+
   // profiling
   bool profile = false;
   std::vector<hipEvent_t> ev_free;
@@ -450,6 +457,9 @@ void sdcas_destroy(sdcas_ctx* c) {
   c->dd_link.release();
   c->dd_counts.release();
   c->dist.release();
+  c->sm_d_files.release();
+  c->sm_nodes.release();
+  c->sm_pieces.release();
   if (c->h_stage) (void)hipHostFree(c->h_stage);
   for (auto e : c->ev_free) (void)hipEventDestroy(e);
   for (auto& p : c->ev_leaf) (void)hipEventDestroy(p.first), (void)hipEventDestroy(p.second);
@@ -912,6 +922,98 @@ int sdcas_dev_dedup_apply(sdcas_ctx* c, const uint64_t* d_ids, const uint32_t* d
   hipError_t e = dd_apply(d_ids, d_slot, (uint32_t)n, d_result, chunk_size ? chunk_size : SDCAS_IDENTIFIER_CHUNK_SIZE,
                           d_link, (unsigned long long*)d_counts, st);
   return e ? c->hip_fail(e, "dedup_apply") : SDCAS_OK;
+}
+
+// ---- device-resident big-message stream (C4, file_checksum of huge files) --------
+
+int sdcas_dev_stream_begin(sdcas_ctx* c, const uint64_t* lens, size_t nfiles) {
+  if (!c || (nfiles && !lens)) return SDCAS_E_INVALID;
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipSetDevice(c->device);
+  c->sm_files.assign(nfiles, FileDesc{});
+  uint64_t nodes = 0;
+  for (size_t i = 0; i < nfiles; ++i) {
+    const uint64_t C = chunks_of(lens[i]);
+    if (C <= kTile) return c->fail(SDCAS_E_INVALID, "stream message %zu: %llu bytes (must exceed 1 MiB)", i,
+                                   (unsigned long long)lens[i]);
+    c->sm_files[i].C = C;
+    c->sm_files[i].node_base = nodes;
+    c->sm_files[i].out_index = i;
+    nodes += bigfile_node_count(C);
+  }
+  hipError_t e;
+  if ((e = c->sm_nodes.ensure(8 * nodes + 8)) || (e = c->sm_d_files.ensure(nfiles + 1)))
+    return c->hip_fail(e, "stream workspace");
+  if (nfiles && (e = hipMemcpy(c->sm_d_files.p, c->sm_files.data(), sizeof(FileDesc) * nfiles,
+                               hipMemcpyHostToDevice)))
+    return c->hip_fail(e, "stream descs");
+  c->sm_active = true;
+  return SDCAS_OK;
+}
+
+int sdcas_dev_stream_update(sdcas_ctx* c, size_t nseg, const uint64_t* h_file, const uint64_t* h_msg_off,
+                            const uint64_t* h_len, const uint64_t* h_dev_addr, void* stream) {
+  if (!c || (nseg && (!h_file || !h_msg_off || !h_len || !h_dev_addr))) return SDCAS_E_INVALID;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->sm_active) return c->fail(SDCAS_E_INVALID, "stream_update without stream_begin");
+  (void)hipSetDevice(c->device);
+  const uint64_t piece_bytes = 1024ull * kTile;
+  uint64_t base = ~0ull;
+  for (size_t k = 0; k < nseg; ++k) base = std::min(base, h_dev_addr[k]);
+  std::vector<PieceDesc> pieces;
+  for (size_t k = 0; k < nseg; ++k) {
+    if (h_file[k] >= c->sm_files.size()) return c->fail(SDCAS_E_INVALID, "segment %zu: no such message", k);
+    const FileDesc& fd = c->sm_files[h_file[k]];
+    const uint64_t mlen = fd.C * 1024;  // upper bound; the last chunk may be short
+    const uint64_t off = h_msg_off[k], len = h_len[k];
+    if ((off % piece_bytes) || (h_dev_addr[k] & 15) || !len || off + len > mlen ||
+        ((len % piece_bytes) && chunks_of(off + len) != fd.C))
+      return c->fail(SDCAS_E_INVALID, "segment %zu: offset/length not on 1 MiB pieces", k);
+    for (uint64_t o = 0; o < len; o += piece_bytes) {
+      PieceDesc pd{};
+      pd.off = h_dev_addr[k] - base + o;
+      pd.j0 = (off + o) / 1024;
+      pd.node_base = fd.node_base;
+      pd.len = (uint32_t)std::min<uint64_t>(piece_bytes, len - o);
+      pieces.push_back(pd);
+    }
+  }
+  if (pieces.empty()) return SDCAS_OK;
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  hipError_t e;
+  if ((e = c->sm_pieces.ensure(pieces.size()))) return c->hip_fail(e, "piece descs");
+  // stream-ordered: a previous update's kernel on `st` has finished reading
+  // the descriptor buffer before this copy lands
+  if ((e = hipMemcpyAsync(c->sm_pieces.p, pieces.data(), sizeof(PieceDesc) * pieces.size(), hipMemcpyHostToDevice,
+                          st)) ||
+      (e = hipStreamSynchronize(st)))
+    return c->hip_fail(e, "H2D piece descs");
+  hipEvent_t a = nullptr, b = nullptr;
+  if (c->profile) {
+    a = c->event();
+    b = c->event();
+    (void)hipEventRecord(a, st);
+  }
+  e = piece_hash(reinterpret_cast<const uint8_t*>(base), c->sm_pieces.p, (uint32_t)pieces.size(), c->sm_nodes.p, st);
+  if (c->profile) {
+    (void)hipEventRecord(b, st);
+    c->ev_leaf.push_back({a, b});
+    c->ev_all.push_back({c->event(), c->event()});
+    (void)hipEventRecord(c->ev_all.back().first, st);
+    (void)hipEventRecord(c->ev_all.back().second, st);
+  }
+  return e ? c->hip_fail(e, "piece_hash") : SDCAS_OK;
+}
+
+int sdcas_dev_stream_finish(sdcas_ctx* c, uint8_t* d_out32, void* stream) {
+  if (!c || !d_out32) return SDCAS_E_INVALID;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->sm_active) return c->fail(SDCAS_E_INVALID, "stream_finish without stream_begin");
+  (void)hipSetDevice(c->device);
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  c->sm_active = false;
+  hipError_t e = bigfile_finish(c->sm_d_files.p, (uint32_t)c->sm_files.size(), c->sm_nodes.p, d_out32, st);
+  return e ? c->hip_fail(e, "bigfile_finish") : SDCAS_OK;
 }
 
 }  // extern "C"

@@ -188,6 +188,19 @@ class Engine:
         self._check(self.L.sdcas_dev_dedup(self.ctx, keys, has_key, status or None, int(n), chunk_size,
                                            out_link, counts or None, stream or None), "dev_dedup")
 
+    def dev_stream_begin(self, lens):
+        """device-resident big-message session (sdcas_dev_stream_*): lens > 1 MiB each"""
+        lens = _arr(lens, np.uint64)
+        self._check(self.L.sdcas_dev_stream_begin(self.ctx, _ptr(lens), lens.size), "dev_stream_begin")
+
+    def dev_stream_update(self, files, msg_offs, lens, dev_addrs, stream=0):
+        f, o, l, a = (_arr(x, np.uint64) for x in (files, msg_offs, lens, dev_addrs))
+        self._check(self.L.sdcas_dev_stream_update(self.ctx, f.size, _ptr(f), _ptr(o), _ptr(l), _ptr(a),
+                                                   stream or None), "dev_stream_update")
+
+    def dev_stream_finish(self, out32, stream=0):
+        self._check(self.L.sdcas_dev_stream_finish(self.ctx, out32, stream or None), "dev_stream_finish")
+
     def dev_profile(self, enable=True):
         self._check(self.L.sdcas_dev_profile(self.ctx, 1 if enable else 0), "dev_profile")
 
