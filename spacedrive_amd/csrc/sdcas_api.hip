@@ -63,6 +63,26 @@ struct DevBuf {
   }
 };
 
+// One pinned staging slot: message bytes, per-message metadata and results,
+// their device twins, and the event that fences the slot's GPU work.
+struct Slot {
+  uint8_t* h = nullptr;   // pinned message bytes
+  size_t h_cap = 0;
+  uint64_t* hm = nullptr;  // pinned: offs[cap_n] | lens[cap_n] | results (32 B per message)
+  size_t cap_n = 0;
+  DevBuf<uint8_t> d_blob;
+  DevBuf<uint64_t> d_meta;  // offs | lens (or piece descriptors)
+  DevBuf<uint8_t> d_res;
+  hipEvent_t ev = nullptr;
+  bool busy = false, res32 = false;
+  size_t n = 0;
+  uint64_t used = 0, chunks = 0;
+  std::vector<size_t> idx;  // caller index of message k
+  uint64_t* offs() { return hm; }
+  uint64_t* lens() { return hm + cap_n; }
+  uint8_t* res() { return reinterpret_cast<uint8_t*>(hm + 2 * cap_n); }
+};
+
 }  // namespace
 
 struct sdcas_ctx {
@@ -79,14 +99,10 @@ struct sdcas_ctx {
   DevBuf<uint8_t> ws_scan;
 
   // host-API device buffers
-  DevBuf<uint8_t> d_blob;
-  DevBuf<uint64_t> d_offs, d_lens, d_keys;
   DevBuf<uint8_t> d_out32;
-  DevBuf<PieceDesc> d_pieces;
   DevBuf<FileDesc> d_files;
   DevBuf<uint32_t> d_file_nodes;
-  uint8_t* h_stage = nullptr;
-  size_t h_stage_cap = 0;
+  Slot slots[2];  // double-buffered pinned staging (host fills one, GPU hashes the other)
 
   // dedup
   DedupWorkspace dws;
@@ -160,17 +176,6 @@ int reserve_ws(sdcas_ctx* c, size_t max_msgs, uint64_t max_chunks) {
   return SDCAS_OK;
 }
 
-int ensure_stage(sdcas_ctx* c, size_t bytes) {
-  if (bytes <= c->h_stage_cap) return SDCAS_OK;
-  if (c->h_stage) (void)hipHostFree(c->h_stage);
-  c->h_stage = nullptr;
-  c->h_stage_cap = 0;
-  hipError_t e = hipHostMalloc(&c->h_stage, bytes, hipHostMallocDefault);
-  if (e) return c->hip_fail(e, "pinned staging");
-  c->h_stage_cap = bytes;
-  return SDCAS_OK;
-}
-
 // Enqueue the hash of n device messages (the one launch sequence every API
 // ends in), with optional HIP-event profiling of the leaf kernel.
 int launch_batch(sdcas_ctx* c, const uint8_t* blob, const uint64_t* offs, const uint64_t* lens, uint32_t n,
@@ -190,39 +195,111 @@ int launch_batch(sdcas_ctx* c, const uint8_t* blob, const uint64_t* offs, const 
   return SDCAS_OK;
 }
 
-// Hash messages already packed in c->h_stage at 16-aligned offsets; results
-// to host arrays (out32 and/or keys, indexed from 0).
-int run_staged(sdcas_ctx* c, const std::vector<uint64_t>& offs, const std::vector<uint64_t>& lens,
-               uint64_t stage_bytes, uint64_t chunks, uint8_t* out32, uint64_t* keys) {
-  const uint32_t n = (uint32_t)offs.size();
-  if (!n) return SDCAS_OK;
-  int rc;
-  if ((rc = reserve_ws(c, std::max<size_t>(n, c->ws.cap_msgs), std::max<uint64_t>(chunks, c->ws.cap_chunks))))
-    return rc;
+// ---- double-buffered pinned staging ------------------------------------------
+//
+// Host work (file reads, or copies out of the caller's buffer) fills one
+// pinned slot while the GPU copies and hashes the other: each slot's H2D,
+// kernels and D2H are enqueued on the context stream and fenced by the slot's
+// event, which is waited for only when the slot is about to be refilled.
+
+int slot_prepare(sdcas_ctx* c, Slot& s, uint64_t bytes, size_t n) {
   hipError_t e;
-  if ((e = c->d_blob.ensure(stage_bytes + kSlack))) return c->hip_fail(e, "device blob");
-  if ((e = c->d_offs.ensure(n)) || (e = c->d_lens.ensure(n))) return c->hip_fail(e, "device offsets");
-  if (out32 && (e = c->d_out32.ensure(32ull * n))) return c->hip_fail(e, "device digests");
-  if (keys && (e = c->d_keys.ensure(n))) return c->hip_fail(e, "device keys");
-  hipStream_t st = c->stream;
-  if ((e = hipMemcpyAsync(c->d_blob.p, c->h_stage, stage_bytes, hipMemcpyHostToDevice, st)) ||
-      (e = hipMemcpyAsync(c->d_offs.p, offs.data(), 8ull * n, hipMemcpyHostToDevice, st)) ||
-      (e = hipMemcpyAsync(c->d_lens.p, lens.data(), 8ull * n, hipMemcpyHostToDevice, st)))
-    return c->hip_fail(e, "H2D");
-  if ((rc = launch_batch(c, c->d_blob.p, c->d_offs.p, c->d_lens.p, n, out32 ? c->d_out32.p : nullptr,
-                         keys ? c->d_keys.p : nullptr, st)))
-    return rc;
-  if (out32 && (e = hipMemcpyAsync(out32, c->d_out32.p, 32ull * n, hipMemcpyDeviceToHost, st)))
-    return c->hip_fail(e, "D2H digests");
-  if (keys && (e = hipMemcpyAsync(keys, c->d_keys.p, 8ull * n, hipMemcpyDeviceToHost, st)))
-    return c->hip_fail(e, "D2H keys");
-  if ((e = hipStreamSynchronize(st))) return c->hip_fail(e, "sync");
+  if (bytes + kSlack > s.h_cap) {
+    if (s.h) (void)hipHostFree(s.h);
+    s.h = nullptr;
+    s.h_cap = 0;
+    if ((e = hipHostMalloc(&s.h, bytes + kSlack, hipHostMallocDefault))) return c->hip_fail(e, "pinned staging");
+    s.h_cap = bytes + kSlack;
+  }
+  if (n > s.cap_n) {
+    if (s.hm) (void)hipHostFree(s.hm);
+    s.hm = nullptr;
+    s.cap_n = 0;
+    const size_t want = std::max<size_t>(n, 1024);
+    // offs[cap_n] | lens[cap_n] | results (32 B per message)
+    if ((e = hipHostMalloc(&s.hm, 48 * want, hipHostMallocDefault))) return c->hip_fail(e, "pinned metadata");
+    s.cap_n = want;
+  }
+  if ((e = s.d_blob.ensure(s.h_cap)) || (e = s.d_meta.ensure(2 * s.cap_n)) || (e = s.d_res.ensure(32 * s.cap_n)))
+    return c->hip_fail(e, "device staging");
+  if (!s.ev && (e = hipEventCreateWithFlags(&s.ev, hipEventDisableTiming))) return c->hip_fail(e, "event");
   return SDCAS_OK;
 }
 
-// Big messages (> 1 MiB) from host memory: stream 1 MiB pieces through the
-// staging buffer; `fill(dst, off, len)` provides message bytes [off, off+len)
-// and returns a status (0 ok). Digests go to out32[k] for message k.
+void slot_release(Slot& s) {
+  if (s.h) (void)hipHostFree(s.h);
+  if (s.hm) (void)hipHostFree(s.hm);
+  s.h = nullptr;
+  s.hm = nullptr;
+  s.h_cap = s.cap_n = 0;
+  s.d_blob.release();
+  s.d_meta.release();
+  s.d_res.release();
+  if (s.ev) (void)hipEventDestroy(s.ev);
+  s.ev = nullptr;
+}
+
+// Both slots sized for `cap` staging bytes, and the kernel workspace for the
+// largest batch such a slot can hold, so that no buffer is reallocated while
+// the other slot's work is in flight.
+int slots_prepare(sdcas_ctx* c, uint64_t cap, size_t cap_n) {
+  int rc;
+  for (Slot& s : c->slots)
+    if ((rc = slot_prepare(c, s, cap, cap_n))) return rc;
+  if (cap_n > c->ws.cap_msgs || cap / 1024 + cap_n > c->ws.cap_chunks) {
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e) return c->hip_fail(e, "sync");
+    return reserve_ws(c, std::max<size_t>(cap_n, c->ws.cap_msgs),
+                      std::max<uint64_t>(cap / 1024 + cap_n, c->ws.cap_chunks));
+  }
+  return SDCAS_OK;
+}
+
+// Enqueue the slot's batch: s.n messages at s.offs()/s.lens() in s.h (s.used
+// bytes, s.chunks chunks); results land in s.res() (digests if res32, else
+// cas keys) once s.ev has fired.
+int slot_submit(sdcas_ctx* c, Slot& s, bool res32) {
+  s.res32 = res32;
+  if (!s.n) return SDCAS_OK;
+  int rc;
+  hipStream_t st = c->stream;
+  hipError_t e;
+  if (s.n > c->ws.cap_msgs || s.chunks > c->ws.cap_chunks) {
+    // growing the kernel workspace frees buffers the other slot's kernels may
+    // still be using: drain the stream first (rare: slots are pre-reserved)
+    if ((e = hipStreamSynchronize(st))) return c->hip_fail(e, "sync");
+    if ((rc = reserve_ws(c, std::max<size_t>(s.n, c->ws.cap_msgs), std::max<uint64_t>(s.chunks, c->ws.cap_chunks))))
+      return rc;
+  }
+  if ((e = hipMemcpyAsync(s.d_blob.p, s.h, s.used, hipMemcpyHostToDevice, st)) ||
+      (e = hipMemcpyAsync(s.d_meta.p, s.hm, 8 * s.n, hipMemcpyHostToDevice, st)) ||
+      (e = hipMemcpyAsync(s.d_meta.p + s.cap_n, s.hm + s.cap_n, 8 * s.n, hipMemcpyHostToDevice, st)))
+    return c->hip_fail(e, "H2D");
+  if ((rc = launch_batch(c, s.d_blob.p, s.d_meta.p, s.d_meta.p + s.cap_n, (uint32_t)s.n, res32 ? s.d_res.p : nullptr,
+                         res32 ? nullptr : reinterpret_cast<uint64_t*>(s.d_res.p), st)))
+    return rc;
+  if ((e = hipMemcpyAsync(s.res(), s.d_res.p, (res32 ? 32 : 8) * s.n, hipMemcpyDeviceToHost, st)) ||
+      (e = hipEventRecord(s.ev, st)))
+    return c->hip_fail(e, "D2H");
+  s.busy = true;
+  return SDCAS_OK;
+}
+
+// Wait for the slot's batch and hand message k's result to sink(k, ptr).
+template <class Sink>
+int slot_complete(sdcas_ctx* c, Slot& s, Sink sink) {
+  if (!s.busy) return SDCAS_OK;
+  s.busy = false;
+  hipError_t e = hipEventSynchronize(s.ev);
+  if (e) return c->hip_fail(e, "batch");
+  for (size_t k = 0; k < s.n; ++k) sink(k, s.res() + (s.res32 ? 32 : 8) * k);
+  return SDCAS_OK;
+}
+
+// Big messages (> 1 MiB) from host memory: 1 MiB pieces streamed through the
+// two staging slots (one window filled by `fill` while the GPU hashes the
+// other); `fill(k, dst, off, len)` provides bytes [off, off+len) of item k
+// and returns a status (0 ok). Digests go to out32_host[32 * out_index].
 struct BigItem {
   uint64_t len;
   uint64_t out_index;
@@ -235,8 +312,9 @@ int run_big(sdcas_ctx* c, const std::vector<BigItem>& items, uint8_t* out32_host
   int rc;
   const uint64_t piece_bytes = 1024ull * kTile;
   const uint64_t window = std::max<uint64_t>(piece_bytes, (c->staging_bytes / piece_bytes) * piece_bytes);
-  if ((rc = ensure_stage(c, window + kSlack))) return rc;
-  if ((e = c->d_blob.ensure(window + kSlack))) return c->hip_fail(e, "device blob");
+  const size_t max_pieces = (size_t)(window / piece_bytes);
+  for (Slot& s : c->slots)
+    if ((rc = slot_prepare(c, s, window, 2 * max_pieces))) return rc;
   std::vector<FileDesc> files(items.size());
   uint64_t nodes = 0;
   for (size_t i = 0; i < items.size(); ++i) {
@@ -248,32 +326,42 @@ int run_big(sdcas_ctx* c, const std::vector<BigItem>& items, uint8_t* out32_host
   if ((e = c->d_file_nodes.ensure(8 * nodes + 8))) return c->hip_fail(e, "file nodes");
   if ((e = c->d_files.ensure(items.size()))) return c->hip_fail(e, "file descs");
   if ((e = c->d_out32.ensure(32 * items.size()))) return c->hip_fail(e, "device digests");
-  const uint32_t max_pieces = (uint32_t)(window / piece_bytes);
-  if ((e = c->d_pieces.ensure(max_pieces))) return c->hip_fail(e, "piece descs");
   hipStream_t st = c->stream;
-  std::vector<PieceDesc> pieces;
+  int cur = 0;
+  size_t npieces = 0;
   uint64_t used = 0;
-  auto flush = [&]() -> int {
-    if (pieces.empty()) return SDCAS_OK;
-    hipError_t ee;
-    if ((ee = hipMemcpyAsync(c->d_blob.p, c->h_stage, used, hipMemcpyHostToDevice, st)) ||
-        (ee = hipMemcpyAsync(c->d_pieces.p, pieces.data(), sizeof(PieceDesc) * pieces.size(),
-                             hipMemcpyHostToDevice, st)))
-      return c->hip_fail(ee, "H2D pieces");
-    if ((ee = piece_hash(c->d_blob.p, c->d_pieces.p, (uint32_t)pieces.size(), c->d_file_nodes.p, st)))
-      return c->hip_fail(ee, "piece_hash");
-    // the staging buffer is reused by the next window
-    if ((ee = hipStreamSynchronize(st))) return c->hip_fail(ee, "sync");
-    pieces.clear();
-    used = 0;
-    return SDCAS_OK;
+  auto wait_slot = [&](Slot& s) -> int {
+    if (!s.busy) return SDCAS_OK;
+    s.busy = false;
+    hipError_t ee = hipEventSynchronize(s.ev);
+    return ee ? c->hip_fail(ee, "piece window") : SDCAS_OK;
   };
+  auto flush = [&]() -> int {
+    if (!npieces) return SDCAS_OK;
+    Slot& s = c->slots[cur];
+    PieceDesc* hp = reinterpret_cast<PieceDesc*>(s.hm);
+    PieceDesc* dp = reinterpret_cast<PieceDesc*>(s.d_meta.p);
+    hipError_t ee;
+    if ((ee = hipMemcpyAsync(s.d_blob.p, s.h, used, hipMemcpyHostToDevice, st)) ||
+        (ee = hipMemcpyAsync(dp, hp, sizeof(PieceDesc) * npieces, hipMemcpyHostToDevice, st)))
+      return c->hip_fail(ee, "H2D pieces");
+    if ((ee = piece_hash(s.d_blob.p, dp, (uint32_t)npieces, c->d_file_nodes.p, st)))
+      return c->hip_fail(ee, "piece_hash");
+    if ((ee = hipEventRecord(s.ev, st))) return c->hip_fail(ee, "event");
+    s.busy = true;
+    cur ^= 1;
+    npieces = 0;
+    used = 0;
+    return wait_slot(c->slots[cur]);  // the next window's buffers are free again
+  };
+  if ((rc = wait_slot(c->slots[cur]))) return rc;
   for (size_t i = 0; i < items.size(); ++i) {
     const uint64_t len = items[i].len;
     for (uint64_t off = 0; off < len; off += piece_bytes) {
       const uint32_t pl = (uint32_t)std::min<uint64_t>(piece_bytes, len - off);
       if (used + pl > window && (rc = flush())) return rc;
-      int st_i = fill(i, c->h_stage + used, off, pl);
+      Slot& s = c->slots[cur];
+      int st_i = fill(i, s.h + used, off, pl);
       if (st_i) {
         if (status) status[items[i].out_index] = st_i;
         break;
@@ -283,11 +371,13 @@ int run_big(sdcas_ctx* c, const std::vector<BigItem>& items, uint8_t* out32_host
       pd.j0 = off / 1024;
       pd.node_base = files[i].node_base;
       pd.len = pl;
-      pieces.push_back(pd);
+      reinterpret_cast<PieceDesc*>(s.hm)[npieces++] = pd;
       used += align16(pl);
     }
   }
   if ((rc = flush())) return rc;
+  for (Slot& s : c->slots)
+    if ((rc = wait_slot(s))) return rc;
   if ((e = hipMemcpyAsync(c->d_files.p, files.data(), sizeof(FileDesc) * files.size(), hipMemcpyHostToDevice,
                           st)))
     return c->hip_fail(e, "H2D files");
@@ -300,6 +390,7 @@ int run_big(sdcas_ctx* c, const std::vector<BigItem>& items, uint8_t* out32_host
   for (size_t i = 0; i < items.size(); ++i) memcpy(out32_host + 32 * items[i].out_index, &tmp[32 * i], 32);
   return SDCAS_OK;
 }
+
 
 // ---- file I/O with the reference's read pattern ---------------------------
 
@@ -444,14 +535,13 @@ void sdcas_destroy(sdcas_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (auto* b : {&c->ws_S, &c->ws_total, &c->d_offs, &c->d_lens, &c->d_keys, &c->dd_key_a, &c->dd_key_b,
+  for (auto* b : {&c->ws_S, &c->ws_total, &c->dd_key_a, &c->dd_key_b,
                   &c->dd_keys, &c->dd_ekeys, &c->dd_ekeys_sorted})
     b->release();
   for (auto* b : {&c->ws_tile_first, &c->ws_nodes, &c->d_file_nodes, &c->dd_idx_a, &c->dd_idx_b, &c->dd_head,
                   &c->dd_nvalid, &c->dd_eidx})
     b->release();
-  for (auto* b : {&c->ws_scan, &c->d_blob, &c->d_out32, &c->dd_valid, &c->dd_temp, &c->dd_has}) b->release();
-  c->d_pieces.release();
+  for (auto* b : {&c->ws_scan, &c->d_out32, &c->dd_valid, &c->dd_temp, &c->dd_has}) b->release();
   c->d_files.release();
   c->dd_status.release();
   c->dd_link.release();
@@ -460,7 +550,7 @@ void sdcas_destroy(sdcas_ctx* c) {
   c->sm_d_files.release();
   c->sm_nodes.release();
   c->sm_pieces.release();
-  if (c->h_stage) (void)hipHostFree(c->h_stage);
+  for (Slot& s : c->slots) slot_release(s);
   for (auto e : c->ev_free) (void)hipEventDestroy(e);
   for (auto& p : c->ev_leaf) (void)hipEventDestroy(p.first), (void)hipEventDestroy(p.second);
   for (auto& p : c->ev_all) (void)hipEventDestroy(p.first), (void)hipEventDestroy(p.second);
@@ -558,42 +648,60 @@ static int hash_host_messages(sdcas_ctx* c, const uint8_t* blob, const uint64_t*
   (void)hipSetDevice(c->device);
   const uint64_t big_cut = 1024ull * kTile;  // > 1 MiB: piece path
   const uint64_t cap = c->staging_bytes;
+  const size_t cap_n = (size_t)(cap / 128) + 1;
   int rc;
-  if ((rc = ensure_stage(c, cap + kSlack))) return rc;
-  std::vector<uint64_t> offs, ls;
-  std::vector<size_t> idx;
+  if ((rc = slots_prepare(c, cap, cap_n))) return rc;
   std::vector<BigItem> big;
-  uint64_t used = 0, chunks = 0;
-  std::vector<uint8_t> tmp32;
-  auto flush = [&]() -> int {
-    if (offs.empty()) return SDCAS_OK;
-    tmp32.resize(32 * offs.size());
-    std::vector<uint64_t> tk(keys ? offs.size() : 0);
-    int r = run_staged(c, offs, ls, used, chunks, out32 ? tmp32.data() : nullptr, keys ? tk.data() : nullptr);
-    if (r) return r;
-    for (size_t k = 0; k < idx.size(); ++k) {
-      if (out32) memcpy(out32 + 32 * idx[k], &tmp32[32 * k], 32);
-      if (keys) keys[idx[k]] = tk[k];
-    }
-    offs.clear(), ls.clear(), idx.clear();
-    used = chunks = 0;
-    return SDCAS_OK;
+  int cur = 0;
+  auto begin = [&](Slot& s) -> int {
+    const int r = slot_complete(c, s, [&](size_t k, const uint8_t* res) {
+      const size_t i = s.idx[k];
+      if (out32) memcpy(out32 + 32 * i, res, 32);
+      if (keys) {
+        uint64_t kk = 0;
+        if (s.res32)
+          for (int t = 0; t < 8; ++t) kk = (kk << 8) | res[t];
+        else
+          memcpy(&kk, res, 8);
+        keys[i] = kk;
+      }
+    });
+    s.n = 0, s.used = 0, s.chunks = 0;
+    s.idx.clear();
+    return r;
   };
+  // the copy into pinned staging is the host-side cost of this path: it runs
+  // on the I/O threads, one slot at a time, while the GPU hashes the other
+  auto fill_submit = [&](Slot& s) -> int {
+    parallel_for(c->io_threads, s.n, [&](size_t k) {
+      memcpy(s.h + s.offs()[k], blob + offsets[s.idx[k]], s.lens()[k]);
+    });
+    return slot_submit(c, s, out32 != nullptr);
+  };
+  if ((rc = begin(c->slots[cur]))) return rc;
   for (size_t i = 0; i < n; ++i) {
     const uint64_t L = lens[i];
     if (L > big_cut) {
       big.push_back({L, i});
       continue;
     }
-    if (used + align16(L) > cap && (rc = flush())) return rc;
-    memcpy(c->h_stage + used, blob + offsets[i], L);
-    offs.push_back(used);
-    ls.push_back(L);
-    idx.push_back(i);
-    used += align16(L);
-    chunks += chunks_of(L);
+    Slot* s = &c->slots[cur];
+    if (s->used + align16(L) > cap || s->n == cap_n) {
+      if ((rc = fill_submit(*s))) return rc;
+      cur ^= 1;
+      s = &c->slots[cur];
+      if ((rc = begin(*s))) return rc;
+    }
+    s->offs()[s->n] = s->used;
+    s->lens()[s->n] = L;
+    s->idx.push_back(i);
+    s->n++;
+    s->used += align16(L);
+    s->chunks += chunks_of(L);
   }
-  if ((rc = flush())) return rc;
+  if ((rc = fill_submit(c->slots[cur]))) return rc;
+  for (Slot& s : c->slots)
+    if ((rc = begin(s))) return rc;
   if (!big.empty()) {
     std::vector<uint8_t> d32(32 * n);
     rc = run_big(c, big, d32.data(),
@@ -633,45 +741,47 @@ int sdcas_cas_ids(sdcas_ctx* c, const char* const* paths, const uint64_t* sizes,
   std::lock_guard<std::mutex> g(c->mu);
   (void)hipSetDevice(c->device);
   const uint64_t cap = c->staging_bytes;
+  const size_t cap_n = (size_t)(cap / 128) + 1;
   int rc;
-  if ((rc = ensure_stage(c, cap + kSlack))) return rc;
+  if ((rc = slots_prepare(c, cap, cap_n))) return rc;
   // slot sizes: the message the indexer's size predicts (cas.rs:27); a file
   // that grew is retried in a later batch with its actual size
   std::vector<uint64_t> want(n);
   for (size_t i = 0; i < n; ++i) want[i] = sdcas_cas_message_len(sizes[i]);
   std::vector<size_t> todo(n);
   for (size_t i = 0; i < n; ++i) todo[i] = i;
+  int cur = 0;
+  auto drain = [&](Slot& s) -> int {
+    return slot_complete(c, s, [&](size_t k, const uint8_t* r) { memcpy(&out_keys[s.idx[k]], r, 8); });
+  };
   for (int round = 0; round < 4 && !todo.empty(); ++round) {
     std::vector<size_t> retry;
     size_t p = 0;
     while (p < todo.size()) {
-      // batch [p, q) fitting the staging buffer
+      // batch [p, q) fitting one staging slot (a message larger than the slot
+      // — a whole-file cas message of a file grown past it — gets its own)
+      Slot& s = c->slots[cur];
+      if ((rc = drain(s))) return rc;
       std::vector<uint64_t> slot_off;
       uint64_t used = 0;
       size_t q = p;
-      while (q < todo.size()) {
+      while (q < todo.size() && q - p < cap_n) {
         const uint64_t need = align16(want[todo[q]]);
-        if (need > cap) {
-          // a single message beyond staging: only a whole-file cas message of
-          // a file grown past staging size; give it its own staging round
-          if ((rc = ensure_stage(c, need + kSlack))) return rc;
-        }
-        if (q > p && used + need > std::max<uint64_t>(cap, c->h_stage_cap - kSlack)) break;
+        if (q > p && used + need > cap) break;
         slot_off.push_back(used);
         used += need;
         ++q;
       }
+      if ((rc = slot_prepare(c, s, std::max<uint64_t>(used, cap), cap_n))) return rc;
       const size_t m = q - p;
       std::vector<uint64_t> mlen(m), retry_len(m);
       std::vector<int32_t> st(m);
       parallel_for(c->io_threads, m, [&](size_t k) {
         const size_t i = todo[p + k];
-        st[k] = read_cas_message(paths[i], sizes[i], c->h_stage + slot_off[k], align16(want[i]), &mlen[k],
-                                 &retry_len[k]);
+        st[k] = read_cas_message(paths[i], sizes[i], s.h + slot_off[k], align16(want[i]), &mlen[k], &retry_len[k]);
       });
-      std::vector<uint64_t> offs, ls;
-      std::vector<size_t> idx;
-      uint64_t chunks = 0;
+      s.n = 0, s.chunks = 0, s.used = used;
+      s.idx.clear();
       for (size_t k = 0; k < m; ++k) {
         const size_t i = todo[p + k];
         if (retry_len[k] && !st[k]) {
@@ -681,16 +791,18 @@ int sdcas_cas_ids(sdcas_ctx* c, const char* const* paths, const uint64_t* sizes,
         }
         out_status[i] = st[k];
         if (st[k]) continue;
-        offs.push_back(slot_off[k]);
-        ls.push_back(mlen[k]);
-        idx.push_back(i);
-        chunks += chunks_of(mlen[k]);
+        s.offs()[s.n] = slot_off[k];
+        s.lens()[s.n] = mlen[k];
+        s.idx.push_back(i);
+        s.n++;
+        s.chunks += chunks_of(mlen[k]);
       }
-      std::vector<uint64_t> tk(offs.size());
-      if ((rc = run_staged(c, offs, ls, used, chunks, nullptr, tk.data()))) return rc;
-      for (size_t k = 0; k < idx.size(); ++k) out_keys[idx[k]] = tk[k];
+      if ((rc = slot_submit(c, s, false))) return rc;
+      cur ^= 1;
       p = q;
     }
+    for (Slot& s : c->slots)
+      if ((rc = drain(s))) return rc;
     todo.swap(retry);
   }
   for (size_t i : todo) out_status[i] = EAGAIN;  // kept growing while being read
@@ -702,8 +814,9 @@ int sdcas_checksums(sdcas_ctx* c, const char* const* paths, size_t n, uint8_t* o
   std::lock_guard<std::mutex> g(c->mu);
   (void)hipSetDevice(c->device);
   const uint64_t cap = c->staging_bytes, big_cut = 1024ull * kTile;
+  const size_t cap_n = (size_t)(cap / 128) + 1;
   int rc;
-  if ((rc = ensure_stage(c, cap + kSlack))) return rc;
+  if ((rc = slots_prepare(c, cap, cap_n))) return rc;
   // file lengths first (hash.rs reads to EOF; a regular file's EOF is its length)
   std::vector<uint64_t> flen(n);
   std::vector<int32_t> fst(n);
@@ -721,12 +834,18 @@ int sdcas_checksums(sdcas_ctx* c, const char* const* paths, size_t n, uint8_t* o
     if (flen[i] > big_cut) big.push_back({flen[i], i});
     else small.push_back(i);
   }
+  int cur = 0;
+  auto drain = [&](Slot& s) -> int {
+    return slot_complete(c, s, [&](size_t k, const uint8_t* r) { memcpy(out32 + 32 * s.idx[k], r, 32); });
+  };
   size_t p = 0;
   while (p < small.size()) {
+    Slot& s = c->slots[cur];
+    if ((rc = drain(s))) return rc;
     std::vector<uint64_t> slot;
     uint64_t used = 0;
     size_t q = p;
-    while (q < small.size() && (q == p || used + align16(flen[small[q]]) <= cap)) {
+    while (q < small.size() && q - p < cap_n && (q == p || used + align16(flen[small[q]]) <= cap)) {
       slot.push_back(used);
       used += align16(flen[small[q]]);
       ++q;
@@ -742,33 +861,37 @@ int sdcas_checksums(sdcas_ctx* c, const char* const* paths, size_t n, uint8_t* o
         return;
       }
       bool over = false;
-      st[k] = read_whole(fd, c->h_stage + slot[k], flen[i], &got[k], &over);
+      st[k] = read_whole(fd, s.h + slot[k], flen[i], &got[k], &over);
       close(fd);
     });
-    std::vector<uint64_t> offs, ls;
-    std::vector<size_t> idx;
-    uint64_t chunks = 0;
+    s.n = 0, s.chunks = 0, s.used = used;
+    s.idx.clear();
     for (size_t k = 0; k < m; ++k) {
       const size_t i = small[p + k];
       out_status[i] = st[k];
       if (st[k]) continue;
-      offs.push_back(slot[k]);
-      ls.push_back(got[k]);
-      idx.push_back(i);
-      chunks += chunks_of(got[k]);
+      s.offs()[s.n] = slot[k];
+      s.lens()[s.n] = got[k];
+      s.idx.push_back(i);
+      s.n++;
+      s.chunks += chunks_of(got[k]);
     }
-    std::vector<uint8_t> d32(32 * offs.size());
-    if ((rc = run_staged(c, offs, ls, used, chunks, d32.data(), nullptr))) return rc;
-    for (size_t k = 0; k < idx.size(); ++k) memcpy(out32 + 32 * idx[k], &d32[32 * k], 32);
+    if ((rc = slot_submit(c, s, true))) return rc;
+    cur ^= 1;
     p = q;
   }
+  for (Slot& s : c->slots)
+    if ((rc = drain(s))) return rc;
   if (!big.empty()) {
-    std::vector<int> fds(big.size(), -1);
-    for (size_t k = 0; k < big.size(); ++k) fds[k] = open(paths[big[k].out_index], O_RDONLY | O_CLOEXEC);
+    std::vector<int> fds(big.size(), -1), oerr(big.size(), 0);
+    for (size_t k = 0; k < big.size(); ++k) {
+      fds[k] = open(paths[big[k].out_index], O_RDONLY | O_CLOEXEC);
+      if (fds[k] < 0) oerr[k] = errno ? errno : EIO;
+    }
     std::vector<uint8_t> d32(32 * n);
     rc = run_big(c, big, d32.data(),
                  [&](size_t k, uint8_t* dst, uint64_t off, uint32_t len) -> int {
-                   if (fds[k] < 0) return errno ? errno : EIO;
+                   if (fds[k] < 0) return oerr[k];
                    return pread_exact(fds[k], dst, len, off);  // hash.rs: 1 MiB reads to EOF
                  },
                  out_status);
@@ -780,6 +903,7 @@ int sdcas_checksums(sdcas_ctx* c, const char* const* paths, size_t n, uint8_t* o
   }
   return SDCAS_OK;
 }
+
 
 // ---- dedup -----------------------------------------------------------------
 

@@ -211,3 +211,33 @@ def test_dedup_small_cases(eng):
     assert out.tolist() == [0, 1] and created == 2
     out, created, linked = eng.identifier_dedup(np.zeros(0, np.uint64), np.zeros(0, np.uint8))
     assert out.size == 0 and created == 0
+
+
+def test_pipelined_staging_many_batches(oracle, tmp_path):
+    """tiny staging slots force dozens of double-buffered batches (host fills
+    one pinned slot while the GPU hashes the other) on every host API"""
+    from spacedrive_amd import Engine
+    rng = np.random.default_rng(55)
+    lens = np.concatenate([rng.integers(0, 300_000, 400), np.array([2 * 1048576 + 77, 1048577])])
+    msgs = [rng.integers(0, 256, int(L), dtype=np.uint8).tobytes() for L in lens]
+    with Engine(staging_bytes=1 << 20, io_threads=4) as e:
+        out = e.hash_messages(*e.pack(msgs))
+        keys = e.cas_ids_from_messages(*e.pack(msgs))
+        for m, d, k in zip(msgs, out, keys):
+            want = oracle.hash(m)
+            assert bytes(d).hex() == want, len(m)
+            assert f"{int(k):016x}" == want[:16]
+        paths, sizes = [], []
+        for i, m in enumerate(msgs[:150]):
+            p = tmp_path / f"f{i}"
+            p.write_bytes(m)
+            paths.append(str(p))
+            sizes.append(len(m))
+        ck, st = e.generate_cas_ids(paths, sizes)
+        assert not st.any()
+        for p, s, k in zip(paths, sizes, ck):
+            assert f"{int(k):016x}" == oracle.generate_cas_id(p, s)
+        d32, st = e.file_checksums(paths)
+        assert not st.any()
+        for m, d in zip(msgs[:150], d32):
+            assert bytes(d).hex() == oracle.hash(m)
