@@ -37,6 +37,9 @@ int sdcas_dev_last_kernel_ms(sdcas_ctx *ctx, float *leaf_ms, float *total_ms);
 /* Tuning: select the leaf/tree kernel variant (-1 = default). Returns the
  * number of variants. */
 int sdcas_dev_set_leaf_variant(sdcas_ctx *ctx, int variant);
+/* Tuning: hash messages in length-sorted slot order (1, default) or in caller
+ * order (0). Results are identical either way. */
+int sdcas_dev_set_sort(sdcas_ctx *ctx, int enable);
 
 #ifdef __cplusplus
 }

@@ -27,7 +27,7 @@ ABI_SYMBOLS = [
     "sdcas_dev_dedup_apply", "sdcas_dev_stream_begin", "sdcas_dev_stream_update", "sdcas_dev_stream_finish",
     # bench / test plumbing
     "sdcas_dev_synth_cas_messages", "sdcas_dev_synth_content", "sdcas_dev_dedup", "sdcas_dev_profile",
-    "sdcas_dev_last_kernel_ms", "sdcas_dev_set_leaf_variant",
+    "sdcas_dev_last_kernel_ms", "sdcas_dev_set_leaf_variant", "sdcas_dev_set_sort",
 ]
 
 
@@ -91,6 +91,7 @@ def load():
     L.sdcas_dev_last_kernel_ms.argtypes = [_vp, ctypes.POINTER(ctypes.c_float),
                                            ctypes.POINTER(ctypes.c_float)]
     L.sdcas_dev_set_leaf_variant.argtypes = [_vp, ctypes.c_int]
+    L.sdcas_dev_set_sort.argtypes = [_vp, ctypes.c_int]
     L.sdcas_dev_dedup_combine.argtypes = [_vp, _vp, _vp, _vp, _vp, _sz, ctypes.c_uint32, _vp, _vp, _vp, _vp]
     L.sdcas_dev_dedup_resolve.argtypes = [_vp, _vp, _sz, _vp, _sz, _vp, _vp]
     L.sdcas_dev_dedup_apply.argtypes = [_vp, _vp, _vp, _sz, _vp, _sz, _vp, _vp, _vp]

@@ -20,6 +20,14 @@ struct BatchWorkspace {
   uint32_t cap_msgs = 0;
   uint64_t cap_chunks = 0;
   int variant = -1;  // leaf kernel variant (-1: default / SDCAS_LEAF_VARIANT)
+  // length-sorted slot order (messages of equal length share waves, so the
+  // lanes of a wave run the same number of blocks): perm[slot-order index] =
+  // caller index; soffs/slens = offsets/lengths in slot order
+  int sort = 1;
+  uint32_t* perm = nullptr;        // [cap_msgs]
+  uint64_t* soffs = nullptr;       // [cap_msgs]
+  uint64_t* slens = nullptr;       // [cap_msgs]
+  uint32_t* sort_keys = nullptr;   // [512] shape-bin counts and cursors
 };
 
 size_t batch_scan_temp_bytes(uint32_t max_msgs);

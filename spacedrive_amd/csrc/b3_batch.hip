@@ -118,6 +118,32 @@ __device__ __forceinline__ void hash_chunk_pf(const uint8_t* __restrict__ p, uin
   }
 }
 
+// Same, unrolled by two blocks with ping-pong message registers (no
+// register copies between blocks; block b+1's loads fly while b compresses).
+__device__ __forceinline__ void hash_chunk_pp(const uint8_t* __restrict__ p, uint32_t clen, uint64_t j, bool root,
+                                              uint32_t (&cv)[8]) {
+  set_iv(cv);
+  const uint32_t nb = clen == 0 ? 1 : (clen + BLOCK_LEN - 1) / BLOCK_LEN;
+  const uint32_t endf = CHUNK_END | (root ? ROOT : 0u);
+  uint32_t m0[16], m1[16];
+  load_full_block(p, m0);
+#pragma unroll 1
+  for (uint32_t b = 0; b < nb; b += 2) {
+    load_full_block(p + min(b + 1, nb - 1) * BLOCK_LEN, m1);
+    {
+      const uint32_t blen = min(BLOCK_LEN, clen - b * BLOCK_LEN);
+      if (blen < BLOCK_LEN) mask_tail(m0, blen);
+      compress(cv, m0, j, blen, (b == 0 ? CHUNK_START : 0u) | (b + 1 == nb ? endf : 0u));
+    }
+    if (b + 1 < nb) {
+      load_full_block(p + min(b + 2, nb - 1) * BLOCK_LEN, m0);
+      const uint32_t blen = min(BLOCK_LEN, clen - (b + 1) * BLOCK_LEN);
+      if (blen < BLOCK_LEN) mask_tail(m1, blen);
+      compress(cv, m1, j, blen, b + 2 == nb ? endf : 0u);
+    }
+  }
+}
+
 // DIAGNOSTIC ONLY (wrong digests, never the default): PF=2 compresses
 // register-made blocks without touching memory (pure VALU rate); PF=3 streams
 // the chunk's blocks and folds them with XOR, no compression (pure load rate).
@@ -160,14 +186,14 @@ __device__ __forceinline__ uint32_t enc_task(uint32_t l, uint32_t r, uint32_t ms
   return l | (r << 10) | (msg << 20) | (root ? 0x80000000u : 0u);
 }
 
-template <int WG, int PF, int TR = 1, int STAGGER = 0>
+template <int WG, int PF, int TR = 1, int STAGGER = 0, int PRIO = 0>
 __global__ void __launch_bounds__(WG) k_leaf_tree(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ offs,
                                                    const uint64_t* __restrict__ lens, uint32_t n,
                                                    const uint64_t* __restrict__ S,
                                                    const uint32_t* __restrict__ tile_first,
                                                    const uint64_t* __restrict__ total_p, uint64_t cap_chunks,
                                                    uint32_t* __restrict__ nodes, uint8_t* __restrict__ out32,
-                                                   uint64_t* __restrict__ out_keys) {
+                                                   uint64_t* __restrict__ out_keys, const uint32_t* __restrict__ perm) {
   __shared__ uint32_t cvs[kTile][8];   // chunk / node chaining values, by slot
   __shared__ uint64_t sS[kTile + 1];   // S[] of the tile's messages
   __shared__ uint16_t smsg[kTile];     // slot -> message index in the tile (kNoMsg: past the end)
@@ -182,7 +208,7 @@ __global__ void __launch_bounds__(WG) k_leaf_tree(const uint8_t* __restrict__ bl
     // Co-resident workgroups run identical tiles in lockstep, so their
     // barrier-bound tree phases coincide and leave the CU's SIMDs idle.
     // Offset them once by a fraction of a tile (speed only).
-    const uint32_t phase = (blockIdx.x / (gridDim.x / STAGGER)) % STAGGER;
+    const uint32_t phase = (blockIdx.x / (gridDim.x / (STAGGER ? STAGGER : 1))) % (STAGGER ? STAGGER : 1);
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     const uint64_t wait = (uint64_t)phase * 25000 / STAGGER;  // 100 MHz ticks: ~250 us per tile
     while (__builtin_amdgcn_s_memrealtime() - t0 < wait) __builtin_amdgcn_s_sleep(100);
@@ -261,11 +287,12 @@ __global__ void __launch_bounds__(WG) k_leaf_tree(const uint8_t* __restrict__ bl
       const uint32_t clen = len == 0 ? 0u : (uint32_t)min<uint64_t>(CHUNK_LEN, len - j * CHUNK_LEN);
       const bool root = (C == 1);
       uint32_t cv[8];
-      if (PF >= 2) hash_chunk_diag(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv, PF);
+      if (PF == 4) hash_chunk_pp(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
+      else if (PF >= 2) hash_chunk_diag(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv, PF);
       else if (PF) hash_chunk_pf(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
       else hash_chunk(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
       if (root) {
-        store_digest(m, cv, out32, out_keys);
+        store_digest(perm ? perm[m] : m, cv, out32, out_keys);
       } else {
 #pragma unroll
         for (int i = 0; i < 8; ++i) cvs[s][i] = cv[i];
@@ -274,6 +301,7 @@ __global__ void __launch_bounds__(WG) k_leaf_tree(const uint8_t* __restrict__ bl
     __syncthreads();
 
     // (3) the tree, level by level: every task of a level is independent
+    if (PRIO) __builtin_amdgcn_s_setprio(PRIO);  // the few tree waves gate the barrier: let them issue first
     for (uint32_t k = 1; TR && k <= 10; ++k) {
       const uint32_t T = ntask[k];
       if (T == 0) continue;
@@ -290,7 +318,8 @@ __global__ void __launch_bounds__(WG) k_leaf_tree(const uint8_t* __restrict__ bl
         }
         parent(a, b, root, o);
         if (root) {
-          store_digest(m0 + ((e >> 20) & 2047u), o, out32, out_keys);
+          const uint32_t mm = m0 + ((e >> 20) & 2047u);
+          store_digest(perm ? perm[mm] : mm, o, out32, out_keys);
         } else {
 #pragma unroll
           for (int q = 0; q < 8; ++q) cvs[l][q] = o[q];
@@ -298,6 +327,7 @@ __global__ void __launch_bounds__(WG) k_leaf_tree(const uint8_t* __restrict__ bl
       }
       __syncthreads();
     }
+    if (PRIO) __builtin_amdgcn_s_setprio(0);
 
     // (4) messages crossing a tile boundary: their maximal in-tile nodes go to
     // HBM at their first slot, for k_finish
@@ -319,16 +349,24 @@ __global__ void __launch_bounds__(WG) k_leaf_tree(const uint8_t* __restrict__ bl
   }
 }
 
+// Messages crossing tile boundaries: one lane per tile boundary t (the
+// message holding slot t*kTile, when it started in tile t-1 — its first
+// crossing), so the launch is dense (~ one active lane per tile) instead of a
+// lane per message. The lane walks the message's maximal nodes left to right
+// (a closed-form function of (chunk index, chunk count, slot in tile)) and
+// merges them with the BLAKE3 subtree-stack rule; the last merge is ROOT.
 __global__ void __launch_bounds__(256) k_finish(const uint64_t* __restrict__ lens, uint32_t n,
-                                                const uint64_t* __restrict__ S, const uint64_t* __restrict__ total_p,
-                                                uint64_t cap_chunks, const uint32_t* __restrict__ nodes,
+                                                const uint64_t* __restrict__ S, const uint32_t* __restrict__ tile_first,
+                                                const uint64_t* __restrict__ total_p, uint64_t cap_chunks,
+                                                const uint32_t* __restrict__ nodes, const uint32_t* __restrict__ perm,
                                                 uint8_t* __restrict__ out32, uint64_t* __restrict__ out_keys) {
-  const uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= n || *total_p > cap_chunks) return;
-  const uint64_t C = chunk_count(lens[m]);
-  if (C == 1) return;
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t total = *total_p;
+  if (total > cap_chunks || t == 0 || t * kTile >= total) return;
+  const uint32_t m = tile_first[t];
   const uint64_t s0 = S[m];
-  if (s0 / kTile == (s0 + C - 1) / kTile) return;  // lies in one tile: folded by k_leaf_tree
+  if (s0 >= t * kTile || s0 / kTile != t - 1) return;  // starts on the boundary / crossed an earlier one first
+  const uint64_t C = chunk_count(lens[m]);
   uint32_t stack[kMaxStack][8];
   int depth = 0;
   uint64_t j = 0;
@@ -355,7 +393,7 @@ __global__ void __launch_bounds__(256) k_finish(const uint64_t* __restrict__ len
 #pragma unroll
         for (int i = 0; i < 8; ++i) cv[i] = o[i];
       }
-      store_digest(m, cv, out32, out_keys);
+      store_digest(perm ? perm[m] : m, cv, out32, out_keys);
     } else {
 #pragma unroll
       for (int i = 0; i < 8; ++i) stack[depth][i] = cv[i];
@@ -363,6 +401,70 @@ __global__ void __launch_bounds__(256) k_finish(const uint64_t* __restrict__ len
     }
   }
 }
+
+// Slot order by message shape: key = min(chunks, 15) << 4 | (blocks in the
+// last chunk - 1). Single-chunk messages — whose lanes otherwise run 1..16
+// blocks side by side in one wave — end up grouped by block count;
+// multi-chunk messages have one short chunk each and are merely clustered.
+// A counting sort over the 256 shape bins (histogram, then a scatter that
+// reserves each workgroup's range per bin): order inside a bin is not
+// specified, which changes nothing but the slot a message lands in.
+constexpr uint32_t kShapeBins = 256;
+constexpr uint32_t kScatterPerWG = 4096;
+
+__device__ __forceinline__ uint32_t shape_key(uint64_t L) {
+  const uint64_t C = chunk_count(L);
+  const uint64_t last = L - (C - 1) * CHUNK_LEN;  // 0..1024
+  const uint32_t blocks = last == 0 ? 1u : (uint32_t)((last + BLOCK_LEN - 1) / BLOCK_LEN);
+  return ((uint32_t)min<uint64_t>(C, 15) << 4) | (blocks - 1);
+}
+
+__global__ void __launch_bounds__(256) k_shape_hist(const uint64_t* __restrict__ lens, uint32_t n,
+                                                    uint32_t* __restrict__ counts) {
+  __shared__ uint32_t h[kShapeBins];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) atomicAdd(&h[shape_key(lens[i])], 1u);
+  __syncthreads();
+  if (h[threadIdx.x]) atomicAdd(&counts[threadIdx.x], h[threadIdx.x]);
+}
+
+__global__ void __launch_bounds__(256) k_shape_scatter(const uint64_t* __restrict__ offs,
+                                                       const uint64_t* __restrict__ lens, uint32_t n,
+                                                       const uint32_t* __restrict__ counts,
+                                                       uint32_t* __restrict__ cursor, uint32_t* __restrict__ perm,
+                                                       uint64_t* __restrict__ soffs, uint64_t* __restrict__ slens) {
+  __shared__ uint32_t start[kShapeBins], h[kShapeBins], rank[kShapeBins];
+  const uint32_t t = threadIdx.x;
+  // exclusive scan of the global bin counts (256 entries, one per thread)
+  start[t] = counts[t];
+  h[t] = 0;
+  rank[t] = 0;
+  __syncthreads();
+  for (uint32_t d = 1; d < kShapeBins; d <<= 1) {
+    const uint32_t v = t >= d ? start[t - d] : 0u;
+    __syncthreads();
+    start[t] += v;
+    __syncthreads();
+  }
+  const uint32_t excl = start[t] - counts[t];
+  __syncthreads();
+  start[t] = excl;
+  const uint32_t lo = blockIdx.x * kScatterPerWG, hi = min(n, lo + kScatterPerWG);
+  for (uint32_t i = lo + t; i < hi; i += 256) atomicAdd(&h[shape_key(lens[i])], 1u);
+  __syncthreads();
+  if (h[t]) start[t] += atomicAdd(&cursor[t], h[t]);  // this workgroup's range in bin t
+  __syncthreads();
+  for (uint32_t i = lo + t; i < hi; i += 256) {
+    const uint64_t L = lens[i];
+    const uint32_t k = shape_key(L);
+    const uint32_t pos = start[k] + atomicAdd(&rank[k], 1u);
+    perm[pos] = i;
+    soffs[pos] = offs[i];
+    slens[pos] = L;
+  }
+}
+
 
 // ---- big files: 1 MiB pieces -----------------------------------------------
 //
@@ -612,6 +714,10 @@ static const LeafVariant kLeafVariants[] = {
     // 8, 9: workgroups staggered by 1/3 and 1/2 of a tile
     {(const void*)k_leaf_tree<512, 1, 1, 3>, 512},
     {(const void*)k_leaf_tree<512, 1, 1, 2>, 512},
+    // 10: ping-pong block loop; 11: tree waves at priority 1; 12: both
+    {(const void*)k_leaf_tree<512, 4>, 512},
+    {(const void*)k_leaf_tree<512, 1, 1, 0, 1>, 512},
+    {(const void*)k_leaf_tree<512, 4, 1, 0, 1>, 512},
 };
 constexpr int kNumLeafVariants = sizeof(kLeafVariants) / sizeof(kLeafVariants[0]);
 constexpr int kDefaultLeafVariant = 1;
@@ -629,7 +735,7 @@ int leaf_variant() {
 }
 
 int batch_grid(int device, int variant) {
-  static int cached[64][8] = {{0}};
+  static int cached[64][32] = {{0}};
   if (device >= 0 && device < 64 && cached[device][variant]) return cached[device][variant];
   int cus = 256, per = 1;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
@@ -644,11 +750,23 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
                       uint32_t n, uint8_t* out32, uint64_t* out_keys, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
   if (n == 0) return hipSuccess;
   if (n > ws.cap_msgs) return hipErrorInvalidValue;
+  const uint32_t tb = 256;
+  hipError_t e;
+  const uint32_t* perm = nullptr;
+  if (ws.sort && n > 1 && ws.perm) {
+    uint32_t* counts = ws.sort_keys;  // [256] bin sizes, [256] per-bin cursors
+    if ((e = hipMemsetAsync(counts, 0, 2 * kShapeBins * sizeof(uint32_t), st))) return e;
+    const uint32_t hb = std::min<uint32_t>((n + 255) / 256, 1024u);
+    hipLaunchKernelGGL(k_shape_hist, dim3(hb), dim3(256), 0, st, lens, n, counts);
+    hipLaunchKernelGGL(k_shape_scatter, dim3((n + kScatterPerWG - 1) / kScatterPerWG), dim3(256), 0, st, offs, lens,
+                       n, counts, counts + kShapeBins, ws.perm, ws.soffs, ws.slens);
+    offs = ws.soffs;
+    lens = ws.slens;
+    perm = ws.perm;
+  }
   hipcub::TransformInputIterator<uint64_t, ChunkCountOp, const uint64_t*> it(lens, ChunkCountOp());
   size_t tmp = ws.scan_tmp_bytes;
-  hipError_t e = hipcub::DeviceScan::ExclusiveSum(ws.scan_tmp, tmp, it, ws.S, (int)n, st);
-  if (e != hipSuccess) return e;
-  const uint32_t tb = 256;
+  if ((e = hipcub::DeviceScan::ExclusiveSum(ws.scan_tmp, tmp, it, ws.S, (int)n, st))) return e;
   hipLaunchKernelGGL(k_tile_first, dim3((n + tb - 1) / tb), dim3(tb), 0, st, lens, ws.S, n, ws.cap_chunks,
                      ws.tile_first, ws.total);
   if (ev0) (void)hipEventRecord(ev0, st);
@@ -657,14 +775,16 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
     int dev = 0;
     (void)hipGetDevice(&dev);
     const int grid = batch_grid(dev, v);
-    void* args[] = {(void*)&blob, (void*)&offs, (void*)&lens, (void*)&n, (void*)&ws.S, (void*)&ws.tile_first,
-                    (void*)&ws.total, (void*)&ws.cap_chunks, (void*)&ws.nodes, (void*)&out32, (void*)&out_keys};
+    void* args[] = {(void*)&blob,     (void*)&offs,          (void*)&lens,       (void*)&n,
+                    (void*)&ws.S,     (void*)&ws.tile_first, (void*)&ws.total,   (void*)&ws.cap_chunks,
+                    (void*)&ws.nodes, (void*)&out32,         (void*)&out_keys,   (void*)&perm};
     hipError_t le = hipLaunchKernel(kLeafVariants[v].fn, dim3(grid), dim3(kLeafVariants[v].wg), args, 0, st);
     if (le != hipSuccess) return le;
   }
   if (ev1) (void)hipEventRecord(ev1, st);
-  hipLaunchKernelGGL(k_finish, dim3((n + tb - 1) / tb), dim3(tb), 0, st, lens, n, ws.S, ws.total, ws.cap_chunks,
-                     ws.nodes, out32, out_keys);
+  const uint64_t tiles = ws.cap_chunks / kTile + 1;
+  hipLaunchKernelGGL(k_finish, dim3((uint32_t)((tiles + tb - 1) / tb)), dim3(tb), 0, st, lens, n, ws.S, ws.tile_first,
+                     ws.total, ws.cap_chunks, ws.nodes, perm, out32, out_keys);
   return hipGetLastError();
 }
 

@@ -94,8 +94,8 @@ struct sdcas_ctx {
   uint64_t staging_bytes = 256ull << 20;
 
   BatchWorkspace ws;
-  DevBuf<uint64_t> ws_S, ws_total;
-  DevBuf<uint32_t> ws_tile_first, ws_nodes;
+  DevBuf<uint64_t> ws_S, ws_total, ws_soffs, ws_slens;
+  DevBuf<uint32_t> ws_tile_first, ws_nodes, ws_perm, ws_sort_keys;
   DevBuf<uint8_t> ws_scan;
 
   // host-API device buffers
@@ -164,13 +164,21 @@ int reserve_ws(sdcas_ctx* c, size_t max_msgs, uint64_t max_chunks) {
   if ((e = c->ws_nodes.ensure(8 * (tiles * kTile)))) return c->hip_fail(e, "workspace nodes");
   size_t tb = batch_scan_temp_bytes((uint32_t)std::max<size_t>(max_msgs, 1));
   if ((e = c->ws_scan.ensure(tb))) return c->hip_fail(e, "workspace scan");
+  if ((e = c->ws_perm.ensure(max_msgs + 1)) || (e = c->ws_soffs.ensure(max_msgs + 1)) ||
+      (e = c->ws_slens.ensure(max_msgs + 1)) || (e = c->ws_sort_keys.ensure(512)))
+    return c->hip_fail(e, "workspace sort");
   c->ws.S = c->ws_S.p;
   c->ws.total = c->ws_total.p;
   c->ws.tile_first = c->ws_tile_first.p;
   c->ws.nodes = c->ws_nodes.p;
   c->ws.scan_tmp = c->ws_scan.p;
   c->ws.scan_tmp_bytes = c->ws_scan.cap;
-  c->ws.cap_msgs = (uint32_t)(c->ws_S.cap - 1);
+  c->ws.perm = c->ws_perm.p;
+  c->ws.soffs = c->ws_soffs.p;
+  c->ws.slens = c->ws_slens.p;
+  c->ws.cap_msgs =
+      (uint32_t)std::min<size_t>({c->ws_S.cap - 1, c->ws_perm.cap - 1, c->ws_soffs.cap - 1, c->ws_slens.cap - 1});
+  c->ws.sort_keys = c->ws_sort_keys.p;
   // every tile the leaf kernel may touch needs a tile_first entry and kTile node slots
   c->ws.cap_chunks = std::min<uint64_t>((c->ws_tile_first.cap - 1) * kTile, c->ws_nodes.cap / 8 - kTile);
   return SDCAS_OK;
@@ -535,10 +543,10 @@ void sdcas_destroy(sdcas_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (auto* b : {&c->ws_S, &c->ws_total, &c->dd_key_a, &c->dd_key_b,
+  for (auto* b : {&c->ws_S, &c->ws_total, &c->ws_soffs, &c->ws_slens, &c->dd_key_a, &c->dd_key_b,
                   &c->dd_keys, &c->dd_ekeys, &c->dd_ekeys_sorted})
     b->release();
-  for (auto* b : {&c->ws_tile_first, &c->ws_nodes, &c->d_file_nodes, &c->dd_idx_a, &c->dd_idx_b, &c->dd_head,
+  for (auto* b : {&c->ws_tile_first, &c->ws_nodes, &c->ws_perm, &c->ws_sort_keys, &c->d_file_nodes, &c->dd_idx_a, &c->dd_idx_b, &c->dd_head,
                   &c->dd_nvalid, &c->dd_eidx})
     b->release();
   for (auto* b : {&c->ws_scan, &c->d_out32, &c->dd_valid, &c->dd_temp, &c->dd_has}) b->release();
@@ -980,6 +988,13 @@ int sdcas_dev_dedup(sdcas_ctx* c, const uint64_t* d_keys, const uint8_t* d_has_k
   hipError_t e = dedup_run(c->dws, d_keys, d_has_key, d_status, (uint32_t)n, (uint32_t)chunk_size, nullptr, nullptr,
                            0, d_out_link, (unsigned long long*)d_counts, st);
   if (e) return c->hip_fail(e, "dev_dedup");
+  return SDCAS_OK;
+}
+
+int sdcas_dev_set_sort(sdcas_ctx* c, int enable) {
+  if (!c) return SDCAS_E_INVALID;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->ws.sort = enable ? 1 : 0;
   return SDCAS_OK;
 }
 

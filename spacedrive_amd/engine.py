@@ -208,6 +208,10 @@ class Engine:
         """tuning knob: leaf/tree kernel variant (-1 = default); returns the variant count"""
         return self.L.sdcas_dev_set_leaf_variant(self.ctx, int(v))
 
+    def dev_set_sort(self, enable):
+        """tuning knob: length-sorted slot order (default on); results identical"""
+        self._check(self.L.sdcas_dev_set_sort(self.ctx, 1 if enable else 0), "dev_set_sort")
+
     def dev_kernel_ms(self):
         a, b = ctypes.c_float(0), ctypes.c_float(0)
         self._check(self.L.sdcas_dev_last_kernel_ms(self.ctx, ctypes.byref(a), ctypes.byref(b)), "ms")

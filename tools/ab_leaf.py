@@ -20,19 +20,21 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--variants", default="")
     ap.add_argument("--align", type=int, default=128, help="message start alignment in HBM")
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c5"])
+    ap.add_argument("--sorts", default="1", help="comma list of slot orders to try: 1 length-sorted, 0 caller order")
     a = ap.parse_args()
     import torch
     from spacedrive_amd import Engine
     dev = torch.device("cuda", 0)
     n = a.files
-    sizes, keys = bench.c2_files(bench.SEED_C2, 0, n)
-    lens = sizes + np.uint64(8)
+    sizes, keys, _ = bench.files_of(a.workload, 0, n)
+    lens = bench.S.cas_msg_len(sizes)
     A = np.uint64(a.align)
     padded = (lens + A - np.uint64(1)) // A * A
     offs = np.zeros(n, np.uint64)
     offs[1:] = np.cumsum(padded[:-1])
     total = int(offs[-1] + padded[-1]) + 64
-    chunks = int(((lens + np.uint64(1023)) // np.uint64(1024)).sum())
+    chunks = int(np.maximum(np.uint64(1), (lens + np.uint64(1023)) // np.uint64(1024)).sum())
     eng = Engine()
     t = lambda x: torch.from_numpy(np.ascontiguousarray(x).view(np.int64)).to(dev)
     d_blob = torch.empty(total, dtype=torch.uint8, device=dev)
@@ -41,12 +43,14 @@ def main():
     sp = torch.cuda.current_stream().cuda_stream
     eng.dev_synth_cas_messages(dk.data_ptr(), ds.data_ptr(), do.data_ptr(), n, d_blob.data_ptr(), sp)
     nv = eng.dev_set_leaf_variant(-1)
-    vs = [int(v) for v in a.variants.split(",")] if a.variants else list(range(nv))
+    vl = [int(v) for v in a.variants.split(",")] if a.variants else list(range(nv))
+    vs = [(v, int(so)) for v in vl for so in a.sorts.split(",")]
     outs = {}
     res = {v: [] for v in vs}
     for r in range(a.rounds):
         for v in vs:
-            eng.dev_set_leaf_variant(v)
+            eng.dev_set_leaf_variant(v[0])
+            eng.dev_set_sort(v[1])
             out = torch.zeros(n, dtype=torch.int64, device=dev)
             eng.dev_hash_messages(d_blob.data_ptr(), do.data_ptr(), dl.data_ptr(), n, 0, out.data_ptr(), sp)
             eng.dev_sync(sp)
@@ -64,7 +68,7 @@ def main():
         leafs = sorted(x[0] for x in res[v])
         seqs = sorted(x[1] for x in res[v])
         same = np.array_equal(outs[v], ref)
-        print(f"variant {v}: leaf med {leafs[len(leafs)//2]:.3f} min {leafs[0]:.3f} ms "
+        print(f"variant {v[0]} sort {v[1]}: leaf med {leafs[len(leafs)//2]:.3f} min {leafs[0]:.3f} ms "
               f"({msg / leafs[0] / 1e6:.0f} GB/s), seq med {seqs[len(seqs)//2]:.3f} ms, agree={same}",
               flush=True)
     eng.close()
