@@ -99,16 +99,19 @@ __device__ __forceinline__ void hash_chunk(const uint8_t* __restrict__ p, uint32
 // compressed (software pipelining: one 64-byte block per lane in flight while
 // the VALU works). The load address is clamped to the chunk's last block, so
 // the final iteration re-reads it harmlessly instead of running off the end.
+template <bool NT = false>
 __device__ __forceinline__ void hash_chunk_pf(const uint8_t* __restrict__ p, uint32_t clen, uint64_t j, bool root,
                                               uint32_t (&cv)[8]) {
   set_iv(cv);
   const uint32_t nb = clen == 0 ? 1 : (clen + BLOCK_LEN - 1) / BLOCK_LEN;
   uint32_t m[16];
-  load_full_block(p, m);
+  if (NT) load_full_block_nt(p, m);
+  else load_full_block(p, m);
 #pragma unroll 1
   for (uint32_t b = 0; b < nb; ++b) {
     uint32_t nx[16];
-    load_full_block(p + min(b + 1, nb - 1) * BLOCK_LEN, nx);
+    if (NT) load_full_block_nt(p + min(b + 1, nb - 1) * BLOCK_LEN, nx);
+    else load_full_block(p + min(b + 1, nb - 1) * BLOCK_LEN, nx);
     const uint32_t blen = min(BLOCK_LEN, clen - b * BLOCK_LEN);
     if (blen < BLOCK_LEN) mask_tail(m, blen);
     const uint32_t flags = (b == 0 ? CHUNK_START : 0u) | (b + 1 == nb ? (CHUNK_END | (root ? ROOT : 0u)) : 0u);
@@ -288,6 +291,7 @@ __global__ void __launch_bounds__(WG) k_leaf_tree(const uint8_t* __restrict__ bl
       const bool root = (C == 1);
       uint32_t cv[8];
       if (PF == 4) hash_chunk_pp(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
+      else if (PF == 5) hash_chunk_pf<true>(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
       else if (PF >= 2) hash_chunk_diag(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv, PF);
       else if (PF) hash_chunk_pf(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
       else hash_chunk(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
@@ -718,6 +722,8 @@ static const LeafVariant kLeafVariants[] = {
     {(const void*)k_leaf_tree<512, 4>, 512},
     {(const void*)k_leaf_tree<512, 1, 1, 0, 1>, 512},
     {(const void*)k_leaf_tree<512, 4, 1, 0, 1>, 512},
+    // 13: non-temporal (streaming) message loads
+    {(const void*)k_leaf_tree<512, 5>, 512},
 };
 constexpr int kNumLeafVariants = sizeof(kLeafVariants) / sizeof(kLeafVariants[0]);
 constexpr int kDefaultLeafVariant = 1;

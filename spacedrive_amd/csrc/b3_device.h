@@ -106,6 +106,18 @@ __device__ __forceinline__ void load_full_block(const uint8_t* p, uint32_t (&m)[
   m[12] = d.x; m[13] = d.y; m[14] = d.z; m[15] = d.w;
 }
 
+// the same with non-temporal (streaming) loads: message bytes are read once
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void load_full_block_nt(const uint8_t* p, uint32_t (&m)[16]) {
+  const u32x4* q = reinterpret_cast<const u32x4*>(p);
+  u32x4 a = __builtin_nontemporal_load(q), b = __builtin_nontemporal_load(q + 1);
+  u32x4 c = __builtin_nontemporal_load(q + 2), d = __builtin_nontemporal_load(q + 3);
+  m[0] = a.x; m[1] = a.y; m[2] = a.z; m[3] = a.w;
+  m[4] = b.x; m[5] = b.y; m[6] = b.z; m[7] = b.w;
+  m[8] = c.x; m[9] = c.y; m[10] = c.z; m[11] = c.w;
+  m[12] = d.x; m[13] = d.y; m[14] = d.z; m[15] = d.w;
+}
+
 // Zero the bytes of a just-loaded block that lie past `blen` (< 64): the last
 // block of a message is loaded as a full 64-byte block (the blob carries at
 // least 64 readable bytes after every message, see sdcas.h) and masked here,
