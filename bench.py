@@ -150,6 +150,48 @@ def cpu_baseline(gpu_keys, sample, threads):
     return base, parity
 
 
+def cpu_baseline_files(gpu_keys, sizes, ckeys, mode, threads, what):
+    """CPU baseline over a bounded sample of any synthetic corpus (c3/c4/c5):
+    mode 0 = cas messages (cas.rs:25-58), mode 1 = whole-file checksum
+    (hash.rs:15-21). Messages are built untimed, then hashed on one thread and
+    on `threads` threads by the oracle's SIMD-class hasher. The oracle keys
+    (first 8 digest bytes) are compared with the GPU's on the same files."""
+    from tests._oracle import load_oracle
+    o = load_oracle()
+    f = o.lib.oracle_cpu_bench_files
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                  ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_double),
+                  ctypes.POINTER(ctypes.c_int), ctypes.c_char_p]
+    sizes = np.ascontiguousarray(sizes, dtype=np.uint64)
+    ckeys = np.ascontiguousarray(ckeys, dtype=np.uint64)
+    n = sizes.size
+    keys = np.zeros(n, np.uint64)
+    nbytes = ctypes.c_uint64(0)
+    secs = (ctypes.c_double * 2)()
+    kind = ctypes.c_int(0)
+    ver = ctypes.create_string_buffer(32)
+    rc = f(ckeys.ctypes.data, sizes.ctypes.data, n, mode, threads, 1, keys.ctypes.data, ctypes.byref(nbytes),
+           secs, ctypes.byref(kind), ver)
+    if rc != 0:
+        return None, None
+    hasher = f"upstream BLAKE3 C {ver.value.decode()} SIMD (llvm_blake3 in ROCm libclang-cpp)" if kind.value \
+        else "scalar BLAKE3 restatement (oracle/blake3_ref.c)"
+    gb = nbytes.value / 1e9
+    if mode == 1:
+        base = {"value": gb / secs[0], "unit": "GB/s", "files_per_s": n / secs[0]}
+        allc = {"value": gb / secs[1], "cores": threads, "files_per_s": n / secs[1]}
+    else:
+        base = {"value": n / secs[0], "unit": "files/s", "gbps": gb / secs[0]}
+        allc = {"value": n / secs[1], "cores": threads, "gbps": gb / secs[1]}
+    base.update({"cores": 1, "kind": "port", "seconds": secs[0], "all_cores": allc,
+                 "sample": f"{what} = {gb:.2f} GB of {'file content' if mode else 'cas messages'} in host RAM, "
+                           f"hashed by {hasher}, one thread (the reference hashes on one runtime thread per "
+                           f"step); storage I/O excluded"})
+    parity = {"checked_files": int(n), "mismatches": int((keys != gpu_keys).sum()), "oracle": hasher}
+    return base, parity
+
+
 def sample_parity(gpu_keys, sizes, ckeys, count, seed=1):
     """CPU oracle keys of `count` files spread over the batch (incl. sampled)"""
     from tests._oracle import load_oracle
@@ -279,6 +321,22 @@ def run_c4(args, torch, dist, dev, rank, world, distributed):
                            "tests/test_gpu_stream.py (multi-piece messages up to 4 GiB + 1)"},
     }
     out["roofline"]["frac"] = out["roofline"]["achieved"] / HBM_PEAK_GBS if out["roofline"]["achieved"] else None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # bounded sample: the first files (in corpus order) up to c4_cpu_gib
+        pick, acc = [], 0
+        for f in mine:
+            if acc >= int(args.c4_cpu_gib) << 30:
+                break
+            pick.append(f)
+            acc += int(sizes[f])
+        dig = out32.cpu().numpy()[[local[f] for f in pick]]
+        gk = np.zeros(len(pick), np.uint64)
+        for b in range(8):  # digest bytes 0..7 big-endian = the oracle's key
+            gk = (gk << np.uint64(8)) | dig[:, b].astype(np.uint64)
+        base, parity = cpu_baseline_files(gk, sizes[pick], ckeys[pick], 1, args.cpu_threads,
+                                          f"C4 files {pick[0]}..{pick[-1]} ({len(pick)} files)")
+        out["cpu_baseline"] = base
+        out["parity"]["cpu_baseline_sample"] = parity
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()
@@ -291,11 +349,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--files", type=int, default=0, help="files per GPU (default: the workload's)")
-    ap.add_argument("--cpu-sample", type=int, default=1_000_000)
+    ap.add_argument("--cpu-sample", type=int, default=0, help="files in the CPU-baseline sample (0: all of rank 0's)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--c4-total-gib", type=int, default=256)
     ap.add_argument("--window-gib", type=int, default=64)
+    ap.add_argument("--c4-cpu-gib", type=int, default=16, help="C4 CPU-baseline sample size")
     args = ap.parse_args()
     W = WORKLOADS[args.workload]
 
@@ -439,7 +498,13 @@ def main():
     if rank == 0 and world == 1:
         gk = d_out.cpu().numpy().view(np.uint64)
         if args.workload == "c2" and not args.no_cpu_baseline:
-            base, parity = cpu_baseline(gk, min(args.cpu_sample, n), args.cpu_threads)
+            base, parity = cpu_baseline(gk, min(args.cpu_sample or n, n), args.cpu_threads)
+            out["cpu_baseline"] = base
+            out["parity"] = parity
+        elif not args.no_cpu_baseline:
+            m = min(args.cpu_sample or n, n)
+            base, parity = cpu_baseline_files(gk[:m], sizes[:m], keys[:m], 0, args.cpu_threads,
+                                              f"{args.workload.upper()} files [0,{m}) of rank 0")
             out["cpu_baseline"] = base
             out["parity"] = parity
         else:

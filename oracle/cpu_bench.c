@@ -125,6 +125,93 @@ static double run_hash(const uint8_t *blob, const uint64_t *offs, const uint64_t
   return dt;
 }
 
+/* ---- generic synthetic files: C3/C4/C5 ------------------------------------ */
+
+/* content bytes [off, off + len) of stream `key` into dst */
+static void gen_content(uint64_t key, uint64_t off, uint64_t len, uint8_t *dst) {
+  uint64_t w = off >> 3, end = off + len, pos = off;
+  while (pos < end) {
+    uint64_t x = sds_content_word(key, w);
+    uint64_t wlo = w << 3, from = pos - wlo, take = 8 - from;
+    if (take > end - pos) take = end - pos;
+    memcpy(dst + (pos - off), (const uint8_t *)&x + from, take);
+    pos += take;
+    w++;
+  }
+}
+
+typedef struct {
+  const uint64_t *keys, *sizes, *offs, *lens;
+  uint8_t *blob;
+  int mode;
+  size_t lo, hi;
+} fgen_t;
+
+static void *fgen_worker(void *arg) {
+  fgen_t *g = (fgen_t *)arg;
+  for (size_t i = g->lo; i < g->hi; i++) {
+    uint8_t *m = g->blob + g->offs[i];
+    uint64_t size = g->sizes[i], key = g->keys[i];
+    if (g->mode == 1) { /* file_checksum: the whole content (hash.rs:15-21) */
+      gen_content(key, 0, size, m);
+      continue;
+    }
+    for (int b = 0; b < 8; b++) m[b] = (uint8_t)(size >> (8 * b)); /* cas.rs:25 */
+    if (size <= SDS_MINIMUM_FILE_SIZE) {
+      gen_content(key, 0, size, m + 8);
+    } else { /* cas.rs:35-58 */
+      uint64_t jump = (size - 2 * SDS_HEADER_OR_FOOTER_SIZE) / SDS_SAMPLE_COUNT;
+      uint8_t *p = m + 8;
+      gen_content(key, 0, SDS_HEADER_OR_FOOTER_SIZE, p);
+      p += SDS_HEADER_OR_FOOTER_SIZE;
+      for (uint64_t k = 0; k < SDS_SAMPLE_COUNT; k++, p += SDS_SAMPLE_SIZE)
+        gen_content(key, SDS_HEADER_OR_FOOTER_SIZE + k * jump, SDS_SAMPLE_SIZE, p);
+      gen_content(key, size - SDS_HEADER_OR_FOOTER_SIZE, SDS_HEADER_OR_FOOTER_SIZE, p);
+    }
+  }
+  return NULL;
+}
+
+/* Messages of n synthetic files (content key, size) — mode 0: cas_id
+ * messages, mode 1: whole content (checksum) — built untimed in parallel,
+ * then hashed and timed on one thread (secs[0]) and on `threads` threads
+ * (secs[1]). out_keys[i] = cas key of message i (first 8 digest bytes). */
+int oracle_cpu_bench_files(const uint64_t *keys, const uint64_t *sizes, size_t n, int mode, int threads,
+                           int prefer_upstream, uint64_t *out_keys, uint64_t *bytes, double *secs, int *kind,
+                           char *version_out) {
+  uint64_t *offs = (uint64_t *)malloc(sizeof(uint64_t) * (n + 1));
+  uint64_t *lens = (uint64_t *)malloc(sizeof(uint64_t) * (n + 1));
+  uint64_t total = 0, hashed = 0;
+  for (size_t i = 0; i < n; i++) {
+    lens[i] = mode == 1 ? sizes[i] : sds_cas_msg_len(sizes[i]);
+    offs[i] = total;
+    total += (lens[i] + 15) & ~15ull;
+    hashed += lens[i];
+  }
+  uint8_t *blob = (uint8_t *)malloc(total + 64);
+  if (!blob) return -1;
+  int gt = threads < 1 ? 1 : threads;
+  fgen_t *gj = (fgen_t *)calloc((size_t)gt, sizeof(fgen_t));
+  pthread_t *th = (pthread_t *)calloc((size_t)gt, sizeof(pthread_t));
+  for (int t = 0; t < gt; t++) {
+    gj[t] = (fgen_t){keys, sizes, offs, lens, blob, mode, n * t / gt, n * (t + 1) / gt};
+    pthread_create(&th[t], NULL, fgen_worker, &gj[t]);
+  }
+  for (int t = 0; t < gt; t++) pthread_join(th[t], NULL);
+  free(gj);
+  free(th);
+  int up = prefer_upstream && load_upstream();
+  if (kind) *kind = up;
+  if (version_out) strcpy(version_out, up ? up_version : "scalar");
+  secs[0] = run_hash(blob, offs, lens, out_keys, n, 1, up);
+  secs[1] = threads > 1 ? run_hash(blob, offs, lens, out_keys, n, threads, up) : secs[0];
+  if (bytes) *bytes = hashed;
+  free(blob);
+  free(offs);
+  free(lens);
+  return 0;
+}
+
 /* Build the cas messages of C2 files [0, count) (untimed, in parallel), then
  * time hashing them: secs[0] with ONE thread (the reference's shape), and
  * secs[1] with `threads` threads (all host cores given to this job).

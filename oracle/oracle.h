@@ -82,6 +82,11 @@ int64_t oracle_identifier_dedup(size_t n, const uint64_t *keys, const uint8_t *h
  * [0, count) already in memory; secs[0] one thread, secs[1] `threads` threads */
 int oracle_cpu_bench_c2(uint64_t seed, size_t count, int threads, int prefer_upstream, uint64_t *keys,
                         uint64_t *bytes, double *secs, int *kind, char *version_out);
+/* the same for any synthetic files (keys, sizes): mode 0 cas_id messages
+ * (C3, C5), mode 1 whole-content checksums (C4) */
+int oracle_cpu_bench_files(const uint64_t *keys, const uint64_t *sizes, size_t n, int mode, int threads,
+                           int prefer_upstream, uint64_t *out_keys, uint64_t *bytes, double *secs, int *kind,
+                           char *version_out);
 
 #ifdef __cplusplus
 }

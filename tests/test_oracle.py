@@ -126,3 +126,22 @@ def test_dedup_existing_and_errors(oracle):
 def test_mix64_python_matches_header():
     # sds_mix64(0) reference value computed from the header's definition
     assert int(mix64(np.uint64(0))) == 0xE220A8397B1DCDAF
+
+
+def test_cpu_bench_files_keys(oracle):
+    """bench.py's CPU-baseline leg (oracle_cpu_bench_files) hashes the same
+    cas messages / whole-file contents as the per-file oracle"""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from spacedrive_amd import synth as S
+    sizes = np.array([0, 1, 1023, 1024, 1025, 102400, 102401, 300_000, 5 << 20], np.uint64)
+    ckeys = np.array([S.content_key(S.SEED_C3, i) for i in range(sizes.size)], np.uint64)
+    want = np.array([oracle.synth_cas_key(int(k), int(s)) for k, s in zip(ckeys, sizes)], np.uint64)
+    base, par = bench.cpu_baseline_files(want, sizes, ckeys, 0, 2, "unit")
+    assert par["mismatches"] == 0 and base["unit"] == "files/s"
+    sel = sizes <= (1 << 20)
+    want1 = np.array([int(oracle.synth_checksum(int(k), int(s))[:16], 16) for k, s in zip(ckeys[sel], sizes[sel])],
+                     np.uint64)
+    base, par = bench.cpu_baseline_files(want1, sizes[sel], ckeys[sel], 1, 2, "unit")
+    assert par["mismatches"] == 0 and base["unit"] == "GB/s"
