@@ -1,0 +1,280 @@
+// sdcore.hpp — C++ host mirror of sd-core's content-identification path,
+// layered on the C ABI of libsdcas.so (include/sdcas.h).
+//
+// The reference host is Rust (sd-core); there is no Rust toolchain in this
+// image, so the host side above the C ABI is written in C++ with the
+// reference's names, argument meaning and error behaviour:
+//
+//   generate_cas_id / generate_cas_ids   core/src/object/cas.rs:23-62
+//   file_checksum / file_checksums       core/src/object/validation/hash.rs:9-25
+//   FileMetadata::new (batched)          core/src/object/file_identifier/mod.rs:48-96
+//   identifier_job_step                  core/src/object/file_identifier/mod.rs:98-350
+//   run_file_identifier_job              core/src/object/file_identifier/file_identifier_job.rs:33-319
+//   run_object_validator_job             core/src/object/validation/validator_job.rs:38-200
+//
+// The database side (prisma in sd-core) is the abstract `Library`; a
+// `MemoryLibrary` implements it over in-memory tables with the reference's
+// query semantics (filters, DB order, cursor) for tests and examples.
+//
+// Hashing runs on the GPU through libsdcas. There is no CPU fallback in this
+// layer: when the engine cannot open (no device) `Engine::open` throws
+// `LibraryError`, which is the point where the Rust host keeps its own CPU
+// path (include/sdcas.h, "Conventions").
+#pragma once
+
+#include <array>
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <optional>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "sdcas.h"
+
+namespace sdcore {
+
+// std::io::Error as the Rust host sees it (crates/utils/src/error.rs:5-22
+// FileIOError = path + io::Error): an errno, or UnexpectedEof from read_exact
+// (cas.rs:36,43,56), which has no errno.
+struct IoError {
+  int code = 0;
+  std::string path;
+  bool unexpected_eof() const { return code == SDCAS_STATUS_UNEXPECTED_EOF; }
+  std::string message() const;
+};
+
+// io::Result<T>
+template <class T>
+class Result {
+ public:
+  Result(T v) : v_(std::move(v)) {}
+  Result(IoError e) : e_(std::move(e)) {}
+  bool ok() const { return v_.has_value(); }
+  const T& value() const {
+    if (!v_) throw std::logic_error("Result::value on an error: " + e_.message());
+    return *v_;
+  }
+  const IoError& error() const { return e_; }
+
+ private:
+  std::optional<T> v_;
+  IoError e_;
+};
+
+// A library failure (negative SDCAS_E_* return): the whole batch must take the
+// host's CPU path.
+class LibraryError : public std::runtime_error {
+ public:
+  LibraryError(int code, const std::string& what) : std::runtime_error(what), code(code) {}
+  int code;
+};
+
+class Engine {
+ public:
+  struct Options {
+    int device = -1;             // HIP device ordinal, -1: current
+    uint32_t io_threads = 0;     // reader threads (0: library default)
+    uint64_t staging_bytes = 0;  // pinned staging per slot (0: library default)
+  };
+  static std::unique_ptr<Engine> open(const Options& opts);
+  static std::unique_ptr<Engine> open() { return open(Options{}); }
+  ~Engine();
+  Engine(const Engine&) = delete;
+  Engine& operator=(const Engine&) = delete;
+
+  // cas.rs:23-62 over a batch: (path, size from fs::metadata) -> 16 lowercase hex
+  std::vector<Result<std::string>> generate_cas_ids(const std::vector<std::pair<std::string, uint64_t>>& files);
+  // hash.rs:11-25 over a batch: path -> 64 lowercase hex
+  std::vector<Result<std::string>> file_checksums(const std::vector<std::string>& paths);
+
+  // the canonical group-by of mod.rs:149-254 (sdcas_dedup encoding of out_link)
+  struct Dedup {
+    std::vector<int64_t> link;
+    int64_t created = 0, linked = 0;
+  };
+  Dedup dedup(const std::vector<uint64_t>& keys, const std::vector<uint8_t>& has_key,
+              const std::vector<int32_t>& status, size_t chunk_size, const std::vector<uint64_t>& existing_keys);
+
+  sdcas_ctx* raw() { return ctx_; }
+
+ private:
+  explicit Engine(sdcas_ctx* c) : ctx_(c) {}
+  [[noreturn]] void fail(int rc, const char* what) const;
+  sdcas_ctx* ctx_;
+};
+
+// single-file forms with the reference signatures (cas.rs:23, hash.rs:11)
+Result<std::string> generate_cas_id(Engine& engine, const std::string& path, uint64_t size);
+Result<std::string> file_checksum(Engine& engine, const std::string& path);
+
+// cas key <-> the 16-hex cas_id string (cas.rs:61: to_hex()[..16])
+std::string key_to_hex(uint64_t key);
+uint64_t hex_to_key(const std::string& cas_id);
+
+// ---- rows (the prisma columns this path reads or writes) -------------------
+
+using ObjectKind = int32_t;  // sd_file_ext::kind::ObjectKind discriminant; 0 = Unknown
+using PubId = std::array<uint8_t, 16>;
+
+struct Location {  // location::Data (id, path)
+  int32_t id = 0;
+  std::string path;
+};
+
+// file_path, with the columns of file_path_for_file_identifier and
+// file_path_for_object_validator (crates/file-path-helper/src/lib.rs:30-47)
+struct FilePathRow {
+  int32_t id = 0;
+  PubId pub_id{};
+  int32_t location_id = 0;
+  std::string materialized_path = "/";  // "/" or "/a/b/" (isolated_file_path_data.rs)
+  std::string name, extension;
+  bool is_dir = false;
+  uint64_t size_in_bytes = 0;
+  std::optional<std::string> cas_id;
+  std::optional<int32_t> object_id;
+  std::optional<std::string> integrity_checksum;
+  int64_t date_created = 0;
+  // Extension::resolve_conflicting (crates/file-ext/src/magic.rs:176-230) is
+  // outside this path: the kind is supplied with the row
+  ObjectKind kind = 0;
+};
+
+struct ObjectRow {  // object (id, pub_id, kind, date_created)
+  int32_t id = 0;
+  PubId pub_id{};
+  ObjectKind kind = 0;
+  int64_t date_created = 0;
+};
+
+// location path joined with the row's relative path (assemble_relative_path /
+// join_location_relative_path, isolated_file_path_data.rs:533-560)
+std::string full_path(const Location& location, const FilePathRow& row);
+
+// ---- the database seam ------------------------------------------------------
+
+class Library {
+ public:
+  virtual ~Library() = default;
+  // orphan_path_filters (file_identifier_job.rs:251-283): (object_id IS NULL OR
+  // cas_id IS NULL) AND is_dir = false AND location_id = ? AND size != 0
+  // [AND materialized_path LIKE sub%] [AND id >= cursor], ORDER BY id
+  virtual size_t count_orphan_file_paths(int32_t location_id, const std::string& sub_materialized_path) = 0;
+  virtual std::vector<FilePathRow> get_orphan_file_paths(int32_t location_id, int32_t cursor,
+                                                         const std::string& sub_materialized_path, size_t take) = 0;
+  // mod.rs:157-178: file_path.cas_id = ? per processed file
+  virtual void set_cas_id(int32_t file_path_id, const std::optional<std::string>& cas_id) = 0;
+  // mod.rs:181-188: Objects having a file_path whose cas_id is in `cas_ids`,
+  // in DB order, each with the cas_ids of its file_paths
+  virtual std::vector<std::pair<int32_t, std::vector<std::string>>> existing_objects(
+      const std::vector<std::string>& cas_ids) = 0;
+  // mod.rs:290-327: object::create_unchecked(kind, date_created) -> object id
+  virtual int32_t create_object(ObjectKind kind, int64_t date_created) = 0;
+  // connect_file_path_to_object (mod.rs:352-377)
+  virtual void connect(int32_t file_path_id, int32_t object_id) = 0;
+  // validator_job.rs:107-123: location_id = ? AND is_dir = false AND
+  // integrity_checksum IS NULL [AND materialized_path LIKE sub%]
+  virtual std::vector<FilePathRow> file_paths_without_checksum(int32_t location_id,
+                                                               const std::string& sub_materialized_path) = 0;
+  virtual void set_integrity_checksum(int32_t file_path_id, const std::string& checksum) = 0;
+};
+
+// In-memory tables with the reference's query semantics (ids ascending = DB order)
+class MemoryLibrary : public Library {
+ public:
+  std::vector<FilePathRow> file_paths;  // kept sorted by id
+  std::vector<ObjectRow> objects;       // ids ascending
+
+  FilePathRow& add_file_path(FilePathRow row);  // assigns id and pub_id when 0
+  const FilePathRow* file_path(int32_t id) const;
+
+  size_t count_orphan_file_paths(int32_t location_id, const std::string& sub) override;
+  std::vector<FilePathRow> get_orphan_file_paths(int32_t location_id, int32_t cursor, const std::string& sub,
+                                                 size_t take) override;
+  void set_cas_id(int32_t file_path_id, const std::optional<std::string>& cas_id) override;
+  std::vector<std::pair<int32_t, std::vector<std::string>>> existing_objects(
+      const std::vector<std::string>& cas_ids) override;
+  int32_t create_object(ObjectKind kind, int64_t date_created) override;
+  void connect(int32_t file_path_id, int32_t object_id) override;
+  std::vector<FilePathRow> file_paths_without_checksum(int32_t location_id, const std::string& sub) override;
+  void set_integrity_checksum(int32_t file_path_id, const std::string& checksum) override;
+
+ private:
+  FilePathRow* find(int32_t id);
+  bool orphan(const FilePathRow& r, int32_t location_id, const std::string& sub) const;
+  int32_t next_file_path_id_ = 1, next_object_id_ = 1;
+};
+
+// ---- file_identifier ----------------------------------------------------------
+
+// FileMetadata (mod.rs:48-53)
+struct FileMetadata {
+  std::optional<std::string> cas_id;  // None for an empty file (mod.rs:78-86)
+  ObjectKind kind = 0;
+  uint64_t len = 0;  // fs_metadata.len()
+};
+
+// FileMetadata::new for a batch of (full path, kind): fs::metadata, the
+// is_dir assertion (mod.rs:67-70, std::logic_error here), cas_id only for
+// len != 0, one generate_cas_ids call for the batch (the join_all of
+// mod.rs:105-147). Errors carry the path (FileIOError).
+std::vector<Result<FileMetadata>> file_metadata_batch(Engine& engine,
+                                                      const std::vector<std::pair<std::string, ObjectKind>>& files);
+
+// identifier_job_step (mod.rs:98-350) over `file_paths` in id order. A batch
+// longer than `chunk_size` (the reference's CHUNK_SIZE = 100) gives the
+// result of the reference's consecutive steps over its 100-row chunks: the
+// group-by keeps chunk semantics (intra-chunk duplicates each create an
+// Object; later chunks link to the first Object). Returns (total_created,
+// total_linked) as mod.rs:349 does.
+std::pair<size_t, size_t> identifier_job_step(Engine& engine, Library& db, const Location& location,
+                                              const std::vector<FilePathRow>& file_paths,
+                                              size_t chunk_size = SDCAS_IDENTIFIER_CHUNK_SIZE);
+
+// FileIdentifierJobRunMetadata (file_identifier_job.rs:54-71)
+struct FileIdentifierJobRunMetadata {
+  int32_t cursor = 0;
+  size_t total_orphan_paths = 0;
+  size_t total_objects_created = 0;
+  size_t total_objects_linked = 0;
+  size_t total_objects_ignored = 0;
+  size_t steps = 0;
+  bool early_finish = false;  // JobError::EarlyFinish (file_identifier_job.rs:184-191)
+};
+
+// FileIdentifierJobInit (file_identifier_job.rs:33-37); batch = rows per step
+// (the reference fetches CHUNK_SIZE = 100; a multiple of 100 batches several
+// reference steps into one GPU call with identical results)
+struct FileIdentifierJobInit {
+  Location location;
+  std::string sub_materialized_path;  // "" or "/sub/dir/"
+  size_t batch = SDCAS_IDENTIFIER_CHUNK_SIZE;
+};
+
+// init (count orphans, cursor = first orphan id, ceil(count / batch) steps)
+// then execute_step per step (fetch `batch` orphans with id >= cursor, run
+// identifier_job_step, advance the cursor to the last row)
+FileIdentifierJobRunMetadata run_file_identifier_job(Engine& engine, Library& db, const FileIdentifierJobInit& init);
+
+// ---- object validator -----------------------------------------------------------
+
+struct ObjectValidatorJobInit {  // validator_job.rs:38-42
+  Location location;
+  std::string sub_materialized_path;
+  size_t batch = SDCAS_IDENTIFIER_CHUNK_SIZE;  // the reference runs one file per step
+};
+
+struct ObjectValidatorReport {
+  size_t task_count = 0;   // rows selected at init
+  size_t checksummed = 0;  // integrity_checksum written
+  // the first file whose checksum failed: the reference's execute_step returns
+  // ValidatorError::FileIO (validator_job.rs:154-156) and the job stops there
+  std::optional<IoError> error;
+};
+
+ObjectValidatorReport run_object_validator_job(Engine& engine, Library& db, const ObjectValidatorJobInit& init);
+
+}  // namespace sdcore

@@ -147,6 +147,85 @@ __device__ __forceinline__ void hash_chunk_pp(const uint8_t* __restrict__ p, uin
   }
 }
 
+// Same, two blocks of prefetch distance (three rotating message register
+// sets, unrolled by three): block b+2's loads fly while b compresses.
+#define B3_PF2_STEP(cur, nxt_blk)                                                              \
+  {                                                                                            \
+    const uint32_t blen = min(BLOCK_LEN, clen - b * BLOCK_LEN);                                \
+    if (blen < BLOCK_LEN) mask_tail(cur, blen);                                                \
+    compress(cv, cur, j, blen, (b == 0 ? CHUNK_START : 0u) | (b + 1 == nb ? endf : 0u));       \
+    if (++b >= nb) break;                                                                      \
+    load_full_block(p + min(nxt_blk, nb - 1) * BLOCK_LEN, cur);                                \
+  }
+__device__ __forceinline__ void hash_chunk_pf2(const uint8_t* __restrict__ p, uint32_t clen, uint64_t j, bool root,
+                                               uint32_t (&cv)[8]) {
+  set_iv(cv);
+  const uint32_t nb = clen == 0 ? 1 : (clen + BLOCK_LEN - 1) / BLOCK_LEN;
+  const uint32_t endf = CHUNK_END | (root ? ROOT : 0u);
+  uint32_t x[16], y[16], z[16];
+  load_full_block(p, x);
+  load_full_block(p + min(1u, nb - 1) * BLOCK_LEN, y);
+  load_full_block(p + min(2u, nb - 1) * BLOCK_LEN, z);
+  uint32_t b = 0;
+#pragma unroll 1
+  for (;;) {
+    B3_PF2_STEP(x, b + 2)
+    B3_PF2_STEP(y, b + 2)
+    B3_PF2_STEP(z, b + 2)
+  }
+}
+#undef B3_PF2_STEP
+
+// Same, loading 128 bytes (two blocks, one L2 line of a 128-byte aligned
+// chunk) per step into one register set while the previous pair compresses.
+// The pair load at an odd last block is cut to 64 bytes so nothing past the
+// guaranteed 64-byte tail is read.
+__device__ __forceinline__ void load_pair(const uint8_t* p, uint32_t b, uint32_t nb, uint32_t (&m)[32]) {
+  const uint4* q = reinterpret_cast<const uint4*>(p + b * BLOCK_LEN);
+  uint4 r[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[i] = q[i];
+  if (b + 1 < nb) {
+#pragma unroll
+    for (int i = 4; i < 8; ++i) r[i] = q[i];
+  } else {
+#pragma unroll
+    for (int i = 4; i < 8; ++i) r[i] = r[i - 4];
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    m[4 * i] = r[i].x; m[4 * i + 1] = r[i].y; m[4 * i + 2] = r[i].z; m[4 * i + 3] = r[i].w;
+  }
+}
+__device__ __forceinline__ void hash_chunk_pair(const uint8_t* __restrict__ p, uint32_t clen, uint64_t j, bool root,
+                                                uint32_t (&cv)[8]) {
+  set_iv(cv);
+  const uint32_t nb = clen == 0 ? 1 : (clen + BLOCK_LEN - 1) / BLOCK_LEN;
+  const uint32_t endf = CHUNK_END | (root ? ROOT : 0u);
+  uint32_t cur[32];
+  load_pair(p, 0, nb, cur);
+#pragma unroll 1
+  for (uint32_t b = 0; b < nb; b += 2) {
+    uint32_t nx[32];
+    load_pair(p, min(b + 2, (nb - 1) & ~1u), nb, nx);
+    uint32_t m[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m[i] = cur[i];
+    uint32_t blen = min(BLOCK_LEN, clen - b * BLOCK_LEN);
+    if (blen < BLOCK_LEN) mask_tail(m, blen);
+    compress(cv, m, j, blen, (b == 0 ? CHUNK_START : 0u) | (b + 1 == nb ? endf : 0u));
+    if (b + 1 < nb) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) m[i] = cur[16 + i];
+      blen = min(BLOCK_LEN, clen - (b + 1) * BLOCK_LEN);
+      if (blen < BLOCK_LEN) mask_tail(m, blen);
+      compress(cv, m, j, blen, b + 2 == nb ? endf : 0u);
+    }
+#pragma unroll
+    for (int i = 0; i < 32; ++i) cur[i] = nx[i];
+  }
+}
+
 // DIAGNOSTIC ONLY (wrong digests, never the default): PF=2 compresses
 // register-made blocks without touching memory (pure VALU rate); PF=3 streams
 // the chunk's blocks and folds them with XOR, no compression (pure load rate).
@@ -290,7 +369,9 @@ __global__ void __launch_bounds__(WG) k_leaf_tree(const uint8_t* __restrict__ bl
       const uint32_t clen = len == 0 ? 0u : (uint32_t)min<uint64_t>(CHUNK_LEN, len - j * CHUNK_LEN);
       const bool root = (C == 1);
       uint32_t cv[8];
-      if (PF == 4) hash_chunk_pp(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
+      if (PF == 6) hash_chunk_pf2(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
+      else if (PF == 7) hash_chunk_pair(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
+      else if (PF == 4) hash_chunk_pp(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
       else if (PF == 5) hash_chunk_pf<true>(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
       else if (PF >= 2) hash_chunk_diag(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv, PF);
       else if (PF) hash_chunk_pf(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
@@ -343,6 +424,224 @@ __global__ void __launch_bounds__(WG) k_leaf_tree(const uint8_t* __restrict__ bl
       const uint64_t C = chunk_count(lens[m0 + mi]);
       if (C == 1 || (S0 >= tbase && S0 + C <= tbase + kTile)) continue;  // single chunk / spine done in (3)
       const uint64_t j = tbase + s - S0;
+      const uint32_t k = node_level(j, C, s);
+      if (parent_in_tile(j, C, s, k)) continue;
+      uint4* o = reinterpret_cast<uint4*>(nodes + 8ull * (tbase + s));
+      o[0] = make_uint4(cvs[s][0], cvs[s][1], cvs[s][2], cvs[s][3]);
+      o[1] = make_uint4(cvs[s][4], cvs[s][5], cvs[s][6], cvs[s][7]);
+    }
+    __syncthreads();
+  }
+}
+
+// k_leaf_slim: k_leaf_tree's algorithm with a 39 KB LDS image, so four
+// 512-thread workgroups (8 waves per SIMD) fit in a CU's 160 KB when the
+// kernel also fits 64 VGPRs (__launch_bounds__ MINW = 8):
+//   * message starts relative to the tile as u16 (a message other than the
+//     tile's first starts inside it: 1..1024); the first message's start is
+//     the uniform S[m0];
+//   * tree tasks as u16 (left slot | ROOT << 15): the right child of a level-k
+//     task is always 2^(k-1) slots further and a root's message is the owner
+//     of its left slot; tasks are counted per level first, then written
+//     compacted (a tile holds at most kTile - 1 parent compressions).
+constexpr uint16_t kTaskRoot = 0x8000;
+
+// leaf-order bin of chunk j of a message of `len` bytes: 16 - blocks (full
+// chunks first), 0..15
+__device__ __forceinline__ uint32_t leaf_bin(uint64_t len, uint64_t j) {
+  const uint64_t rest = len - j * CHUNK_LEN;
+  const uint32_t clen = len == 0 ? 0u : (uint32_t)min<uint64_t>(CHUNK_LEN, rest);
+  const uint32_t nb = clen == 0 ? 1u : (clen + BLOCK_LEN - 1) / BLOCK_LEN;
+  return 16u - nb;
+}
+
+template <int WG, int PF, int MINW, int ORD = 0>
+__global__ void __launch_bounds__(WG, MINW) k_leaf_slim(const uint8_t* __restrict__ blob,
+                                                        const uint64_t* __restrict__ offs,
+                                                        const uint64_t* __restrict__ lens, uint32_t n,
+                                                        const uint64_t* __restrict__ S,
+                                                        const uint32_t* __restrict__ tile_first,
+                                                        const uint64_t* __restrict__ total_p, uint64_t cap_chunks,
+                                                        uint32_t* __restrict__ nodes, uint8_t* __restrict__ out32,
+                                                        uint64_t* __restrict__ out_keys,
+                                                        const uint32_t* __restrict__ perm) {
+  __shared__ uint32_t cvs[kTile][8];
+  __shared__ uint16_t srel[kTile + 2];
+  __shared__ uint16_t smsg[kTile];
+  __shared__ uint16_t task[kTile];
+  __shared__ uint32_t ntask[12], tbase_k[12];
+  // ORD: leaf order by block count (slots whose chunks have the same number
+  // of blocks share waves, so a partial last chunk does not idle 63 lanes)
+  __shared__ uint16_t order[ORD ? kTile : 1];
+  __shared__ uint32_t obin[ORD ? 17 : 1];
+
+  const uint64_t total = *total_p;
+  if (total > cap_chunks) return;
+  const uint64_t ntiles = (total + kTile - 1) / kTile;
+  const uint32_t tid = threadIdx.x;
+
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const uint64_t tbase = tile * kTile;
+    const uint32_t m0 = tile_first[tile];
+    const uint32_t m1 = (tile + 1 < ntiles) ? tile_first[tile + 1] : n - 1;
+    const uint32_t cnt = m1 - m0 + 1;  // <= kTile + 1
+    const uint64_t lead = tbase - S[m0];  // chunks of the first message before this tile
+    for (uint32_t i = tid + 1; i < cnt; i += WG) srel[i] = (uint16_t)(S[m0 + i] - tbase);
+    if (tid < 12) ntask[tid] = 0;
+    if (ORD && tid < 17) obin[tid] = 0;
+    __syncthreads();
+
+    // (1a) slot -> message; count the tree tasks of every level
+#pragma unroll 1
+    for (uint32_t s = tid; s < kTile; s += WG) {
+      if (tbase + s >= total) {
+        smsg[s] = kNoMsg;
+        continue;
+      }
+      uint32_t lo = 0, hi = cnt - 1;  // last message starting at or before slot s
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (srel[mid] <= s) lo = mid;
+        else hi = mid - 1;
+      }
+      smsg[s] = (uint16_t)lo;
+      const uint64_t j = lo ? (uint64_t)(s - srel[lo]) : lead + s;
+      const uint64_t len = lens[m0 + lo];
+      const uint64_t C = chunk_count(len);
+      if (ORD) atomicAdd(&obin[leaf_bin(len, j)], 1u);
+      if (C == 1) continue;
+      const uint32_t K = node_level(j, C, s);
+      for (uint32_t k = 1; k <= K; ++k) atomicAdd(&ntask[k], 1u);
+      // a message lying wholly in the tile starts here: its spine steps
+      if (j == 0 && (lo || lead == 0) && s + C <= kTile) {
+        const uint32_t c = (uint32_t)C;
+        if (!(c & (c - 1))) {
+          atomicAdd(&ntask[31 - __clz(c)], 1u);
+        } else {
+          uint32_t rem = c & (c - 1);  // the lowest part is not a step of its own
+          while (rem) {
+            const uint32_t part = rem & (0u - rem);
+            atomicAdd(&ntask[32 - __clz(part)], 1u);
+            rem -= part;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t acc = 0;
+      for (int k = 1; k <= 10; ++k) {
+        tbase_k[k] = acc;
+        acc += ntask[k];
+        ntask[k] = 0;
+      }
+      tbase_k[11] = acc;
+      if (ORD) {
+        uint32_t o = 0;
+        for (int b = 0; b < 17; ++b) {
+          const uint32_t c = obin[b];
+          obin[b] = o;
+          o += c;
+        }
+      }
+    }
+    __syncthreads();
+    // (1b) write the tasks, compacted by level
+#pragma unroll 1
+    for (uint32_t s = tid; s < kTile; s += WG) {
+      const uint32_t mi = smsg[s];
+      if (mi == kNoMsg) continue;
+      const uint64_t j = mi ? (uint64_t)(s - srel[mi]) : lead + s;
+      const uint64_t len1 = lens[m0 + mi];
+      const uint64_t C = chunk_count(len1);
+      if (ORD) order[atomicAdd(&obin[leaf_bin(len1, j)], 1u)] = (uint16_t)s;
+      if (C == 1) continue;
+      const uint32_t K = node_level(j, C, s);
+      for (uint32_t k = 1; k <= K; ++k) task[tbase_k[k] + atomicAdd(&ntask[k], 1u)] = (uint16_t)s;
+      if (j == 0 && (mi || lead == 0) && s + C <= kTile) {
+        const uint32_t c = (uint32_t)C;
+        if (!(c & (c - 1))) {
+          const uint32_t k = 31 - __clz(c);
+          task[tbase_k[k] + atomicAdd(&ntask[k], 1u)] = (uint16_t)(s | kTaskRoot);
+        } else {
+          // right-to-left fold over the binary decomposition of c
+          uint32_t rem = c, part = rem & (0u - rem);
+          uint32_t pos = c - part;
+          rem -= part;
+          while (rem) {
+            part = rem & (0u - rem);
+            pos -= part;
+            const uint32_t k = 32 - __clz(part);
+            task[tbase_k[k] + atomicAdd(&ntask[k], 1u)] = (uint16_t)((s + pos) | (rem == part ? kTaskRoot : 0u));
+            rem -= part;
+          }
+        }
+      }
+    }
+
+    // (2) leaves
+    if (ORD) __syncthreads();  // order[] is complete
+    const uint32_t nleaf = ORD ? obin[16] : kTile;
+#pragma unroll 1
+    for (uint32_t i = tid; i < nleaf; i += WG) {
+      const uint32_t s = ORD ? order[i] : i;
+      const uint32_t mi = smsg[s];
+      if (mi == kNoMsg) continue;
+      const uint32_t m = m0 + mi;
+      const uint64_t j = mi ? (uint64_t)(s - srel[mi]) : lead + s;
+      const uint64_t len = lens[m];
+      const uint32_t clen = len == 0 ? 0u : (uint32_t)min<uint64_t>(CHUNK_LEN, len - j * CHUNK_LEN);
+      const bool root = len <= CHUNK_LEN;
+      uint32_t cv[8];
+      if (PF) hash_chunk_pf(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
+      else hash_chunk(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
+      if (root) {
+        store_digest(perm ? perm[m] : m, cv, out32, out_keys);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) cvs[s][i] = cv[i];
+      }
+    }
+    __syncthreads();
+
+    // (3) the tree, level by level
+    for (uint32_t k = 1; k <= 10; ++k) {
+      const uint32_t T = ntask[k];
+      if (T == 0) continue;
+      const uint32_t base = tbase_k[k], half = 1u << (k - 1);
+#pragma unroll 1
+      for (uint32_t t = tid; t < T; t += WG) {
+        const uint32_t e = task[base + t];
+        const uint32_t l = e & 1023u, r = l + half;
+        const bool root = e & kTaskRoot;
+        uint32_t a[8], b[8], o[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          a[q] = cvs[l][q];
+          b[q] = cvs[r][q];
+        }
+        parent(a, b, root, o);
+        if (root) {
+          const uint32_t mm = m0 + smsg[l];
+          store_digest(perm ? perm[mm] : mm, o, out32, out_keys);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) cvs[l][q] = o[q];
+        }
+      }
+      __syncthreads();
+    }
+
+    // (4) maximal in-tile nodes of messages crossing a tile boundary
+#pragma unroll 1
+    for (uint32_t s = tid; s < kTile; s += WG) {
+      const uint32_t mi = smsg[s];
+      if (mi == kNoMsg) continue;
+      const uint64_t C = chunk_count(lens[m0 + mi]);
+      if (C == 1) continue;
+      const bool inside = mi ? (srel[mi] + C <= kTile) : (lead == 0 && C <= kTile);
+      if (inside) continue;
+      const uint64_t j = mi ? (uint64_t)(s - srel[mi]) : lead + s;
       const uint32_t k = node_level(j, C, s);
       if (parent_in_tile(j, C, s, k)) continue;
       uint4* o = reinterpret_cast<uint4*>(nodes + 8ull * (tbase + s));
@@ -483,9 +782,10 @@ __global__ void __launch_bounds__(256) k_shape_scatter(const uint64_t* __restric
 // may arrive over many launches (streamed windows); k_bigfile_finish merges a
 // file's list once all of it is there.
 
-__global__ void __launch_bounds__(kWG) k_piece_tree(const uint8_t* __restrict__ blob,
-                                                    const PieceDesc* __restrict__ pieces, uint32_t npieces,
-                                                    uint32_t* __restrict__ file_nodes) {
+template <int PF, int MINW>
+__global__ void __launch_bounds__(kWG, MINW) k_piece_tree(const uint8_t* __restrict__ blob,
+                                                          const PieceDesc* __restrict__ pieces, uint32_t npieces,
+                                                          uint32_t* __restrict__ file_nodes) {
   __shared__ uint32_t cvs[kTile][8];
   __shared__ uint16_t task[kTile / 2];
   __shared__ uint32_t ntask[16];
@@ -498,7 +798,8 @@ __global__ void __launch_bounds__(kWG) k_piece_tree(const uint8_t* __restrict__ 
     for (uint32_t s = tid; s < nchunks; s += kWG) {
       const uint32_t clen = min(CHUNK_LEN, pd.len - s * CHUNK_LEN);
       uint32_t cv[8];
-      hash_chunk(blob + pd.off + (uint64_t)s * CHUNK_LEN, clen, pd.j0 + s, false, cv);
+      if (PF) hash_chunk_pf(blob + pd.off + (uint64_t)s * CHUNK_LEN, clen, pd.j0 + s, false, cv);
+      else hash_chunk(blob + pd.off + (uint64_t)s * CHUNK_LEN, clen, pd.j0 + s, false, cv);
 #pragma unroll
       for (int i = 0; i < 8; ++i) cvs[s][i] = cv[i];
     }
@@ -724,6 +1025,16 @@ static const LeafVariant kLeafVariants[] = {
     {(const void*)k_leaf_tree<512, 4, 1, 0, 1>, 512},
     // 13: non-temporal (streaming) message loads
     {(const void*)k_leaf_tree<512, 5>, 512},
+    // 14-16: compact LDS (4 workgroups per CU); min waves/SIMD 8, 6; 17: no prefetch
+    {(const void*)k_leaf_slim<512, 1, 8>, 512},
+    {(const void*)k_leaf_slim<512, 1, 6>, 512},
+    {(const void*)k_leaf_slim<512, 0, 8>, 512},
+    // 18: prefetch distance two blocks; 19: 128-byte pair loads
+    {(const void*)k_leaf_tree<512, 6>, 512},
+    {(const void*)k_leaf_tree<512, 7>, 512},
+    // 20, 21: compact LDS + leaf order by block count (6 waves/SIMD); the same without prefetch
+    {(const void*)k_leaf_slim<512, 1, 6, 1>, 512},
+    {(const void*)k_leaf_slim<512, 0, 6, 1>, 512},
 };
 constexpr int kNumLeafVariants = sizeof(kLeafVariants) / sizeof(kLeafVariants[0]);
 constexpr int kDefaultLeafVariant = 1;
@@ -797,7 +1108,14 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
 hipError_t piece_hash(const uint8_t* blob, const PieceDesc* pieces, uint32_t npieces, uint32_t* file_nodes,
                       hipStream_t st) {
   if (!npieces) return hipSuccess;
-  hipLaunchKernelGGL(k_piece_tree, dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
+  // SDCAS_PIECE_VARIANT (A/B): 0 = plain block loop, 1 = block prefetch at 8 waves/SIMD (default)
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("SDCAS_PIECE_VARIANT");
+    v = e ? atoi(e) : 1;
+  }
+  if (v == 0) hipLaunchKernelGGL((k_piece_tree<0, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
+  else hipLaunchKernelGGL((k_piece_tree<1, 8>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   return hipGetLastError();
 }
 

@@ -1,0 +1,377 @@
+// sdcore.cpp — C++ host mirror of sd-core's content-identification path over
+// libsdcas (see include/sdcore.hpp for the reference file:line of each entry).
+#include "sdcore.hpp"
+
+#include <sys/stat.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cstring>
+#include <set>
+#include <unordered_map>
+
+namespace sdcore {
+
+std::string IoError::message() const {
+  std::string m = unexpected_eof() ? "failed to fill whole buffer" : std::strerror(code);
+  return path.empty() ? m : m + " <path='" + path + "'>";
+}
+
+// ---- Engine -------------------------------------------------------------------
+
+void Engine::fail(int rc, const char* what) const {
+  throw LibraryError(rc, std::string(what) + ": " + sdcas_last_error(ctx_));
+}
+
+std::unique_ptr<Engine> Engine::open(const Options& o) {
+  sdcas_options opts{o.device, o.io_threads, o.staging_bytes};
+  sdcas_ctx* c = nullptr;
+  const int rc = sdcas_init(&opts, &c);
+  if (rc != SDCAS_OK) {
+    std::string msg = c ? sdcas_last_error(c) : "sdcas_init failed";
+    if (c) sdcas_destroy(c);
+    throw LibraryError(rc, msg);
+  }
+  return std::unique_ptr<Engine>(new Engine(c));
+}
+
+Engine::~Engine() { sdcas_destroy(ctx_); }
+
+std::string key_to_hex(uint64_t key) {
+  char b[17];
+  sdcas_key_to_hex(key, b);
+  return std::string(b, 16);
+}
+
+uint64_t hex_to_key(const std::string& cas_id) {
+  if (cas_id.size() != 16) throw std::invalid_argument("cas_id must be 16 hex chars: " + cas_id);
+  return std::stoull(cas_id, nullptr, 16);
+}
+
+std::vector<Result<std::string>> Engine::generate_cas_ids(
+    const std::vector<std::pair<std::string, uint64_t>>& files) {
+  const size_t n = files.size();
+  std::vector<const char*> paths(n);
+  std::vector<uint64_t> sizes(n), keys(n);
+  std::vector<int32_t> st(n);
+  for (size_t i = 0; i < n; ++i) {
+    paths[i] = files[i].first.c_str();
+    sizes[i] = files[i].second;
+  }
+  if (n) {
+    const int rc = sdcas_cas_ids(ctx_, paths.data(), sizes.data(), n, keys.data(), st.data());
+    if (rc != SDCAS_OK) fail(rc, "sdcas_cas_ids");
+  }
+  std::vector<Result<std::string>> out;
+  out.reserve(n);
+  for (size_t i = 0; i < n; ++i) {
+    if (st[i]) out.emplace_back(IoError{st[i], files[i].first});
+    else out.emplace_back(key_to_hex(keys[i]));
+  }
+  return out;
+}
+
+std::vector<Result<std::string>> Engine::file_checksums(const std::vector<std::string>& files) {
+  const size_t n = files.size();
+  std::vector<const char*> paths(n);
+  std::vector<uint8_t> d(32 * n);
+  std::vector<int32_t> st(n);
+  for (size_t i = 0; i < n; ++i) paths[i] = files[i].c_str();
+  if (n) {
+    const int rc = sdcas_checksums(ctx_, paths.data(), n, d.data(), st.data());
+    if (rc != SDCAS_OK) fail(rc, "sdcas_checksums");
+  }
+  std::vector<Result<std::string>> out;
+  out.reserve(n);
+  for (size_t i = 0; i < n; ++i) {
+    if (st[i]) {
+      out.emplace_back(IoError{st[i], files[i]});
+    } else {
+      char h[65];
+      sdcas_digest_to_hex(&d[32 * i], h);
+      out.emplace_back(std::string(h, 64));
+    }
+  }
+  return out;
+}
+
+Engine::Dedup Engine::dedup(const std::vector<uint64_t>& keys, const std::vector<uint8_t>& has_key,
+                            const std::vector<int32_t>& status, size_t chunk_size,
+                            const std::vector<uint64_t>& existing_keys) {
+  const size_t n = keys.size();
+  if (has_key.size() != n || (!status.empty() && status.size() != n))
+    throw std::invalid_argument("dedup: keys / has_key / status lengths differ");
+  Dedup r;
+  r.link.assign(n, 0);
+  if (!n) return r;
+  const int rc = sdcas_dedup(ctx_, keys.data(), has_key.data(), status.empty() ? nullptr : status.data(), n,
+                             chunk_size, existing_keys.empty() ? nullptr : existing_keys.data(),
+                             existing_keys.size(), r.link.data(), &r.created, &r.linked);
+  if (rc != SDCAS_OK) fail(rc, "sdcas_dedup");
+  return r;
+}
+
+Result<std::string> generate_cas_id(Engine& engine, const std::string& path, uint64_t size) {
+  return std::move(engine.generate_cas_ids({{path, size}})[0]);
+}
+
+Result<std::string> file_checksum(Engine& engine, const std::string& path) {
+  return std::move(engine.file_checksums({path})[0]);
+}
+
+// ---- paths --------------------------------------------------------------------
+
+std::string full_path(const Location& location, const FilePathRow& row) {
+  // assemble_relative_path: materialized_path without its leading '/', then
+  // name, then ".extension" for a file with a non-empty extension
+  std::string rel = row.materialized_path.size() > 1 ? row.materialized_path.substr(1) : std::string();
+  rel += row.name;
+  if (!row.is_dir && !row.extension.empty()) rel += "." + row.extension;
+  std::string base = location.path;
+  if (!base.empty() && base.back() != '/') base += '/';
+  return base + rel;
+}
+
+// ---- MemoryLibrary ------------------------------------------------------------------
+
+static PubId pub_id_of(uint32_t tag, int32_t id) {
+  PubId p{};
+  std::memcpy(p.data(), &tag, 4);
+  std::memcpy(p.data() + 4, &id, 4);
+  return p;
+}
+
+FilePathRow& MemoryLibrary::add_file_path(FilePathRow row) {
+  if (row.id == 0) row.id = next_file_path_id_;
+  next_file_path_id_ = std::max(next_file_path_id_, row.id + 1);
+  if (row.pub_id == PubId{}) row.pub_id = pub_id_of(0x46504154u, row.id);
+  auto it = std::lower_bound(file_paths.begin(), file_paths.end(), row.id,
+                             [](const FilePathRow& a, int32_t id) { return a.id < id; });
+  if (it != file_paths.end() && it->id == row.id) throw std::invalid_argument("duplicate file_path id");
+  return *file_paths.insert(it, std::move(row));
+}
+
+FilePathRow* MemoryLibrary::find(int32_t id) {
+  auto it = std::lower_bound(file_paths.begin(), file_paths.end(), id,
+                             [](const FilePathRow& a, int32_t v) { return a.id < v; });
+  return it != file_paths.end() && it->id == id ? &*it : nullptr;
+}
+
+const FilePathRow* MemoryLibrary::file_path(int32_t id) const {
+  return const_cast<MemoryLibrary*>(this)->find(id);
+}
+
+static bool under(const FilePathRow& r, const std::string& sub) {
+  return sub.empty() || r.materialized_path.compare(0, sub.size(), sub) == 0;
+}
+
+bool MemoryLibrary::orphan(const FilePathRow& r, int32_t location_id, const std::string& sub) const {
+  return (!r.object_id || !r.cas_id) && !r.is_dir && r.location_id == location_id && r.size_in_bytes != 0 &&
+         under(r, sub);
+}
+
+size_t MemoryLibrary::count_orphan_file_paths(int32_t location_id, const std::string& sub) {
+  return (size_t)std::count_if(file_paths.begin(), file_paths.end(),
+                               [&](const FilePathRow& r) { return orphan(r, location_id, sub); });
+}
+
+std::vector<FilePathRow> MemoryLibrary::get_orphan_file_paths(int32_t location_id, int32_t cursor,
+                                                              const std::string& sub, size_t take) {
+  std::vector<FilePathRow> out;
+  for (const auto& r : file_paths) {
+    if (out.size() >= take) break;
+    if (r.id >= cursor && orphan(r, location_id, sub)) out.push_back(r);
+  }
+  return out;
+}
+
+void MemoryLibrary::set_cas_id(int32_t id, const std::optional<std::string>& cas_id) {
+  if (auto* r = find(id)) r->cas_id = cas_id;
+}
+
+std::vector<std::pair<int32_t, std::vector<std::string>>> MemoryLibrary::existing_objects(
+    const std::vector<std::string>& cas_ids) {
+  const std::set<std::string> want(cas_ids.begin(), cas_ids.end());
+  std::map<int32_t, std::vector<std::string>> by_object;  // object id order = DB order
+  std::set<int32_t> hit;
+  for (const auto& r : file_paths) {
+    if (!r.object_id) continue;
+    if (r.cas_id && want.count(*r.cas_id)) hit.insert(*r.object_id);
+  }
+  for (const auto& r : file_paths)
+    if (r.object_id && hit.count(*r.object_id) && r.cas_id) by_object[*r.object_id].push_back(*r.cas_id);
+  return {by_object.begin(), by_object.end()};
+}
+
+int32_t MemoryLibrary::create_object(ObjectKind kind, int64_t date_created) {
+  ObjectRow o;
+  o.id = next_object_id_++;
+  o.pub_id = pub_id_of(0x4F424A54u, o.id);
+  o.kind = kind;
+  o.date_created = date_created;
+  objects.push_back(o);
+  return o.id;
+}
+
+void MemoryLibrary::connect(int32_t file_path_id, int32_t object_id) {
+  if (auto* r = find(file_path_id)) r->object_id = object_id;
+}
+
+std::vector<FilePathRow> MemoryLibrary::file_paths_without_checksum(int32_t location_id, const std::string& sub) {
+  std::vector<FilePathRow> out;
+  for (const auto& r : file_paths)
+    if (r.location_id == location_id && !r.is_dir && !r.integrity_checksum && under(r, sub)) out.push_back(r);
+  return out;
+}
+
+void MemoryLibrary::set_integrity_checksum(int32_t id, const std::string& checksum) {
+  if (auto* r = find(id)) r->integrity_checksum = checksum;
+}
+
+// ---- file_identifier ----------------------------------------------------------------
+
+std::vector<Result<FileMetadata>> file_metadata_batch(Engine& engine,
+                                                      const std::vector<std::pair<std::string, ObjectKind>>& files) {
+  const size_t n = files.size();
+  std::vector<std::optional<IoError>> err(n);
+  std::vector<FileMetadata> md(n);
+  std::vector<std::pair<std::string, uint64_t>> to_hash;
+  std::vector<size_t> hashed_index;
+  for (size_t i = 0; i < n; ++i) {
+    struct stat sb;
+    if (::stat(files[i].first.c_str(), &sb) != 0) {  // fs::metadata (mod.rs:63-65)
+      err[i] = IoError{errno, files[i].first};
+      continue;
+    }
+    if (S_ISDIR(sb.st_mode)) throw std::logic_error("We can't generate cas_id for directories");  // mod.rs:67-70
+    md[i].kind = files[i].second;
+    md[i].len = (uint64_t)sb.st_size;
+    if (md[i].len != 0) {  // mod.rs:78-86: empty files get no cas_id
+      to_hash.emplace_back(files[i].first, md[i].len);
+      hashed_index.push_back(i);
+    }
+  }
+  auto cas = engine.generate_cas_ids(to_hash);
+  for (size_t k = 0; k < cas.size(); ++k) {
+    const size_t i = hashed_index[k];
+    if (cas[k].ok()) md[i].cas_id = cas[k].value();
+    else err[i] = cas[k].error();
+  }
+  std::vector<Result<FileMetadata>> out;
+  out.reserve(n);
+  for (size_t i = 0; i < n; ++i) {
+    if (err[i]) out.emplace_back(*err[i]);
+    else out.emplace_back(std::move(md[i]));
+  }
+  return out;
+}
+
+std::pair<size_t, size_t> identifier_job_step(Engine& engine, Library& db, const Location& location,
+                                              const std::vector<FilePathRow>& file_paths, size_t chunk_size) {
+  const size_t n = file_paths.size();
+  std::vector<std::pair<std::string, ObjectKind>> files(n);
+  for (size_t i = 0; i < n; ++i) files[i] = {full_path(location, file_paths[i]), file_paths[i].kind};
+  // FileMetadata::new for every row (mod.rs:105-147): failing files are
+  // logged and left out of the rest of the step (mod.rs:125-141)
+  auto md = file_metadata_batch(engine, files);
+
+  std::vector<uint64_t> keys(n, 0);
+  std::vector<uint8_t> has_key(n, 0);
+  std::vector<int32_t> status(n, 0);
+  std::vector<std::string> unique;
+  std::set<std::string> seen;
+  for (size_t i = 0; i < n; ++i) {
+    if (!md[i].ok()) {
+      status[i] = md[i].error().code;
+      continue;
+    }
+    const auto& cas = md[i].value().cas_id;
+    if (cas) {
+      keys[i] = hex_to_key(*cas);
+      has_key[i] = 1;
+      if (seen.insert(*cas).second) unique.push_back(*cas);
+    }
+    db.set_cas_id(file_paths[i].id, cas);  // mod.rs:157-178
+  }
+  // existing Objects carrying any of these cas_ids, DB order (mod.rs:181-188);
+  // one existing-key entry per (object, cas_id) so "the first object whose
+  // file_paths carry the cas_id" (mod.rs:214-224) is the first entry
+  auto existing = db.existing_objects(unique);
+  std::vector<uint64_t> ekeys;
+  std::vector<int32_t> eobj;
+  for (const auto& [oid, cas_ids] : existing)
+    for (const auto& c : cas_ids) {
+      ekeys.push_back(hex_to_key(c));
+      eobj.push_back(oid);
+    }
+  auto d = engine.dedup(keys, has_key, status, chunk_size, ekeys);
+  // links and new Objects (mod.rs:202-342): new Objects take the kind and
+  // date_created of their file (mod.rs:266-291)
+  std::vector<int32_t> created_object(n, 0);
+  for (size_t i = 0; i < n; ++i) {
+    const int64_t l = d.link[i];
+    if (l == INT64_MIN) continue;
+    if (l == (int64_t)i) {
+      created_object[i] = db.create_object(md[i].value().kind, file_paths[i].date_created);
+      db.connect(file_paths[i].id, created_object[i]);
+    } else if (l >= 0) {
+      db.connect(file_paths[i].id, created_object[(size_t)l]);
+    } else {
+      db.connect(file_paths[i].id, eobj[(size_t)(-(l + 1))]);
+    }
+  }
+  return {(size_t)d.created, (size_t)d.linked};
+}
+
+FileIdentifierJobRunMetadata run_file_identifier_job(Engine& engine, Library& db, const FileIdentifierJobInit& init) {
+  FileIdentifierJobRunMetadata meta;
+  const size_t batch = std::max<size_t>(1, init.batch);
+  const int32_t loc = init.location.id;
+  // init (file_identifier_job.rs:125-176)
+  meta.total_orphan_paths = db.count_orphan_file_paths(loc, init.sub_materialized_path);
+  if (meta.total_orphan_paths == 0) return meta;
+  auto first = db.get_orphan_file_paths(loc, 0, init.sub_materialized_path, 1);
+  meta.cursor = first.empty() ? 0 : first[0].id;
+  const size_t task_count = (meta.total_orphan_paths + batch - 1) / batch;
+  // execute_step (file_identifier_job.rs:178-223)
+  for (size_t step = 0; step < task_count; ++step) {
+    auto rows = db.get_orphan_file_paths(loc, meta.cursor, init.sub_materialized_path, batch);
+    if (rows.empty()) {
+      meta.early_finish = true;
+      break;
+    }
+    auto [created, linked] = identifier_job_step(engine, db, init.location, rows);
+    meta.total_objects_created += created;
+    meta.total_objects_linked += linked;
+    meta.cursor = rows.back().id;  // process_identifier_file_paths (mod.rs:394-403)
+    ++meta.steps;
+  }
+  return meta;
+}
+
+// ---- object validator -----------------------------------------------------------------
+
+ObjectValidatorReport run_object_validator_job(Engine& engine, Library& db, const ObjectValidatorJobInit& init) {
+  ObjectValidatorReport rep;
+  auto rows = db.file_paths_without_checksum(init.location.id, init.sub_materialized_path);
+  rep.task_count = rows.size();
+  const size_t batch = std::max<size_t>(1, init.batch);
+  for (size_t lo = 0; lo < rows.size(); lo += batch) {
+    const size_t hi = std::min(rows.size(), lo + batch);
+    std::vector<std::string> paths;
+    for (size_t i = lo; i < hi; ++i) paths.push_back(full_path(init.location, rows[i]));
+    auto sums = engine.file_checksums(paths);
+    for (size_t i = lo; i < hi; ++i) {
+      const auto& r = sums[i - lo];
+      if (!r.ok()) {  // validator_job.rs:154-156: the step fails with FileIO
+        rep.error = r.error();
+        return rep;
+      }
+      db.set_integrity_checksum(rows[i].id, r.value());  // validator_job.rs:158-172
+      ++rep.checksummed;
+    }
+  }
+  return rep;
+}
+
+}  // namespace sdcore

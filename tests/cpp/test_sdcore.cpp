@@ -1,0 +1,286 @@
+// Tests of the C++ host mirror (include/sdcore.hpp) against the CPU oracle.
+// TEST INFRASTRUCTURE: links oracle/build/liboracle.so as the checker.
+//
+//   test_sdcore            full run on a GPU (cas_ids, checksums, errors,
+//                          identifier job at batch 100 and 1000, validator)
+//   test_sdcore --no-gpu   checks that Engine::open fails loudly (LibraryError)
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../../oracle/oracle.h"
+#include "sdcore.hpp"
+
+using namespace sdcore;
+
+static int failures = 0;
+#define CHECK(cond, ...)                                       \
+  do {                                                         \
+    if (!(cond)) {                                             \
+      ++failures;                                              \
+      std::fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__); \
+      std::fprintf(stderr, __VA_ARGS__);                       \
+      std::fprintf(stderr, "\n");                              \
+    }                                                          \
+  } while (0)
+
+static void write_file(const std::string& path, const std::vector<uint8_t>& data) {
+  FILE* f = std::fopen(path.c_str(), "wb");
+  if (!f) {
+    std::perror(path.c_str());
+    std::exit(2);
+  }
+  if (!data.empty()) std::fwrite(data.data(), 1, data.size(), f);
+  std::fclose(f);
+}
+
+static std::vector<uint8_t> content(uint64_t seed, size_t n) {
+  std::mt19937_64 g(seed);
+  std::vector<uint8_t> v(n);
+  for (size_t i = 0; i < n; i += 8) {
+    const uint64_t x = g();
+    std::memcpy(&v[i], &x, std::min<size_t>(8, n - i));
+  }
+  return v;
+}
+
+static std::string oracle_cas(const std::string& p, uint64_t size, int* st) {
+  char h[17];
+  *st = oracle_generate_cas_id(p.c_str(), size, h);
+  return *st ? std::string() : std::string(h, 16);
+}
+
+static std::string oracle_sum(const std::string& p) {
+  char h[65];
+  return oracle_file_checksum(p.c_str(), h) ? std::string() : std::string(h, 64);
+}
+
+static void test_hashes(Engine& eng, const std::string& dir) {
+  const std::vector<size_t> sizes = {0, 1, 1023, 1024, 1025, 65536, 102400, 102401, 300000, (3u << 20) + 17};
+  std::vector<std::pair<std::string, uint64_t>> files;
+  std::vector<std::string> paths;
+  for (size_t i = 0; i < sizes.size(); ++i) {
+    const std::string p = dir + "/h" + std::to_string(i) + ".bin";
+    write_file(p, content(100 + i, sizes[i]));
+    files.emplace_back(p, sizes[i]);
+    paths.push_back(p);
+  }
+  auto cas = eng.generate_cas_ids(files);
+  auto sums = eng.file_checksums(paths);
+  for (size_t i = 0; i < sizes.size(); ++i) {
+    int st;
+    const std::string want = oracle_cas(paths[i], sizes[i], &st);
+    CHECK(cas[i].ok() && cas[i].value() == want, "cas_id size %zu", sizes[i]);
+    CHECK(sums[i].ok() && sums[i].value() == oracle_sum(paths[i]), "checksum size %zu", sizes[i]);
+  }
+  // single-file forms (cas.rs:23, hash.rs:11)
+  auto one = generate_cas_id(eng, paths[3], sizes[3]);
+  CHECK(one.ok() && one.value() == cas[3].value(), "generate_cas_id single");
+  auto s1 = file_checksum(eng, paths[9]);
+  CHECK(s1.ok() && s1.value() == sums[9].value(), "file_checksum single");
+  // errors: a missing file is ENOENT; a file shorter than the sampled
+  // windows of its recorded size is UnexpectedEof (cas.rs:36,43,56)
+  auto miss = generate_cas_id(eng, dir + "/missing.bin", 5000);
+  CHECK(!miss.ok() && miss.error().code == ENOENT, "missing file -> ENOENT (%d)", miss.ok() ? 0 : miss.error().code);
+  const std::string shrunk = dir + "/shrunk.bin";
+  write_file(shrunk, content(7, 20000));
+  auto eof = generate_cas_id(eng, shrunk, 500000);
+  int st;
+  oracle_cas(shrunk, 500000, &st);
+  CHECK(!eof.ok() && eof.error().unexpected_eof() && st == ORACLE_STATUS_UNEXPECTED_EOF, "shrunk -> UnexpectedEof");
+  auto sm = file_checksum(eng, dir + "/missing.bin");
+  CHECK(!sm.ok() && sm.error().code == ENOENT, "checksum missing -> ENOENT");
+  // file_metadata_batch: empty files have no cas_id (mod.rs:78-86)
+  auto md = file_metadata_batch(eng, {{paths[0], 3}, {paths[4], 1}, {dir + "/missing.bin", 0}});
+  CHECK(md[0].ok() && !md[0].value().cas_id && md[0].value().kind == 3, "empty file metadata");
+  CHECK(md[1].ok() && md[1].value().cas_id == cas[4].value() && md[1].value().len == 1025, "metadata cas_id");
+  CHECK(!md[2].ok() && md[2].error().code == ENOENT, "metadata of a missing file");
+  std::printf("hashes: %zu files ok\n", sizes.size());
+}
+
+// a location of `n` files: contents drawn from `distinct` seeds (duplicates in
+// and across 100-row chunks), some empty, one row whose file is missing
+struct Corpus {
+  MemoryLibrary lib;
+  Location loc;
+  std::vector<uint64_t> keys;
+  std::vector<uint8_t> has_key;
+  std::vector<int32_t> status;
+  std::vector<uint64_t> existing;  // pre-existing Object keys, DB order
+};
+
+static Corpus make_corpus(const std::string& dir, size_t n, size_t distinct) {
+  Corpus c;
+  c.loc = {1, dir};
+  std::mt19937_64 g(42);
+  mkdir((dir + "/sub").c_str(), 0755);
+  // two pre-existing Objects, each with an identified file_path
+  for (int e = 0; e < 2; ++e) {
+    const std::string name = "old" + std::to_string(e);
+    const auto data = content(1000 + e, 5000);  // the same contents as seeds 0 and 1 below
+    write_file(dir + "/" + name + ".dat", data);
+    int st;
+    const std::string cas = oracle_cas(dir + "/" + name + ".dat", data.size(), &st);
+    const int32_t oid = c.lib.create_object(0, 0);
+    FilePathRow r;
+    r.location_id = 1;
+    r.name = name;
+    r.extension = "dat";
+    r.size_in_bytes = data.size();
+    r.cas_id = cas;
+    r.object_id = oid;
+    c.lib.add_file_path(r);
+    c.existing.push_back(hex_to_key(cas));
+  }
+  for (size_t i = 0; i < n; ++i) {
+    FilePathRow r;
+    r.location_id = 1;
+    r.materialized_path = (i % 3 == 0) ? "/sub/" : "/";
+    r.name = "f" + std::to_string(i);
+    r.extension = (i % 5 == 0) ? "" : "bin";
+    r.date_created = (int64_t)i;
+    r.kind = (int32_t)(i % 7);
+    const std::string p = full_path(c.loc, r);
+    size_t which = g() % distinct;
+    if (which % 13 == 5 && i % 100 == 99) ++which;  // an empty file at a chunk end would be re-fetched (cursor id >= last)
+    size_t size = which % 13 == 5 ? 0 : 100 + (which * 7919) % 150000;
+    std::vector<uint8_t> data = which < 2 ? content(1000 + which, 5000) : content(which, size);
+    const bool missing = (i == n / 2);
+    if (!missing) write_file(p, data);
+    r.size_in_bytes = data.empty() ? 1 : data.size();  // DB size: non-zero (orphan filter)
+    c.lib.add_file_path(r);
+    int st = 0;
+    const std::string cas = missing || data.empty() ? std::string() : oracle_cas(p, data.size(), &st);
+    c.keys.push_back(cas.empty() ? 0 : hex_to_key(cas));
+    c.has_key.push_back(!cas.empty());
+    c.status.push_back(missing ? ENOENT : st);
+  }
+  return c;
+}
+
+static void test_identifier_job(Engine& eng, const std::string& dir) {
+  const size_t n = 1000;
+  std::vector<std::vector<int32_t>> objects_by_batch;
+  for (size_t batch : {100, 1000}) {
+    const std::string d = dir + "/loc" + std::to_string(batch);
+    mkdir(d.c_str(), 0755);
+    Corpus c = make_corpus(d, n, 300);
+    // the oracle: reference chunks of 100 over the orphans in id order
+    std::vector<int64_t> link(n);
+    int64_t linked = 0;
+    const int64_t created = oracle_identifier_dedup(n, c.keys.data(), c.has_key.data(), c.status.data(), 100,
+                                                    c.existing.size(), c.existing.data(), link.data(), &linked);
+    FileIdentifierJobInit init{c.loc, "", batch};
+    auto meta = run_file_identifier_job(eng, c.lib, init);
+    CHECK(meta.total_orphan_paths == n, "orphans %zu", meta.total_orphan_paths);
+    CHECK((int64_t)meta.total_objects_created == created && (int64_t)meta.total_objects_linked == linked,
+          "batch %zu: created/linked %zu/%zu, oracle %lld/%lld", batch, meta.total_objects_created,
+          meta.total_objects_linked, (long long)created, (long long)linked);
+    CHECK(meta.steps == (n + batch - 1) / batch, "steps %zu", meta.steps);
+    // every file's Object follows the oracle's link
+    std::vector<int32_t> obj(n, 0);
+    for (size_t i = 0; i < n; ++i) obj[i] = c.lib.file_path((int32_t)(i + 3))->object_id.value_or(-1);
+    for (size_t i = 0; i < n; ++i) {
+      const int64_t l = link[i];
+      if (l == INT64_MIN) CHECK(obj[i] == -1, "dropped file %zu has an Object", i);
+      else if (l < 0) CHECK(obj[i] == (int32_t)(-(l + 1)) + 1, "file %zu -> existing %lld got %d", i, (long long)l, obj[i]);
+      else if (l < (int64_t)i) CHECK(obj[i] == obj[(size_t)l], "file %zu shares file %lld's Object", i, (long long)l);
+      else CHECK(obj[i] > 2, "file %zu owns a new Object", i);
+    }
+    // new Objects carry their file's kind and date_created (mod.rs:266-291)
+    for (size_t i = 0; i < n; ++i)
+      if (link[i] == (int64_t)i) {
+        const auto& o = c.lib.objects[(size_t)obj[i] - 1];
+        CHECK(o.kind == (int32_t)(i % 7) && o.date_created == (int64_t)i, "object of file %zu", i);
+      }
+    // cas_id written per processed file (mod.rs:157-178)
+    for (size_t i = 0; i < n; ++i) {
+      const auto* r = c.lib.file_path((int32_t)(i + 3));
+      if (c.status[i]) CHECK(!r->cas_id, "failed file %zu has a cas_id", i);
+      else if (c.has_key[i]) CHECK(r->cas_id && hex_to_key(*r->cas_id) == c.keys[i], "cas_id of file %zu", i);
+    }
+    // a second run finds only the failed row (and the empty files, which
+    // keep cas_id NULL and are orphans again, as in the reference)
+    size_t empties = 0;
+    for (size_t i = 0; i < n; ++i) empties += !c.status[i] && !c.has_key[i];
+    CHECK(c.lib.count_orphan_file_paths(1, "") == 1 + empties, "orphans left %zu", c.lib.count_orphan_file_paths(1, ""));
+    // sub-path filter (materialized_path LIKE '/sub/%')
+    size_t sub = 0;
+    for (const auto& r : c.lib.file_paths) sub += r.materialized_path == "/sub/" && (!r.object_id || !r.cas_id);
+    CHECK(c.lib.count_orphan_file_paths(1, "/sub/") == sub, "sub orphans");
+    objects_by_batch.push_back(obj);
+    std::printf("identifier job batch %zu: created %zu linked %zu steps %zu\n", batch, meta.total_objects_created,
+                meta.total_objects_linked, meta.steps);
+  }
+  CHECK(objects_by_batch[0] == objects_by_batch[1], "batch 100 and batch 1000 give the same Objects");
+}
+
+static void test_validator(Engine& eng, const std::string& dir) {
+  const std::string d = dir + "/val";
+  mkdir(d.c_str(), 0755);
+  MemoryLibrary lib;
+  Location loc{2, d};
+  std::vector<std::string> paths;
+  for (int i = 0; i < 250; ++i) {
+    FilePathRow r;
+    r.location_id = 2;
+    r.name = "v" + std::to_string(i);
+    r.extension = "bin";
+    r.size_in_bytes = 1;
+    if (i == 7) r.integrity_checksum = std::string(64, '0');  // already validated: not selected
+    const auto& row = lib.add_file_path(r);
+    write_file(full_path(loc, row), content(5000 + i, i == 11 ? (2u << 20) + 5 : 37 * i));
+    paths.push_back(full_path(loc, row));
+  }
+  ObjectValidatorJobInit init{loc, "", 64};
+  auto rep = run_object_validator_job(eng, lib, init);
+  CHECK(rep.task_count == 249 && rep.checksummed == 249 && !rep.error, "validator %zu/%zu", rep.checksummed,
+        rep.task_count);
+  for (int i = 0; i < 250; ++i) {
+    const auto* r = lib.file_path(i + 1);
+    if (i == 7) CHECK(*r->integrity_checksum == std::string(64, '0'), "pre-validated row changed");
+    else CHECK(r->integrity_checksum && *r->integrity_checksum == oracle_sum(paths[i]), "checksum %d", i);
+  }
+  // a missing file stops the job at that row (validator_job.rs:154-156)
+  MemoryLibrary lib2;
+  for (int i = 0; i < 5; ++i) {
+    FilePathRow r;
+    r.location_id = 2;
+    r.name = i == 3 ? "gone" : "v" + std::to_string(i);
+    r.extension = "bin";
+    lib2.add_file_path(r);
+  }
+  auto rep2 = run_object_validator_job(eng, lib2, init);
+  CHECK(rep2.error && rep2.error->code == ENOENT && rep2.checksummed == 3, "validator error stop");
+  std::printf("validator: %zu checksums ok\n", rep.checksummed);
+}
+
+int main(int argc, char** argv) {
+  if (argc > 1 && std::strcmp(argv[1], "--no-gpu") == 0) {
+    try {
+      auto e = Engine::open();
+      std::fprintf(stderr, "Engine::open succeeded without a GPU\n");
+      return 1;
+    } catch (const LibraryError& e) {
+      std::printf("Engine::open -> LibraryError %d (%s)\n", e.code, e.what());
+      return e.code == SDCAS_E_NO_DEVICE ? 0 : 1;
+    }
+  }
+  char tmpl[] = "/tmp/sdcore_testXXXXXX";
+  const std::string dir = mkdtemp(tmpl);
+  auto eng = Engine::open();
+  test_hashes(*eng, dir);
+  test_identifier_job(*eng, dir);
+  test_validator(*eng, dir);
+  std::string cmd = "rm -rf " + dir;
+  if (std::system(cmd.c_str()) != 0) std::fprintf(stderr, "cleanup failed\n");
+  std::printf("%s (%d failures)\n", failures ? "FAILED" : "ALL OK", failures);
+  return failures ? 1 : 0;
+}
