@@ -18,6 +18,8 @@
 // passes; no atomics.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+
+#include <algorithm>
 #include <stdint.h>
 
 #include "dedup.h"
@@ -83,12 +85,13 @@ __global__ void k_dedup_count(const int64_t* __restrict__ out_link, const uint8_
   __shared__ unsigned long long sc[2];
   if (threadIdx.x < 2) sc[threadIdx.x] = 0;
   __syncthreads();
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  // grid-stride over a bounded grid: one global atomic pair per workgroup
+  // (thousands of workgroups adding to one address serialise in L2)
   unsigned long long c = 0, l = 0;
-  if (i < n) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const int64_t v = out_link[i];
-    if (v == (int64_t)i) c = 1;
-    else if (v != INT64_MIN && valid[i]) l = 1;
+    if (v == (int64_t)i) c += 1;
+    else if (v != INT64_MIN && valid[i]) l += 1;
   }
   // wave-level sums, then one LDS atomic per wave
   for (int off = 32; off > 0; off >>= 1) {
@@ -156,7 +159,8 @@ hipError_t dedup_run(DedupWorkspace& w, const uint64_t* keys, const uint8_t* has
                      eidx_sorted, ne, chunk_size, out_link);
   if (d_counts) {
     (void)hipMemsetAsync(d_counts, 0, 2 * sizeof(unsigned long long), st);
-    hipLaunchKernelGGL(k_dedup_count, dim3(nb), dim3(tb), 0, st, out_link, w.valid, n, d_counts);
+    hipLaunchKernelGGL(k_dedup_count, dim3(std::min<uint32_t>(nb, 1024)), dim3(tb), 0, st, out_link, w.valid, n,
+                       d_counts);
   }
   return hipGetLastError();
 }

@@ -126,9 +126,10 @@ __global__ void k_dd_apply(const uint64_t* __restrict__ ids, const uint32_t* __r
   __shared__ unsigned long long sc[2];
   if (threadIdx.x < 2) sc[threadIdx.x] = 0;
   __syncthreads();
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  // grid-stride over a bounded grid: one global atomic pair per workgroup
+  // (thousands of workgroups adding to one address serialise in L2)
   unsigned long long c = 0, l = 0;
-  if (i < n) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint32_t s = slot[i];
     const int64_t me = (int64_t)ids[i];
     int64_t v;
@@ -142,8 +143,8 @@ __global__ void k_dd_apply(const uint64_t* __restrict__ ids, const uint32_t* __r
       else v = ((uint64_t)me / cs == (uint64_t)r / cs) ? me : r;  // created in the key's first chunk
     }
     link[i] = v;
-    if (v == me) c = 1;
-    else if (v != INT64_MIN) l = 1;
+    if (v == me) c += 1;
+    else if (v != INT64_MIN) l += 1;
   }
   for (int off = 32; off > 0; off >>= 1) {
     c += __shfl_down(c, off);
@@ -273,7 +274,7 @@ hipError_t dd_resolve(DistWs& w, const uint64_t* frec, uint32_t nf, const uint64
 hipError_t dd_apply(const uint64_t* ids, const uint32_t* slot, uint32_t n, const int64_t* result, uint64_t chunk_size,
                     int64_t* link, unsigned long long* counts, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_dd_apply, dim3(blocks(n)), dim3(TB), 0, st, ids, slot, n, result, chunk_size ? chunk_size : 100,
+  hipLaunchKernelGGL(k_dd_apply, dim3(blocks(n) < 1024 ? blocks(n) : 1024), dim3(TB), 0, st, ids, slot, n, result, chunk_size ? chunk_size : 100,
                      link, counts);
   return hipGetLastError();
 }
