@@ -18,7 +18,8 @@ struct BatchWorkspace {
   void* scan_tmp = nullptr;
   size_t scan_tmp_bytes = 0;
   uint32_t cap_msgs = 0;
-  uint64_t cap_chunks = 0;
+  uint64_t cap_chunks = 0;  // chunks a batch of up to cap_msgs messages may hold
+  uint64_t cap_slots = 0;   // slots the workspace holds (chunks + the quad layout's padding)
   int variant = -1;  // leaf kernel variant (-1: default / SDCAS_LEAF_VARIANT)
   // length-sorted slot order (messages of equal length share waves, so the
   // lanes of a wave run the same number of blocks): perm[slot-order index] =

@@ -652,6 +652,351 @@ __global__ void __launch_bounds__(WG, MINW) k_leaf_slim(const uint8_t* __restric
   }
 }
 
+// ---- quad layout: four consecutive chunks per lane ----------------------------
+//
+// The in-tile tree of k_leaf_tree parks a workgroup's waves at one barrier per
+// level while a few waves compress (profiles/r01_pmc_sq_variants_c2.json: 18 %
+// of wave time). Here every lane owns an aligned group of four chunk slots of
+// one message and reduces it in registers — P(P(c0,c1), P(c2,c3)), a BLAKE3
+// tree node because the group is aligned inside the message — so levels 1 and
+// 2 need no barrier, a tile holds 2048 slots for the same 32 KB of node LDS,
+// and the barrier-bound levels start at 3 (8 chunks). The leaf phase per lane
+// grows to 64 compressions + 3 parents, the tree phase keeps its length, so
+// the parked share of a tile halves.
+//
+// Slot layout (requires the shape-sorted order, single-chunk messages first):
+// a single-chunk message takes one slot; the last of them is padded so the
+// first multi-chunk message starts on a multiple of 4; a multi-chunk message
+// takes its chunk count rounded up to 4 (the padding slots are dead). Every
+// node starts on an even slot, so node CVs live at cvs[slot / 2].
+constexpr uint32_t kQTile = 2048;
+
+template <uint32_t TILE>
+__host__ __device__ inline uint32_t node_level_t(uint64_t j, uint64_t C, uint32_t s) {
+  uint32_t k = 0;
+  for (;;) {
+    uint64_t w = 2ull << k;
+    if ((j & (w - 1)) || j + w > C || w >= C || (uint64_t)s + w > TILE) break;
+    ++k;
+  }
+  return k;
+}
+
+template <uint32_t TILE>
+__host__ __device__ inline bool parent_in_tile_t(uint64_t j, uint64_t C, uint32_t s, uint32_t k) {
+  uint64_t w = 1ull << k;
+  if (!((j >> k) & 1)) return false;
+  return j + w <= C && 2 * w < C && s >= w && (uint64_t)s + w <= TILE;
+}
+
+__host__ __device__ inline uint64_t quad_slots(const uint64_t* lens, uint32_t n, uint32_t i) {
+  const uint64_t C = chunk_count(lens[i]);
+  if (C > 1) return (C + 3) & ~3ull;
+  if (i + 1 < n && chunk_count(lens[i + 1]) > 1) return 1 + ((4 - ((i + 1) & 3)) & 3);
+  return 1;
+}
+
+struct QuadSlotsOp {
+  const uint64_t* lens;
+  uint32_t n;
+  __host__ __device__ uint64_t operator()(uint32_t i) const { return quad_slots(lens, n, i); }
+};
+
+__global__ void k_tile_first_q(const uint64_t* __restrict__ lens, const uint64_t* __restrict__ S, uint32_t n,
+                               uint64_t cap_slots, uint32_t* __restrict__ tile_first, uint64_t* __restrict__ total) {
+  uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= n) return;
+  const uint64_t s0 = S[m], Q = quad_slots(lens, n, m);
+  if (m == n - 1) *total = s0 + Q;
+  for (uint64_t t = (s0 + kQTile - 1) / kQTile; t * kQTile < s0 + Q && t * kQTile < cap_slots; ++t) tile_first[t] = m;
+}
+
+template <int PF>
+__device__ __forceinline__ void quad_chunk(const uint8_t* __restrict__ base, uint64_t len, uint64_t j, bool root,
+                                           uint32_t (&cv)[8]) {
+  const uint32_t clen = len == 0 ? 0u : (uint32_t)min<uint64_t>(CHUNK_LEN, len - j * CHUNK_LEN);
+  if (PF) hash_chunk_pf(base + j * CHUNK_LEN, clen, j, root, cv);
+  else hash_chunk(base + j * CHUNK_LEN, clen, j, root, cv);
+}
+
+__device__ __forceinline__ void lds_get(const uint32_t (*cvs)[8], uint32_t i, uint32_t (&o)[8]) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) o[q] = cvs[i][q];
+}
+__device__ __forceinline__ void lds_put(uint32_t (*cvs)[8], uint32_t i, const uint32_t (&v)[8]) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) cvs[i][q] = v[q];
+}
+
+template <int PF>
+__global__ void __launch_bounds__(512, 6) k_leaf_quad(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ offs,
+                                                   const uint64_t* __restrict__ lens, uint32_t n,
+                                                   const uint64_t* __restrict__ S,
+                                                   const uint32_t* __restrict__ tile_first,
+                                                   const uint64_t* __restrict__ total_p, uint64_t cap_slots,
+                                                   uint32_t* __restrict__ nodes, uint8_t* __restrict__ out32,
+                                                   uint64_t* __restrict__ out_keys,
+                                                   const uint32_t* __restrict__ perm) {
+  constexpr uint32_t T = kQTile, WG = 512;
+  __shared__ uint32_t cvs[T / 2][8];  // node CVs by first slot / 2
+  __shared__ uint16_t srel[T + 2];    // message starts relative to the tile (messages 1..)
+  __shared__ uint16_t smsg[T];        // slot -> message in the tile
+  __shared__ uint16_t task[T / 4];    // level >= 3 merges of group nodes: < T / 4
+  __shared__ uint32_t ntask[13], tbase_k[13];
+
+  const uint64_t total = *total_p;
+  if (total > cap_slots) return;
+  const uint64_t ntiles = (total + T - 1) / T;
+  const uint32_t tid = threadIdx.x;
+
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const uint64_t tbase = tile * T;
+    const uint32_t m0 = tile_first[tile];
+    const uint32_t m1 = (tile + 1 < ntiles) ? tile_first[tile + 1] : n - 1;
+    const uint32_t cnt = m1 - m0 + 1;
+    const uint64_t lead = tbase - S[m0];
+    for (uint32_t i = tid + 1; i < cnt; i += WG) srel[i] = (uint16_t)(S[m0 + i] - tbase);
+    if (tid < 13) ntask[tid] = 0;
+    __syncthreads();
+
+    // (1a) slot -> message; count the level >= 3 merges: regular nodes of 8+
+    // chunks, and the spine of every multi-group message lying in the tile
+#pragma unroll 1
+    for (uint32_t s = tid; s < T; s += WG) {
+      if (tbase + s >= total) {
+        smsg[s] = kNoMsg;
+        continue;
+      }
+      uint32_t lo = 0, hi = cnt - 1;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (srel[mid] <= s) lo = mid;
+        else hi = mid - 1;
+      }
+      smsg[s] = (uint16_t)lo;
+      const uint64_t j = lo ? (uint64_t)(s - srel[lo]) : lead + s;
+      const uint64_t C = chunk_count(lens[m0 + lo]);
+      if (C <= 4 || j >= C) continue;
+      const uint32_t K = node_level_t<T>(j, C, s);
+      for (uint32_t k = 3; k <= K; ++k) atomicAdd(&ntask[k], 1u);
+      if (j == 0 && (lo || lead == 0) && s + C <= T) {
+        const uint32_t c = (uint32_t)C;
+        if (!(c & (c - 1))) {
+          atomicAdd(&ntask[31 - __clz(c)], 1u);
+        } else {
+          uint32_t rem = c & ~3u;
+          if (!(c & 3)) rem &= rem - 1;  // the lowest 4+ part is the fold's start, not a step
+          while (rem) {
+            const uint32_t part = rem & (0u - rem);
+            atomicAdd(&ntask[32 - __clz(part)], 1u);
+            rem -= part;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t acc = 0;
+      for (int k = 3; k <= 11; ++k) {
+        tbase_k[k] = acc;
+        acc += ntask[k];
+        ntask[k] = 0;
+      }
+    }
+    __syncthreads();
+    // (1b) write the merges, compacted by level
+#pragma unroll 1
+    for (uint32_t s = tid; s < T; s += WG) {
+      const uint32_t mi = smsg[s];
+      if (mi == kNoMsg) continue;
+      const uint64_t j = mi ? (uint64_t)(s - srel[mi]) : lead + s;
+      const uint64_t C = chunk_count(lens[m0 + mi]);
+      if (C <= 4 || j >= C) continue;
+      const uint32_t K = node_level_t<T>(j, C, s);
+      for (uint32_t k = 3; k <= K; ++k) task[tbase_k[k] + atomicAdd(&ntask[k], 1u)] = (uint16_t)s;
+      if (j == 0 && (mi || lead == 0) && s + C <= T) {
+        const uint32_t c = (uint32_t)C;
+        if (!(c & (c - 1))) {
+          const uint32_t k = 31 - __clz(c);
+          task[tbase_k[k] + atomicAdd(&ntask[k], 1u)] = (uint16_t)(s | kTaskRoot);
+        } else {
+          // right-to-left fold: the tail (< 4 chunks, folded in its group)
+          // or the lowest part is the accumulator; each higher part merges in
+          uint32_t rem = c & ~3u, pos;
+          if (c & 3) {
+            pos = c & ~3u;
+          } else {
+            pos = c - (rem & (0u - rem));
+            rem &= rem - 1;
+          }
+          while (rem) {
+            const uint32_t part = rem & (0u - rem);
+            pos -= part;
+            const uint32_t k = 32 - __clz(part);
+            task[tbase_k[k] + atomicAdd(&ntask[k], 1u)] = (uint16_t)((s + pos) | (rem == part ? kTaskRoot : 0u));
+            rem -= part;
+          }
+        }
+      }
+    }
+
+    // (2) groups: four chunk slots per lane, reduced in registers
+#pragma unroll 1
+    for (uint32_t g = tid; g < T / 4; g += WG) {
+      const uint32_t s = 4 * g;
+      const uint32_t mi = smsg[s];
+      if (mi == kNoMsg) continue;
+      const uint32_t m = m0 + mi;
+      const uint64_t len = lens[m];
+      const uint64_t C = chunk_count(len);
+      if (C == 1) {
+        // up to four single-chunk messages (or the padding after the last)
+#pragma unroll 1
+        for (uint32_t q = 0; q < 4; ++q) {
+          const uint32_t mq = smsg[s + q];
+          if (mq == kNoMsg) break;
+          const uint64_t jq = mq ? (uint64_t)(s + q - srel[mq]) : lead + s + q;
+          if (jq != 0) continue;
+          const uint32_t mm = m0 + mq;
+          uint32_t cv[8];
+          quad_chunk<PF>(blob + offs[mm], lens[mm], 0, true, cv);
+          store_digest(perm ? perm[mm] : mm, cv, out32, out_keys);
+        }
+        continue;
+      }
+      const uint64_t rel0 = mi ? srel[mi] : 0;
+      const uint64_t j0 = mi ? (uint64_t)s - rel0 : lead + s;
+      const uint32_t nv = (uint32_t)min<uint64_t>(4, C - j0);
+      // the last three chunks of a message lying in the tile are folded here
+      // (the spine's first step); a crossing message keeps P(c0,c1) and c2
+      const bool fold3 = nv == 3 && (C == 3 || ((mi || lead == 0) && rel0 + C <= T));
+      const uint8_t* base = blob + offs[m];
+      // chunks one by one; the group's nodes stack up in cvs[2g], cvs[2g+1]
+      // and merge as pairs complete (one hash and one parent call site keep
+      // the register footprint of a single chunk)
+      uint32_t depth = 0;
+#pragma unroll 1
+      for (uint32_t q = 0; q < nv; ++q) {
+        uint32_t cv[8];
+        quad_chunk<PF>(base, len, j0 + q, false, cv);
+        uint32_t merges = q == 1 ? 1u : (q == 3 ? 2u : 0u);
+        if (q == 2 && fold3) merges = 1;
+        bool root = false;
+#pragma unroll 1
+        for (uint32_t t = 0; t < merges; ++t) {
+          uint32_t a[8];
+          lds_get(cvs, 2 * g + depth - 1, a);
+          root = depth == 1 && j0 == 0 && q + 1 == C;  // the merge that completes the whole message
+          parent(a, cv, root, cv);
+          --depth;
+        }
+        if (root) {
+          store_digest(perm ? perm[m] : m, cv, out32, out_keys);
+          break;
+        }
+        lds_put(cvs, 2 * g + depth, cv);
+        ++depth;
+      }
+    }
+    __syncthreads();
+
+    // (3) the tree above the groups, level by level
+    for (uint32_t k = 3; k <= 11; ++k) {
+      const uint32_t Tk = ntask[k];
+      if (Tk == 0) continue;
+      const uint32_t base = tbase_k[k], half = 1u << (k - 1);
+#pragma unroll 1
+      for (uint32_t t = tid; t < Tk; t += WG) {
+        const uint32_t e = task[base + t];
+        const uint32_t l = e & (T - 1), r = l + half;
+        const bool root = e & kTaskRoot;
+        uint32_t a[8], b[8], o[8];
+        lds_get(cvs, l >> 1, a);
+        lds_get(cvs, r >> 1, b);
+        parent(a, b, root, o);
+        if (root) {
+          const uint32_t mm = m0 + smsg[l];
+          store_digest(perm ? perm[mm] : mm, o, out32, out_keys);
+        } else {
+          lds_put(cvs, l >> 1, o);
+        }
+      }
+      __syncthreads();
+    }
+
+    // (4) maximal in-tile nodes of messages crossing a tile boundary
+#pragma unroll 1
+    for (uint32_t s = tid; s < T; s += WG) {
+      const uint32_t mi = smsg[s];
+      if (mi == kNoMsg) continue;
+      const uint64_t C = chunk_count(lens[m0 + mi]);
+      if (C <= 4) continue;
+      const uint64_t rel0 = mi ? srel[mi] : 0;
+      if ((mi || lead == 0) && rel0 + C <= T) continue;
+      const uint64_t j = mi ? (uint64_t)s - rel0 : lead + s;
+      if (j >= C) continue;
+      const uint32_t k = node_level_t<T>(j, C, s);
+      if (parent_in_tile_t<T>(j, C, s, k)) continue;
+      uint4* o = reinterpret_cast<uint4*>(nodes + 8ull * (tbase + s));
+      const uint32_t i = s >> 1;
+      o[0] = make_uint4(cvs[i][0], cvs[i][1], cvs[i][2], cvs[i][3]);
+      o[1] = make_uint4(cvs[i][4], cvs[i][5], cvs[i][6], cvs[i][7]);
+    }
+    __syncthreads();
+  }
+}
+
+// k_finish for the quad layout: a message crossing tile boundaries, walked
+// by one lane per boundary (the message whose real chunks reach across it)
+__global__ void __launch_bounds__(256) k_finish_q(const uint64_t* __restrict__ lens, uint32_t n,
+                                                  const uint64_t* __restrict__ S,
+                                                  const uint32_t* __restrict__ tile_first,
+                                                  const uint64_t* __restrict__ total_p, uint64_t cap_slots,
+                                                  const uint32_t* __restrict__ nodes,
+                                                  const uint32_t* __restrict__ perm, uint8_t* __restrict__ out32,
+                                                  uint64_t* __restrict__ out_keys) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t total = *total_p;
+  if (total > cap_slots || t == 0 || t * kQTile >= total) return;
+  const uint32_t m = tile_first[t];
+  const uint64_t s0 = S[m];
+  if (s0 >= t * kQTile || s0 / kQTile != t - 1) return;
+  const uint64_t C = chunk_count(lens[m]);
+  if (s0 + C <= t * kQTile) return;  // only its padding reaches the boundary
+  uint32_t stack[kMaxStack][8];
+  int depth = 0;
+  uint64_t j = 0;
+  while (j < C) {
+    const uint64_t g = s0 + j;
+    const uint32_t k = node_level_t<kQTile>(j, C, (uint32_t)(g % kQTile));
+    const uint4* p = reinterpret_cast<const uint4*>(nodes + 8ull * g);
+    uint4 a = p[0], b = p[1];
+    uint32_t cv[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    const int keep = __popcll(j);
+    while (depth > keep) {
+      uint32_t o[8];
+      parent(stack[depth - 2], stack[depth - 1], false, o);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) stack[depth - 2][i] = o[i];
+      --depth;
+    }
+    j += 1ull << k;
+    if (j == C) {
+      for (int d = depth - 1; d >= 0; --d) {
+        uint32_t o[8];
+        parent(stack[d], cv, d == 0, o);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) cv[i] = o[i];
+      }
+      store_digest(perm ? perm[m] : m, cv, out32, out_keys);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) stack[depth][i] = cv[i];
+      ++depth;
+    }
+  }
+}
+
 // Messages crossing tile boundaries: one lane per tile boundary t (the
 // message holding slot t*kTile, when it started in tile t-1 — its first
 // crossing), so the launch is dense (~ one active lane per tile) instead of a
@@ -992,11 +1337,15 @@ __global__ void __launch_bounds__(kWG) k_bigfile_finish(const FileDesc* __restri
 
 // ---------------------------------------------------------------------------
 
+using QuadIt = hipcub::TransformInputIterator<uint64_t, QuadSlotsOp, hipcub::CountingInputIterator<uint32_t>>;
+
 size_t batch_scan_temp_bytes(uint32_t max_msgs) {
-  size_t bytes = 0;
+  size_t bytes = 0, qbytes = 0;
   hipcub::TransformInputIterator<uint64_t, ChunkCountOp, const uint64_t*> it(nullptr, ChunkCountOp());
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, it, (uint64_t*)nullptr, (int)max_msgs);
-  return bytes;
+  QuadIt qit(hipcub::CountingInputIterator<uint32_t>(0), QuadSlotsOp{nullptr, max_msgs});
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, qbytes, qit, (uint64_t*)nullptr, (int)max_msgs);
+  return std::max(bytes, qbytes);
 }
 
 // leaf/tree kernel variants (workgroup size x block prefetch); the default is
@@ -1004,6 +1353,7 @@ size_t batch_scan_temp_bytes(uint32_t max_msgs) {
 struct LeafVariant {
   const void* fn;
   int wg;
+  int quad = 0;  // 1: quad slot layout (k_leaf_quad / k_finish_q, needs the shape-sorted order)
 };
 static const LeafVariant kLeafVariants[] = {
     {(const void*)k_leaf_tree<512, 0>, 512},
@@ -1035,6 +1385,9 @@ static const LeafVariant kLeafVariants[] = {
     // 20, 21: compact LDS + leaf order by block count (6 waves/SIMD); the same without prefetch
     {(const void*)k_leaf_slim<512, 1, 6, 1>, 512},
     {(const void*)k_leaf_slim<512, 0, 6, 1>, 512},
+    // 22, 23: quad layout (four chunks per lane, 2048-slot tiles); without prefetch
+    {(const void*)k_leaf_quad<1>, 512, 1},
+    {(const void*)k_leaf_quad<0>, 512, 1},
 };
 constexpr int kNumLeafVariants = sizeof(kLeafVariants) / sizeof(kLeafVariants[0]);
 constexpr int kDefaultLeafVariant = 1;
@@ -1081,27 +1434,42 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
     lens = ws.slens;
     perm = ws.perm;
   }
-  hipcub::TransformInputIterator<uint64_t, ChunkCountOp, const uint64_t*> it(lens, ChunkCountOp());
+  int v = ws.variant >= 0 && ws.variant < kNumLeafVariants ? ws.variant : leaf_variant();
+  const bool quad = kLeafVariants[v].quad && (perm || n == 1);
+  if (kLeafVariants[v].quad && !quad) v = 1;  // the quad layout needs the shape-sorted order
   size_t tmp = ws.scan_tmp_bytes;
-  if ((e = hipcub::DeviceScan::ExclusiveSum(ws.scan_tmp, tmp, it, ws.S, (int)n, st))) return e;
-  hipLaunchKernelGGL(k_tile_first, dim3((n + tb - 1) / tb), dim3(tb), 0, st, lens, ws.S, n, ws.cap_chunks,
-                     ws.tile_first, ws.total);
+  if (quad) {
+    QuadIt qit(hipcub::CountingInputIterator<uint32_t>(0), QuadSlotsOp{lens, n});
+    if ((e = hipcub::DeviceScan::ExclusiveSum(ws.scan_tmp, tmp, qit, ws.S, (int)n, st))) return e;
+    hipLaunchKernelGGL(k_tile_first_q, dim3((n + tb - 1) / tb), dim3(tb), 0, st, lens, ws.S, n, ws.cap_slots,
+                       ws.tile_first, ws.total);
+  } else {
+    hipcub::TransformInputIterator<uint64_t, ChunkCountOp, const uint64_t*> it(lens, ChunkCountOp());
+    if ((e = hipcub::DeviceScan::ExclusiveSum(ws.scan_tmp, tmp, it, ws.S, (int)n, st))) return e;
+    hipLaunchKernelGGL(k_tile_first, dim3((n + tb - 1) / tb), dim3(tb), 0, st, lens, ws.S, n, ws.cap_slots,
+                       ws.tile_first, ws.total);
+  }
   if (ev0) (void)hipEventRecord(ev0, st);
   {
-    const int v = ws.variant >= 0 && ws.variant < kNumLeafVariants ? ws.variant : leaf_variant();
     int dev = 0;
     (void)hipGetDevice(&dev);
     const int grid = batch_grid(dev, v);
     void* args[] = {(void*)&blob,     (void*)&offs,          (void*)&lens,       (void*)&n,
-                    (void*)&ws.S,     (void*)&ws.tile_first, (void*)&ws.total,   (void*)&ws.cap_chunks,
+                    (void*)&ws.S,     (void*)&ws.tile_first, (void*)&ws.total,   (void*)&ws.cap_slots,
                     (void*)&ws.nodes, (void*)&out32,         (void*)&out_keys,   (void*)&perm};
     hipError_t le = hipLaunchKernel(kLeafVariants[v].fn, dim3(grid), dim3(kLeafVariants[v].wg), args, 0, st);
     if (le != hipSuccess) return le;
   }
   if (ev1) (void)hipEventRecord(ev1, st);
-  const uint64_t tiles = ws.cap_chunks / kTile + 1;
-  hipLaunchKernelGGL(k_finish, dim3((uint32_t)((tiles + tb - 1) / tb)), dim3(tb), 0, st, lens, n, ws.S, ws.tile_first,
-                     ws.total, ws.cap_chunks, ws.nodes, perm, out32, out_keys);
+  if (quad) {
+    const uint64_t tiles = ws.cap_slots / kQTile + 1;
+    hipLaunchKernelGGL(k_finish_q, dim3((uint32_t)((tiles + tb - 1) / tb)), dim3(tb), 0, st, lens, n, ws.S,
+                       ws.tile_first, ws.total, ws.cap_slots, ws.nodes, perm, out32, out_keys);
+  } else {
+    const uint64_t tiles = ws.cap_slots / kTile + 1;
+    hipLaunchKernelGGL(k_finish, dim3((uint32_t)((tiles + tb - 1) / tb)), dim3(tb), 0, st, lens, n, ws.S,
+                       ws.tile_first, ws.total, ws.cap_slots, ws.nodes, perm, out32, out_keys);
+  }
   return hipGetLastError();
 }
 

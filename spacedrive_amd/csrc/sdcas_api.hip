@@ -157,8 +157,10 @@ namespace {
 int reserve_ws(sdcas_ctx* c, size_t max_msgs, uint64_t max_chunks) {
   hipError_t e;
   if (max_msgs > 0xFFFFFFF0ull) return c->fail(SDCAS_E_CAPACITY, "batch of %zu messages exceeds 2^32", max_msgs);
-  const uint64_t tiles = max_chunks / kTile + 2;
   if ((e = c->ws_S.ensure(max_msgs + 1))) return c->hip_fail(e, "workspace S");
+  // room for the quad layout's padding too: < 4 dead slots per message (of
+  // as many messages as the workspace takes)
+  const uint64_t tiles = (max_chunks + 3 * (uint64_t)(c->ws_S.cap - 1) + 8) / kTile + 2;
   if ((e = c->ws_total.ensure(2))) return c->hip_fail(e, "workspace total");
   if ((e = c->ws_tile_first.ensure(tiles))) return c->hip_fail(e, "workspace tile_first");
   if ((e = c->ws_nodes.ensure(8 * (tiles * kTile)))) return c->hip_fail(e, "workspace nodes");
@@ -179,8 +181,10 @@ int reserve_ws(sdcas_ctx* c, size_t max_msgs, uint64_t max_chunks) {
   c->ws.cap_msgs =
       (uint32_t)std::min<size_t>({c->ws_S.cap - 1, c->ws_perm.cap - 1, c->ws_soffs.cap - 1, c->ws_slens.cap - 1});
   c->ws.sort_keys = c->ws_sort_keys.p;
-  // every tile the leaf kernel may touch needs a tile_first entry and kTile node slots
-  c->ws.cap_chunks = std::min<uint64_t>((c->ws_tile_first.cap - 1) * kTile, c->ws_nodes.cap / 8 - kTile);
+  // every tile the leaf kernel may touch needs a tile_first entry and its node slots
+  c->ws.cap_slots = std::min<uint64_t>((c->ws_tile_first.cap - 1) * kTile, c->ws_nodes.cap / 8 - 2 * kTile);
+  const uint64_t pad = 3 * (uint64_t)(c->ws_S.cap - 1) + 8;
+  c->ws.cap_chunks = c->ws.cap_slots > pad ? c->ws.cap_slots - pad : 0;
   return SDCAS_OK;
 }
 
@@ -610,9 +614,9 @@ int sdcas_dev_sync(sdcas_ctx* c, void* stream) {
   if (e) return c->hip_fail(e, "sync");
   uint64_t total = 0;
   if (c->ws.total && (e = hipMemcpy(&total, c->ws.total, 8, hipMemcpyDeviceToHost))) return c->hip_fail(e, "total");
-  if (total > c->ws.cap_chunks)
-    return c->fail(SDCAS_E_CAPACITY, "batch of %llu chunks exceeds reserved %llu", (unsigned long long)total,
-                   (unsigned long long)c->ws.cap_chunks);
+  if (total > c->ws.cap_slots)
+    return c->fail(SDCAS_E_CAPACITY, "batch of %llu chunk slots exceeds reserved %llu", (unsigned long long)total,
+                   (unsigned long long)c->ws.cap_slots);
   return SDCAS_OK;
 }
 
