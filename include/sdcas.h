@@ -186,7 +186,10 @@ int sdcas_dedup(sdcas_ctx *ctx, const uint64_t *keys, const uint8_t *has_key, co
  *
  * combine: d_ids[n] ascending; d_has_key / d_status may be NULL (all
  *   present / all ok). Writes d_rec[2*u], d_rec[2*u+1] = (cas key, min id)
- *   for each distinct key u (capacity 2*n u64), d_slot[i] = record of file i
+ *   per key (a key whose top 32 bits another key shares may take more
+ *   than one record: resolve's minimum covers all of them; capacity 2*n
+ *   u64), records grouped by owner in ascending key order of their top 32
+ *   bits, d_slot[i] = record of file i
  *   (0xFFFFFFFF no cas_id, 0xFFFFFFFE dropped; may be NULL), and
  *   out_starts[0..world] (host) = first record of each owner; out_starts[world]
  *   is the record count.

@@ -45,6 +45,7 @@ struct DistWs {
   };
   Buf<uint64_t> key_a, key_b, umin, ukey, emin;
   Buf<uint32_t> idx_a, idx_b, scan, nvalid, starts;
+  Buf<uint32_t> hi_a, hi_b;  // top 32 key bits: the combine's sort key
   Buf<uint8_t> valid, temp;
   void release();
 };

@@ -47,17 +47,49 @@ __global__ void k_dd_flags(const uint64_t* __restrict__ skey, const uint32_t* __
   flag[p] = (p < nv && (p == 0 || skey[p] != skey[p - 1])) ? 1u : 0u;
 }
 
-__global__ void k_dd_emit(const uint64_t* __restrict__ skey, const uint32_t* __restrict__ sidx,
-                          const uint32_t* __restrict__ scan, const uint32_t* __restrict__ nv_p,
-                          const uint64_t* __restrict__ ids, uint64_t* __restrict__ rec, uint32_t* __restrict__ slot) {
+// The combine's sort entries: key = top 32 key bits, value = (low 32 key
+// bits, file index) — the full key travels with the entry, so no pass after
+// the sort gathers it (the tail keeps 0xFFFFFFFF fillers, which the stable
+// sort leaves behind every real entry)
+__global__ void k_dd_hi(const uint64_t* __restrict__ ckey, const uint32_t* __restrict__ cidx,
+                        const uint32_t* __restrict__ nv_p, uint32_t n, uint32_t* __restrict__ hi,
+                        uint64_t* __restrict__ val) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const bool real = p < *nv_p;
+  const uint64_t k = real ? ckey[p] : ~0ull;
+  hi[p] = (uint32_t)(k >> 32);
+  val[p] = (k << 32) | (real ? cidx[p] : 0u);
+}
+
+__device__ __forceinline__ uint64_t hv_key(const uint32_t* hi, const uint64_t* val, uint32_t p) {
+  return ((uint64_t)hi[p] << 32) | (val[p] >> 32);
+}
+
+// run heads of the sorted entries by FULL key: distinct keys sharing their
+// top bits may interleave, which splits a key into several runs but never
+// merges two keys
+__global__ void k_dd_flags_hv(const uint32_t* __restrict__ hi, const uint64_t* __restrict__ val,
+                              const uint32_t* __restrict__ nv_p, uint32_t n, uint32_t* __restrict__ flag) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const uint32_t nv = *nv_p;
+  flag[p] = (p < nv && (p == 0 || hv_key(hi, val, p) != hv_key(hi, val, p - 1))) ? 1u : 0u;
+}
+
+__global__ void k_dd_emit_hv(const uint32_t* __restrict__ hi, const uint64_t* __restrict__ val,
+                             const uint32_t* __restrict__ scan, const uint32_t* __restrict__ nv_p,
+                             const uint64_t* __restrict__ ids, uint64_t* __restrict__ rec,
+                             uint32_t* __restrict__ slot) {
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= *nv_p) return;
   const uint32_t u = scan[p] - 1;
-  const uint32_t i = sidx[p];
+  const uint32_t i = (uint32_t)val[p];
   if (slot) slot[i] = u;
-  if (p == 0 || skey[p] != skey[p - 1]) {
+  const uint64_t key = hv_key(hi, val, p);
+  if (p == 0 || key != hv_key(hi, val, p - 1)) {
     // stable sort + ascending ids: the run's first entry carries the minimum
-    rec[2 * (uint64_t)u] = skey[p];
+    rec[2 * (uint64_t)u] = key;
     rec[2 * (uint64_t)u + 1] = ids[i];
   }
 }
@@ -167,6 +199,10 @@ hipError_t ensure_temp(DistWs& w, uint32_t n) {
                                       (uint64_t*)nullptr, (uint32_t*)nullptr, (int)n);
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const uint64_t*)nullptr, (uint64_t*)nullptr,
                                            (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
+  size_t b2 = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b2, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                           (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)n, 0, 32);
+  b = b > b2 ? b : b2;
   (void)hipcub::DeviceScan::InclusiveSum(nullptr, c, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
   size_t m = a > b ? a : b;
   m = m > c ? m : c;
@@ -198,7 +234,8 @@ hipError_t sort_and_scan(DistWs& w, uint32_t n, const uint32_t* nv_p, hipStream_
 
 void DistWs::release() {
   key_a.release(); key_b.release(); umin.release(); ukey.release(); emin.release();
-  idx_a.release(); idx_b.release(); scan.release(); nvalid.release(); starts.release();
+  idx_a.release(); idx_b.release(); scan.release(); nvalid.release(); starts.release(); hi_a.release();
+  hi_b.release();
   valid.release(); temp.release();
 }
 
@@ -222,9 +259,26 @@ hipError_t dd_combine(DistWs& w, const uint64_t* keys, const uint8_t* has_key, c
   tmp = w.temp.cap;
   if ((e = hipcub::DeviceSelect::Flagged(w.temp.p, tmp, w.idx_a.p, w.valid.p, w.idx_b.p, w.nvalid.p, (int)n, st)))
     return e;
-  if ((e = sort_and_scan(w, n, w.nvalid.p, st))) return e;
-  hipLaunchKernelGGL(k_dd_emit, dim3(blocks(n)), dim3(TB), 0, st, w.key_b.p, w.idx_a.p, w.scan.p, w.nvalid.p, ids, rec,
-                     slot);
+  // The combine only has to bring equal keys together and order the owners
+  // (top 12 bits): a stable sort of (top 32 key bits, file index) pairs does
+  // both in half the passes over 2/3 of the bytes of a full 64-bit sort.
+  // Distinct keys sharing their top 32 bits (~n^2 / 2^33 pairs) may
+  // interleave and split a key into several records; resolve takes the
+  // minimum over all records of a key, so the answer is unchanged.
+  if ((e = w.hi_a.ensure(n)) || (e = w.hi_b.ensure(n))) return e;
+  // entries (hi32 | lo32:index) from the compacted key_a / idx_b into
+  // hi_a / key_b, sorted into hi_b / key_a
+  hipLaunchKernelGGL(k_dd_hi, dim3(blocks(n)), dim3(TB), 0, st, w.key_a.p, w.idx_b.p, w.nvalid.p, n, w.hi_a.p,
+                     w.key_b.p);
+  tmp = w.temp.cap;
+  if ((e = hipcub::DeviceRadixSort::SortPairs(w.temp.p, tmp, w.hi_a.p, w.hi_b.p, w.key_b.p, w.key_a.p, (int)n, 0, 32,
+                                              st)))
+    return e;
+  hipLaunchKernelGGL(k_dd_flags_hv, dim3(blocks(n)), dim3(TB), 0, st, w.hi_b.p, w.key_a.p, w.nvalid.p, n, w.scan.p);
+  tmp = w.temp.cap;
+  if ((e = hipcub::DeviceScan::InclusiveSum(w.temp.p, tmp, w.scan.p, w.scan.p, (int)n, st))) return e;
+  hipLaunchKernelGGL(k_dd_emit_hv, dim3(blocks(n)), dim3(TB), 0, st, w.hi_b.p, w.key_a.p, w.scan.p, w.nvalid.p, ids,
+                     rec, slot);
   hipLaunchKernelGGL(k_dd_starts, dim3(blocks(world + 1)), dim3(TB), 0, st, rec, w.scan.p, w.nvalid.p, world,
                      w.starts.p);
   uint32_t hs[1025];

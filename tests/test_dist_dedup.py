@@ -71,6 +71,28 @@ def test_virtual_protocol_numpy_vs_oracle(oracle, R):
     assert (c, l) == (wc, wl)
 
 
+def collision_corpus(seed=11, n=8000):
+    """keys drawn from 40 top-32-bit prefixes x 4 low values: many distinct
+    keys share their top 32 bits (the combine's sort key)"""
+    rng = np.random.default_rng(seed)
+    hi = rng.integers(0, 2**32, 40, dtype=np.uint64) << np.uint64(32)
+    pool = (hi[rng.integers(0, 40, 600)] | rng.integers(0, 4, 600, dtype=np.uint64)).astype(np.uint64)
+    keys = pool[rng.integers(0, pool.size, n)]
+    has = (rng.random(n) > 0.02).astype(np.uint8)
+    status = np.where(rng.random(n) < 0.01, 5, 0).astype(np.int32)
+    return keys, has, status, pool[:25].copy()
+
+
+@pytest.mark.parametrize("R", [1, 3])
+def test_virtual_protocol_numpy_top32_collisions(oracle, R):
+    keys, has, status, existing = collision_corpus()
+    shards, ex = shard(keys, has, status, existing, R)
+    links, c, l = dedup_virtual(lambda r: NumpyStages(), shards, 100, ex)
+    want, wc, wl = oracle.identifier_dedup(keys, has, status, 100, existing)
+    assert np.array_equal(np.concatenate([x.numpy() for x in links]), want)
+    assert (c, l) == (wc, wl)
+
+
 def test_owner_is_monotone_and_covers_ranks():
     from spacedrive_amd.dist_dedup import owner_of
     k = np.sort(np.random.default_rng(0).integers(0, 2**64, 10000, dtype=np.uint64))
@@ -124,6 +146,21 @@ def test_device_stages_match_numpy_stages(eng):
     ans_d = st.resolve(rec_d, erec_d)
     ans_n = ns.resolve(rec_d.cpu(), erec_d.cpu())
     assert torch.equal(ans_d.cpu(), ans_n)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R", [1, 3])
+def test_device_stages_top32_collisions(eng, oracle, R):
+    """keys sharing their top 32 bits interleave in the combine's sort and
+    split into several records; the links still equal the oracle's"""
+    from spacedrive_amd.dist_dedup import DeviceStages
+    keys, has, status, existing = collision_corpus()
+    shards, ex = shard(keys, has, status, existing, R, device="cuda")
+    st = DeviceStages(eng)
+    links, c, l = dedup_virtual(lambda r: st, shards, 100, ex)
+    want, wc, wl = oracle.identifier_dedup(keys, has, status, 100, existing)
+    assert np.array_equal(np.concatenate([x.cpu().numpy() for x in links]), want)
+    assert (c, l) == (wc, wl)
 
 
 @pytest.mark.gpu
