@@ -46,6 +46,8 @@ struct DistWs {
   Buf<uint64_t> key_a, key_b, umin, ukey, emin;
   Buf<uint32_t> idx_a, idx_b, scan, nvalid, starts;
   Buf<uint32_t> hi_a, hi_b;  // top 32 key bits: the combine's sort key
+  Buf<uint64_t> tkey, tmin;  // resolve's hash table: keys, (files' min, existing min) per entry
+  Buf<uint32_t> tpos;        // table entry of each received file record
   Buf<uint8_t> valid, temp;
   void release();
 };

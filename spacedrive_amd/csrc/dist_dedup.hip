@@ -13,8 +13,9 @@
 // the owner RESOLVES each key against its slice of existing Objects, and the
 // answers travel back in send order for each rank to APPLY to its files.
 //
-// HBM-bound integer work: radix sorts of (key, index) pairs and streaming
-// passes; per-key minima by 64-bit atomicMin on a unique-key array.
+// HBM-bound integer work: the combine is one stable radix sort of
+// (top 32 key bits | low bits + file index) entries and streaming passes; the
+// resolve is a hash table with 64-bit atomicMin per key, no sort.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -38,14 +39,6 @@ __global__ void k_dd_prepare(const uint8_t* __restrict__ has_key, const int32_t*
   if (slot) slot[i] = !ok ? kSlotDropped : kSlotNoKey;
 }
 
-// run-head flags of a key-sorted array (first nv entries are real)
-__global__ void k_dd_flags(const uint64_t* __restrict__ skey, const uint32_t* __restrict__ nv_p, uint32_t nv_host,
-                           uint32_t n, uint32_t* __restrict__ flag) {
-  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= n) return;
-  const uint32_t nv = nv_p ? *nv_p : nv_host;
-  flag[p] = (p < nv && (p == 0 || skey[p] != skey[p - 1])) ? 1u : 0u;
-}
 
 // The combine's sort entries: key = top 32 key bits, value = (low 32 key
 // bits, file index) — the full key travels with the entry, so no pass after
@@ -109,48 +102,9 @@ __global__ void k_dd_starts(const uint64_t* __restrict__ rec, const uint32_t* __
   starts[r] = r == world ? U : lo;
 }
 
-__global__ void k_dd_split(const uint64_t* __restrict__ rec, uint32_t n, uint64_t* __restrict__ key,
-                           uint32_t* __restrict__ pos) {
-  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= n) return;
-  key[p] = rec[2 * (uint64_t)p];
-  pos[p] = p;
-}
 
-// per unique key: key (optional) and the minimum of the records' values
-__global__ void k_dd_unique_min(const uint64_t* __restrict__ skey, const uint32_t* __restrict__ spos,
-                                const uint32_t* __restrict__ scan, uint32_t n, const uint64_t* __restrict__ rec,
-                                uint64_t* __restrict__ ukey, unsigned long long* __restrict__ umin) {
-  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= n) return;
-  const uint32_t u = scan[p] - 1;
-  if (ukey && (p == 0 || skey[p] != skey[p - 1])) ukey[u] = skey[p];
-  atomicMin(&umin[u], (unsigned long long)rec[2 * (uint64_t)spos[p] + 1]);
-}
 
-__global__ void k_dd_count_of(const uint32_t* __restrict__ scan, uint32_t n, uint32_t* __restrict__ out) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) *out = n ? scan[n - 1] : 0u;
-}
 
-__global__ void k_dd_resolve(const uint64_t* __restrict__ skey, const uint32_t* __restrict__ spos,
-                             const uint32_t* __restrict__ scan, uint32_t nf, const uint64_t* __restrict__ fmin,
-                             const uint64_t* __restrict__ ekey, const uint64_t* __restrict__ emin,
-                             const uint32_t* __restrict__ ne_p, int64_t* __restrict__ result) {
-  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= nf) return;
-  const uint64_t key = skey[p];
-  const uint32_t ne = ne_p ? *ne_p : 0u;
-  uint32_t lo = 0, hi = ne;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (ekey[mid] < key) lo = mid + 1;
-    else hi = mid;
-  }
-  int64_t r;
-  if (lo < ne && ekey[lo] == key) r = -(int64_t)emin[lo] - 1;  // mod.rs:202-238: first existing Object
-  else r = (int64_t)fmin[scan[p] - 1];                           // the key's first file
-  result[spos[p]] = r;
-}
 
 __global__ void k_dd_apply(const uint64_t* __restrict__ ids, const uint32_t* __restrict__ slot, uint32_t n,
                            const int64_t* __restrict__ result, uint64_t cs, int64_t* __restrict__ link,
@@ -217,25 +171,13 @@ hipError_t ensure_n(DistWs& w, uint32_t n) {
   return ensure_temp(w, n);
 }
 
-// sort n (key, pos) pairs from key_a/idx_b into key_b/idx_a, flags + inclusive
-// sum of run heads into scan
-hipError_t sort_and_scan(DistWs& w, uint32_t n, const uint32_t* nv_p, hipStream_t st) {
-  hipError_t e;
-  size_t tmp = w.temp.cap;
-  if ((e = hipcub::DeviceRadixSort::SortPairs(w.temp.p, tmp, w.key_a.p, w.key_b.p, w.idx_b.p, w.idx_a.p, (int)n, 0,
-                                              64, st)))
-    return e;
-  hipLaunchKernelGGL(k_dd_flags, dim3(blocks(n)), dim3(TB), 0, st, w.key_b.p, nv_p, n, n, w.scan.p);
-  tmp = w.temp.cap;
-  return hipcub::DeviceScan::InclusiveSum(w.temp.p, tmp, w.scan.p, w.scan.p, (int)n, st);
-}
 
 }  // namespace
 
 void DistWs::release() {
   key_a.release(); key_b.release(); umin.release(); ukey.release(); emin.release();
   idx_a.release(); idx_b.release(); scan.release(); nvalid.release(); starts.release(); hi_a.release();
-  hi_b.release();
+  hi_b.release(); tkey.release(); tmin.release(); tpos.release();
   valid.release(); temp.release();
 }
 
@@ -294,34 +236,65 @@ hipError_t dd_combine(DistWs& w, const uint64_t* keys, const uint8_t* has_key, c
   return hipGetLastError();
 }
 
+// ---- resolve: per-key minima in an open-addressing hash table -----------------
+//
+// The owner needs, per key, the minimum DB index over the existing Objects'
+// records and the minimum orphan ordinal over the files' records. Both are
+// associative minima, so every record is inserted (linear probing, 64-bit
+// CAS on the key) and min-folded into its entry (64-bit atomicMin); each file
+// record then reads its entry. Three streaming passes over the records and
+// no sort. The all-ones key (a legal cas key) owns the extra entry at `cap`.
+constexpr uint64_t kEmptyKey = ~0ull;
+
+__device__ __forceinline__ uint32_t ht_find(unsigned long long* __restrict__ tkey, uint64_t key, uint32_t mask) {
+  if (key == kEmptyKey) return mask + 1;
+  uint32_t h = (uint32_t)(((key ^ (key >> 31)) * 0x9E3779B97F4A7C15ull) >> 32) & mask;
+  for (;;) {
+    const unsigned long long prev = atomicCAS(&tkey[h], (unsigned long long)kEmptyKey, (unsigned long long)key);
+    if (prev == kEmptyKey || prev == key) return h;
+    h = (h + 1) & mask;
+  }
+}
+
+// rec[2p] = key, rec[2p+1] = value; min-fold value into tmin[2 * entry + side]
+__global__ void k_ht_insert(const uint64_t* __restrict__ rec, uint32_t n, unsigned long long* __restrict__ tkey,
+                            unsigned long long* __restrict__ tmin, uint32_t mask, uint32_t side,
+                            uint32_t* __restrict__ pos_out) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const uint32_t h = ht_find(tkey, rec[2 * (uint64_t)p], mask);
+  atomicMin(&tmin[2 * (uint64_t)h + side], (unsigned long long)rec[2 * (uint64_t)p + 1]);
+  if (pos_out) pos_out[p] = h;
+}
+
+__global__ void k_ht_answer(const uint32_t* __restrict__ pos, uint32_t nf, const uint64_t* __restrict__ tmin,
+                            int64_t* __restrict__ result) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= nf) return;
+  const uint32_t h = pos[p];
+  const uint64_t e = tmin[2 * (uint64_t)h + 1];
+  // mod.rs:202-238: the first existing Object carrying the key; else the
+  // key's first file (mod.rs:246-254)
+  result[p] = e != ~0ull ? -(int64_t)e - 1 : (int64_t)tmin[2 * (uint64_t)h];
+}
+
 hipError_t dd_resolve(DistWs& w, const uint64_t* frec, uint32_t nf, const uint64_t* erec, uint32_t ne,
                       int64_t* result, hipStream_t st) {
   hipError_t e;
-  const uint32_t m = nf > ne ? nf : ne;
-  if (m == 0) return hipSuccess;
-  if ((e = ensure_n(w, m)) || (e = w.umin.ensure(m)) || (e = w.ukey.ensure(ne + 1))) return e;
-  uint64_t* fmin = w.umin.p;  // per unique file key
-  // existing Objects first: unique keys (ukey) + their minimum DB index (emin)
-  uint64_t* emin = nullptr;
-  if (ne) {
-    if ((e = w.emin.ensure(ne))) return e;
-    emin = w.emin.p;
-    if ((e = hipMemsetAsync(emin, 0xFF, sizeof(uint64_t) * ne, st))) return e;
-    hipLaunchKernelGGL(k_dd_split, dim3(blocks(ne)), dim3(TB), 0, st, erec, ne, w.key_a.p, w.idx_b.p);
-    if ((e = sort_and_scan(w, ne, nullptr, st))) return e;
-    hipLaunchKernelGGL(k_dd_unique_min, dim3(blocks(ne)), dim3(TB), 0, st, w.key_b.p, w.idx_a.p, w.scan.p, ne, erec,
-                       w.ukey.p, (unsigned long long*)emin);
-  }
-  hipLaunchKernelGGL(k_dd_count_of, dim3(1), dim3(64), 0, st, w.scan.p, ne, w.nvalid.p + 1);
-  if (nf) {
-    if ((e = hipMemsetAsync(fmin, 0xFF, sizeof(uint64_t) * nf, st))) return e;
-    hipLaunchKernelGGL(k_dd_split, dim3(blocks(nf)), dim3(TB), 0, st, frec, nf, w.key_a.p, w.idx_b.p);
-    if ((e = sort_and_scan(w, nf, nullptr, st))) return e;
-    hipLaunchKernelGGL(k_dd_unique_min, dim3(blocks(nf)), dim3(TB), 0, st, w.key_b.p, w.idx_a.p, w.scan.p, nf, frec,
-                       (uint64_t*)nullptr, (unsigned long long*)fmin);
-    hipLaunchKernelGGL(k_dd_resolve, dim3(blocks(nf)), dim3(TB), 0, st, w.key_b.p, w.idx_a.p, w.scan.p, nf, fmin,
-                       w.ukey.p, emin ? emin : fmin, w.nvalid.p + 1, result);
-  }
+  if (nf == 0) return hipSuccess;  // nothing asks: existing records alone answer no one
+  uint64_t cap = 1024;
+  while (cap < 2 * ((uint64_t)nf + ne)) cap <<= 1;
+  if (cap > (1ull << 31)) return hipErrorInvalidValue;
+  if ((e = w.tkey.ensure(cap + 1)) || (e = w.tmin.ensure(2 * (cap + 1))) || (e = w.tpos.ensure(nf))) return e;
+  const uint32_t mask = (uint32_t)(cap - 1);
+  if ((e = hipMemsetAsync(w.tkey.p, 0xFF, sizeof(uint64_t) * (cap + 1), st)) ||
+      (e = hipMemsetAsync(w.tmin.p, 0xFF, sizeof(uint64_t) * 2 * (cap + 1), st)))
+    return e;
+  auto* tk = reinterpret_cast<unsigned long long*>(w.tkey.p);
+  auto* tm = reinterpret_cast<unsigned long long*>(w.tmin.p);
+  if (ne) hipLaunchKernelGGL(k_ht_insert, dim3(blocks(ne)), dim3(TB), 0, st, erec, ne, tk, tm, mask, 1u, nullptr);
+  hipLaunchKernelGGL(k_ht_insert, dim3(blocks(nf)), dim3(TB), 0, st, frec, nf, tk, tm, mask, 0u, w.tpos.p);
+  hipLaunchKernelGGL(k_ht_answer, dim3(blocks(nf)), dim3(TB), 0, st, w.tpos.p, nf, w.tmin.p, result);
   return hipGetLastError();
 }
 
