@@ -102,7 +102,13 @@ int sdcas_cas_ids(sdcas_ctx *ctx, const char *const *paths, const uint64_t *size
 int sdcas_checksums(sdcas_ctx *ctx, const char *const *paths, size_t n, uint8_t *out32,
                     int32_t *out_status);
 
-/* ---- pre-assembled messages in host memory ----------------------------- */
+/* ---- pre-assembled messages in host memory -----------------------------
+ *
+ * The bytes go through the context's pinned staging slots (a host copy by the
+ * I/O threads, overlapped with the GPU). When `blob` is itself page-locked
+ * (hipHostMalloc / hipHostRegister) and the messages lie in ascending,
+ * non-overlapping ranges at 16-byte aligned offsets, each slot's byte range
+ * is DMA'd straight from the caller's buffer instead (no host copy). */
 
 /* BLAKE3 of n messages blob[offsets[i] .. offsets[i]+lens[i]) -> out32 (32*n B). */
 int sdcas_hash_messages(sdcas_ctx *ctx, const uint8_t *blob, const uint64_t *offsets,

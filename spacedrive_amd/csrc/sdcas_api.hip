@@ -78,6 +78,7 @@ struct Slot {
   size_t n = 0;
   uint64_t used = 0, chunks = 0;
   std::vector<size_t> idx;  // caller index of message k
+  const uint8_t* src = nullptr;  // message bytes DMA'd from here instead of h (a pinned caller buffer)
   uint64_t* offs() { return hm; }
   uint64_t* lens() { return hm + cap_n; }
   uint8_t* res() { return reinterpret_cast<uint8_t*>(hm + 2 * cap_n); }
@@ -283,7 +284,7 @@ int slot_submit(sdcas_ctx* c, Slot& s, bool res32) {
     if ((rc = reserve_ws(c, std::max<size_t>(s.n, c->ws.cap_msgs), std::max<uint64_t>(s.chunks, c->ws.cap_chunks))))
       return rc;
   }
-  if ((e = hipMemcpyAsync(s.d_blob.p, s.h, s.used, hipMemcpyHostToDevice, st)) ||
+  if ((e = hipMemcpyAsync(s.d_blob.p, s.src ? s.src : s.h, s.used, hipMemcpyHostToDevice, st)) ||
       (e = hipMemcpyAsync(s.d_meta.p, s.hm, 8 * s.n, hipMemcpyHostToDevice, st)) ||
       (e = hipMemcpyAsync(s.d_meta.p + s.cap_n, s.hm + s.cap_n, 8 * s.n, hipMemcpyHostToDevice, st)))
     return c->hip_fail(e, "H2D");
@@ -653,6 +654,18 @@ int sdcas_dev_last_kernel_ms(sdcas_ctx* c, float* leaf_ms, float* total_ms) {
 
 int sdcas_hash_messages(sdcas_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* lens, size_t n,
                         uint8_t* out32);
+// page-locked host memory (hipHostMalloc / hipHostRegister)? Pageable
+// pointers make the query fail; its error is cleared.
+static bool host_pinned(const void* p) {
+  hipPointerAttribute_t a;
+  memset(&a, 0, sizeof a);
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeHost && a.hostPointer != nullptr;
+}
+
 static int hash_host_messages(sdcas_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* lens,
                               size_t n, uint8_t* out32, uint64_t* keys) {
   if (!c || (n && (!blob || !offsets || !lens))) return SDCAS_E_INVALID;
@@ -665,6 +678,14 @@ static int hash_host_messages(sdcas_ctx* c, const uint8_t* blob, const uint64_t*
   if ((rc = slots_prepare(c, cap, cap_n))) return rc;
   std::vector<BigItem> big;
   int cur = 0;
+  // Direct DMA: a caller buffer in pinned (page-locked) host memory whose
+  // messages lie in ascending, non-overlapping, 16-byte aligned ranges is
+  // copied range by range straight into the device slot (no host memcpy; the
+  // path then runs at the PCIe H2D rate).
+  bool direct = n > 0 && host_pinned(blob);
+  for (size_t i = 0; direct && i < n; ++i)
+    if ((offsets[i] & 15) || (i && offsets[i] < offsets[i - 1] + lens[i - 1])) direct = false;
+  uint64_t base = 0;  // caller offset of the current direct slot's first byte
   auto begin = [&](Slot& s) -> int {
     const int r = slot_complete(c, s, [&](size_t k, const uint8_t* res) {
       const size_t i = s.idx[k];
@@ -680,14 +701,19 @@ static int hash_host_messages(sdcas_ctx* c, const uint8_t* blob, const uint64_t*
     });
     s.n = 0, s.used = 0, s.chunks = 0;
     s.idx.clear();
+    s.src = nullptr;
     return r;
   };
   // the copy into pinned staging is the host-side cost of this path: it runs
   // on the I/O threads, one slot at a time, while the GPU hashes the other
   auto fill_submit = [&](Slot& s) -> int {
-    parallel_for(c->io_threads, s.n, [&](size_t k) {
-      memcpy(s.h + s.offs()[k], blob + offsets[s.idx[k]], s.lens()[k]);
-    });
+    if (direct) {
+      s.src = blob + base;
+    } else {
+      parallel_for(c->io_threads, s.n, [&](size_t k) {
+        memcpy(s.h + s.offs()[k], blob + offsets[s.idx[k]], s.lens()[k]);
+      });
+    }
     return slot_submit(c, s, out32 != nullptr);
   };
   if ((rc = begin(c->slots[cur]))) return rc;
@@ -698,17 +724,19 @@ static int hash_host_messages(sdcas_ctx* c, const uint8_t* blob, const uint64_t*
       continue;
     }
     Slot* s = &c->slots[cur];
-    if (s->used + align16(L) > cap || s->n == cap_n) {
+    const uint64_t end = direct ? offsets[i] + L - (s->n ? base : offsets[i]) : s->used + align16(L);
+    if (s->n && (end > cap || s->n == cap_n)) {
       if ((rc = fill_submit(*s))) return rc;
       cur ^= 1;
       s = &c->slots[cur];
       if ((rc = begin(*s))) return rc;
     }
-    s->offs()[s->n] = s->used;
+    if (direct && s->n == 0) base = offsets[i];
+    s->offs()[s->n] = direct ? offsets[i] - base : s->used;
     s->lens()[s->n] = L;
     s->idx.push_back(i);
     s->n++;
-    s->used += align16(L);
+    s->used = direct ? offsets[i] + L - base : s->used + align16(L);
     s->chunks += chunks_of(L);
   }
   if ((rc = fill_submit(c->slots[cur]))) return rc;
