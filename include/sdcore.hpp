@@ -24,6 +24,7 @@
 
 #include <array>
 #include <cstdint>
+#include <functional>
 #include <map>
 #include <memory>
 #include <optional>
@@ -180,6 +181,11 @@ class Library {
   virtual std::vector<FilePathRow> file_paths_without_checksum(int32_t location_id,
                                                                const std::string& sub_materialized_path) = 0;
   virtual void set_integrity_checksum(int32_t file_path_id, const std::string& checksum) = 0;
+  // the writes between these calls are one batch (sync.write_ops batches a
+  // step's operations, core/crates/sync/src/manager.rs:70-93): one
+  // transaction in a database; no-ops in memory
+  virtual void begin_batch() {}
+  virtual void end_batch() {}
 };
 
 // In-memory tables with the reference's query semantics (ids ascending = DB order)
@@ -208,6 +214,45 @@ class MemoryLibrary : public Library {
   int32_t next_file_path_id_ = 1, next_object_id_ = 1;
 };
 
+// SQLite tables with the columns of the reference's file_path / object
+// models (core/prisma/schema.prisma) and the reference's queries as prepared
+// statements (the DB side of the join). Differences, both
+// deliberate: an index on file_path(cas_id), which the reference's schema
+// lacks (the existing-Object lookup of mod.rs:181-188 then scans the table),
+// and a `kind_hint` column standing in for Extension::resolve_conflicting.
+// Batches are transactions (begin_batch / end_batch).
+class SqliteLibrary : public Library {
+ public:
+  // path of the database file, or ":memory:"; throws std::runtime_error.
+  // cas_id_index = false keeps the reference's schema (no index on cas_id),
+  // for comparison
+  static std::unique_ptr<SqliteLibrary> open(const std::string& path, bool cas_id_index = true);
+  ~SqliteLibrary() override;
+
+  // insert rows (ids and pub_ids assigned when 0), one transaction
+  void add_file_paths(std::vector<FilePathRow>& rows);
+  std::optional<FilePathRow> file_path(int32_t id);
+  std::vector<ObjectRow> objects();
+
+  size_t count_orphan_file_paths(int32_t location_id, const std::string& sub) override;
+  std::vector<FilePathRow> get_orphan_file_paths(int32_t location_id, int32_t cursor, const std::string& sub,
+                                                 size_t take) override;
+  void set_cas_id(int32_t file_path_id, const std::optional<std::string>& cas_id) override;
+  std::vector<std::pair<int32_t, std::vector<std::string>>> existing_objects(
+      const std::vector<std::string>& cas_ids) override;
+  int32_t create_object(ObjectKind kind, int64_t date_created) override;
+  void connect(int32_t file_path_id, int32_t object_id) override;
+  std::vector<FilePathRow> file_paths_without_checksum(int32_t location_id, const std::string& sub) override;
+  void set_integrity_checksum(int32_t file_path_id, const std::string& checksum) override;
+  void begin_batch() override;
+  void end_batch() override;
+
+ private:
+  struct Impl;
+  explicit SqliteLibrary(std::unique_ptr<Impl> d);
+  std::unique_ptr<Impl> d_;
+};
+
 // ---- file_identifier ----------------------------------------------------------
 
 // FileMetadata (mod.rs:48-53)
@@ -223,6 +268,16 @@ struct FileMetadata {
 // mod.rs:105-147). Errors carry the path (FileIOError).
 std::vector<Result<FileMetadata>> file_metadata_batch(Engine& engine,
                                                       const std::vector<std::pair<std::string, ObjectKind>>& files);
+
+// The DB half of identifier_job_step (mod.rs:157-342): write each file's
+// cas_id, look up the existing Objects of the batch's cas_ids, group (the
+// GPU's sdcas_dedup in identifier_job_step; any function with its encoding
+// here), create Objects and link. md[i] is file_paths[i]'s FileMetadata.
+using GroupBy = std::function<Engine::Dedup(const std::vector<uint64_t>& keys, const std::vector<uint8_t>& has_key,
+                                            const std::vector<int32_t>& status,
+                                            const std::vector<uint64_t>& existing_keys)>;
+std::pair<size_t, size_t> identifier_step_db(Library& db, const std::vector<FilePathRow>& file_paths,
+                                             const std::vector<Result<FileMetadata>>& md, const GroupBy& group_by);
 
 // identifier_job_step (mod.rs:98-350) over `file_paths` in id order. A batch
 // longer than `chunk_size` (the reference's CHUNK_SIZE = 100) gives the

@@ -266,20 +266,16 @@ std::vector<Result<FileMetadata>> file_metadata_batch(Engine& engine,
   return out;
 }
 
-std::pair<size_t, size_t> identifier_job_step(Engine& engine, Library& db, const Location& location,
-                                              const std::vector<FilePathRow>& file_paths, size_t chunk_size) {
+std::pair<size_t, size_t> identifier_step_db(Library& db, const std::vector<FilePathRow>& file_paths,
+                                             const std::vector<Result<FileMetadata>>& md, const GroupBy& group_by) {
   const size_t n = file_paths.size();
-  std::vector<std::pair<std::string, ObjectKind>> files(n);
-  for (size_t i = 0; i < n; ++i) files[i] = {full_path(location, file_paths[i]), file_paths[i].kind};
-  // FileMetadata::new for every row (mod.rs:105-147): failing files are
-  // logged and left out of the rest of the step (mod.rs:125-141)
-  auto md = file_metadata_batch(engine, files);
-
+  if (md.size() != n) throw std::invalid_argument("identifier_step_db: one metadata per file_path");
   std::vector<uint64_t> keys(n, 0);
   std::vector<uint8_t> has_key(n, 0);
   std::vector<int32_t> status(n, 0);
   std::vector<std::string> unique;
   std::set<std::string> seen;
+  db.begin_batch();
   for (size_t i = 0; i < n; ++i) {
     if (!md[i].ok()) {
       status[i] = md[i].error().code;
@@ -293,6 +289,7 @@ std::pair<size_t, size_t> identifier_job_step(Engine& engine, Library& db, const
     }
     db.set_cas_id(file_paths[i].id, cas);  // mod.rs:157-178
   }
+  db.end_batch();
   // existing Objects carrying any of these cas_ids, DB order (mod.rs:181-188);
   // one existing-key entry per (object, cas_id) so "the first object whose
   // file_paths carry the cas_id" (mod.rs:214-224) is the first entry
@@ -304,10 +301,12 @@ std::pair<size_t, size_t> identifier_job_step(Engine& engine, Library& db, const
       ekeys.push_back(hex_to_key(c));
       eobj.push_back(oid);
     }
-  auto d = engine.dedup(keys, has_key, status, chunk_size, ekeys);
+  auto d = group_by(keys, has_key, status, ekeys);
+  if (d.link.size() != n) throw std::logic_error("identifier_step_db: group-by returned a wrong link count");
   // links and new Objects (mod.rs:202-342): new Objects take the kind and
   // date_created of their file (mod.rs:266-291)
   std::vector<int32_t> created_object(n, 0);
+  db.begin_batch();
   for (size_t i = 0; i < n; ++i) {
     const int64_t l = d.link[i];
     if (l == INT64_MIN) continue;
@@ -320,7 +319,23 @@ std::pair<size_t, size_t> identifier_job_step(Engine& engine, Library& db, const
       db.connect(file_paths[i].id, eobj[(size_t)(-(l + 1))]);
     }
   }
+  db.end_batch();
   return {(size_t)d.created, (size_t)d.linked};
+}
+
+std::pair<size_t, size_t> identifier_job_step(Engine& engine, Library& db, const Location& location,
+                                              const std::vector<FilePathRow>& file_paths, size_t chunk_size) {
+  const size_t n = file_paths.size();
+  std::vector<std::pair<std::string, ObjectKind>> files(n);
+  for (size_t i = 0; i < n; ++i) files[i] = {full_path(location, file_paths[i]), file_paths[i].kind};
+  // FileMetadata::new for every row (mod.rs:105-147): failing files are
+  // logged and left out of the rest of the step (mod.rs:125-141)
+  auto md = file_metadata_batch(engine, files);
+  return identifier_step_db(db, file_paths, md,
+                            [&](const std::vector<uint64_t>& k, const std::vector<uint8_t>& h,
+                                const std::vector<int32_t>& st, const std::vector<uint64_t>& e) {
+                              return engine.dedup(k, h, st, chunk_size, e);
+                            });
 }
 
 FileIdentifierJobRunMetadata run_file_identifier_job(Engine& engine, Library& db, const FileIdentifierJobInit& init) {
@@ -361,15 +376,18 @@ ObjectValidatorReport run_object_validator_job(Engine& engine, Library& db, cons
     std::vector<std::string> paths;
     for (size_t i = lo; i < hi; ++i) paths.push_back(full_path(init.location, rows[i]));
     auto sums = engine.file_checksums(paths);
+    db.begin_batch();
     for (size_t i = lo; i < hi; ++i) {
       const auto& r = sums[i - lo];
       if (!r.ok()) {  // validator_job.rs:154-156: the step fails with FileIO
         rep.error = r.error();
+        db.end_batch();
         return rep;
       }
       db.set_integrity_checksum(rows[i].id, r.value());  // validator_job.rs:158-172
       ++rep.checksummed;
     }
+    db.end_batch();
   }
   return rep;
 }

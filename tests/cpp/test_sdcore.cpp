@@ -172,6 +172,12 @@ static void test_identifier_job(Engine& eng, const std::string& dir) {
     const std::string d = dir + "/loc" + std::to_string(batch);
     mkdir(d.c_str(), 0755);
     Corpus c = make_corpus(d, n, 300);
+    // the same library in SQLite (objects first, so their ids match), run
+    // through the same job below
+    auto sql = SqliteLibrary::open(":memory:");
+    for (const auto& o : c.lib.objects) sql->create_object(o.kind, o.date_created);
+    std::vector<FilePathRow> rows = c.lib.file_paths;
+    sql->add_file_paths(rows);
     // the oracle: reference chunks of 100 over the orphans in id order
     std::vector<int64_t> link(n);
     int64_t linked = 0;
@@ -216,6 +222,15 @@ static void test_identifier_job(Engine& eng, const std::string& dir) {
     for (const auto& r : c.lib.file_paths) sub += r.materialized_path == "/sub/" && (!r.object_id || !r.cas_id);
     CHECK(c.lib.count_orphan_file_paths(1, "/sub/") == sub, "sub orphans");
     objects_by_batch.push_back(obj);
+    auto msql = run_file_identifier_job(eng, *sql, init);
+    CHECK(msql.total_objects_created == meta.total_objects_created &&
+              msql.total_objects_linked == meta.total_objects_linked && msql.steps == meta.steps,
+          "sqlite job batch %zu", batch);
+    for (size_t i = 0; i < n; ++i) {
+      auto r = sql->file_path((int32_t)(i + 3));
+      CHECK(r && r->object_id.value_or(-1) == obj[i] && r->cas_id == c.lib.file_path((int32_t)(i + 3))->cas_id,
+            "sqlite file %zu", i);
+    }
     std::printf("identifier job batch %zu: created %zu linked %zu steps %zu\n", batch, meta.total_objects_created,
                 meta.total_objects_linked, meta.steps);
   }

@@ -1,0 +1,275 @@
+// CPU tests of the DB side of the identifier join:
+// SqliteLibrary against MemoryLibrary (the reference's query semantics in
+// memory) and the oracle's chunked group-by, without a GPU.
+// TEST INFRASTRUCTURE: links oracle/build/liboracle.so as the checker.
+//
+//   test_sdcore_db            query parity + a simulated identifier job on both
+//   test_sdcore_db --bench N  DB-side rows/s of the identifier step over N
+//                             file_paths in a SQLite file (one JSON line)
+#include <unistd.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../../oracle/oracle.h"
+#include "sdcore.hpp"
+
+using namespace sdcore;
+
+static int failures = 0;
+#define CHECK(cond, ...)                                       \
+  do {                                                         \
+    if (!(cond)) {                                             \
+      ++failures;                                              \
+      std::fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__); \
+      std::fprintf(stderr, __VA_ARGS__);                       \
+      std::fprintf(stderr, "\n");                              \
+    }                                                          \
+  } while (0)
+
+static uint64_t mix(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+// rows of two locations: files and dirs, empty DB sizes, a sub directory,
+// already identified rows (cas_id + object) and validated ones
+static std::vector<FilePathRow> make_rows(size_t n, uint64_t seed) {
+  std::mt19937_64 g(seed);
+  std::vector<FilePathRow> rows;
+  for (size_t i = 0; i < n; ++i) {
+    FilePathRow r;
+    r.location_id = (g() % 10) ? 1 : 2;
+    r.materialized_path = (g() % 3) ? "/" : ((g() % 2) ? "/sub/" : "/sub/deeper/");
+    r.name = "f" + std::to_string(i);
+    r.extension = (g() % 4) ? "bin" : "";
+    r.is_dir = (g() % 25) == 0;
+    r.size_in_bytes = (g() % 40) ? 1 + g() % 200000 : 0;
+    r.date_created = (int64_t)(1700000000 + i);
+    r.kind = (int32_t)(g() % 9);
+    if (g() % 11 == 0) r.integrity_checksum = std::string(64, 'a');
+    rows.push_back(r);
+  }
+  return rows;
+}
+
+// FileMetadata per row: cas ids from a pool (duplicates in and across
+// chunks), some empty files (None), some I/O errors
+static std::vector<Result<FileMetadata>> make_metadata(const std::vector<FilePathRow>& rows, size_t pool) {
+  std::vector<Result<FileMetadata>> md;
+  for (const auto& r : rows) {
+    const uint64_t h = mix((uint64_t)r.id * 7919);
+    if (h % 97 == 0) {
+      md.emplace_back(IoError{ENOENT, r.name});
+      continue;
+    }
+    FileMetadata m;
+    m.kind = r.kind;
+    m.len = r.size_in_bytes;
+    if (h % 31 != 0) m.cas_id = key_to_hex(mix(h % pool));
+    md.emplace_back(m);
+  }
+  return md;
+}
+
+static GroupBy oracle_group_by(size_t chunk_size) {
+  return [chunk_size](const std::vector<uint64_t>& k, const std::vector<uint8_t>& h, const std::vector<int32_t>& st,
+                      const std::vector<uint64_t>& e) {
+    Engine::Dedup d;
+    d.link.assign(k.size(), 0);
+    int64_t linked = 0;
+    d.created = oracle_identifier_dedup(k.size(), k.data(), h.data(), st.data(), chunk_size, e.size(),
+                                        e.empty() ? nullptr : e.data(), d.link.data(), &linked);
+    d.linked = linked;
+    return d;
+  };
+}
+
+// the identifier job's loop (file_identifier_job.rs:125-223) with the
+// metadata supplied instead of read from files
+static FileIdentifierJobRunMetadata run_job(Library& db, int32_t loc, size_t batch, uint64_t pool) {
+  FileIdentifierJobRunMetadata meta;
+  meta.total_orphan_paths = db.count_orphan_file_paths(loc, "");
+  if (!meta.total_orphan_paths) return meta;
+  meta.cursor = db.get_orphan_file_paths(loc, 0, "", 1)[0].id;
+  const size_t tasks = (meta.total_orphan_paths + batch - 1) / batch;
+  for (size_t t = 0; t < tasks; ++t) {
+    auto rows = db.get_orphan_file_paths(loc, meta.cursor, "", batch);
+    if (rows.empty()) break;
+    auto md = make_metadata(rows, pool);
+    auto [c, l] = identifier_step_db(db, rows, md, oracle_group_by(100));
+    meta.total_objects_created += c;
+    meta.total_objects_linked += l;
+    meta.cursor = rows.back().id;
+    ++meta.steps;
+  }
+  return meta;
+}
+
+static bool same_row(const FilePathRow& a, const FilePathRow& b) {
+  return a.id == b.id && a.pub_id == b.pub_id && a.location_id == b.location_id &&
+         a.materialized_path == b.materialized_path && a.name == b.name && a.extension == b.extension &&
+         a.is_dir == b.is_dir && a.size_in_bytes == b.size_in_bytes && a.cas_id == b.cas_id &&
+         a.object_id == b.object_id && a.integrity_checksum == b.integrity_checksum &&
+         a.date_created == b.date_created && a.kind == b.kind;
+}
+
+static bool same_rows(const std::vector<FilePathRow>& a, const std::vector<FilePathRow>& b) {
+  if (a.size() != b.size()) return false;
+  for (size_t i = 0; i < a.size(); ++i)
+    if (!same_row(a[i], b[i])) return false;
+  return true;
+}
+
+static void test_parity(bool cas_index) {
+  MemoryLibrary mem;
+  auto sql = SqliteLibrary::open(":memory:", cas_index);
+  auto rows = make_rows(3000, 5);
+  for (auto& r : rows) r = mem.add_file_path(r);
+  sql->add_file_paths(rows);
+  // an identified slice with Objects, in both
+  for (int32_t id = 1; id <= 3000; id += 17) {
+    const auto* r = mem.file_path(id);
+    if (r->is_dir || r->size_in_bytes == 0) continue;
+    const std::string cas = key_to_hex(mix((uint64_t)id % 50));
+    mem.set_cas_id(id, cas);
+    sql->set_cas_id(id, cas);
+    const int32_t om = mem.create_object(3, id), os = sql->create_object(3, id);
+    CHECK(om == os, "object ids %d %d", om, os);
+    mem.connect(id, om);
+    sql->connect(id, os);
+  }
+  for (int32_t loc : {1, 2})
+    for (const char* sub : {"", "/sub/", "/sub/deeper/", "/nope/"}) {
+      CHECK(mem.count_orphan_file_paths(loc, sub) == sql->count_orphan_file_paths(loc, sub), "count %d %s", loc, sub);
+      for (int32_t cursor : {0, 1, 500, 2999, 5000})
+        for (size_t take : {1, 100, 10000})
+          CHECK(same_rows(mem.get_orphan_file_paths(loc, cursor, sub, take),
+                          sql->get_orphan_file_paths(loc, cursor, sub, take)),
+                "orphans loc %d sub %s cursor %d take %zu", loc, sub, cursor, take);
+      CHECK(same_rows(mem.file_paths_without_checksum(loc, sub), sql->file_paths_without_checksum(loc, sub)),
+            "without checksum %d %s", loc, sub);
+    }
+  std::vector<std::string> want;
+  for (int k = 0; k < 60; k += 3) want.push_back(key_to_hex(mix((uint64_t)k)));
+  CHECK(mem.existing_objects(want) == sql->existing_objects(want), "existing objects");
+  CHECK(sql->existing_objects({}).empty(), "existing objects of nothing");
+
+  // the identifier job on both, against the oracle's counts
+  for (int32_t loc : {1, 2}) {
+    // (the job re-reads a chunk's last row when it stays an orphan — an
+    // I/O error, an empty file — as the reference's `id >= cursor` does, so
+    // the parity is memory vs SQLite, not the fixed chunks of the oracle)
+    const auto orphans = mem.get_orphan_file_paths(loc, 0, "", 1u << 30);
+    auto jm = run_job(mem, loc, 100, 400);
+    auto js = run_job(*sql, loc, 100, 400);
+    CHECK(jm.total_objects_created == js.total_objects_created && jm.total_objects_linked == js.total_objects_linked &&
+              jm.steps == js.steps && jm.cursor == js.cursor,
+          "job loc %d: memory %zu/%zu sqlite %zu/%zu", loc, jm.total_objects_created, jm.total_objects_linked,
+          js.total_objects_created, js.total_objects_linked);
+    std::printf("job loc %d: %zu orphans, created %zu linked %zu in %zu steps (memory == sqlite)\n", loc,
+                orphans.size(), js.total_objects_created, js.total_objects_linked, js.steps);
+  }
+  for (int32_t id = 1; id <= 3000; ++id) {
+    auto s = sql->file_path(id);
+    CHECK(s && same_row(*mem.file_path(id), *s), "row %d after the job", id);
+  }
+  auto so = sql->objects();
+  CHECK(so.size() == mem.objects.size(), "object count %zu %zu", so.size(), mem.objects.size());
+  for (size_t i = 0; i < so.size() && i < mem.objects.size(); ++i)
+    CHECK(so[i].id == mem.objects[i].id && so[i].kind == mem.objects[i].kind &&
+              so[i].date_created == mem.objects[i].date_created,
+          "object %zu", i);
+  // validator writes
+  for (const auto& r : sql->file_paths_without_checksum(1, "/sub/")) {
+    sql->set_integrity_checksum(r.id, std::string(64, 'b'));
+    mem.set_integrity_checksum(r.id, std::string(64, 'b'));
+  }
+  CHECK(same_rows(mem.file_paths_without_checksum(1, ""), sql->file_paths_without_checksum(1, "")), "validator");
+}
+
+// forwards everything but the batch hooks: every write its own transaction
+struct Autocommit : Library {
+  Library& d;
+  explicit Autocommit(Library& x) : d(x) {}
+  size_t count_orphan_file_paths(int32_t l, const std::string& s) override { return d.count_orphan_file_paths(l, s); }
+  std::vector<FilePathRow> get_orphan_file_paths(int32_t l, int32_t c, const std::string& s, size_t t) override {
+    return d.get_orphan_file_paths(l, c, s, t);
+  }
+  void set_cas_id(int32_t i, const std::optional<std::string>& c) override { d.set_cas_id(i, c); }
+  std::vector<std::pair<int32_t, std::vector<std::string>>> existing_objects(
+      const std::vector<std::string>& c) override {
+    return d.existing_objects(c);
+  }
+  int32_t create_object(ObjectKind k, int64_t t) override { return d.create_object(k, t); }
+  void connect(int32_t f, int32_t o) override { d.connect(f, o); }
+  std::vector<FilePathRow> file_paths_without_checksum(int32_t l, const std::string& s) override {
+    return d.file_paths_without_checksum(l, s);
+  }
+  void set_integrity_checksum(int32_t i, const std::string& c) override { d.set_integrity_checksum(i, c); }
+};
+
+static double now() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+static int bench(size_t n) {
+  std::string out = "{\"what\": \"DB side of the identifier step (SqliteLibrary, WAL, synchronous=NORMAL), "
+                    "group-by by the CPU oracle, metadata synthetic\", \"file_paths\": " + std::to_string(n);
+  struct Mode {
+    const char* name;
+    size_t batch;
+    bool autocommit, cas_index;
+  };
+  // the reference's shape: 100-row steps, a commit per write, no cas_id index
+  // (a bounded sample: it is slow); then this library's batching and index
+  for (Mode m : {Mode{"reference_shape_batch100_autocommit_no_cas_index", 100, true, false},
+                 Mode{"batch100_autocommit", 100, true, true}, Mode{"batch100_txn", 100, false, true},
+                 Mode{"batch10000_txn", 10000, false, true}}) {
+    const size_t rows_n = m.autocommit ? std::min<size_t>(n, 20000) : n;
+    char path[] = "/tmp/sdcore_dbXXXXXX";
+    const int fd = mkstemp(path);
+    if (fd >= 0) close(fd);
+    std::remove(path);
+    {
+      auto sql = SqliteLibrary::open(path, m.cas_index);
+      auto rows = make_rows(rows_n, 9);
+      for (auto& r : rows) {
+        r.location_id = 1;
+        r.is_dir = false;
+        r.size_in_bytes = 1 + r.size_in_bytes;
+        r.integrity_checksum.reset();
+      }
+      sql->add_file_paths(rows);
+      Autocommit ac(*sql);
+      Library& db = m.autocommit ? static_cast<Library&>(ac) : *sql;
+      const double t0 = now();
+      auto meta = run_job(db, 1, m.batch, rows_n / 3);
+      const double dt = now() - t0;
+      char b[256];
+      std::snprintf(b, sizeof b,
+                    ", \"%s\": {\"rows\": %zu, \"seconds\": %.3f, \"rows_per_s\": %.0f, \"created\": %zu, "
+                    "\"linked\": %zu}",
+                    m.name, rows_n, dt, rows_n / dt, meta.total_objects_created, meta.total_objects_linked);
+      out += b;
+    }
+    for (const char* suf : {"", "-wal", "-shm"}) std::remove((std::string(path) + suf).c_str());
+  }
+  std::printf("%s}\n", out.c_str());
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc > 2 && std::strcmp(argv[1], "--bench") == 0) return bench((size_t)std::atoll(argv[2]));
+  test_parity(true);
+  test_parity(false);
+  std::printf("%s (%d failures)\n", failures ? "FAILED" : "ALL OK", failures);
+  return failures ? 1 : 0;
+}

@@ -38,6 +38,18 @@ def test_host_library_links_the_c_abi():
         assert name in syms, name
 
 
+def test_db_side_sqlite_vs_memory():
+    """the DB side of the identifier join: SqliteLibrary
+    queries and a simulated identifier job equal MemoryLibrary's, with and
+    without the cas_id index (CPU only; tests/cpp/test_sdcore_db.cpp)"""
+    db_bin = os.path.join(ROOT, "tests", "cpp", "build", "test_sdcore_db")
+    if not os.path.exists(db_bin):
+        _build()
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "cpp")], check=True)
+    r = subprocess.run([db_bin], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "ALL OK" in r.stdout, r.stdout + r.stderr
+
+
 @pytest.mark.gpu
 def test_host_mirror_on_gpu():
     r = subprocess.run([_build()], capture_output=True, text=True, timeout=300)
