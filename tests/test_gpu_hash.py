@@ -273,3 +273,37 @@ def test_pinned_caller_buffer_direct_dma(oracle):
         perm = rng.permutation(lens.size)
         out2 = e.hash_messages(host, offs[perm], lens[perm])
         assert [bytes(d).hex() for d in out2] == [want[i] for i in perm]
+
+
+def test_concurrent_contexts_and_shared_context(oracle):
+    """sd-core calls from several tokio workers: one context per thread runs
+    concurrently; one context shared by threads serialises internally. Every
+    result stays bit-exact."""
+    import threading
+    from spacedrive_amd import Engine
+    rng = np.random.default_rng(99)
+    batches = [[rng.integers(0, 256, int(L), dtype=np.uint8).tobytes() for L in rng.integers(0, 150_000, 60)]
+               for _ in range(6)]
+    want = [[oracle.hash(m) for m in b] for b in batches]
+    got = [None] * len(batches)
+    errs = []
+
+    def work(i, e):
+        try:
+            got[i] = [bytes(d).hex() for d in e.hash_messages(*e.pack(batches[i]))]
+        except Exception as x:  # surfaced below
+            errs.append(repr(x))
+
+    own = [Engine(staging_bytes=1 << 20, io_threads=2) for _ in range(3)]
+    shared = Engine(staging_bytes=1 << 20, io_threads=2)
+    try:
+        th = [threading.Thread(target=work, args=(i, own[i] if i < 3 else shared)) for i in range(len(batches))]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=120)
+    finally:
+        for e in own + [shared]:
+            e.close()
+    assert not errs, errs
+    assert got == want
