@@ -139,6 +139,8 @@ struct FilePathRow {
   std::optional<int32_t> object_id;
   std::optional<std::string> integrity_checksum;
   int64_t date_created = 0;
+  uint64_t inode = 0;   // FilePathMetadata (crates/file-path-helper/src/lib.rs:125-131)
+  bool hidden = false;
   // Extension::resolve_conflicting (crates/file-ext/src/magic.rs:176-230) is
   // outside this path: the kind is supplied with the row
   ObjectKind kind = 0;
@@ -154,6 +156,20 @@ struct ObjectRow {  // object (id, pub_id, kind, date_created)
 // location path joined with the row's relative path (assemble_relative_path /
 // join_location_relative_path, isolated_file_path_data.rs:533-560)
 std::string full_path(const Location& location, const FilePathRow& row);
+
+// The indexer's walk (core/src/location/indexer/walk.rs:432-560) without
+// indexer rules: every directory and regular file under the location,
+// breadth first, entries of a directory in name order; symlinks skipped
+// (walk.rs: `metadata.is_symlink()`); IsolatedFilePathData::new naming
+// (isolated_file_path_data.rs:49-87): materialized_path "/a/b/", a file's
+// name is Rust's Path::file_stem and its extension Path::extension, a
+// directory keeps its whole file name; hidden = name starts with '.'
+// (lib.rs:133-147). Rows come back with id 0 (the library assigns ids);
+// entries that cannot be read are skipped and reported in `errors`.
+std::vector<FilePathRow> walk_location(const Location& location, std::vector<IoError>* errors = nullptr);
+
+// Rust's Path::file_stem / Path::extension of a file name
+std::pair<std::string, std::optional<std::string>> file_stem_and_extension(const std::string& file_name);
 
 // ---- the database seam ------------------------------------------------------
 

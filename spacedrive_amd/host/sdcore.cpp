@@ -2,6 +2,7 @@
 // libsdcas (see include/sdcore.hpp for the reference file:line of each entry).
 #include "sdcore.hpp"
 
+#include <dirent.h>
 #include <sys/stat.h>
 
 #include <algorithm>
@@ -130,6 +131,70 @@ std::string full_path(const Location& location, const FilePathRow& row) {
   std::string base = location.path;
   if (!base.empty() && base.back() != '/') base += '/';
   return base + rel;
+}
+
+// ---- indexer walk ------------------------------------------------------------------
+
+std::pair<std::string, std::optional<std::string>> file_stem_and_extension(const std::string& name) {
+  // std::path's rsplit_file_at_dot: "..": no extension; the text before the
+  // last dot empty (".bashrc"): no extension; else (before, after)
+  if (name == "..") return {name, std::nullopt};
+  const size_t dot = name.rfind('.');
+  if (dot == std::string::npos) return {name, std::nullopt};
+  if (dot == 0) return {name, std::nullopt};
+  return {name.substr(0, dot), name.substr(dot + 1)};
+}
+
+std::vector<FilePathRow> walk_location(const Location& location, std::vector<IoError>* errors) {
+  std::vector<FilePathRow> out;
+  std::string root = location.path;
+  while (root.size() > 1 && root.back() == '/') root.pop_back();
+  std::vector<std::string> queue{""};  // relative directory paths, "" = the location itself
+  for (size_t qi = 0; qi < queue.size(); ++qi) {
+    const std::string rel = queue[qi];
+    const std::string dir = rel.empty() ? root : root + "/" + rel;
+    DIR* d = opendir(dir.c_str());
+    if (!d) {
+      if (errors) errors->push_back(IoError{errno, dir});
+      continue;
+    }
+    std::vector<std::string> names;
+    while (dirent* e = readdir(d)) {
+      if (!std::strcmp(e->d_name, ".") || !std::strcmp(e->d_name, "..")) continue;
+      names.emplace_back(e->d_name);
+    }
+    closedir(d);
+    std::sort(names.begin(), names.end());
+    for (const auto& name : names) {
+      const std::string full = dir + "/" + name;
+      struct stat sb;
+      if (lstat(full.c_str(), &sb) != 0) {
+        if (errors) errors->push_back(IoError{errno, full});
+        continue;
+      }
+      if (S_ISLNK(sb.st_mode)) continue;
+      const bool is_dir = S_ISDIR(sb.st_mode);
+      if (!is_dir && !S_ISREG(sb.st_mode)) continue;  // sockets, fifos, devices
+      FilePathRow r;
+      r.location_id = location.id;
+      r.is_dir = is_dir;
+      r.materialized_path = rel.empty() ? "/" : "/" + rel + "/";
+      if (is_dir) {
+        r.name = name;
+      } else {
+        auto [stem, ext] = file_stem_and_extension(name);
+        r.name = stem;
+        r.extension = ext.value_or("");
+      }
+      r.size_in_bytes = (uint64_t)sb.st_size;
+      r.inode = (uint64_t)sb.st_ino;
+      r.hidden = !name.empty() && name[0] == '.';
+      r.date_created = (int64_t)sb.st_mtime;  // created_or_now(): birth time is not in struct stat
+      out.push_back(std::move(r));
+      if (is_dir) queue.push_back(rel.empty() ? name : rel + "/" + name);
+    }
+  }
+  return out;
 }
 
 // ---- MemoryLibrary ------------------------------------------------------------------

@@ -98,6 +98,8 @@ struct SqliteLibrary::Impl {
     r.integrity_checksum = col_text(s, 10);
     r.date_created = sqlite3_column_int64(s, 11);
     r.kind = (int32_t)sqlite3_column_int64(s, 12);
+    r.inode = from_be64(sqlite3_column_blob(s, 13), sqlite3_column_bytes(s, 13));
+    r.hidden = sqlite3_column_int64(s, 14) != 0;
     return r;
   }
   std::vector<FilePathRow> rows(Stmt& st) {
@@ -113,7 +115,7 @@ struct SqliteLibrary::Impl {
 
 #define SD_COLS \
   "id, pub_id, location_id, materialized_path, name, extension, is_dir, size_in_bytes_bytes, cas_id, object_id, " \
-  "integrity_checksum, date_created, kind_hint"
+  "integrity_checksum, date_created, kind_hint, inode, hidden"
 // orphan_path_filters (file_identifier_job.rs:251-283)
 #define SD_ORPHAN                                                                                       \
   "(object_id IS NULL OR cas_id IS NULL) AND is_dir = 0 AND location_id = ?1 AND "                      \
@@ -190,8 +192,8 @@ std::unique_ptr<SqliteLibrary> SqliteLibrary::open(const std::string& path, bool
   x.prepare(x.set_checksum, "UPDATE file_path SET integrity_checksum = ?1 WHERE id = ?2");
   x.prepare(x.add_path,
             "INSERT INTO file_path (id, pub_id, location_id, materialized_path, name, extension, is_dir,"
-            " size_in_bytes_bytes, cas_id, object_id, integrity_checksum, date_created, kind_hint)"
-            " VALUES (?1, ?2, ?3, ?4, ?5, ?6, ?7, ?8, ?9, ?10, ?11, ?12, ?13)");
+            " size_in_bytes_bytes, cas_id, object_id, integrity_checksum, date_created, kind_hint, inode, hidden)"
+            " VALUES (?1, ?2, ?3, ?4, ?5, ?6, ?7, ?8, ?9, ?10, ?11, ?12, ?13, ?14, ?15)");
   x.prepare(x.get_path, "SELECT " SD_COLS " FROM file_path WHERE id = ?1");
   x.prepare(x.all_objects, "SELECT id, pub_id, kind, date_created FROM object ORDER BY id");
   {
@@ -240,6 +242,10 @@ void SqliteLibrary::add_file_paths(std::vector<FilePathRow>& rows) {
     x.opt_text(st, 11, r.integrity_checksum);
     sqlite3_bind_int64(st.s, 12, r.date_created);
     sqlite3_bind_int64(st.s, 13, r.kind);
+    uint8_t ino[8];
+    be64(r.inode, ino);
+    sqlite3_bind_blob(st.s, 14, ino, 8, SQLITE_TRANSIENT);
+    sqlite3_bind_int64(st.s, 15, r.hidden ? 1 : 0);
     x.done(st);
   }
   end_batch();

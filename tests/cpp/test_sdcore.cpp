@@ -277,6 +277,63 @@ static void test_validator(Engine& eng, const std::string& dir) {
   std::printf("validator: %zu checksums ok\n", rep.checksummed);
 }
 
+// a location on disk end to end: walk -> SQLite -> identifier job -> validator
+static void test_location_scan(Engine& eng, const std::string& dir) {
+  const std::string root = dir + "/scan";
+  mkdir(root.c_str(), 0755);
+  std::mt19937_64 g(3);
+  std::vector<std::string> subdirs = {"", "docs", "docs/old", "media", "media/raw", ".cache"};
+  for (const auto& d : subdirs)
+    if (!d.empty()) mkdir((root + "/" + d).c_str(), 0755);
+  for (int i = 0; i < 640; ++i) {
+    const auto& d = subdirs[g() % subdirs.size()];
+    const uint64_t which = g() % 220;  // shared contents
+    const size_t size = 1 + (which * 104729) % 300000;
+    const std::string name = "f" + std::to_string(i) + ((i % 4) ? ".dat" : "");
+    write_file(root + (d.empty() ? "" : "/" + d) + "/" + name, content(which + 9000, size));
+  }
+  std::vector<IoError> errs;
+  auto rows = walk_location(Location{3, root}, &errs);
+  CHECK(errs.empty(), "walk errors");
+  auto sql = SqliteLibrary::open(":memory:");
+  sql->add_file_paths(rows);
+  FileIdentifierJobInit init{Location{3, root}, "", 1000};
+  auto meta = run_file_identifier_job(eng, *sql, init);
+  // the oracle over the same orphans (files in id order)
+  std::vector<uint64_t> keys;
+  std::vector<uint8_t> has;
+  std::vector<int32_t> ids;
+  for (const auto& r : rows) {
+    if (r.is_dir) continue;
+    int st;
+    const std::string cas = oracle_cas(full_path(Location{3, root}, r), r.size_in_bytes, &st);
+    keys.push_back(hex_to_key(cas));
+    has.push_back(1);
+    ids.push_back(r.id);
+  }
+  std::vector<int64_t> link(keys.size());
+  int64_t linked = 0;
+  const int64_t created =
+      oracle_identifier_dedup(keys.size(), keys.data(), has.data(), nullptr, 100, 0, nullptr, link.data(), &linked);
+  CHECK((int64_t)meta.total_objects_created == created && (int64_t)meta.total_objects_linked == linked,
+        "scan: created/linked %zu/%zu, oracle %lld/%lld", meta.total_objects_created, meta.total_objects_linked,
+        (long long)created, (long long)linked);
+  for (size_t k = 0; k < ids.size(); ++k) {
+    auto r = sql->file_path(ids[k]);
+    CHECK(r && r->cas_id && hex_to_key(*r->cas_id) == keys[k], "scan cas_id of row %d", ids[k]);
+    if (link[k] >= 0 && link[k] != (int64_t)k)
+      CHECK(r->object_id == sql->file_path(ids[(size_t)link[k]])->object_id, "scan object of row %d", ids[k]);
+  }
+  auto rep = run_object_validator_job(eng, *sql, ObjectValidatorJobInit{Location{3, root}, "", 256});
+  CHECK(rep.task_count == ids.size() && rep.checksummed == ids.size() && !rep.error, "scan validator");
+  for (int32_t id : ids) {
+    auto r = sql->file_path(id);
+    CHECK(r->integrity_checksum == oracle_sum(full_path(Location{3, root}, *r)), "scan checksum of row %d", id);
+  }
+  std::printf("location scan: %zu entries, %zu files, created %zu linked %zu, checksums ok\n", rows.size(),
+              ids.size(), meta.total_objects_created, meta.total_objects_linked);
+}
+
 int main(int argc, char** argv) {
   if (argc > 1 && std::strcmp(argv[1], "--no-gpu") == 0) {
     try {
@@ -294,6 +351,7 @@ int main(int argc, char** argv) {
   test_hashes(*eng, dir);
   test_identifier_job(*eng, dir);
   test_validator(*eng, dir);
+  test_location_scan(*eng, dir);
   std::string cmd = "rm -rf " + dir;
   if (std::system(cmd.c_str()) != 0) std::fprintf(stderr, "cleanup failed\n");
   std::printf("%s (%d failures)\n", failures ? "FAILED" : "ALL OK", failures);

@@ -6,7 +6,10 @@
 //   test_sdcore_db            query parity + a simulated identifier job on both
 //   test_sdcore_db --bench N  DB-side rows/s of the identifier step over N
 //                             file_paths in a SQLite file (one JSON line)
+#include <sys/stat.h>
 #include <unistd.h>
+
+#include <tuple>
 
 #include <chrono>
 #include <cstdio>
@@ -54,6 +57,8 @@ static std::vector<FilePathRow> make_rows(size_t n, uint64_t seed) {
     r.size_in_bytes = (g() % 40) ? 1 + g() % 200000 : 0;
     r.date_created = (int64_t)(1700000000 + i);
     r.kind = (int32_t)(g() % 9);
+    r.inode = g();
+    r.hidden = g() % 7 == 0;
     if (g() % 11 == 0) r.integrity_checksum = std::string(64, 'a');
     rows.push_back(r);
   }
@@ -118,7 +123,7 @@ static bool same_row(const FilePathRow& a, const FilePathRow& b) {
          a.materialized_path == b.materialized_path && a.name == b.name && a.extension == b.extension &&
          a.is_dir == b.is_dir && a.size_in_bytes == b.size_in_bytes && a.cas_id == b.cas_id &&
          a.object_id == b.object_id && a.integrity_checksum == b.integrity_checksum &&
-         a.date_created == b.date_created && a.kind == b.kind;
+         a.date_created == b.date_created && a.kind == b.kind && a.inode == b.inode && a.hidden == b.hidden;
 }
 
 static bool same_rows(const std::vector<FilePathRow>& a, const std::vector<FilePathRow>& b) {
@@ -266,10 +271,67 @@ static int bench(size_t n) {
   return 0;
 }
 
+static void touch(const std::string& p, size_t n) {
+  FILE* f = std::fopen(p.c_str(), "wb");
+  if (!f) return;
+  for (size_t i = 0; i < n; ++i) std::fputc((int)(i * 7), f);
+  std::fclose(f);
+}
+
+// walk_location: IsolatedFilePathData naming, Rust's file_stem / extension,
+// breadth-first order, symlinks skipped
+static void test_walk() {
+  char tmpl[] = "/tmp/sdcore_walkXXXXXX";
+  const std::string root = mkdtemp(tmpl);
+  mkdir((root + "/sub").c_str(), 0755);
+  mkdir((root + "/sub/deeper").c_str(), 0755);
+  mkdir((root + "/x.y").c_str(), 0755);
+  touch(root + "/a.tar.gz", 10);
+  touch(root + "/.bashrc", 3);
+  touch(root + "/foo.", 0);
+  touch(root + "/..hidden", 5);
+  touch(root + "/noext", 1);
+  touch(root + "/sub/b.TXT", 2000);
+  touch(root + "/sub/deeper/c.bin", 200000);
+  if (symlink((root + "/noext").c_str(), (root + "/link.bin").c_str()) != 0) std::perror("symlink");
+  std::vector<IoError> errs;
+  auto rows = walk_location(Location{7, root + "/"}, &errs);
+  // expected in breadth-first, name order
+  std::vector<std::tuple<std::string, std::string, std::string, bool, bool, uint64_t>> exp = {
+      {"/", ".", "hidden", false, true, 5},      // "..hidden": rsplit at the last dot -> (".", "hidden")
+      {"/", ".bashrc", "", false, true, 3},      // a leading dot alone is not an extension
+      {"/", "a.tar", "gz", false, false, 10},
+      {"/", "foo", "", false, false, 0},         // "foo.": extension Some("")
+      {"/", "noext", "", false, false, 1},
+      {"/", "sub", "", true, false, 0},
+      {"/", "x.y", "", true, false, 0},          // directories keep their whole name
+      {"/sub/", "b", "TXT", false, false, 2000},
+      {"/sub/", "deeper", "", true, false, 0},
+      {"/sub/deeper/", "c", "bin", false, false, 200000},
+  };
+  CHECK(errs.empty(), "walk errors");
+  CHECK(rows.size() == exp.size(), "walk found %zu entries, want %zu", rows.size(), exp.size());
+  for (size_t i = 0; i < rows.size() && i < exp.size(); ++i) {
+    const auto& [mp, name, ext, dir, hidden, size] = exp[i];
+    const auto& r = rows[i];
+    CHECK(r.materialized_path == mp && r.name == name && r.extension == ext && r.is_dir == dir &&
+              r.hidden == hidden && (dir || r.size_in_bytes == size) && r.location_id == 7 && r.inode != 0,
+          "walk entry %zu: got (%s, %s, %s, %d, %d, %llu)", i, r.materialized_path.c_str(), r.name.c_str(),
+          r.extension.c_str(), (int)r.is_dir, (int)r.hidden, (unsigned long long)r.size_in_bytes);
+  }
+  // full_path inverts the naming for files with an extension or none
+  CHECK(full_path(Location{7, root}, rows[2]) == root + "/a.tar.gz", "full_path a.tar.gz");
+  CHECK(full_path(Location{7, root}, rows[7]) == root + "/sub/b.TXT", "full_path sub/b.TXT");
+  std::string cmd = "rm -rf " + root;
+  if (std::system(cmd.c_str()) != 0) std::fprintf(stderr, "cleanup failed\n");
+  std::printf("walk: %zu entries ok\n", rows.size());
+}
+
 int main(int argc, char** argv) {
   if (argc > 2 && std::strcmp(argv[1], "--bench") == 0) return bench((size_t)std::atoll(argv[2]));
   test_parity(true);
   test_parity(false);
+  test_walk();
   std::printf("%s (%d failures)\n", failures ? "FAILED" : "ALL OK", failures);
   return failures ? 1 : 0;
 }
