@@ -100,13 +100,16 @@ class DeviceStages:
         return link[:n], counts
 
 
-def _exchange(send, send_counts, group):
-    """all_to_all of rows grouped by destination rank -> (recv, recv_counts)"""
+def _exchange(send, send_counts, group, recv_counts=None):
+    """all_to_all of rows grouped by destination rank -> (recv, recv_counts);
+    recv_counts, when the caller knows them, saves the counts exchange (and
+    its host synchronisation)"""
     dev = send.device
-    sc = torch.tensor(send_counts, dtype=torch.int64, device=dev)
-    rc = torch.empty_like(sc)
-    dist.all_to_all_single(rc, sc, group=group)
-    recv_counts = [int(x) for x in rc.tolist()]
+    if recv_counts is None:
+        sc = torch.tensor(send_counts, dtype=torch.int64, device=dev)
+        rc = torch.empty_like(sc)
+        dist.all_to_all_single(rc, sc, group=group)
+        recv_counts = [int(x) for x in rc.tolist()]
     recv = send.new_empty((sum(recv_counts),) + tuple(send.shape[1:]))
     dist.all_to_all_single(recv, send.contiguous(), recv_counts, list(send_counts), group=group)
     return recv, recv_counts
@@ -119,7 +122,8 @@ def identifier_dedup_distributed(stages, keys, has_key, status, ids, chunk_size=
     keys/has_key/status/ids: this rank's orphan file_paths (ids = their global
     ordinals in orphan order, ascending; has_key 0 = cas_id None; status != 0
     = I/O error). existing_keys/existing_ids: this rank's share of the
-    library's existing Objects (ids = global DB order). Every rank must call
+    library's existing Objects (ids = global DB order; passed on every rank —
+    an empty share as a zero-length tensor — or on none). Every rank must call
     this (it is collective). Returns (link int64[n], created, linked): link
     uses sdcas_dedup's encoding with global ordinals (i = creates, j = links
     to the Object created by file j, -(e+1) = existing Object e, INT64_MIN =
@@ -129,16 +133,21 @@ def identifier_dedup_distributed(stages, keys, has_key, status, ids, chunk_size=
     world = dist.get_world_size(group)
     rec, slot, starts = stages.combine(keys, has_key, status, ids, world)
     counts = [starts[r + 1] - starts[r] for r in range(world)]
-    if existing_keys is not None and existing_keys.numel():
-        erec, _, estarts = stages.combine(existing_keys, None, None, existing_ids, world)
-        ecounts = [estarts[r + 1] - estarts[r] for r in range(world)]
-    else:
-        erec = rec.new_empty((0, 2))
-        ecounts = [0] * world
     frecv, fcounts = _exchange(rec, counts, group)
-    erecv, _ = _exchange(erec, ecounts, group)
+    if existing_keys is not None:
+        # collective: every rank passes its (possibly empty) share, or none does
+        if existing_keys.numel():
+            erec, _, estarts = stages.combine(existing_keys, None, None, existing_ids, world)
+            ecounts = [estarts[r + 1] - estarts[r] for r in range(world)]
+        else:
+            erec, ecounts = rec.new_empty((0, 2)), [0] * world
+        erecv, _ = _exchange(erec, ecounts, group)
+    else:
+        erecv = rec.new_empty((0, 2))
     answer = stages.resolve(frecv, erecv)
-    back, _ = _exchange(answer, fcounts, group)
+    # the answers retrace the file records' route: this rank receives back
+    # exactly what it sent
+    back, _ = _exchange(answer, fcounts, group, recv_counts=counts)
     link, cnt = stages.apply(ids, slot, back, chunk_size)
     dist.all_reduce(cnt, group=group)
     c = cnt.tolist()
