@@ -21,10 +21,11 @@
 //                  inside the tile is reduced level by level (PARENT
 //                  compressions over a compacted task list). (3) the maximal
 //                  such nodes are written to `nodes` at their first slot.
-//   k_finish       lane per multi-chunk message: walks its maximal nodes left
-//                  to right (the decomposition is a closed-form function of
-//                  (chunk index, chunk count, slot in tile)) and merges them
-//                  with the BLAKE3 subtree-stack rule; the last merge is ROOT.
+//   k_finish_t     lane per tile boundary (the message crossing it first):
+//                  walks its maximal nodes left to right (the decomposition is
+//                  a closed-form function of (chunk index, chunk count, slot
+//                  in tile)) and merges them with the BLAKE3 subtree-stack
+//                  rule, the stack in LDS; the last merge is ROOT.
 //
 // The tree a message gets is exactly BLAKE3's left-balanced tree: complete
 // aligned power-of-two subtrees are tree nodes, and the stack merge (merge
@@ -593,7 +594,8 @@ __global__ void __launch_bounds__(WG, MINW) k_leaf_slim(const uint8_t* __restric
       const uint32_t clen = len == 0 ? 0u : (uint32_t)min<uint64_t>(CHUNK_LEN, len - j * CHUNK_LEN);
       const bool root = len <= CHUNK_LEN;
       uint32_t cv[8];
-      if (PF) hash_chunk_pf(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
+      if (PF == 4) hash_chunk_pp(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
+      else if (PF) hash_chunk_pf(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
       else hash_chunk(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
       if (root) {
         store_digest(perm ? perm[m] : m, cv, out32, out_keys);
@@ -946,56 +948,6 @@ __global__ void __launch_bounds__(512, 6) k_leaf_quad(const uint8_t* __restrict_
   }
 }
 
-// k_finish for the quad layout: a message crossing tile boundaries, walked
-// by one lane per boundary (the message whose real chunks reach across it)
-__global__ void __launch_bounds__(256) k_finish_q(const uint64_t* __restrict__ lens, uint32_t n,
-                                                  const uint64_t* __restrict__ S,
-                                                  const uint32_t* __restrict__ tile_first,
-                                                  const uint64_t* __restrict__ total_p, uint64_t cap_slots,
-                                                  const uint32_t* __restrict__ nodes,
-                                                  const uint32_t* __restrict__ perm, uint8_t* __restrict__ out32,
-                                                  uint64_t* __restrict__ out_keys) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t total = *total_p;
-  if (total > cap_slots || t == 0 || t * kQTile >= total) return;
-  const uint32_t m = tile_first[t];
-  const uint64_t s0 = S[m];
-  if (s0 >= t * kQTile || s0 / kQTile != t - 1) return;
-  const uint64_t C = chunk_count(lens[m]);
-  if (s0 + C <= t * kQTile) return;  // only its padding reaches the boundary
-  uint32_t stack[kMaxStack][8];
-  int depth = 0;
-  uint64_t j = 0;
-  while (j < C) {
-    const uint64_t g = s0 + j;
-    const uint32_t k = node_level_t<kQTile>(j, C, (uint32_t)(g % kQTile));
-    const uint4* p = reinterpret_cast<const uint4*>(nodes + 8ull * g);
-    uint4 a = p[0], b = p[1];
-    uint32_t cv[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    const int keep = __popcll(j);
-    while (depth > keep) {
-      uint32_t o[8];
-      parent(stack[depth - 2], stack[depth - 1], false, o);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) stack[depth - 2][i] = o[i];
-      --depth;
-    }
-    j += 1ull << k;
-    if (j == C) {
-      for (int d = depth - 1; d >= 0; --d) {
-        uint32_t o[8];
-        parent(stack[d], cv, d == 0, o);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) cv[i] = o[i];
-      }
-      store_digest(perm ? perm[m] : m, cv, out32, out_keys);
-    } else {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) stack[depth][i] = cv[i];
-      ++depth;
-    }
-  }
-}
 
 // Messages crossing tile boundaries: one lane per tile boundary t (the
 // message holding slot t*kTile, when it started in tile t-1 — its first
@@ -1003,51 +955,93 @@ __global__ void __launch_bounds__(256) k_finish_q(const uint64_t* __restrict__ l
 // lane per message. The lane walks the message's maximal nodes left to right
 // (a closed-form function of (chunk index, chunk count, slot in tile)) and
 // merges them with the BLAKE3 subtree-stack rule; the last merge is ROOT.
-__global__ void __launch_bounds__(256) k_finish(const uint64_t* __restrict__ lens, uint32_t n,
-                                                const uint64_t* __restrict__ S, const uint32_t* __restrict__ tile_first,
-                                                const uint64_t* __restrict__ total_p, uint64_t cap_chunks,
-                                                const uint32_t* __restrict__ nodes, const uint32_t* __restrict__ perm,
-                                                uint8_t* __restrict__ out32, uint64_t* __restrict__ out_keys) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t total = *total_p;
-  if (total > cap_chunks || t == 0 || t * kTile >= total) return;
-  const uint32_t m = tile_first[t];
-  const uint64_t s0 = S[m];
-  if (s0 >= t * kTile || s0 / kTile != t - 1) return;  // starts on the boundary / crossed an earlier one first
-  const uint64_t C = chunk_count(lens[m]);
-  uint32_t stack[kMaxStack][8];
+// The subtree-stack merge of one message's maximal nodes (left to right),
+// the last merge ROOT. `at(d)` is the d-th stack entry (8 words).
+template <uint32_t TILE, class At>
+__device__ __forceinline__ void merge_nodes(const uint32_t* __restrict__ nodes, uint64_t s0, uint64_t C, At at,
+                                            uint32_t (&cv)[8]) {
   int depth = 0;
   uint64_t j = 0;
   while (j < C) {
     const uint64_t g = s0 + j;
-    const uint32_t k = node_level(j, C, (uint32_t)(g % kTile));
+    const uint32_t k = node_level_t<TILE>(j, C, (uint32_t)(g % TILE));
     const uint4* p = reinterpret_cast<const uint4*>(nodes + 8ull * g);
     uint4 a = p[0], b = p[1];
-    uint32_t cv[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    uint32_t v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
     // subtrees completed by the first j chunks are merged before going on
     const int keep = __popcll(j);
     while (depth > keep) {
-      uint32_t o[8];
-      parent(stack[depth - 2], stack[depth - 1], false, o);
+      uint32_t l[8], r[8], o[8];
+      uint32_t *pl = at(depth - 2), *pr = at(depth - 1);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) stack[depth - 2][i] = o[i];
+      for (int i = 0; i < 8; ++i) {
+        l[i] = pl[i];
+        r[i] = pr[i];
+      }
+      parent(l, r, false, o);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) pl[i] = o[i];
       --depth;
     }
     j += 1ull << k;
     if (j == C) {
       for (int d = depth - 1; d >= 0; --d) {
-        uint32_t o[8];
-        parent(stack[d], cv, d == 0, o);
+        uint32_t l[8], o[8];
+        const uint32_t* pl = at(d);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) cv[i] = o[i];
+        for (int i = 0; i < 8; ++i) l[i] = pl[i];
+        parent(l, v, d == 0, o);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = o[i];
       }
-      store_digest(perm ? perm[m] : m, cv, out32, out_keys);
-    } else {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) stack[depth][i] = cv[i];
-      ++depth;
+      for (int i = 0; i < 8; ++i) cv[i] = v[i];
+      return;
     }
+    uint32_t* pp = at(depth);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) pp[i] = v[i];
+    ++depth;
   }
+}
+
+// rare: a message of 2^22+ chunks (4 GiB+) needs a deeper stack than LDS holds
+template <uint32_t TILE>
+__device__ __noinline__ void merge_nodes_deep(const uint32_t* __restrict__ nodes, uint64_t s0, uint64_t C,
+                                              uint32_t (&cv)[8]) {
+  uint32_t stack[kMaxStack][8];
+  merge_nodes<TILE>(nodes, s0, C, [&](int d) { return &stack[d][0]; }, cv);
+}
+
+// Messages crossing tile boundaries: one lane per tile boundary t (the
+// message holding slot t*TILE, when it started in tile t-1 — its first
+// crossing); the merge stack lives in LDS (a private array would live in
+// scratch memory, a round trip to HBM per merge).
+constexpr int kFinishWG = 64, kFinishDepth = 24;
+template <uint32_t TILE>
+__global__ void __launch_bounds__(kFinishWG) k_finish_t(const uint64_t* __restrict__ lens, uint32_t n,
+                                                       const uint64_t* __restrict__ S,
+                                                       const uint32_t* __restrict__ tile_first,
+                                                       const uint64_t* __restrict__ total_p, uint64_t cap_slots,
+                                                       const uint32_t* __restrict__ nodes,
+                                                       const uint32_t* __restrict__ perm, uint8_t* __restrict__ out32,
+                                                       uint64_t* __restrict__ out_keys) {
+  __shared__ uint32_t lstack[kFinishWG][kFinishDepth][8];
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t total = *total_p;
+  if (total > cap_slots || t == 0 || t * TILE >= total) return;
+  const uint32_t m = tile_first[t];
+  const uint64_t s0 = S[m];
+  if (s0 >= t * TILE || s0 / TILE != t - 1) return;  // starts on the boundary / crossed an earlier one first
+  const uint64_t C = chunk_count(lens[m]);
+  if (s0 + C <= t * TILE) return;  // (quad layout) only its padding reaches the boundary
+  uint32_t cv[8];
+  // stack depth <= popcount(j) + 1 <= log2(C) + 1
+  if (C < (1ull << (kFinishDepth - 2)))
+    merge_nodes<TILE>(nodes, s0, C, [&](int d) { return &lstack[threadIdx.x][d][0]; }, cv);
+  else
+    merge_nodes_deep<TILE>(nodes, s0, C, cv);
+  store_digest(perm ? perm[m] : m, cv, out32, out_keys);
 }
 
 // Slot order by message shape: key = min(chunks, 15) << 4 | (blocks in the
@@ -1353,7 +1347,7 @@ size_t batch_scan_temp_bytes(uint32_t max_msgs) {
 struct LeafVariant {
   const void* fn;
   int wg;
-  int quad = 0;  // 1: quad slot layout (k_leaf_quad / k_finish_q, needs the shape-sorted order)
+  int quad = 0;  // 1: quad slot layout (k_leaf_quad / k_finish_t<kQTile>, needs the shape-sorted order)
 };
 static const LeafVariant kLeafVariants[] = {
     {(const void*)k_leaf_tree<512, 0>, 512},
@@ -1388,6 +1382,10 @@ static const LeafVariant kLeafVariants[] = {
     // 22, 23: quad layout (four chunks per lane, 2048-slot tiles); without prefetch
     {(const void*)k_leaf_quad<1>, 512, 1},
     {(const void*)k_leaf_quad<0>, 512, 1},
+    // 24, 25: compact LDS + ping-pong message registers (no copies) under a
+    // 6- and 5-wave register cap
+    {(const void*)k_leaf_slim<512, 4, 6>, 512},
+    {(const void*)k_leaf_slim<512, 4, 5>, 512},
 };
 constexpr int kNumLeafVariants = sizeof(kLeafVariants) / sizeof(kLeafVariants[0]);
 constexpr int kDefaultLeafVariant = 1;
@@ -1463,12 +1461,12 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
   if (ev1) (void)hipEventRecord(ev1, st);
   if (quad) {
     const uint64_t tiles = ws.cap_slots / kQTile + 1;
-    hipLaunchKernelGGL(k_finish_q, dim3((uint32_t)((tiles + tb - 1) / tb)), dim3(tb), 0, st, lens, n, ws.S,
-                       ws.tile_first, ws.total, ws.cap_slots, ws.nodes, perm, out32, out_keys);
+    hipLaunchKernelGGL(k_finish_t<kQTile>, dim3((uint32_t)((tiles + kFinishWG - 1) / kFinishWG)), dim3(kFinishWG), 0,
+                       st, lens, n, ws.S, ws.tile_first, ws.total, ws.cap_slots, ws.nodes, perm, out32, out_keys);
   } else {
     const uint64_t tiles = ws.cap_slots / kTile + 1;
-    hipLaunchKernelGGL(k_finish, dim3((uint32_t)((tiles + tb - 1) / tb)), dim3(tb), 0, st, lens, n, ws.S,
-                       ws.tile_first, ws.total, ws.cap_slots, ws.nodes, perm, out32, out_keys);
+    hipLaunchKernelGGL(k_finish_t<kTile>, dim3((uint32_t)((tiles + kFinishWG - 1) / kFinishWG)), dim3(kFinishWG), 0,
+                       st, lens, n, ws.S, ws.tile_first, ws.total, ws.cap_slots, ws.nodes, perm, out32, out_keys);
   }
   return hipGetLastError();
 }
