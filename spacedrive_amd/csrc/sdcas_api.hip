@@ -423,19 +423,17 @@ int pread_exact(int fd, uint8_t* dst, uint64_t n, uint64_t off) {
   return 0;
 }
 
-// whole file into dst (capacity cap); returns status, *len = bytes read;
-// sets *overflow if the file holds more than cap bytes
-int read_whole(int fd, uint8_t* dst, uint64_t cap, uint64_t* len, bool* overflow) {
+// whole file into dst (capacity cap > expect, the size the indexer or a
+// stat just saw); returns status, *len = bytes read; sets *overflow when the
+// file holds at least cap bytes (it grew). A read that stops short exactly at
+// `expect` is taken as EOF — one pread per unchanged file instead of a second
+// one returning 0; shorter reads keep reading to EOF as fs::read does.
+int read_whole(int fd, uint8_t* dst, uint64_t cap, uint64_t expect, uint64_t* len, bool* overflow) {
   uint64_t got = 0;
   *overflow = false;
   for (;;) {
     if (got == cap) {
-      uint8_t probe;
-      ssize_t r;
-      do r = pread(fd, &probe, 1, (off_t)got);
-      while (r < 0 && errno == EINTR);
-      if (r < 0) return errno;
-      if (r > 0) *overflow = true;
+      *overflow = true;
       break;
     }
     ssize_t r = pread(fd, dst + got, cap - got, (off_t)got);
@@ -445,6 +443,7 @@ int read_whole(int fd, uint8_t* dst, uint64_t cap, uint64_t* len, bool* overflow
     }
     if (r == 0) break;
     got += (uint64_t)r;
+    if (got == expect) break;
   }
   *len = got;
   return 0;
@@ -464,7 +463,7 @@ int read_cas_message(const char* path, uint64_t size, uint8_t* dst, uint64_t cap
     // cas.rs:27-29: fs::read of the file as it is now
     uint64_t got = 0;
     bool over = false;
-    st = read_whole(fd, dst + 8, cap - 8, &got, &over);
+    st = read_whole(fd, dst + 8, cap - 8, size, &got, &over);
     if (!st && over) {
       struct stat sb;
       if (fstat(fd, &sb) == 0) *retry_len = 8 + (uint64_t)sb.st_size + 4096;
@@ -787,7 +786,8 @@ int sdcas_cas_ids(sdcas_ctx* c, const char* const* paths, const uint64_t* sizes,
   // slot sizes: the message the indexer's size predicts (cas.rs:27); a file
   // that grew is retried in a later batch with its actual size
   std::vector<uint64_t> want(n);
-  for (size_t i = 0; i < n; ++i) want[i] = sdcas_cas_message_len(sizes[i]);
+  // (+1: room for the byte that tells a grown file from an unchanged one)
+  for (size_t i = 0; i < n; ++i) want[i] = sdcas_cas_message_len(sizes[i]) + (sizes[i] <= kMin ? 1 : 0);
   std::vector<size_t> todo(n);
   for (size_t i = 0; i < n; ++i) todo[i] = i;
   int cur = 0;
@@ -885,9 +885,9 @@ int sdcas_checksums(sdcas_ctx* c, const char* const* paths, size_t n, uint8_t* o
     std::vector<uint64_t> slot;
     uint64_t used = 0;
     size_t q = p;
-    while (q < small.size() && q - p < cap_n && (q == p || used + align16(flen[small[q]]) <= cap)) {
+    while (q < small.size() && q - p < cap_n && (q == p || used + align16(flen[small[q]] + 1) <= cap)) {
       slot.push_back(used);
-      used += align16(flen[small[q]]);
+      used += align16(flen[small[q]] + 1);
       ++q;
     }
     const size_t m = q - p;
@@ -901,7 +901,10 @@ int sdcas_checksums(sdcas_ctx* c, const char* const* paths, size_t n, uint8_t* o
         return;
       }
       bool over = false;
-      st[k] = read_whole(fd, s.h + slot[k], flen[i], &got[k], &over);
+      // hash.rs stops at its first short read; a file that grew since the
+      // stat above is hashed over its stat length
+      st[k] = read_whole(fd, s.h + slot[k], flen[i] + 1, flen[i], &got[k], &over);
+      if (over) got[k] = flen[i];
       close(fd);
     });
     s.n = 0, s.chunks = 0, s.used = used;
