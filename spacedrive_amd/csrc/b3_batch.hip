@@ -34,6 +34,7 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
+#include <cstdio>
 
 #include "b3_device.h"
 #include "b3_batch.h"
@@ -269,8 +270,78 @@ __device__ __forceinline__ uint32_t enc_task(uint32_t l, uint32_t r, uint32_t ms
   return l | (r << 10) | (msg << 20) | (root ? 0x80000000u : 0u);
 }
 
-template <int WG, int PF, int TR = 1, int STAGGER = 0, int PRIO = 0>
-__global__ void __launch_bounds__(WG) k_leaf_tree(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ offs,
+// leaf-order bin of chunk j of a message of `len` bytes: 16 - blocks (full
+// chunks first), 0..15
+__device__ __forceinline__ uint32_t leaf_bin(uint64_t len, uint64_t j) {
+  const uint64_t rest = len - j * CHUNK_LEN;
+  const uint32_t clen = len == 0 ? 0u : (uint32_t)min<uint64_t>(CHUNK_LEN, rest);
+  const uint32_t nb = clen == 0 ? 1u : (clen + BLOCK_LEN - 1) / BLOCK_LEN;
+  return 16u - nb;
+}
+
+// Leaf order of a tile by block count (ORD): the lanes of a wave run their
+// chunks in lockstep, so a wave holding full chunks next to partial last
+// chunks idles the short lanes (C5's small files: 13 % of lane time). Slots
+// are ranked by bin (16 - blocks; past-the-end slots last) with one ballot
+// per bin per 64-slot group, the 17 x 16 group counts are scanned by one wave,
+// and lane i of the leaf loop takes slot order[i]. The tree and the node
+// layout do not change: a leaf still writes its CV at its own slot.
+constexpr uint32_t kGroups = kTile / 64;
+
+template <int WG>
+__device__ __forceinline__ void leaf_order(uint32_t tid, const uint32_t (&bin)[kTile / WG], uint16_t* __restrict__ order,
+                                           uint16_t* __restrict__ gcnt) {
+  const uint32_t lane = tid & 63;
+  uint32_t rk[kTile / WG];
+#pragma unroll
+  for (uint32_t r = 0; r < kTile / WG; ++r) {
+    const uint32_t g = (tid + r * WG) >> 6;
+    uint32_t mine = 0, cnt_l = 0;
+#pragma unroll 1
+    for (uint32_t b = 0; b < 17; ++b) {
+      const uint64_t m = __ballot(bin[r] == b);
+      if (bin[r] == b) mine = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (lane == b) cnt_l = (uint32_t)__popcll(m);
+    }
+    rk[r] = mine;
+    if (lane < 17) gcnt[lane * kGroups + g] = (uint16_t)cnt_l;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    // exclusive scan of the 17 x kGroups counts in bin-major order
+    constexpr uint32_t kPer = (17 * kGroups + 63) / 64;
+    uint32_t v[kPer], sum = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kPer; ++q) {
+      const uint32_t e = tid * kPer + q;
+      v[q] = e < 17 * kGroups ? gcnt[e] : 0u;
+      sum += v[q];
+    }
+    uint32_t inc = sum;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint32_t t = __shfl_up(inc, d);
+      if (lane >= d) inc += t;
+    }
+    uint32_t acc = inc - sum;
+#pragma unroll
+    for (uint32_t q = 0; q < kPer; ++q) {
+      const uint32_t e = tid * kPer + q;
+      if (e < 17 * kGroups) gcnt[e] = (uint16_t)acc;
+      acc += v[q];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t r = 0; r < kTile / WG; ++r) {
+    const uint32_t s = tid + r * WG;
+    order[gcnt[bin[r] * kGroups + (s >> 6)] + rk[r]] = (uint16_t)s;
+  }
+  __syncthreads();
+}
+
+template <int WG, int PF, int TR = 1, int STAGGER = 0, int PRIO = 0, int ORD = 0>
+__global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ offs,
                                                    const uint64_t* __restrict__ lens, uint32_t n,
                                                    const uint64_t* __restrict__ S,
                                                    const uint32_t* __restrict__ tile_first,
@@ -282,6 +353,7 @@ __global__ void __launch_bounds__(WG) k_leaf_tree(const uint8_t* __restrict__ bl
   __shared__ uint16_t smsg[kTile];     // slot -> message index in the tile (kNoMsg: past the end)
   __shared__ uint32_t task[kTaskCap];  // tree tasks by level (enc_task)
   __shared__ uint32_t ntask[12];
+  __shared__ uint16_t order[ORD ? kTile : 1];  // leaf loop position -> slot
 
   const uint64_t total = *total_p;
   if (total > cap_chunks) return;  // reported by sdcas_dev_sync
@@ -359,8 +431,26 @@ __global__ void __launch_bounds__(WG) k_leaf_tree(const uint8_t* __restrict__ bl
     }
 
     // (2) leaves
+    // Ordering pays only where a tile holds more partial chunks (one per
+    // message) than a wave has lanes — fewer cannot fill a wave of their own —
+    // and not in a run of single-chunk messages, which the shape sort already
+    // grouped by block count. The test is uniform over the workgroup.
+    const bool ord = ORD && cnt > 64 && chunk_count(lens[m0 + cnt - 1]) > 1;
+    if (ord) {
+      uint32_t bin[kTile / WG];
+#pragma unroll
+      for (uint32_t r = 0; r < kTile / WG; ++r) {
+        const uint32_t s = tid + r * WG;
+        const uint32_t mi = smsg[s];
+        bin[r] = mi == kNoMsg ? 16u : leaf_bin(lens[m0 + mi], tbase + s - sS[mi]);
+      }
+      // the per (bin, 64-slot group) counts borrow cvs, which no one reads
+      // between the previous tile's last barrier and this tile's leaves
+      leaf_order<WG>(tid, bin, order, reinterpret_cast<uint16_t*>(&cvs[0][0]));
+    }
 #pragma unroll 1
-    for (uint32_t s = tid; s < kTile; s += WG) {
+    for (uint32_t i = tid; i < kTile; i += WG) {
+      const uint32_t s = ord ? order[i] : i;
       const uint32_t mi = smsg[s];
       if (mi == kNoMsg) continue;
       const uint32_t m = m0 + mi;
@@ -446,15 +536,6 @@ __global__ void __launch_bounds__(WG) k_leaf_tree(const uint8_t* __restrict__ bl
 //     of its left slot; tasks are counted per level first, then written
 //     compacted (a tile holds at most kTile - 1 parent compressions).
 constexpr uint16_t kTaskRoot = 0x8000;
-
-// leaf-order bin of chunk j of a message of `len` bytes: 16 - blocks (full
-// chunks first), 0..15
-__device__ __forceinline__ uint32_t leaf_bin(uint64_t len, uint64_t j) {
-  const uint64_t rest = len - j * CHUNK_LEN;
-  const uint32_t clen = len == 0 ? 0u : (uint32_t)min<uint64_t>(CHUNK_LEN, rest);
-  const uint32_t nb = clen == 0 ? 1u : (clen + BLOCK_LEN - 1) / BLOCK_LEN;
-  return 16u - nb;
-}
 
 template <int WG, int PF, int MINW, int ORD = 0>
 __global__ void __launch_bounds__(WG, MINW) k_leaf_slim(const uint8_t* __restrict__ blob,
@@ -1369,26 +1450,32 @@ static const LeafVariant kLeafVariants[] = {
     {(const void*)k_leaf_tree<512, 4, 1, 0, 1>, 512},
     // 13: non-temporal (streaming) message loads
     {(const void*)k_leaf_tree<512, 5>, 512},
-    // 14-16: compact LDS (4 workgroups per CU); min waves/SIMD 8, 6; 17: no prefetch
+    // 14-16: compact LDS (4 workgroups per CU); min waves/SIMD 8, 6; 16: no prefetch
     {(const void*)k_leaf_slim<512, 1, 8>, 512},
     {(const void*)k_leaf_slim<512, 1, 6>, 512},
     {(const void*)k_leaf_slim<512, 0, 8>, 512},
-    // 18: prefetch distance two blocks; 19: 128-byte pair loads
+    // 17: prefetch distance two blocks; 18: 128-byte pair loads
     {(const void*)k_leaf_tree<512, 6>, 512},
     {(const void*)k_leaf_tree<512, 7>, 512},
-    // 20, 21: compact LDS + leaf order by block count (6 waves/SIMD); the same without prefetch
+    // 19, 20: compact LDS + leaf order by block count (6 waves/SIMD); the same without prefetch
     {(const void*)k_leaf_slim<512, 1, 6, 1>, 512},
     {(const void*)k_leaf_slim<512, 0, 6, 1>, 512},
-    // 22, 23: quad layout (four chunks per lane, 2048-slot tiles); without prefetch
+    // 21, 22: quad layout (four chunks per lane, 2048-slot tiles); without prefetch
     {(const void*)k_leaf_quad<1>, 512, 1},
     {(const void*)k_leaf_quad<0>, 512, 1},
-    // 24, 25: compact LDS + ping-pong message registers (no copies) under a
+    // 23, 24: compact LDS + ping-pong message registers (no copies) under a
     // 6- and 5-wave register cap
     {(const void*)k_leaf_slim<512, 4, 6>, 512},
     {(const void*)k_leaf_slim<512, 4, 5>, 512},
+    // 25: leaf order by block count (ballot ranks, no LDS atomics)
+    {(const void*)k_leaf_tree<512, 1, 1, 0, 0, 1>, 512},
+    // 26-28 diagnostic (wrong results), 25 with: no memory reads; no in-tile tree; neither
+    {(const void*)k_leaf_tree<512, 2, 1, 0, 0, 1>, 512},
+    {(const void*)k_leaf_tree<512, 1, 0, 0, 0, 1>, 512},
+    {(const void*)k_leaf_tree<512, 2, 0, 0, 0, 1>, 512},
 };
 constexpr int kNumLeafVariants = sizeof(kLeafVariants) / sizeof(kLeafVariants[0]);
-constexpr int kDefaultLeafVariant = 1;
+constexpr int kDefaultLeafVariant = 25;
 
 int leaf_variant_count() { return kNumLeafVariants; }
 
@@ -1409,6 +1496,7 @@ int batch_grid(int device, int variant) {
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
   (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kLeafVariants[variant].fn, kLeafVariants[variant].wg, 0);
   if (per < 1) per = 1;
+  if (getenv("SDCAS_DEBUG_GRID")) fprintf(stderr, "leaf variant %d: %d workgroups/CU\n", variant, per);
   int g = cus * per;
   if (device >= 0 && device < 64) cached[device][variant] = g;
   return g;

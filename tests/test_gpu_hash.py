@@ -146,6 +146,29 @@ def test_tile_straddles_vs_oracle(eng, oracle):
         assert bytes(d).hex() == oracle.hash(m), len(m)
 
 
+@pytest.mark.parametrize("variant", [1, 25])
+def test_many_short_multichunk_messages(oracle, variant):
+    """C5-shaped batches — mostly 2..5-chunk messages, so tiles hold far more
+    partial last chunks than a wave has lanes and the leaf kernel's block-count
+    order (variant 25) is taken — next to runs of single-chunk messages and a
+    few long ones; every digest against the oracle, for the plain tile kernel
+    (1) and the ordered one (25)"""
+    from spacedrive_amd import Engine
+    rng = np.random.default_rng(55 + variant)
+    lens = np.concatenate([rng.integers(1025, 5 * 1024 + 1, 12000), rng.integers(0, 1025, 3000),
+                           rng.integers(5 * 1024, 200_000, 300), np.array([1024, 1025, 2048, 2049, 0])])
+    rng.shuffle(lens)
+    msgs = [rng.integers(0, 256, int(L), dtype=np.uint8).tobytes() for L in lens]
+    e = Engine(staging_bytes=64 << 20)
+    try:
+        assert e.dev_set_leaf_variant(variant) > variant
+        out = e.hash_messages(*e.pack(msgs))
+    finally:
+        e.close()
+    bad = [i for i, (m, d) in enumerate(zip(msgs, out)) if bytes(d).hex() != oracle.hash(m)]
+    assert not bad, [len(msgs[i]) for i in bad[:10]]
+
+
 def test_device_api_synthetic_c2_sample(eng, oracle):
     """C2-shaped synthetic corpus generated in HBM, hashed by the device API;
     a random sample of files is re-derived by the CPU oracle"""
