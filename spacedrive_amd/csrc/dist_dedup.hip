@@ -29,30 +29,37 @@ constexpr uint32_t TB = 256;
 inline uint32_t blocks(uint32_t n) { return (n + TB - 1) / TB; }
 
 __global__ void k_dd_prepare(const uint8_t* __restrict__ has_key, const int32_t* __restrict__ status, uint32_t n,
-                             uint8_t* __restrict__ valid, uint32_t* __restrict__ idx, uint32_t* __restrict__ slot) {
+                             uint32_t* __restrict__ flag, uint32_t* __restrict__ slot) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const bool ok = status == nullptr || status[i] == 0;  // mod.rs:125-141: errored files are dropped
   const bool has = has_key == nullptr || has_key[i];    // mod.rs:83-86: empty files have no cas_id
-  valid[i] = ok && has;
-  idx[i] = i;
+  flag[i] = ok && has ? 1u : 0u;
   if (slot) slot[i] = !ok ? kSlotDropped : kSlotNoKey;
 }
 
-
 // The combine's sort entries: key = top 32 key bits, value = (low 32 key
 // bits, file index) — the full key travels with the entry, so no pass after
-// the sort gathers it (the tail keeps 0xFFFFFFFF fillers, which the stable
-// sort leaves behind every real entry)
-__global__ void k_dd_hi(const uint64_t* __restrict__ ckey, const uint32_t* __restrict__ cidx,
-                        const uint32_t* __restrict__ nv_p, uint32_t n, uint32_t* __restrict__ hi,
-                        uint64_t* __restrict__ val) {
-  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= n) return;
-  const bool real = p < *nv_p;
-  const uint64_t k = real ? ckey[p] : ~0ull;
-  hi[p] = (uint32_t)(k >> 32);
-  val[p] = (k << 32) | (real ? cidx[p] : 0u);
+// the sort gathers it. Present files are compacted to the front in file order
+// (pos = inclusive scan of the present flags - 1); the tail [nv, n) keeps
+// all-ones fillers, which the stable sort leaves behind every real entry
+// (a real all-ones key sorts before them: it comes earlier in the input).
+__global__ void k_dd_hi(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ scan, uint32_t n,
+                        uint32_t* __restrict__ hi, uint64_t* __restrict__ val, uint32_t* __restrict__ nv_p) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t nv = scan[n - 1];
+  if (i == 0) *nv_p = nv;
+  const uint32_t c = scan[i];
+  if (c != (i ? scan[i - 1] : 0u)) {
+    const uint64_t k = keys[i];
+    hi[c - 1] = (uint32_t)(k >> 32);
+    val[c - 1] = (k << 32) | i;
+  }
+  if (i >= nv) {
+    hi[i] = 0xFFFFFFFFu;
+    val[i] = 0xFFFFFFFF00000000ull;
+  }
 }
 
 __device__ __forceinline__ uint64_t hv_key(const uint32_t* hi, const uint64_t* val, uint32_t p) {
@@ -149,8 +156,6 @@ __global__ void k_dd_apply(const uint64_t* __restrict__ ids, const uint32_t* __r
 
 hipError_t ensure_temp(DistWs& w, uint32_t n) {
   size_t a = 0, b = 0, c = 0;
-  (void)hipcub::DeviceSelect::Flagged(nullptr, a, (const uint64_t*)nullptr, (const uint8_t*)nullptr,
-                                      (uint64_t*)nullptr, (uint32_t*)nullptr, (int)n);
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const uint64_t*)nullptr, (uint64_t*)nullptr,
                                            (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
   size_t b2 = 0;
@@ -165,8 +170,7 @@ hipError_t ensure_temp(DistWs& w, uint32_t n) {
 
 hipError_t ensure_n(DistWs& w, uint32_t n) {
   hipError_t e;
-  if ((e = w.key_a.ensure(n)) || (e = w.key_b.ensure(n)) || (e = w.idx_a.ensure(n)) || (e = w.idx_b.ensure(n)) ||
-      (e = w.scan.ensure(n)) || (e = w.valid.ensure(n)) || (e = w.nvalid.ensure(4)))
+  if ((e = w.key_a.ensure(n)) || (e = w.key_b.ensure(n)) || (e = w.scan.ensure(n)) || (e = w.nvalid.ensure(4)))
     return e;
   return ensure_temp(w, n);
 }
@@ -192,26 +196,19 @@ hipError_t dd_combine(DistWs& w, const uint64_t* keys, const uint8_t* has_key, c
     return hipSuccess;
   }
   if ((e = ensure_n(w, n))) return e;
-  hipLaunchKernelGGL(k_dd_prepare, dim3(blocks(n)), dim3(TB), 0, st, has_key, status, n, w.valid.p, w.idx_a.p, slot);
-  // compact present (key, index) pairs to the front; the tail keeps UINT64_MAX
-  // fillers that the stable sort leaves behind every real entry
-  if ((e = hipMemsetAsync(w.key_a.p, 0xFF, sizeof(uint64_t) * n, st))) return e;
+  if ((e = w.hi_a.ensure(n)) || (e = w.hi_b.ensure(n))) return e;
+  hipLaunchKernelGGL(k_dd_prepare, dim3(blocks(n)), dim3(TB), 0, st, has_key, status, n, w.scan.p, slot);
   size_t tmp = w.temp.cap;
-  if ((e = hipcub::DeviceSelect::Flagged(w.temp.p, tmp, keys, w.valid.p, w.key_a.p, w.nvalid.p, (int)n, st))) return e;
-  tmp = w.temp.cap;
-  if ((e = hipcub::DeviceSelect::Flagged(w.temp.p, tmp, w.idx_a.p, w.valid.p, w.idx_b.p, w.nvalid.p, (int)n, st)))
-    return e;
+  if ((e = hipcub::DeviceScan::InclusiveSum(w.temp.p, tmp, w.scan.p, w.scan.p, (int)n, st))) return e;
   // The combine only has to bring equal keys together and order the owners
   // (top 12 bits): a stable sort of (top 32 key bits, file index) pairs does
   // both in half the passes over 2/3 of the bytes of a full 64-bit sort.
   // Distinct keys sharing their top 32 bits (~n^2 / 2^33 pairs) may
   // interleave and split a key into several records; resolve takes the
   // minimum over all records of a key, so the answer is unchanged.
-  if ((e = w.hi_a.ensure(n)) || (e = w.hi_b.ensure(n))) return e;
-  // entries (hi32 | lo32:index) from the compacted key_a / idx_b into
-  // hi_a / key_b, sorted into hi_b / key_a
-  hipLaunchKernelGGL(k_dd_hi, dim3(blocks(n)), dim3(TB), 0, st, w.key_a.p, w.idx_b.p, w.nvalid.p, n, w.hi_a.p,
-                     w.key_b.p);
+  // Entries (hi32 | lo32:index) go to hi_a / key_b, sorted into hi_b / key_a.
+  hipLaunchKernelGGL(k_dd_hi, dim3(blocks(n)), dim3(TB), 0, st, keys, w.scan.p, n, w.hi_a.p, w.key_b.p,
+                     w.nvalid.p);
   tmp = w.temp.cap;
   if ((e = hipcub::DeviceRadixSort::SortPairs(w.temp.p, tmp, w.hi_a.p, w.hi_b.p, w.key_b.p, w.key_a.p, (int)n, 0, 32,
                                               st)))
@@ -246,24 +243,36 @@ hipError_t dd_combine(DistWs& w, const uint64_t* keys, const uint8_t* has_key, c
 // no sort. The all-ones key (a legal cas key) owns the extra entry at `cap`.
 constexpr uint64_t kEmptyKey = ~0ull;
 
-__device__ __forceinline__ uint32_t ht_find(unsigned long long* __restrict__ tkey, uint64_t key, uint32_t mask) {
+// Home slot = the key's top bits (cas keys are BLAKE3 output, uniform): the
+// table is ordered like the keys, so the key-sorted runs the owner receives
+// (one per source rank) insert into neighbouring lines instead of scattering
+// one line per record. A slot is read before it is CAS'd, and an entry's
+// minimum before it is atomicMin'd (both only ever decrease from all-ones).
+__device__ __forceinline__ uint32_t ht_find(unsigned long long* __restrict__ tkey, uint64_t key, uint32_t mask,
+                                            uint32_t shift) {
   if (key == kEmptyKey) return mask + 1;
-  uint32_t h = (uint32_t)(((key ^ (key >> 31)) * 0x9E3779B97F4A7C15ull) >> 32) & mask;
+  uint32_t h = (uint32_t)(key >> shift) & mask;
   for (;;) {
-    const unsigned long long prev = atomicCAS(&tkey[h], (unsigned long long)kEmptyKey, (unsigned long long)key);
-    if (prev == kEmptyKey || prev == key) return h;
+    const unsigned long long cur = __hip_atomic_load(&tkey[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == key) return h;
+    if (cur == kEmptyKey) {
+      const unsigned long long prev = atomicCAS(&tkey[h], (unsigned long long)kEmptyKey, (unsigned long long)key);
+      if (prev == kEmptyKey || prev == key) return h;
+    }
     h = (h + 1) & mask;
   }
 }
 
 // rec[2p] = key, rec[2p+1] = value; min-fold value into tmin[2 * entry + side]
 __global__ void k_ht_insert(const uint64_t* __restrict__ rec, uint32_t n, unsigned long long* __restrict__ tkey,
-                            unsigned long long* __restrict__ tmin, uint32_t mask, uint32_t side,
+                            unsigned long long* __restrict__ tmin, uint32_t mask, uint32_t shift, uint32_t side,
                             uint32_t* __restrict__ pos_out) {
   const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n) return;
-  const uint32_t h = ht_find(tkey, rec[2 * (uint64_t)p], mask);
-  atomicMin(&tmin[2 * (uint64_t)h + side], (unsigned long long)rec[2 * (uint64_t)p + 1]);
+  const uint32_t h = ht_find(tkey, rec[2 * (uint64_t)p], mask, shift);
+  const unsigned long long v = rec[2 * (uint64_t)p + 1];
+  unsigned long long* m = &tmin[2 * (uint64_t)h + side];
+  if (__hip_atomic_load(m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > v) atomicMin(m, v);
   if (pos_out) pos_out[p] = h;
 }
 
@@ -287,13 +296,14 @@ hipError_t dd_resolve(DistWs& w, const uint64_t* frec, uint32_t nf, const uint64
   if (cap > (1ull << 31)) return hipErrorInvalidValue;
   if ((e = w.tkey.ensure(cap + 1)) || (e = w.tmin.ensure(2 * (cap + 1))) || (e = w.tpos.ensure(nf))) return e;
   const uint32_t mask = (uint32_t)(cap - 1);
+  const uint32_t shift = 64u - (uint32_t)__builtin_ctzll(cap);
   if ((e = hipMemsetAsync(w.tkey.p, 0xFF, sizeof(uint64_t) * (cap + 1), st)) ||
       (e = hipMemsetAsync(w.tmin.p, 0xFF, sizeof(uint64_t) * 2 * (cap + 1), st)))
     return e;
   auto* tk = reinterpret_cast<unsigned long long*>(w.tkey.p);
   auto* tm = reinterpret_cast<unsigned long long*>(w.tmin.p);
-  if (ne) hipLaunchKernelGGL(k_ht_insert, dim3(blocks(ne)), dim3(TB), 0, st, erec, ne, tk, tm, mask, 1u, nullptr);
-  hipLaunchKernelGGL(k_ht_insert, dim3(blocks(nf)), dim3(TB), 0, st, frec, nf, tk, tm, mask, 0u, w.tpos.p);
+  if (ne) hipLaunchKernelGGL(k_ht_insert, dim3(blocks(ne)), dim3(TB), 0, st, erec, ne, tk, tm, mask, shift, 1u, nullptr);
+  hipLaunchKernelGGL(k_ht_insert, dim3(blocks(nf)), dim3(TB), 0, st, frec, nf, tk, tm, mask, shift, 0u, w.tpos.p);
   hipLaunchKernelGGL(k_ht_answer, dim3(blocks(nf)), dim3(TB), 0, st, w.tpos.p, nf, w.tmin.p, result);
   return hipGetLastError();
 }

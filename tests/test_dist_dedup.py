@@ -164,6 +164,29 @@ def test_device_stages_top32_collisions(eng, oracle, R):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("R", [1, 4])
+def test_device_stages_clustered_keys_wrap(eng, oracle, R):
+    """the resolve table's home slot is the key's top bits: keys packed at the
+    top of the key space (and at its bottom) make long probe chains that wrap
+    past the table's end; the links still equal the oracle's"""
+    from spacedrive_amd.dist_dedup import DeviceStages
+    rng = np.random.default_rng(23)
+    top = (np.uint64(2**64 - 2**20) + rng.integers(0, 2**20 - 1, 3000, dtype=np.uint64)).astype(np.uint64)
+    low = rng.integers(0, 2**16, 1000, dtype=np.uint64)
+    pool = np.concatenate([top, low, np.array([2**64 - 1, 0], np.uint64)])
+    keys = pool[rng.integers(0, pool.size, 12000)]
+    has = (rng.random(keys.size) > 0.02).astype(np.uint8)
+    status = np.where(rng.random(keys.size) < 0.01, 5, 0).astype(np.int32)
+    existing = pool[rng.integers(0, pool.size, 500)]
+    shards, ex = shard(keys, has, status, existing, R, device="cuda")
+    st = DeviceStages(eng)
+    links, c, l = dedup_virtual(lambda r: st, shards, 100, ex)
+    want, wc, wl = oracle.identifier_dedup(keys, has, status, 100, existing)
+    assert np.array_equal(np.concatenate([x.cpu().numpy() for x in links]), want)
+    assert (c, l) == (wc, wl)
+
+
+@pytest.mark.gpu
 def test_device_stages_empty_and_degenerate(eng, oracle):
     from spacedrive_amd.dist_dedup import DeviceStages
     st = DeviceStages(eng)
