@@ -103,6 +103,15 @@ def files_of(workload, rank, n):
     raise ValueError(workload)
 
 
+def max_over_ranks(torch, dist, dev, vals):
+    """element-wise max of a few floats over all ranks (on the GPU over RCCL;
+    on the host for a gloo rehearsal)"""
+    on_dev = dist.get_backend() == "nccl"
+    t = torch.tensor(vals, dtype=torch.float64, device=dev if on_dev else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(x) for x in t.tolist()]
+
+
 def compressions(lens):
     n = lens.astype(np.int64)
     C = np.maximum(1, (n + 1023) // 1024)
@@ -300,9 +309,7 @@ def run_c4(args, torch, dist, dev, rank, world, distributed):
     eng.dev_profile(False)
     hash_s = mean_ms / 1e3 * len(win_args) * args.steps
     if distributed:
-        tt = torch.tensor([hash_s, wall], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        hash_s, wall = (float(x) for x in tt.tolist())
+        hash_s, wall = max_over_ranks(torch, dist, dev, [hash_s, wall])
     total = int(sizes.sum()) * args.steps
     comp = int(sum(int(compressions(np.array([x], np.uint64))[0]) for x in sizes)) * args.steps
     gbs = total / hash_s / 1e9
@@ -374,10 +381,17 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = world > 1
-    torch.cuda.set_device(local if distributed else 0)
+    # one rank per GPU; the modulo only matters for a rehearsal of the N > 1
+    # path with more ranks than GPUs (SDCAS_BENCH_BACKEND=gloo: RCCL refuses
+    # two ranks on one device), never on a node with a GPU per rank
+    torch.cuda.set_device((local % torch.cuda.device_count()) if distributed else 0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    backend = os.environ.get("SDCAS_BENCH_BACKEND", "nccl")
     if distributed:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     elif W["dedup"]:
         # the dedup driver is collective code: a world of one over RCCL
         dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=dev)
@@ -452,9 +466,7 @@ def main():
     eng.dev_profile(False)
     eng.dev_sync(sp)
     if distributed:
-        tt = torch.tensor([dt, leaf_ms, seq_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt, leaf_ms, seq_ms = (float(x) for x in tt.tolist())
+        dt, leaf_ms, seq_ms = max_over_ranks(torch, dist, dev, [dt, leaf_ms, seq_ms])
 
     files_total = n * world * args.steps
     value = files_total / dt
@@ -502,11 +514,11 @@ def main():
         "blake3_gbps": gbps, "roofline": roof,
     }
     if dd is not None:
-        ms = torch.tensor([float(np.mean(dd["ms"]))], dtype=torch.float64, device=dev)
+        ms = float(np.mean(dd["ms"]))
         if distributed:
-            dist.all_reduce(ms, op=dist.ReduceOp.MAX)
+            ms, = max_over_ranks(torch, dist, dev, [ms])
         _, created, linked = dd["last"]
-        out["dedup"] = {"ms_per_step": float(ms.item()), "objects_created": created, "files_linked": linked,
+        out["dedup"] = {"ms_per_step": ms, "objects_created": created, "files_linked": linked,
                         "records_per_gpu": n}
     if rank == 0 and world == 1:
         gk = d_out.cpu().numpy().view(np.uint64)

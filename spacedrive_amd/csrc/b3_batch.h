@@ -13,7 +13,7 @@ constexpr uint32_t kWG = 512;     // threads per workgroup: 2 slots per lane
 struct BatchWorkspace {
   uint64_t* S = nullptr;           // [cap_msgs] first slot of each message
   uint32_t* tile_first = nullptr;  // [cap_tiles] message owning each tile's first slot
-  uint64_t* total = nullptr;       // [2] total slots, error word
+  uint64_t* total = nullptr;       // [4] total slots, error word, leaf tile counter
   uint32_t* nodes = nullptr;       // [cap_chunks * 8] maximal in-tile node CVs, by first slot
   void* scan_tmp = nullptr;
   size_t scan_tmp_bytes = 0;

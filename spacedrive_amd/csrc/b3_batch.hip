@@ -77,7 +77,10 @@ __global__ void k_tile_first(const uint64_t* __restrict__ lens, const uint64_t* 
   uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= n) return;
   uint64_t s0 = S[m], C = chunk_count(lens[m]);
-  if (m == n - 1) *total = s0 + C;
+  if (m == n - 1) {
+    total[0] = s0 + C;
+    total[2] = 0;  // k_leaf_tree<DYN>'s tile counter
+  }
   for (uint64_t t = (s0 + kTile - 1) / kTile; t * kTile < s0 + C && t * kTile < cap_chunks; ++t) tile_first[t] = m;
 }
 
@@ -340,7 +343,7 @@ __device__ __forceinline__ void leaf_order(uint32_t tid, const uint32_t (&bin)[k
   __syncthreads();
 }
 
-template <int WG, int PF, int TR = 1, int STAGGER = 0, int PRIO = 0, int ORD = 0>
+template <int WG, int PF, int TR = 1, int STAGGER = 0, int PRIO = 0, int ORD = 0, int DYN = 0>
 __global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ offs,
                                                    const uint64_t* __restrict__ lens, uint32_t n,
                                                    const uint64_t* __restrict__ S,
@@ -354,6 +357,7 @@ __global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __
   __shared__ uint32_t task[kTaskCap];  // tree tasks by level (enc_task)
   __shared__ uint32_t ntask[12];
   __shared__ uint16_t order[ORD ? kTile : 1];  // leaf loop position -> slot
+  __shared__ uint64_t next_tile;
 
   const uint64_t total = *total_p;
   if (total > cap_chunks) return;  // reported by sdcas_dev_sync
@@ -369,13 +373,20 @@ __global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __
     while (__builtin_amdgcn_s_memrealtime() - t0 < wait) __builtin_amdgcn_s_sleep(100);
   }
 
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  // DYN: tiles after the first are handed out by a global counter (total_p[2],
+  // zeroed by k_tile_first) instead of round-robin, so a workgroup that drew
+  // cheap tiles takes more and the grid drains within about one tile; the
+  // next tile is claimed at the start of the current one (the atomic's
+  // latency hides behind the tile) and read after its last barrier
+  unsigned long long* tile_ctr = reinterpret_cast<unsigned long long*>(const_cast<uint64_t*>(total_p) + 2);
+  for (uint64_t tile = blockIdx.x; tile < ntiles;) {
     const uint64_t tbase = tile * kTile;
     const uint32_t m0 = tile_first[tile];
     const uint32_t m1 = (tile + 1 < ntiles) ? tile_first[tile + 1] : n - 1;
     const uint32_t cnt = m1 - m0 + 1;  // <= kTile + 1
     for (uint32_t i = tid; i < cnt; i += WG) sS[i] = S[m0 + i];
     if (tid < 12) ntask[tid] = 0;
+    if (DYN && tid == 0) next_tile = gridDim.x + atomicAdd(tile_ctr, 1ull);
     __syncthreads();
 
     // (1) slot -> message, and the tree schedule: every aligned complete
@@ -522,6 +533,7 @@ __global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __
       o[1] = make_uint4(cvs[s][4], cvs[s][5], cvs[s][6], cvs[s][7]);
     }
     __syncthreads();
+    tile = DYN ? next_tile : tile + gridDim.x;
   }
 }
 
@@ -1473,9 +1485,11 @@ static const LeafVariant kLeafVariants[] = {
     {(const void*)k_leaf_tree<512, 2, 1, 0, 0, 1>, 512},
     {(const void*)k_leaf_tree<512, 1, 0, 0, 0, 1>, 512},
     {(const void*)k_leaf_tree<512, 2, 0, 0, 0, 1>, 512},
+    // 29: 25 with tiles handed out by a global counter (dynamic schedule)
+    {(const void*)k_leaf_tree<512, 1, 1, 0, 0, 1, 1>, 512},
 };
 constexpr int kNumLeafVariants = sizeof(kLeafVariants) / sizeof(kLeafVariants[0]);
-constexpr int kDefaultLeafVariant = 25;
+constexpr int kDefaultLeafVariant = 29;
 
 int leaf_variant_count() { return kNumLeafVariants; }
 

@@ -162,7 +162,7 @@ int reserve_ws(sdcas_ctx* c, size_t max_msgs, uint64_t max_chunks) {
   // room for the quad layout's padding too: < 4 dead slots per message (of
   // as many messages as the workspace takes)
   const uint64_t tiles = (max_chunks + 3 * (uint64_t)(c->ws_S.cap - 1) + 8) / kTile + 2;
-  if ((e = c->ws_total.ensure(2))) return c->hip_fail(e, "workspace total");
+  if ((e = c->ws_total.ensure(4))) return c->hip_fail(e, "workspace total");
   if ((e = c->ws_tile_first.ensure(tiles))) return c->hip_fail(e, "workspace tile_first");
   if ((e = c->ws_nodes.ensure(8 * (tiles * kTile)))) return c->hip_fail(e, "workspace nodes");
   size_t tb = batch_scan_temp_bytes((uint32_t)std::max<size_t>(max_msgs, 1));
