@@ -549,7 +549,7 @@ __global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __
 //     compacted (a tile holds at most kTile - 1 parent compressions).
 constexpr uint16_t kTaskRoot = 0x8000;
 
-template <int WG, int PF, int MINW, int ORD = 0>
+template <int WG, int PF, int MINW, int ORD = 0, int DYN = 0>
 __global__ void __launch_bounds__(WG, MINW) k_leaf_slim(const uint8_t* __restrict__ blob,
                                                         const uint64_t* __restrict__ offs,
                                                         const uint64_t* __restrict__ lens, uint32_t n,
@@ -568,13 +568,15 @@ __global__ void __launch_bounds__(WG, MINW) k_leaf_slim(const uint8_t* __restric
   // of blocks share waves, so a partial last chunk does not idle 63 lanes)
   __shared__ uint16_t order[ORD ? kTile : 1];
   __shared__ uint32_t obin[ORD ? 17 : 1];
+  __shared__ uint64_t next_tile;  // DYN: k_leaf_tree's global tile counter
 
   const uint64_t total = *total_p;
   if (total > cap_chunks) return;
   const uint64_t ntiles = (total + kTile - 1) / kTile;
   const uint32_t tid = threadIdx.x;
+  unsigned long long* tile_ctr = reinterpret_cast<unsigned long long*>(const_cast<uint64_t*>(total_p) + 2);
 
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  for (uint64_t tile = blockIdx.x; tile < ntiles;) {
     const uint64_t tbase = tile * kTile;
     const uint32_t m0 = tile_first[tile];
     const uint32_t m1 = (tile + 1 < ntiles) ? tile_first[tile + 1] : n - 1;
@@ -583,6 +585,7 @@ __global__ void __launch_bounds__(WG, MINW) k_leaf_slim(const uint8_t* __restric
     for (uint32_t i = tid + 1; i < cnt; i += WG) srel[i] = (uint16_t)(S[m0 + i] - tbase);
     if (tid < 12) ntask[tid] = 0;
     if (ORD && tid < 17) obin[tid] = 0;
+    if (DYN && tid == 0) next_tile = gridDim.x + atomicAdd(tile_ctr, 1ull);
     __syncthreads();
 
     // (1a) slot -> message; count the tree tasks of every level
@@ -744,6 +747,7 @@ __global__ void __launch_bounds__(WG, MINW) k_leaf_slim(const uint8_t* __restric
       o[1] = make_uint4(cvs[s][4], cvs[s][5], cvs[s][6], cvs[s][7]);
     }
     __syncthreads();
+    tile = DYN ? next_tile : tile + gridDim.x;
   }
 }
 
@@ -1487,6 +1491,14 @@ static const LeafVariant kLeafVariants[] = {
     {(const void*)k_leaf_tree<512, 2, 0, 0, 0, 1>, 512},
     // 29: 25 with tiles handed out by a global counter (dynamic schedule)
     {(const void*)k_leaf_tree<512, 1, 1, 0, 0, 1, 1>, 512},
+    // 30-33: compact LDS with the dynamic schedule: 8 waves/SIMD; 6 + leaf
+    // order; 8 + leaf order; 30 without prefetch
+    {(const void*)k_leaf_slim<512, 1, 8, 0, 1>, 512},
+    {(const void*)k_leaf_slim<512, 1, 6, 1, 1>, 512},
+    {(const void*)k_leaf_slim<512, 1, 8, 1, 1>, 512},
+    {(const void*)k_leaf_slim<512, 0, 8, 0, 1>, 512},
+    // 34: 29 at 1024 threads per workgroup (one chunk per lane)
+    {(const void*)k_leaf_tree<1024, 1, 1, 0, 0, 1, 1>, 1024},
 };
 constexpr int kNumLeafVariants = sizeof(kLeafVariants) / sizeof(kLeafVariants[0]);
 constexpr int kDefaultLeafVariant = 29;
@@ -1504,7 +1516,7 @@ int leaf_variant() {
 }
 
 int batch_grid(int device, int variant) {
-  static int cached[64][32] = {{0}};
+  static int cached[64][64] = {{0}};
   if (device >= 0 && device < 64 && cached[device][variant]) return cached[device][variant];
   int cus = 256, per = 1;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
