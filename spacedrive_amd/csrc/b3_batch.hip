@@ -1218,7 +1218,7 @@ __global__ void __launch_bounds__(256) k_shape_scatter(const uint64_t* __restric
 // may arrive over many launches (streamed windows); k_bigfile_finish merges a
 // file's list once all of it is there.
 
-template <int PF, int MINW>
+template <int PF, int MINW, int DIRECT = 0>
 __global__ void __launch_bounds__(kWG, MINW) k_piece_tree(const uint8_t* __restrict__ blob,
                                                           const PieceDesc* __restrict__ pieces, uint32_t npieces,
                                                           uint32_t* __restrict__ file_nodes) {
@@ -1242,14 +1242,22 @@ __global__ void __launch_bounds__(kWG, MINW) k_piece_tree(const uint8_t* __restr
     __syncthreads();
     for (uint32_t k = 1; (1u << k) <= kTile; ++k) {
       const uint32_t w = 1u << k;
-      for (uint32_t s = tid; s < nchunks; s += kWG)
-        if (!(s & (w - 1)) && s + w <= nchunks) task[atomicAdd(&ntask[k], 1u)] = (uint16_t)s;
-      __syncthreads();
-      const uint32_t T = ntask[k];
-      if (T == 0) break;
+      uint32_t T;
+      if (DIRECT) {
+        // the complete aligned level-k nodes of a piece are its first
+        // nchunks >> k multiples of 2^k: task t is node t, no list needed
+        T = nchunks >> k;
+        if (T == 0) break;
+      } else {
+        for (uint32_t s = tid; s < nchunks; s += kWG)
+          if (!(s & (w - 1)) && s + w <= nchunks) task[atomicAdd(&ntask[k], 1u)] = (uint16_t)s;
+        __syncthreads();
+        T = ntask[k];
+        if (T == 0) break;
+      }
 #pragma unroll 1
       for (uint32_t t = tid; t < T; t += kWG) {
-        const uint32_t s = task[t];
+        const uint32_t s = DIRECT ? t << k : task[t];
         uint32_t l[8], r[8], o[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -1588,13 +1596,18 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
 hipError_t piece_hash(const uint8_t* blob, const PieceDesc* pieces, uint32_t npieces, uint32_t* file_nodes,
                       hipStream_t st) {
   if (!npieces) return hipSuccess;
-  // SDCAS_PIECE_VARIANT (A/B): 0 = plain block loop, 1 = block prefetch at 8 waves/SIMD (default)
+  // SDCAS_PIECE_VARIANT (A/B): 0 = plain block loop, 1 = block prefetch at 8 waves/SIMD (default),
+  // 2 = 1 with tree tasks indexed directly (one barrier per level), 3 = 2 at 6 waves/SIMD
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("SDCAS_PIECE_VARIANT");
     v = e ? atoi(e) : 1;
   }
   if (v == 0) hipLaunchKernelGGL((k_piece_tree<0, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
+  else if (v == 2)
+    hipLaunchKernelGGL((k_piece_tree<1, 8, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
+  else if (v == 3)
+    hipLaunchKernelGGL((k_piece_tree<1, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   else hipLaunchKernelGGL((k_piece_tree<1, 8>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   return hipGetLastError();
 }
