@@ -514,11 +514,11 @@ def main():
         "blake3_gbps": gbps, "roofline": roof,
     }
     if dd is not None:
-        ms = float(np.mean(dd["ms"]))
+        ms, med = float(np.mean(dd["ms"])), float(np.median(dd["ms"]))
         if distributed:
-            ms, = max_over_ranks(torch, dist, dev, [ms])
+            ms, med = max_over_ranks(torch, dist, dev, [ms, med])
         _, created, linked = dd["last"]
-        out["dedup"] = {"ms_per_step": ms, "objects_created": created, "files_linked": linked,
+        out["dedup"] = {"ms_per_step": ms, "ms_median": med, "objects_created": created, "files_linked": linked,
                         "records_per_gpu": n}
     if rank == 0 and world == 1:
         gk = d_out.cpu().numpy().view(np.uint64)

@@ -1507,9 +1507,15 @@ static const LeafVariant kLeafVariants[] = {
     {(const void*)k_leaf_slim<512, 0, 8, 0, 1>, 512},
     // 34: 29 at 1024 threads per workgroup (one chunk per lane)
     {(const void*)k_leaf_tree<1024, 1, 1, 0, 0, 1, 1>, 1024},
+    // 35-38: 29 without the leaf order; with ping-pong blocks; with tree
+    // waves at priority 1; with prefetch distance two
+    {(const void*)k_leaf_tree<512, 1, 1, 0, 0, 0, 1>, 512},
+    {(const void*)k_leaf_tree<512, 4, 1, 0, 0, 1, 1>, 512},
+    {(const void*)k_leaf_tree<512, 1, 1, 0, 1, 1, 1>, 512},
+    {(const void*)k_leaf_tree<512, 6, 1, 0, 0, 1, 1>, 512},
 };
 constexpr int kNumLeafVariants = sizeof(kLeafVariants) / sizeof(kLeafVariants[0]);
-constexpr int kDefaultLeafVariant = 29;
+constexpr int kDefaultLeafVariant = 36;
 
 int leaf_variant_count() { return kNumLeafVariants; }
 
