@@ -131,9 +131,12 @@ def identifier_dedup_distributed(stages, keys, has_key, status, ids, chunk_size=
     would return summed over the job (mod.rs:349).
     """
     world = dist.get_world_size(group)
+    # a world of one exchanges with itself: its records are already where
+    # the collectives would deliver them, so the exchanges are skipped
+    solo = world == 1
     rec, slot, starts = stages.combine(keys, has_key, status, ids, world)
     counts = [starts[r + 1] - starts[r] for r in range(world)]
-    frecv, fcounts = _exchange(rec, counts, group)
+    frecv, fcounts = (rec, counts) if solo else _exchange(rec, counts, group)
     if existing_keys is not None:
         # collective: every rank passes its (possibly empty) share, or none does
         if existing_keys.numel():
@@ -141,15 +144,16 @@ def identifier_dedup_distributed(stages, keys, has_key, status, ids, chunk_size=
             ecounts = [estarts[r + 1] - estarts[r] for r in range(world)]
         else:
             erec, ecounts = rec.new_empty((0, 2)), [0] * world
-        erecv, _ = _exchange(erec, ecounts, group)
+        erecv = erec if solo else _exchange(erec, ecounts, group)[0]
     else:
         erecv = rec.new_empty((0, 2))
     answer = stages.resolve(frecv, erecv)
     # the answers retrace the file records' route: this rank receives back
     # exactly what it sent
-    back, _ = _exchange(answer, fcounts, group, recv_counts=counts)
+    back = answer if solo else _exchange(answer, fcounts, group, recv_counts=counts)[0]
     link, cnt = stages.apply(ids, slot, back, chunk_size)
-    dist.all_reduce(cnt, group=group)
+    if not solo:
+        dist.all_reduce(cnt, group=group)
     c = cnt.tolist()
     return link, int(c[0]), int(c[1])
 

@@ -45,7 +45,7 @@ def _gloo_worker(rank, world, port, outdir, seed, n, chunk_size):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,chunk_size", [(2, 100), (4, 7), (3, 1)])
+@pytest.mark.parametrize("world,chunk_size", [(1, 100), (2, 100), (4, 7), (3, 1)])
 def test_gloo_protocol_vs_oracle(oracle, world, chunk_size):
     import torch.multiprocessing as mp
     seed, n = 1000 + world, 3000
