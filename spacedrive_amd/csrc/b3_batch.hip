@@ -1102,6 +1102,79 @@ __device__ __forceinline__ void merge_nodes(const uint32_t* __restrict__ nodes, 
   }
 }
 
+// merge_nodes without divergence between lanes: every lane runs the same
+// bookkeeping (loads and pushes, no compression) up to its next compression,
+// then the wave issues ONE parent compression for all lanes that need one —
+// the merge of the stack's top two nodes or a fold of the final node into
+// the stack. merge_nodes' nested loops, run by 64 lanes whose node lists
+// differ, execute the union of their compression sequences instead.
+template <uint32_t TILE, class At>
+__device__ __forceinline__ void merge_nodes_flat(const uint32_t* __restrict__ nodes, uint64_t s0, uint64_t C, At at,
+                                                 uint32_t (&cv)[8]) {
+  int depth = 0, keep = 0;
+  uint64_t j = 0;
+  uint32_t k = 0;
+  bool have = false, done = false;
+  uint32_t v[8];
+  for (;;) {
+    int op = 0;  // 1: merge the stack's top two; 2: fold the final node into the top
+    while (!done) {
+      if (!have) {
+        const uint64_t g = s0 + j;
+        k = node_level_t<TILE>(j, C, (uint32_t)(g % TILE));
+        const uint4* p = reinterpret_cast<const uint4*>(nodes + 8ull * g);
+        const uint4 a = p[0], b = p[1];
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+        v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        keep = __popcll(j);  // subtrees completed by the first j chunks merge first
+        have = true;
+      }
+      if (depth > keep) {
+        op = 1;
+        break;
+      }
+      if (j + (1ull << k) < C) {
+        uint32_t* pp = at(depth);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) pp[i] = v[i];
+        ++depth;
+        j += 1ull << k;
+        have = false;
+        continue;
+      }
+      if (depth == 0) {  // the final node has absorbed the whole stack: it is the root's output
+#pragma unroll
+        for (int i = 0; i < 8; ++i) cv[i] = v[i];
+        done = true;
+        break;
+      }
+      op = 2;
+      break;
+    }
+    if (__builtin_amdgcn_ballot_w64(op != 0) == 0) return;
+    if (op) {
+      uint32_t l[8], r[8], o[8];
+      const uint32_t* pl = at(op == 1 ? depth - 2 : depth - 1);
+      const uint32_t* pr = at(depth - 1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        l[i] = pl[i];
+        r[i] = op == 1 ? pr[i] : v[i];
+      }
+      parent(l, r, op == 2 && depth == 1, o);
+      if (op == 1) {
+        uint32_t* po = at(depth - 2);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) po[i] = o[i];
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = o[i];
+      }
+      --depth;
+    }
+  }
+}
+
 // rare: a message of 2^22+ chunks (4 GiB+) needs a deeper stack than LDS holds
 template <uint32_t TILE>
 __device__ __noinline__ void merge_nodes_deep(const uint32_t* __restrict__ nodes, uint64_t s0, uint64_t C,
@@ -1135,7 +1208,7 @@ __global__ void __launch_bounds__(kFinishWG) k_finish_t(const uint64_t* __restri
   uint32_t cv[8];
   // stack depth <= popcount(j) + 1 <= log2(C) + 1
   if (C < (1ull << (kFinishDepth - 2)))
-    merge_nodes<TILE>(nodes, s0, C, [&](int d) { return &lstack[threadIdx.x][d][0]; }, cv);
+    merge_nodes_flat<TILE>(nodes, s0, C, [&](int d) { return &lstack[threadIdx.x][d][0]; }, cv);
   else
     merge_nodes_deep<TILE>(nodes, s0, C, cv);
   store_digest(perm ? perm[m] : m, cv, out32, out_keys);
