@@ -1586,6 +1586,11 @@ static const LeafVariant kLeafVariants[] = {
     {(const void*)k_leaf_tree<512, 4, 1, 0, 0, 1, 1>, 512},
     {(const void*)k_leaf_tree<512, 1, 1, 0, 1, 1, 1>, 512},
     {(const void*)k_leaf_tree<512, 6, 1, 0, 0, 1, 1>, 512},
+    // 39-41 diagnostic (wrong results), 36 with: no in-tile tree; no memory
+    // reads (block loop of 29); neither
+    {(const void*)k_leaf_tree<512, 4, 0, 0, 0, 1, 1>, 512},
+    {(const void*)k_leaf_tree<512, 2, 1, 0, 0, 1, 1>, 512},
+    {(const void*)k_leaf_tree<512, 2, 0, 0, 0, 1, 1>, 512},
 };
 constexpr int kNumLeafVariants = sizeof(kLeafVariants) / sizeof(kLeafVariants[0]);
 constexpr int kDefaultLeafVariant = 36;
