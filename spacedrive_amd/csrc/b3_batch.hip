@@ -1307,7 +1307,8 @@ __global__ void __launch_bounds__(kWG, MINW) k_piece_tree(const uint8_t* __restr
     for (uint32_t s = tid; s < nchunks; s += kWG) {
       const uint32_t clen = min(CHUNK_LEN, pd.len - s * CHUNK_LEN);
       uint32_t cv[8];
-      if (PF) hash_chunk_pf(blob + pd.off + (uint64_t)s * CHUNK_LEN, clen, pd.j0 + s, false, cv);
+      if (PF == 4) hash_chunk_pp(blob + pd.off + (uint64_t)s * CHUNK_LEN, clen, pd.j0 + s, false, cv);
+      else if (PF) hash_chunk_pf(blob + pd.off + (uint64_t)s * CHUNK_LEN, clen, pd.j0 + s, false, cv);
       else hash_chunk(blob + pd.off + (uint64_t)s * CHUNK_LEN, clen, pd.j0 + s, false, cv);
 #pragma unroll
       for (int i = 0; i < 8; ++i) cvs[s][i] = cv[i];
@@ -1591,6 +1592,8 @@ static const LeafVariant kLeafVariants[] = {
     {(const void*)k_leaf_tree<512, 4, 0, 0, 0, 1, 1>, 512},
     {(const void*)k_leaf_tree<512, 2, 1, 0, 0, 1, 1>, 512},
     {(const void*)k_leaf_tree<512, 2, 0, 0, 0, 1, 1>, 512},
+    // 42: 29 with 128-byte pair loads (a lane reads a whole L2 line at once)
+    {(const void*)k_leaf_tree<512, 7, 1, 0, 0, 1, 1>, 512},
 };
 constexpr int kNumLeafVariants = sizeof(kLeafVariants) / sizeof(kLeafVariants[0]);
 constexpr int kDefaultLeafVariant = 36;
@@ -1680,18 +1683,23 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
 hipError_t piece_hash(const uint8_t* blob, const PieceDesc* pieces, uint32_t npieces, uint32_t* file_nodes,
                       hipStream_t st) {
   if (!npieces) return hipSuccess;
-  // SDCAS_PIECE_VARIANT (A/B): 0 = plain block loop, 1 = block prefetch at 8 waves/SIMD (default),
-  // 2 = 1 with tree tasks indexed directly (one barrier per level), 3 = 2 at 6 waves/SIMD
+  // SDCAS_PIECE_VARIANT (A/B): 0 = plain block loop, 1 = block prefetch at 8 waves/SIMD,
+  // 2 = 1 with tree tasks indexed directly (one barrier per level), 3 = 2 at 6 waves/SIMD,
+  // 4, 5 = 2 with the ping-pong block loop at 6 / 8 waves/SIMD (4: default, +2 % on C4)
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("SDCAS_PIECE_VARIANT");
-    v = e ? atoi(e) : 1;
+    v = e ? atoi(e) : 4;
   }
   if (v == 0) hipLaunchKernelGGL((k_piece_tree<0, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   else if (v == 2)
     hipLaunchKernelGGL((k_piece_tree<1, 8, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   else if (v == 3)
     hipLaunchKernelGGL((k_piece_tree<1, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
+  else if (v == 4)
+    hipLaunchKernelGGL((k_piece_tree<4, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
+  else if (v == 5)
+    hipLaunchKernelGGL((k_piece_tree<4, 8, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   else hipLaunchKernelGGL((k_piece_tree<1, 8>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   return hipGetLastError();
 }
