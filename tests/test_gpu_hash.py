@@ -146,13 +146,38 @@ def test_tile_straddles_vs_oracle(eng, oracle):
         assert bytes(d).hex() == oracle.hash(m), len(m)
 
 
-@pytest.mark.parametrize("variant", [1, 25])
+@pytest.mark.parametrize("variant", [1, 29, 36])
+def test_tile_straddles_per_variant(oracle, variant):
+    """the straddle corpus through each production leaf variant, in caller
+    order (shape sort off) so messages straddle tiles at every level"""
+    from spacedrive_amd import Engine
+    rng = np.random.default_rng(70 + variant)
+    lens = []
+    for c in [1, 2, 3, 7, 8, 9, 16, 17, 31, 32, 33, 64, 65, 127, 128, 129, 255, 256, 257, 511, 512, 513, 1000,
+              1023, 1024, 1025, 2049]:
+        lens += [c * 1024, c * 1024 - 1, c * 1024 + 1]
+    lens = np.array(lens * 2)
+    rng.shuffle(lens)
+    msgs = [rng.integers(0, 256, int(L), dtype=np.uint8).tobytes() for L in lens]
+    e = Engine(staging_bytes=64 << 20)
+    try:
+        assert e.dev_set_leaf_variant(variant) > variant
+        e.dev_set_sort(0)
+        out = e.hash_messages(*e.pack(msgs))
+    finally:
+        e.close()
+    bad = [i for i, (m, d) in enumerate(zip(msgs, out)) if bytes(d).hex() != oracle.hash(m)]
+    assert not bad, [len(msgs[i]) for i in bad[:10]]
+
+
+@pytest.mark.parametrize("variant", [1, 25, 29, 36])
 def test_many_short_multichunk_messages(oracle, variant):
     """C5-shaped batches — mostly 2..5-chunk messages, so tiles hold far more
     partial last chunks than a wave has lanes and the leaf kernel's block-count
     order (variant 25) is taken — next to runs of single-chunk messages and a
     few long ones; every digest against the oracle, for the plain tile kernel
-    (1) and the ordered one (25)"""
+    (1), the ordered one (25), with tiles handed out by the global counter (29)
+    and with the ping-pong block loop (36, the default)"""
     from spacedrive_amd import Engine
     rng = np.random.default_rng(55 + variant)
     lens = np.concatenate([rng.integers(1025, 5 * 1024 + 1, 12000), rng.integers(0, 1025, 3000),
