@@ -88,6 +88,14 @@ int oracle_cpu_bench_files(const uint64_t *keys, const uint64_t *sizes, size_t n
                            int prefer_upstream, uint64_t *out_keys, uint64_t *bytes, double *secs, int *kind,
                            char *version_out);
 
+/* periodic.c: BLAKE3 of messages whose content repeats with a period of 2^k
+ * chunks (the >= 4 TiB checksum fixture); upstream = hash each period with
+ * llvm_blake3_compress_subtree_wide (1.8.2) instead of the scalar oracle */
+int oracle_periodic_upstream_available(void);
+int oracle_subtree_cv(const uint8_t *p, size_t len, uint64_t counter, int upstream, uint32_t out[8]);
+int oracle_periodic_checksum(const uint8_t *period, size_t plen, uint64_t total, int threads, int upstream,
+                             uint8_t out[32]);
+
 #ifdef __cplusplus
 }
 #endif

@@ -38,6 +38,10 @@ class Oracle:
                                               ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
                                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_identifier_dedup.restype = ctypes.c_int64
+        L.oracle_subtree_cv.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int,
+                                        ctypes.c_void_p]
+        L.oracle_periodic_checksum.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int,
+                                               ctypes.c_int, ctypes.c_void_p]
 
     def hash(self, data: bytes) -> str:
         buf = np.frombuffer(bytes(data), dtype=np.uint8)
@@ -75,6 +79,22 @@ class Oracle:
     def synth_checksum(self, content_key, size):
         out = ctypes.create_string_buffer(32)
         self.lib.oracle_synth_checksum(content_key, size, out)
+        return out.raw.hex()
+
+    def subtree_cv(self, data: np.ndarray, counter: int, upstream: bool) -> bytes:
+        """CV of the complete subtree `data` (2^k chunks) starting at chunk `counter`"""
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        out = ctypes.create_string_buffer(32)
+        rc = self.lib.oracle_subtree_cv(data.ctypes.data, data.size, counter, int(upstream), out)
+        assert rc == 0, rc
+        return out.raw
+
+    def periodic_checksum(self, period: np.ndarray, total: int, upstream: bool, threads: int = 4) -> str:
+        """BLAKE3 of `total` bytes of `period` (2^k chunks) repeated (oracle/periodic.c)"""
+        period = np.ascontiguousarray(period, dtype=np.uint8)
+        out = ctypes.create_string_buffer(32)
+        rc = self.lib.oracle_periodic_checksum(period.ctypes.data, period.size, total, threads, int(upstream), out)
+        assert rc == 0, rc
         return out.raw.hex()
 
     def identifier_dedup(self, keys, has_key, status=None, chunk_size=100, existing_keys=()):

@@ -96,3 +96,39 @@ def test_stream_rejects_bad_segments(eng):
         eng.dev_stream_update([0], [MiB // 2], [MiB], [buf.data_ptr()])  # not on a piece boundary
     with pytest.raises(N.SdcasError):
         eng.dev_stream_update([1], [0], [MiB], [buf.data_ptr()])  # no such message
+
+
+def test_stream_over_4tib_golden(eng):
+    """file_checksum of a 4 TiB + 1 MiB + 17 byte file: chunk counters reach
+    2^32 + 1024, so the high counter word (v13) and a 2^22-piece root merge
+    are exercised. The content repeats with a 1 MiB period, so every segment
+    is the same resident 1 MiB buffer; the expected value is the committed
+    fixture from upstream BLAKE3 C 1.8.2 (oracle/gen_golden_periodic.py)."""
+    import json
+    import os
+    from tests._oracle import GOLDEN
+    with open(os.path.join(GOLDEN, "checksums_periodic.json")) as f:
+        doc = json.load(f)
+    assert doc["period"] == MiB
+    period = (np.arange(MiB, dtype=np.uint64) % np.uint64(251)).astype(np.uint8)
+    dev = torch.zeros(MiB + 4096, dtype=torch.uint8, device="cuda")
+    dev[:MiB].copy_(torch.from_numpy(period))
+    torch.cuda.synchronize()
+    for c in doc["cases"]:
+        n = c["size"]
+        q, r = divmod(n, MiB)
+        offs = np.arange(q + (r > 0), dtype=np.uint64) * np.uint64(MiB)
+        lens = np.full(offs.size, MiB, np.uint64)
+        if r:
+            lens[-1] = r
+        out = torch.zeros((1, 32), dtype=torch.uint8, device="cuda")
+        eng.dev_stream_begin([n])
+        # two updates: the high-counter pieces arrive first
+        h = offs.size - 3
+        for part in (slice(h, None), slice(0, h)):
+            k = offs[part].size
+            eng.dev_stream_update(np.zeros(k, np.uint64), offs[part], lens[part],
+                                  np.full(k, dev.data_ptr(), np.uint64))
+        eng.dev_stream_finish(out.data_ptr())
+        eng.dev_sync()
+        assert bytes(out.cpu().numpy()[0]).hex() == c["checksum"], n

@@ -145,3 +145,35 @@ def test_cpu_bench_files_keys(oracle):
                      np.uint64)
     base, par = bench.cpu_baseline_files(want1, sizes[sel], ckeys[sel], 1, 2, "unit")
     assert par["mismatches"] == 0 and base["unit"] == "GB/s"
+
+
+def test_periodic_checksum_matches_whole_hash(oracle):
+    """oracle/periodic.c (the >= 4 TiB fixture's construction) equals the
+    whole-message hash of materialised periodic messages, scalar and upstream"""
+    period = content("pattern251", 0, 1 << 20)
+    for plen in (1024, 8192, 1 << 20):
+        p = period[:plen]
+        for total in (plen + 1, 3 * plen + 17, 8 * plen, 13 * plen + plen // 2 + 1, (24 << 20) + 1025):
+            want = oracle.hash(np.resize(p, total).tobytes())
+            assert oracle.periodic_checksum(p, total, upstream=False) == want, (plen, total)
+            assert oracle.periodic_checksum(p, total, upstream=True) == want, (plen, total)
+
+
+def test_subtree_cv_high_counter(oracle):
+    """chunk counters >= 2^32 (the high word v13): the scalar oracle's subtree
+    CVs equal upstream BLAKE3 C 1.8.2's (llvm_blake3_compress_subtree_wide),
+    and the high word changes the result"""
+    p = content("pattern251", 0, 1 << 20)
+    cvs = {}
+    for c in (0, (1 << 32) - 1024, 1 << 32, (1 << 32) + 1024, (3 << 32) + (5 << 10), (1 << 52)):
+        cvs[c] = oracle.subtree_cv(p, c, upstream=False)
+        assert cvs[c] == oracle.subtree_cv(p, c, upstream=True), c
+    assert cvs[0] != cvs[1 << 32]
+    small = p[:4096]
+    assert oracle.subtree_cv(small, 1 << 32, False) == oracle.subtree_cv(small, 1 << 32, True)
+
+
+def test_periodic_golden_is_large():
+    """the periodic fixture reaches chunk counters >= 2^32"""
+    cases = golden("checksums_periodic.json")
+    assert cases and all(c["size"] > (4 << 40) for c in cases)
