@@ -118,6 +118,32 @@ uint64_t hex_to_key(const std::string& cas_id);
 // ---- rows (the prisma columns this path reads or writes) -------------------
 
 using ObjectKind = int32_t;  // sd_file_ext::kind::ObjectKind discriminant; 0 = Unknown
+// the discriminants of crates/file-ext/src/kind.rs:4-59
+enum : ObjectKind {
+  ObjectKindUnknown = 0, ObjectKindDocument = 1, ObjectKindFolder = 2, ObjectKindText = 3, ObjectKindPackage = 4,
+  ObjectKindImage = 5, ObjectKindAudio = 6, ObjectKindVideo = 7, ObjectKindArchive = 8, ObjectKindExecutable = 9,
+  ObjectKindAlias = 10, ObjectKindEncrypted = 11, ObjectKindKey = 12, ObjectKindLink = 13,
+  ObjectKindWebPageArchive = 14, ObjectKindWidget = 15, ObjectKindAlbum = 16, ObjectKindCollection = 17,
+  ObjectKindFont = 18, ObjectKindMesh = 19, ObjectKindCode = 20, ObjectKindDatabase = 21, ObjectKindBook = 22,
+  ObjectKindConfig = 23, ObjectKindDotfile = 24, ObjectKindScreenshot = 25,
+};
+// FilePathRow::kind / file_metadata_batch: derive the kind from the path
+constexpr ObjectKind kKindFromPath = -1;
+
+// ---- kind detection (crates/file-ext, file_ext.cpp) ---------------------------
+
+// Extension::from_str (magic.rs:63-79): the ObjectKinds of the categories
+// accepting `ext` (case-insensitive), in the Extension enum's order; empty =
+// None, one = Known, two = Conflicts ("ts", "mts": Video and Code)
+std::vector<ObjectKind> extension_kinds(const std::string& ext);
+// Extension::resolve_conflicting(path, false) (magic.rs:176-235) as an
+// ObjectKind: nullopt when the path has no (UTF-8) extension, the extension
+// is unknown, the file does not open, or a conflict is not "ts"/"mts" as
+// written; "ts"/"mts" are Video when the file has the MPEG-TS magic bytes,
+// else Code
+std::optional<ObjectKind> resolve_conflicting_kind(const std::string& path);
+// FileMetadata::new's kind (mod.rs:72-76): the above, or Unknown
+ObjectKind object_kind_of(const std::string& path);
 using PubId = std::array<uint8_t, 16>;
 
 struct Location {  // location::Data (id, path)
@@ -141,9 +167,9 @@ struct FilePathRow {
   int64_t date_created = 0;
   uint64_t inode = 0;   // FilePathMetadata (crates/file-path-helper/src/lib.rs:125-131)
   bool hidden = false;
-  // Extension::resolve_conflicting (crates/file-ext/src/magic.rs:176-230) is
-  // outside this path: the kind is supplied with the row
-  ObjectKind kind = 0;
+  // kKindFromPath: FileMetadata::new derives it (object_kind_of, mod.rs:72-76);
+  // >= 0: a kind already known to the caller, used as is
+  ObjectKind kind = kKindFromPath;
 };
 
 struct ObjectRow {  // object (id, pub_id, kind, date_created)
@@ -235,7 +261,8 @@ class MemoryLibrary : public Library {
 // statements (the DB side of the join). Differences, both
 // deliberate: an index on file_path(cas_id), which the reference's schema
 // lacks (the existing-Object lookup of mod.rs:181-188 then scans the table),
-// and a `kind_hint` column standing in for Extension::resolve_conflicting.
+// and a `kind_hint` column carrying FilePathRow::kind (kKindFromPath unless a
+// caller supplies a kind).
 // Batches are transactions (begin_batch / end_batch).
 class SqliteLibrary : public Library {
  public:
@@ -279,7 +306,8 @@ struct FileMetadata {
 };
 
 // FileMetadata::new for a batch of (full path, kind): fs::metadata, the
-// is_dir assertion (mod.rs:67-70, std::logic_error here), cas_id only for
+// is_dir assertion (mod.rs:67-70, std::logic_error here), the kind from the
+// path (object_kind_of) unless the pair carries one (>= 0), cas_id only for
 // len != 0, one generate_cas_ids call for the batch (the join_all of
 // mod.rs:105-147). Errors carry the path (FileIOError).
 std::vector<Result<FileMetadata>> file_metadata_batch(Engine& engine,

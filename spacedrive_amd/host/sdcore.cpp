@@ -309,7 +309,7 @@ std::vector<Result<FileMetadata>> file_metadata_batch(Engine& engine,
       continue;
     }
     if (S_ISDIR(sb.st_mode)) throw std::logic_error("We can't generate cas_id for directories");  // mod.rs:67-70
-    md[i].kind = files[i].second;
+    md[i].kind = files[i].second >= 0 ? files[i].second : object_kind_of(files[i].first);  // mod.rs:72-76
     md[i].len = (uint64_t)sb.st_size;
     if (md[i].len != 0) {  // mod.rs:78-86: empty files get no cas_id
       to_hash.emplace_back(files[i].first, md[i].len);

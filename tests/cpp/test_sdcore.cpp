@@ -102,6 +102,14 @@ static void test_hashes(Engine& eng, const std::string& dir) {
   CHECK(md[0].ok() && !md[0].value().cas_id && md[0].value().kind == 3, "empty file metadata");
   CHECK(md[1].ok() && md[1].value().cas_id == cas[4].value() && md[1].value().len == 1025, "metadata cas_id");
   CHECK(!md[2].ok() && md[2].error().code == ENOENT, "metadata of a missing file");
+  // the kind from the path (mod.rs:72-76, Extension::resolve_conflicting)
+  write_file(dir + "/clip.ts", {0x47, 0x40, 0x11, 0x10});
+  write_file(dir + "/app.ts", {'l', 'e', 't'});
+  auto mk = file_metadata_batch(eng, {{dir + "/clip.ts", kKindFromPath}, {dir + "/app.ts", kKindFromPath},
+                                      {paths[4], kKindFromPath}});
+  CHECK(mk[0].ok() && mk[0].value().kind == ObjectKindVideo && mk[1].ok() && mk[1].value().kind == ObjectKindCode &&
+            mk[2].ok() && mk[2].value().kind == object_kind_of(paths[4]),
+        "metadata kinds from paths");
   std::printf("hashes: %zu files ok\n", sizes.size());
 }
 

@@ -327,11 +327,91 @@ static void test_walk() {
   std::printf("walk: %zu entries ok\n", rows.size());
 }
 
+static void write_bytes(const std::string& p, const std::string& bytes) {
+  FILE* f = std::fopen(p.c_str(), "wb");
+  if (!f) { std::perror(p.c_str()); return; }
+  std::fwrite(bytes.data(), 1, bytes.size(), f);
+  std::fclose(f);
+}
+
+// kind detection (crates/file-ext: extensions.rs, magic.rs:176-235) as
+// FileMetadata::new uses it; cases derived by hand from the reference tables
+// and its extension_from_str test (extensions.rs:370-389). Its magic_bytes
+// test (extensions.rs:391-564) passes bare extensions as paths and needs the
+// absent packages/test-files corpus, so the magic cases here are synthetic.
+static void test_kind() {
+  // Extension::from_str
+  CHECK(extension_kinds("jpg") == std::vector<ObjectKind>{ObjectKindImage}, "jpg");
+  CHECK((extension_kinds("ts") == std::vector<ObjectKind>{ObjectKindVideo, ObjectKindCode}), "ts conflicts");
+  CHECK((extension_kinds("MTS") == std::vector<ObjectKind>{ObjectKindVideo, ObjectKindCode}), "MTS conflicts");
+  CHECK(extension_kinds("jeff").empty(), "jeff");
+  CHECK(extension_kinds("").empty() && extension_kinds("j pg").empty(), "empty / space");
+  CHECK(extension_kinds("3GP") == std::vector<ObjectKind>{ObjectKindVideo}, "3gp (serde rename)");
+  CHECK(extension_kinds("7z") == std::vector<ObjectKind>{ObjectKindArchive}, "7z (serde rename)");
+  CHECK(extension_kinds("_3gp").empty() && extension_kinds("_7z").empty(), "variant identifiers are not names");
+  CHECK(extension_kinds("\xE2\x84\xAA" "ey") == std::vector<ObjectKind>{ObjectKindDocument}, "Kelvin sign lowercases to k");
+  CHECK(extension_kinds("caf\xC3\xA9").empty(), "non-ASCII");
+  const std::pair<const char*, ObjectKind> one[] = {
+      {"pdf", ObjectKindDocument}, {"key", ObjectKindDocument}, {"hwp", ObjectKindDocument},
+      {"mkv", ObjectKindVideo},    {"f4v", ObjectKindVideo},    {"raw", ObjectKindImage},
+      {"rw2", ObjectKindImage},    {"flac", ObjectKindAudio},   {"ast", ObjectKindAudio},
+      {"bz2", ObjectKindArchive},  {"jar", ObjectKindExecutable}, {"bat", ObjectKindExecutable},
+      {"markdown", ObjectKindText}, {"bytes", ObjectKindEncrypted}, {"block", ObjectKindEncrypted},
+      {"pub", ObjectKindKey},      {"keychain", ObjectKindKey}, {"woff2", ObjectKindFont},
+      {"obj", ObjectKindMesh},     {"php6", ObjectKindCode},    {"dockerfile", ObjectKindCode},
+      {"r", ObjectKindCode},       {"mdx", ObjectKindCode},     {"db", ObjectKindDatabase},
+      {"azw3", ObjectKindBook},    {"tsconfig", ObjectKindConfig}, {"CSV", ObjectKindConfig},
+  };
+  for (const auto& [e, k] : one)
+    CHECK(extension_kinds(e) == std::vector<ObjectKind>{k}, "extension %s", e);
+  // resolve_conflicting on real files
+  char tmpl[] = "/tmp/sdcore_kindXXXXXX";
+  const std::string d = mkdtemp(tmpl);
+  const std::string mpeg_ts("\x47\x40\x11\x10", 4);
+  struct Case { std::string name, bytes; ObjectKind want; const char* why; };
+  const Case cases[] = {
+      {"clip.ts", mpeg_ts, ObjectKindVideo, "ts with the MPEG-TS sync byte"},
+      {"app.ts", "export const x = 1;\n", ObjectKindCode, "typescript"},
+      {"empty.ts", "", ObjectKindCode, "empty ts: the magic read fails -> Code"},
+      {"clip.mts", mpeg_ts, ObjectKindVideo, "mts, sync byte first"},
+      {"m2ts.mts", std::string("\x00\x00\x00\x47\x40", 5), ObjectKindVideo, "mts, sync byte at offset 3"},
+      {"short.mts", "abc", ObjectKindCode, "mts shorter than the 4-byte window"},
+      {"mod.mts", "export {}\n", ObjectKindCode, "typescript module"},
+      {"UPPER.TS", mpeg_ts, ObjectKindUnknown, "conflict matched on the extension as written"},
+      {"Photo.JPG", "x", ObjectKindImage, "case-insensitive"},
+      {"notes.md", "# hi", ObjectKindText, "text"},
+      {"a.tar.gz", "", ObjectKindArchive, "last extension"},
+      {"Makefile", "all:", ObjectKindUnknown, "no extension"},
+      {".bashrc", "x", ObjectKindUnknown, "dotfile: no extension"},
+      {"trail.", "x", ObjectKindUnknown, "empty extension"},
+      {"data.bin", "x", ObjectKindUnknown, "unknown extension"},
+      {"k.\xE2\x84\xAA" "ey", "x", ObjectKindDocument, "Kelvin sign"},
+      {"bad.\xFF" "ts", "x", ObjectKindUnknown, "extension not UTF-8"},
+  };
+  for (const auto& c : cases) {
+    write_bytes(d + "/" + c.name, c.bytes);
+    const ObjectKind got = object_kind_of(d + "/" + c.name);
+    CHECK(got == c.want, "kind of %s (%s): %d, want %d", c.name.c_str(), c.why, got, c.want);
+  }
+  CHECK(object_kind_of(d + "/missing.jpg") == ObjectKindUnknown, "a file that does not open -> Unknown");
+  // "x/." names x (a trailing "." is not a component); a file does not open
+  // as a directory, a directory opens but its magic read fails -> Code
+  CHECK(object_kind_of(d + "/clip.ts/.") == ObjectKindUnknown, "regular file with a trailing /.");
+  mkdir((d + "/dir.ts").c_str(), 0755);
+  CHECK(object_kind_of(d + "/dir.ts/.") == ObjectKindCode && object_kind_of(d + "/dir.ts//") == ObjectKindCode,
+        "directory named *.ts");
+  CHECK(!resolve_conflicting_kind(d + "/..") && !resolve_conflicting_kind("/"), "no file name");
+  std::string cmd = "rm -rf " + d;
+  if (std::system(cmd.c_str()) != 0) std::fprintf(stderr, "cleanup failed\n");
+  std::printf("kind: %zu files ok\n", sizeof cases / sizeof cases[0]);
+}
+
 int main(int argc, char** argv) {
   if (argc > 2 && std::strcmp(argv[1], "--bench") == 0) return bench((size_t)std::atoll(argv[2]));
   test_parity(true);
   test_parity(false);
   test_walk();
+  test_kind();
   std::printf("%s (%d failures)\n", failures ? "FAILED" : "ALL OK", failures);
   return failures ? 1 : 0;
 }

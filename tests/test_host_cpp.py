@@ -34,7 +34,8 @@ def test_host_library_links_the_c_abi():
     syms = subprocess.run(["nm", "-DC", "--defined-only", lib], capture_output=True, text=True).stdout
     for name in ("sdcore::generate_cas_id", "sdcore::file_checksum", "sdcore::identifier_job_step",
                  "sdcore::run_file_identifier_job", "sdcore::run_object_validator_job",
-                 "sdcore::file_metadata_batch", "sdcore::Engine::open"):
+                 "sdcore::file_metadata_batch", "sdcore::Engine::open", "sdcore::object_kind_of",
+                 "sdcore::resolve_conflicting_kind", "sdcore::extension_kinds"):
         assert name in syms, name
 
 
