@@ -13,6 +13,8 @@
 #include <cstring>
 #include <random>
 #include <string>
+#include <map>
+#include <set>
 #include <vector>
 
 #include "../../oracle/oracle.h"
@@ -297,7 +299,8 @@ static void test_location_scan(Engine& eng, const std::string& dir) {
     const auto& d = subdirs[g() % subdirs.size()];
     const uint64_t which = g() % 220;  // shared contents
     const size_t size = 1 + (which * 104729) % 300000;
-    const std::string name = "f" + std::to_string(i) + ((i % 4) ? ".dat" : "");
+    static const char* const exts[] = {"", ".dat", ".JPG", ".ts", ".md", ".mts", ".json"};
+    const std::string name = "f" + std::to_string(i) + exts[i % 7];
     write_file(root + (d.empty() ? "" : "/" + d) + "/" + name, content(which + 9000, size));
   }
   std::vector<IoError> errs;
@@ -332,6 +335,19 @@ static void test_location_scan(Engine& eng, const std::string& dir) {
     if (link[k] >= 0 && link[k] != (int64_t)k)
       CHECK(r->object_id == sql->file_path(ids[(size_t)link[k]])->object_id, "scan object of row %d", ids[k]);
   }
+  // a created Object takes its file's kind (mod.rs:266-291), derived from the
+  // path by FileMetadata::new (mod.rs:72-76)
+  std::map<int32_t, ObjectKind> object_kind;
+  for (const auto& o : sql->objects()) object_kind[o.id] = o.kind;
+  std::set<ObjectKind> kinds_seen;
+  for (size_t k = 0; k < ids.size(); ++k) {
+    if (link[k] != (int64_t)k) continue;
+    auto r = sql->file_path(ids[k]);
+    const ObjectKind want = object_kind_of(full_path(Location{3, root}, *r));
+    kinds_seen.insert(want);
+    CHECK(r->object_id && object_kind[*r->object_id] == want, "scan kind of row %d", ids[k]);
+  }
+  CHECK(kinds_seen.size() >= 5, "scan saw %zu kinds", kinds_seen.size());
   auto rep = run_object_validator_job(eng, *sql, ObjectValidatorJobInit{Location{3, root}, "", 256});
   CHECK(rep.task_count == ids.size() && rep.checksummed == ids.size() && !rep.error, "scan validator");
   for (int32_t id : ids) {
