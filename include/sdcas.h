@@ -212,6 +212,14 @@ int sdcas_dev_dedup_resolve(sdcas_ctx *ctx, const uint64_t *d_frec, size_t nf, c
 int sdcas_dev_dedup_apply(sdcas_ctx *ctx, const uint64_t *d_ids, const uint32_t *d_slot, size_t n,
                           const int64_t *d_result, size_t chunk_size, int64_t *d_link, uint64_t *d_counts,
                           void *stream);
+/* A world of one: the three stages without the combine (nothing is
+ * exchanged, so files and existing Objects go straight into resolve's table):
+ * the same d_link / d_counts as combine -> resolve -> apply. d_ekeys/d_eids
+ * [ne]: existing Objects' cas keys and DB indices (may be NULL when ne == 0). */
+int sdcas_dev_dedup_local(sdcas_ctx *ctx, const uint64_t *d_keys, const uint8_t *d_has_key,
+                          const int32_t *d_status, const uint64_t *d_ids, size_t n, const uint64_t *d_ekeys,
+                          const uint64_t *d_eids, size_t ne, size_t chunk_size, int64_t *d_link,
+                          uint64_t *d_counts, void *stream);
 
 /* ---- helpers ------------------------------------------------------------ */
 

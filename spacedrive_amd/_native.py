@@ -24,7 +24,7 @@ ABI_SYMBOLS = [
     "sdcas_checksums", "sdcas_hash_messages", "sdcas_cas_ids_from_messages", "sdcas_dev_reserve",
     "sdcas_dev_hash_messages", "sdcas_dev_sync", "sdcas_dedup", "sdcas_key_to_hex",
     "sdcas_digest_to_hex", "sdcas_cas_message_len", "sdcas_dev_dedup_combine", "sdcas_dev_dedup_resolve",
-    "sdcas_dev_dedup_apply", "sdcas_dev_stream_begin", "sdcas_dev_stream_update", "sdcas_dev_stream_finish",
+    "sdcas_dev_dedup_apply", "sdcas_dev_dedup_local", "sdcas_dev_stream_begin", "sdcas_dev_stream_update", "sdcas_dev_stream_finish",
     # bench / test plumbing
     "sdcas_dev_synth_cas_messages", "sdcas_dev_synth_content", "sdcas_dev_dedup", "sdcas_dev_profile",
     "sdcas_dev_last_kernel_ms", "sdcas_dev_set_leaf_variant", "sdcas_dev_set_sort",
@@ -95,6 +95,7 @@ def load():
     L.sdcas_dev_dedup_combine.argtypes = [_vp, _vp, _vp, _vp, _vp, _sz, ctypes.c_uint32, _vp, _vp, _vp, _vp]
     L.sdcas_dev_dedup_resolve.argtypes = [_vp, _vp, _sz, _vp, _sz, _vp, _vp]
     L.sdcas_dev_dedup_apply.argtypes = [_vp, _vp, _vp, _sz, _vp, _sz, _vp, _vp, _vp]
+    L.sdcas_dev_dedup_local.argtypes = [_vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _sz, _sz, _vp, _vp, _vp]
     L.sdcas_dev_stream_begin.argtypes = [_vp, _vp, _sz]
     L.sdcas_dev_stream_update.argtypes = [_vp, _sz, _vp, _vp, _vp, _vp, _vp]
     L.sdcas_dev_stream_finish.argtypes = [_vp, _vp, _vp]

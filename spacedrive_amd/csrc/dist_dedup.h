@@ -78,4 +78,11 @@ hipError_t dd_resolve(DistWs& w, const uint64_t* frec, uint32_t nf, const uint64
 hipError_t dd_apply(const uint64_t* ids, const uint32_t* slot, uint32_t n, const int64_t* result,
                     uint64_t chunk_size, int64_t* link, unsigned long long* counts, hipStream_t st);
 
+// Stages 1-3 fused for a world of one (no exchange, so no combine): files
+// and existing Objects (ekeys/eids[ne], eids = DB order) go straight into the
+// resolve table. Same link / counts as combine -> resolve -> apply.
+hipError_t dd_local(DistWs& w, const uint64_t* keys, const uint8_t* has_key, const int32_t* status,
+                    const uint64_t* ids, uint32_t n, const uint64_t* ekeys, const uint64_t* eids, uint32_t ne,
+                    uint64_t chunk_size, int64_t* link, unsigned long long* counts, hipStream_t st);
+
 }  // namespace sdcas

@@ -308,6 +308,103 @@ hipError_t dd_resolve(DistWs& w, const uint64_t* frec, uint32_t nf, const uint64
   return hipGetLastError();
 }
 
+// ---- a world of one: no exchange, hence no combine ---------------------------
+//
+// The combine exists to shrink what crosses the exchange and to group it by
+// owner. With one rank there is nothing to exchange: every present file's
+// (key, ordinal) and every existing Object's (key, DB index) go straight into
+// the resolve table, and each file reads its answer from its own entry.
+
+// side 0: files (pos[i] = entry, or the slot code of a file without one);
+// side 1: existing Objects (pos null, has_key / status null)
+__global__ void k_solo_insert(const uint64_t* __restrict__ keys, const uint8_t* __restrict__ has_key,
+                              const int32_t* __restrict__ status, const uint64_t* __restrict__ ids, uint32_t n,
+                              unsigned long long* __restrict__ tkey, unsigned long long* __restrict__ tmin,
+                              uint32_t mask, uint32_t shift, uint32_t side, uint32_t* __restrict__ pos) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const bool ok = status == nullptr || status[i] == 0;  // mod.rs:125-141
+  const bool has = has_key == nullptr || has_key[i];    // mod.rs:83-86
+  if (!(ok && has)) {
+    if (pos) pos[i] = !ok ? kSlotDropped : kSlotNoKey;
+    return;
+  }
+  const uint32_t h = ht_find(tkey, keys[i], mask, shift);
+  const unsigned long long v = ids[i];
+  unsigned long long* m = &tmin[2 * (uint64_t)h + side];
+  if (__hip_atomic_load(m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > v) atomicMin(m, v);
+  if (pos) pos[i] = h;
+}
+
+// k_dd_apply with the answer read from the file's own table entry
+__global__ void k_solo_apply(const uint64_t* __restrict__ ids, const uint32_t* __restrict__ pos, uint32_t n,
+                             const uint64_t* __restrict__ tmin, uint64_t cs, int64_t* __restrict__ link,
+                             unsigned long long* __restrict__ counts) {
+  __shared__ unsigned long long sc[2];
+  if (threadIdx.x < 2) sc[threadIdx.x] = 0;
+  __syncthreads();
+  unsigned long long c = 0, l = 0;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t h = pos[i];
+    const int64_t me = (int64_t)ids[i];
+    int64_t v;
+    if (h == kSlotDropped) {
+      v = INT64_MIN;
+    } else if (h == kSlotNoKey) {
+      v = me;  // mod.rs:246-254: a file without cas_id gets its own Object
+    } else {
+      const uint64_t e = tmin[2 * (uint64_t)h + 1];
+      // mod.rs:202-238: the first existing Object; else the key's first file,
+      // whose chunk creates one Object per file (mod.rs:246-254)
+      const int64_t r = e != ~0ull ? -(int64_t)e - 1 : (int64_t)tmin[2 * (uint64_t)h];
+      if (r < 0) v = r;
+      else v = ((uint64_t)me / cs == (uint64_t)r / cs) ? me : r;
+    }
+    link[i] = v;
+    if (v == me) c += 1;
+    else if (v != INT64_MIN) l += 1;
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    c += __shfl_down(c, off);
+    l += __shfl_down(l, off);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&sc[0], c);
+    atomicAdd(&sc[1], l);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && counts) {
+    atomicAdd(&counts[0], sc[0]);
+    atomicAdd(&counts[1], sc[1]);
+  }
+}
+
+hipError_t dd_local(DistWs& w, const uint64_t* keys, const uint8_t* has_key, const int32_t* status,
+                    const uint64_t* ids, uint32_t n, const uint64_t* ekeys, const uint64_t* eids, uint32_t ne,
+                    uint64_t chunk_size, int64_t* link, unsigned long long* counts, hipStream_t st) {
+  hipError_t e;
+  if (n == 0) return hipSuccess;
+  uint64_t cap = 1024;
+  while (cap < 2 * ((uint64_t)n + ne)) cap <<= 1;
+  if (cap > (1ull << 31)) return hipErrorInvalidValue;
+  if ((e = w.tkey.ensure(cap + 1)) || (e = w.tmin.ensure(2 * (cap + 1))) || (e = w.tpos.ensure(n))) return e;
+  const uint32_t mask = (uint32_t)(cap - 1);
+  const uint32_t shift = 64u - (uint32_t)__builtin_ctzll(cap);
+  if ((e = hipMemsetAsync(w.tkey.p, 0xFF, sizeof(uint64_t) * (cap + 1), st)) ||
+      (e = hipMemsetAsync(w.tmin.p, 0xFF, sizeof(uint64_t) * 2 * (cap + 1), st)))
+    return e;
+  auto* tk = reinterpret_cast<unsigned long long*>(w.tkey.p);
+  auto* tm = reinterpret_cast<unsigned long long*>(w.tmin.p);
+  if (ne)
+    hipLaunchKernelGGL(k_solo_insert, dim3(blocks(ne)), dim3(TB), 0, st, ekeys, nullptr, nullptr, eids, ne, tk, tm,
+                       mask, shift, 1u, nullptr);
+  hipLaunchKernelGGL(k_solo_insert, dim3(blocks(n)), dim3(TB), 0, st, keys, has_key, status, ids, n, tk, tm, mask,
+                     shift, 0u, w.tpos.p);
+  hipLaunchKernelGGL(k_solo_apply, dim3(blocks(n) < 1024 ? blocks(n) : 1024), dim3(TB), 0, st, ids, w.tpos.p, n,
+                     w.tmin.p, chunk_size ? chunk_size : 100, link, counts);
+  return hipGetLastError();
+}
+
 hipError_t dd_apply(const uint64_t* ids, const uint32_t* slot, uint32_t n, const int64_t* result, uint64_t chunk_size,
                     int64_t* link, unsigned long long* counts, hipStream_t st) {
   if (n == 0) return hipSuccess;

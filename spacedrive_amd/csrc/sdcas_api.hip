@@ -1085,6 +1085,20 @@ int sdcas_dev_dedup_resolve(sdcas_ctx* c, const uint64_t* d_frec, size_t nf, con
   return e ? c->hip_fail(e, "dedup_resolve") : SDCAS_OK;
 }
 
+int sdcas_dev_dedup_local(sdcas_ctx* c, const uint64_t* d_keys, const uint8_t* d_has_key, const int32_t* d_status,
+                          const uint64_t* d_ids, size_t n, const uint64_t* d_ekeys, const uint64_t* d_eids, size_t ne,
+                          size_t chunk_size, int64_t* d_link, uint64_t* d_counts, void* stream) {
+  if (!c || (n && (!d_keys || !d_ids || !d_link)) || (ne && (!d_ekeys || !d_eids))) return SDCAS_E_INVALID;
+  if (n > 0xFFFFFFF0ull || ne > 0xFFFFFFF0ull) return c->fail(SDCAS_E_CAPACITY, "dedup_local: > 2^32 records");
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipSetDevice(c->device);
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  hipError_t e = dd_local(c->dist, d_keys, d_has_key, d_status, d_ids, (uint32_t)n, d_ekeys, d_eids, (uint32_t)ne,
+                          chunk_size ? chunk_size : SDCAS_IDENTIFIER_CHUNK_SIZE, d_link,
+                          (unsigned long long*)d_counts, st);
+  return e ? c->hip_fail(e, "dedup_local") : SDCAS_OK;
+}
+
 int sdcas_dev_dedup_apply(sdcas_ctx* c, const uint64_t* d_ids, const uint32_t* d_slot, size_t n,
                           const int64_t* d_result, size_t chunk_size, int64_t* d_link, uint64_t* d_counts,
                           void* stream) {

@@ -19,7 +19,8 @@ lowest orphan ordinal carrying the key — plus a per-file rule, so it shards:
                Object / the Object created by the key's first file
 
 The device stages (1, 3, 5) are libsdcas's HIP kernels
-(sdcas_dev_dedup_{combine,resolve,apply}); the exchanges are
+(sdcas_dev_dedup_{combine,resolve,apply}; a world of one runs them fused
+without the combine, sdcas_dev_dedup_local); the exchanges are
 torch.distributed all_to_all_single (backend "nccl" = RCCL over xGMI). The
 `stages` object is pluggable only so that the collective protocol can be
 exercised with gloo on CPU by the test-suite's numpy stages
@@ -87,6 +88,21 @@ class DeviceStages:
         self.eng._check(rc, "sdcas_dev_dedup_resolve")
         return result[:nf]
 
+    def local(self, keys, has_key, status, ids, chunk_size, existing_keys=None, existing_ids=None):
+        """combine + resolve + apply for a world of one (nothing to exchange,
+        so no combine): -> (link int64[n], counts int64[2]) on the device"""
+        n = int(ids.numel())
+        link = torch.empty(max(n, 1), dtype=torch.int64, device=ids.device)
+        counts = torch.zeros(2, dtype=torch.int64, device=ids.device)
+        ne = int(existing_keys.numel()) if existing_keys is not None else 0
+        p = lambda t: t.data_ptr() if t is not None and t.numel() else None
+        rc = self.eng.L.sdcas_dev_dedup_local(self.eng.ctx, p(keys), p(has_key), p(status), p(ids), n,
+                                              p(existing_keys) if ne else None, p(existing_ids) if ne else None,
+                                              ne, int(chunk_size), p(link), counts.data_ptr(), self._enter())
+        self._leave(keys, has_key, status, ids, existing_keys, existing_ids, link, counts)
+        self.eng._check(rc, "sdcas_dev_dedup_local")
+        return link[:n], counts
+
     def apply(self, ids, slot, result, chunk_size):
         """-> (link int64[n], counts int64[2] = (created, linked)) on the device"""
         n = int(ids.numel())
@@ -132,8 +148,14 @@ def identifier_dedup_distributed(stages, keys, has_key, status, ids, chunk_size=
     """
     world = dist.get_world_size(group)
     # a world of one exchanges with itself: its records are already where
-    # the collectives would deliver them, so the exchanges are skipped
+    # the collectives would deliver them, so the exchanges are skipped, and
+    # without an exchange the combine has nothing to shrink or group: stages
+    # that offer the fused single-rank path take it
     solo = world == 1
+    if solo and hasattr(stages, "local"):
+        link, cnt = stages.local(keys, has_key, status, ids, chunk_size, existing_keys, existing_ids)
+        c = cnt.tolist()
+        return link, int(c[0]), int(c[1])
     rec, slot, starts = stages.combine(keys, has_key, status, ids, world)
     counts = [starts[r + 1] - starts[r] for r in range(world)]
     frecv, fcounts = (rec, counts) if solo else _exchange(rec, counts, group)

@@ -224,3 +224,50 @@ def test_rccl_world1(eng, oracle):
     want, wc, wl = oracle.identifier_dedup(keys, has, status, 100, existing)
     assert np.array_equal(link.cpu().numpy(), want)
     assert (c, l) == (wc, wl)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("corpus,chunk_size", [("default", 100), ("default", 7), ("default", 1),
+                                               ("collisions", 100), ("clustered", 100)])
+def test_device_local_vs_oracle(eng, oracle, corpus, chunk_size):
+    """the fused single-rank path (sdcas_dev_dedup_local: no combine, files and
+    existing Objects straight into the resolve table) against the oracle"""
+    from spacedrive_amd.dist_dedup import DeviceStages
+    if corpus == "default":
+        keys, has, status, existing = make_corpus(91, 40000, pool=6000)
+        keys[:2] = np.uint64(2**64 - 1)  # the table's empty marker is a legal key
+        existing = np.concatenate([existing, np.array([2**64 - 1], np.uint64)])
+    elif corpus == "collisions":
+        keys, has, status, existing = collision_corpus()
+    else:
+        rng = np.random.default_rng(29)
+        pool = np.concatenate([(np.uint64(2**64 - 2**20) + rng.integers(0, 2**20 - 1, 3000, dtype=np.uint64)),
+                               rng.integers(0, 2**16, 1000, dtype=np.uint64),
+                               np.array([2**64 - 1, 0], np.uint64)]).astype(np.uint64)
+        keys = pool[rng.integers(0, pool.size, 12000)]
+        has = (rng.random(keys.size) > 0.02).astype(np.uint8)
+        status = np.where(rng.random(keys.size) < 0.01, 5, 0).astype(np.int32)
+        existing = pool[rng.integers(0, pool.size, 500)]
+    (k, h, s, ids), = shard(keys, has, status, existing, 1, device="cuda")[0]
+    ek = torch.from_numpy(existing.view(np.int64)).cuda()
+    eids = torch.arange(existing.size, dtype=torch.int64, device="cuda")
+    st = DeviceStages(eng)
+    for with_existing in (True, False):
+        link, cnt = st.local(k, h, s, ids, chunk_size, ek if with_existing else None,
+                             eids if with_existing else None)
+        want, wc, wl = oracle.identifier_dedup(keys, has, status, chunk_size,
+                                               existing if with_existing else np.zeros(0, np.uint64))
+        assert np.array_equal(link.cpu().numpy(), want)
+        assert tuple(cnt.tolist()) == (wc, wl)
+    # degenerate: no files; files without cas_ids or with errors only
+    z = torch.zeros(0, dtype=torch.int64, device="cuda")
+    link, cnt = st.local(z, z.to(torch.uint8), z.to(torch.int32), z, 100)
+    assert link.numel() == 0 and cnt.tolist() == [0, 0]
+    k2 = torch.tensor([5, 5, 6], dtype=torch.int64, device="cuda")
+    h2 = torch.tensor([0, 1, 1], dtype=torch.uint8, device="cuda")
+    s2 = torch.tensor([0, 3, 3], dtype=torch.int32, device="cuda")
+    i2 = torch.arange(3, dtype=torch.int64, device="cuda")
+    link, cnt = st.local(k2, h2, s2, i2, 100)
+    want, wc, wl = oracle.identifier_dedup(np.array([5, 5, 6], np.uint64), np.array([0, 1, 1], np.uint8),
+                                           np.array([0, 3, 3], np.int32), 100, np.zeros(0, np.uint64))
+    assert np.array_equal(link.cpu().numpy(), want) and tuple(cnt.tolist()) == (wc, wl)
