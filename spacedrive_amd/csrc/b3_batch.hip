@@ -231,6 +231,33 @@ __device__ __forceinline__ void hash_chunk_pair(const uint8_t* __restrict__ p, u
   }
 }
 
+// Same two register sets as the ping-pong loop, but both 64-byte halves of a
+// 128-byte line are requested together (no prefetch across lines): the second
+// half never waits in L2 for a compression and cannot be evicted before it is
+// read; the load latency is left to the other waves of the SIMD.
+__device__ __forceinline__ void hash_chunk_ps(const uint8_t* __restrict__ p, uint32_t clen, uint64_t j, bool root,
+                                              uint32_t (&cv)[8]) {
+  set_iv(cv);
+  const uint32_t nb = clen == 0 ? 1 : (clen + BLOCK_LEN - 1) / BLOCK_LEN;
+  const uint32_t endf = CHUNK_END | (root ? ROOT : 0u);
+  uint32_t m0[16], m1[16];
+#pragma unroll 1
+  for (uint32_t b = 0; b < nb; b += 2) {
+    load_full_block(p + b * BLOCK_LEN, m0);
+    load_full_block(p + min(b + 1, nb - 1) * BLOCK_LEN, m1);
+    {
+      const uint32_t blen = min(BLOCK_LEN, clen - b * BLOCK_LEN);
+      if (blen < BLOCK_LEN) mask_tail(m0, blen);
+      compress(cv, m0, j, blen, (b == 0 ? CHUNK_START : 0u) | (b + 1 == nb ? endf : 0u));
+    }
+    if (b + 1 < nb) {
+      const uint32_t blen = min(BLOCK_LEN, clen - (b + 1) * BLOCK_LEN);
+      if (blen < BLOCK_LEN) mask_tail(m1, blen);
+      compress(cv, m1, j, blen, b + 2 == nb ? endf : 0u);
+    }
+  }
+}
+
 // DIAGNOSTIC ONLY (wrong digests, never the default): PF=2 compresses
 // register-made blocks without touching memory (pure VALU rate); PF=3 streams
 // the chunk's blocks and folds them with XOR, no compression (pure load rate).
@@ -471,7 +498,8 @@ __global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __
       const uint32_t clen = len == 0 ? 0u : (uint32_t)min<uint64_t>(CHUNK_LEN, len - j * CHUNK_LEN);
       const bool root = (C == 1);
       uint32_t cv[8];
-      if (PF == 6) hash_chunk_pf2(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
+      if (PF == 8) hash_chunk_ps(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
+      else if (PF == 6) hash_chunk_pf2(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
       else if (PF == 7) hash_chunk_pair(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
       else if (PF == 4) hash_chunk_pp(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
       else if (PF == 5) hash_chunk_pf<true>(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
@@ -1307,7 +1335,8 @@ __global__ void __launch_bounds__(kWG, MINW) k_piece_tree(const uint8_t* __restr
     for (uint32_t s = tid; s < nchunks; s += kWG) {
       const uint32_t clen = min(CHUNK_LEN, pd.len - s * CHUNK_LEN);
       uint32_t cv[8];
-      if (PF == 4) hash_chunk_pp(blob + pd.off + (uint64_t)s * CHUNK_LEN, clen, pd.j0 + s, false, cv);
+      if (PF == 8) hash_chunk_ps(blob + pd.off + (uint64_t)s * CHUNK_LEN, clen, pd.j0 + s, false, cv);
+      else if (PF == 4) hash_chunk_pp(blob + pd.off + (uint64_t)s * CHUNK_LEN, clen, pd.j0 + s, false, cv);
       else if (PF) hash_chunk_pf(blob + pd.off + (uint64_t)s * CHUNK_LEN, clen, pd.j0 + s, false, cv);
       else hash_chunk(blob + pd.off + (uint64_t)s * CHUNK_LEN, clen, pd.j0 + s, false, cv);
 #pragma unroll
@@ -1594,9 +1623,11 @@ static const LeafVariant kLeafVariants[] = {
     {(const void*)k_leaf_tree<512, 2, 0, 0, 0, 1, 1>, 512},
     // 42: 29 with 128-byte pair loads (a lane reads a whole L2 line at once)
     {(const void*)k_leaf_tree<512, 7, 1, 0, 0, 1, 1>, 512},
+    // 43: 36 with both halves of a line loaded together, no prefetch
+    {(const void*)k_leaf_tree<512, 8, 1, 0, 0, 1, 1>, 512},
 };
 constexpr int kNumLeafVariants = sizeof(kLeafVariants) / sizeof(kLeafVariants[0]);
-constexpr int kDefaultLeafVariant = 36;
+constexpr int kDefaultLeafVariant = 43;
 
 int leaf_variant_count() { return kNumLeafVariants; }
 
@@ -1700,6 +1731,8 @@ hipError_t piece_hash(const uint8_t* blob, const PieceDesc* pieces, uint32_t npi
     hipLaunchKernelGGL((k_piece_tree<4, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   else if (v == 5)
     hipLaunchKernelGGL((k_piece_tree<4, 8, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
+  else if (v == 6)  // 4 with both halves of a line loaded together
+    hipLaunchKernelGGL((k_piece_tree<8, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   else hipLaunchKernelGGL((k_piece_tree<1, 8>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   return hipGetLastError();
 }

@@ -146,7 +146,7 @@ def test_tile_straddles_vs_oracle(eng, oracle):
         assert bytes(d).hex() == oracle.hash(m), len(m)
 
 
-@pytest.mark.parametrize("variant", [1, 29, 36])
+@pytest.mark.parametrize("variant", [1, 29, 36, 43])
 def test_tile_straddles_per_variant(oracle, variant):
     """the straddle corpus through each production leaf variant, in caller
     order (shape sort off) so messages straddle tiles at every level"""
@@ -170,14 +170,15 @@ def test_tile_straddles_per_variant(oracle, variant):
     assert not bad, [len(msgs[i]) for i in bad[:10]]
 
 
-@pytest.mark.parametrize("variant", [1, 25, 29, 36])
+@pytest.mark.parametrize("variant", [1, 25, 29, 36, 43])
 def test_many_short_multichunk_messages(oracle, variant):
     """C5-shaped batches — mostly 2..5-chunk messages, so tiles hold far more
     partial last chunks than a wave has lanes and the leaf kernel's block-count
     order (variant 25) is taken — next to runs of single-chunk messages and a
     few long ones; every digest against the oracle, for the plain tile kernel
     (1), the ordered one (25), with tiles handed out by the global counter (29)
-    and with the ping-pong block loop (36, the default)"""
+    with the ping-pong block loop (36) and with line-pair loads (43, the
+    default)"""
     from spacedrive_amd import Engine
     rng = np.random.default_rng(55 + variant)
     lens = np.concatenate([rng.integers(1025, 5 * 1024 + 1, 12000), rng.integers(0, 1025, 3000),

@@ -3,7 +3,7 @@
 # MI355X_MICROARCH.md prescribes). Usage: tools/pmc_traffic.sh <outdir> [variant]
 set -u
 OUT=${1:-gpurun_out/pmc_traffic}
-VAR=${2:-36}  # the default leaf variant (kDefaultLeafVariant)
+VAR=${2:-43}  # the default leaf variant (kDefaultLeafVariant)
 R=$(pwd)
 mkdir -p $OUT
 export TMPDIR=/tmp

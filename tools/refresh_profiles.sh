@@ -12,4 +12,4 @@ for w in c2 c5; do
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$OUT/prof_$w -o $w --output-format csv \
      -- python $R/bench.py --workload $w --steps 5 --warmup 2 --no-cpu-baseline > $R/$OUT/prof_$w.log 2>&1)
 done
-tools/pmc_traffic.sh $OUT/pmc 36 > $OUT/pmc.log 2>&1  # 36 = the default leaf variant
+tools/pmc_traffic.sh $OUT/pmc 43 > $OUT/pmc.log 2>&1  # 43 = the default leaf variant
