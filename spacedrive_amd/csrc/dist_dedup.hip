@@ -315,12 +315,31 @@ hipError_t dd_resolve(DistWs& w, const uint64_t* frec, uint32_t nf, const uint64
 // (key, ordinal) and every existing Object's (key, DB index) go straight into
 // the resolve table, and each file reads its answer from its own entry.
 
-// side 0: files (pos[i] = entry, or the slot code of a file without one);
-// side 1: existing Objects (pos null, has_key / status null)
+// The table: one 16-byte entry per slot, (key, minimum file ordinal), so an
+// insert touches one line; the existing Objects' minima live in a side array
+// (emin), allocated and read only when there are existing Objects.
+__device__ __forceinline__ uint32_t ht_find_kv(unsigned long long* __restrict__ tab, uint64_t key, uint32_t mask,
+                                               uint32_t shift) {
+  if (key == kEmptyKey) return mask + 1;
+  uint32_t h = (uint32_t)(key >> shift) & mask;
+  for (;;) {
+    const unsigned long long cur = __hip_atomic_load(&tab[2 * (uint64_t)h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == key) return h;
+    if (cur == kEmptyKey) {
+      const unsigned long long prev =
+          atomicCAS(&tab[2 * (uint64_t)h], (unsigned long long)kEmptyKey, (unsigned long long)key);
+      if (prev == kEmptyKey || prev == key) return h;
+    }
+    h = (h + 1) & mask;
+  }
+}
+
+// files (emin null): pos[i] = entry, or the slot code of a file without one;
+// existing Objects (emin set): min-fold the DB index into emin[entry]
 __global__ void k_solo_insert(const uint64_t* __restrict__ keys, const uint8_t* __restrict__ has_key,
                               const int32_t* __restrict__ status, const uint64_t* __restrict__ ids, uint32_t n,
-                              unsigned long long* __restrict__ tkey, unsigned long long* __restrict__ tmin,
-                              uint32_t mask, uint32_t shift, uint32_t side, uint32_t* __restrict__ pos) {
+                              unsigned long long* __restrict__ tab, unsigned long long* __restrict__ emin,
+                              uint32_t mask, uint32_t shift, uint32_t* __restrict__ pos) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const bool ok = status == nullptr || status[i] == 0;  // mod.rs:125-141
@@ -329,17 +348,17 @@ __global__ void k_solo_insert(const uint64_t* __restrict__ keys, const uint8_t* 
     if (pos) pos[i] = !ok ? kSlotDropped : kSlotNoKey;
     return;
   }
-  const uint32_t h = ht_find(tkey, keys[i], mask, shift);
+  const uint32_t h = ht_find_kv(tab, keys[i], mask, shift);
   const unsigned long long v = ids[i];
-  unsigned long long* m = &tmin[2 * (uint64_t)h + side];
+  unsigned long long* m = emin ? &emin[h] : &tab[2 * (uint64_t)h + 1];
   if (__hip_atomic_load(m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > v) atomicMin(m, v);
   if (pos) pos[i] = h;
 }
 
 // k_dd_apply with the answer read from the file's own table entry
 __global__ void k_solo_apply(const uint64_t* __restrict__ ids, const uint32_t* __restrict__ pos, uint32_t n,
-                             const uint64_t* __restrict__ tmin, uint64_t cs, int64_t* __restrict__ link,
-                             unsigned long long* __restrict__ counts) {
+                             const uint64_t* __restrict__ tab, const uint64_t* __restrict__ emin, uint64_t cs,
+                             int64_t* __restrict__ link, unsigned long long* __restrict__ counts) {
   __shared__ unsigned long long sc[2];
   if (threadIdx.x < 2) sc[threadIdx.x] = 0;
   __syncthreads();
@@ -353,10 +372,10 @@ __global__ void k_solo_apply(const uint64_t* __restrict__ ids, const uint32_t* _
     } else if (h == kSlotNoKey) {
       v = me;  // mod.rs:246-254: a file without cas_id gets its own Object
     } else {
-      const uint64_t e = tmin[2 * (uint64_t)h + 1];
+      const uint64_t e = emin ? emin[h] : ~0ull;
       // mod.rs:202-238: the first existing Object; else the key's first file,
       // whose chunk creates one Object per file (mod.rs:246-254)
-      const int64_t r = e != ~0ull ? -(int64_t)e - 1 : (int64_t)tmin[2 * (uint64_t)h];
+      const int64_t r = e != ~0ull ? -(int64_t)e - 1 : (int64_t)tab[2 * (uint64_t)h + 1];
       if (r < 0) v = r;
       else v = ((uint64_t)me / cs == (uint64_t)r / cs) ? me : r;
     }
@@ -387,21 +406,22 @@ hipError_t dd_local(DistWs& w, const uint64_t* keys, const uint8_t* has_key, con
   uint64_t cap = 1024;
   while (cap < 2 * ((uint64_t)n + ne)) cap <<= 1;
   if (cap > (1ull << 31)) return hipErrorInvalidValue;
-  if ((e = w.tkey.ensure(cap + 1)) || (e = w.tmin.ensure(2 * (cap + 1))) || (e = w.tpos.ensure(n))) return e;
+  // (key, file minimum) pairs in tmin, existing minima in tkey (when ne > 0)
+  if ((e = w.tmin.ensure(2 * (cap + 1))) || (e = w.tpos.ensure(n)) || (ne && (e = w.tkey.ensure(cap + 1)))) return e;
   const uint32_t mask = (uint32_t)(cap - 1);
   const uint32_t shift = 64u - (uint32_t)__builtin_ctzll(cap);
-  if ((e = hipMemsetAsync(w.tkey.p, 0xFF, sizeof(uint64_t) * (cap + 1), st)) ||
-      (e = hipMemsetAsync(w.tmin.p, 0xFF, sizeof(uint64_t) * 2 * (cap + 1), st)))
+  if ((e = hipMemsetAsync(w.tmin.p, 0xFF, sizeof(uint64_t) * 2 * (cap + 1), st)) ||
+      (ne && (e = hipMemsetAsync(w.tkey.p, 0xFF, sizeof(uint64_t) * (cap + 1), st))))
     return e;
-  auto* tk = reinterpret_cast<unsigned long long*>(w.tkey.p);
-  auto* tm = reinterpret_cast<unsigned long long*>(w.tmin.p);
+  auto* tab = reinterpret_cast<unsigned long long*>(w.tmin.p);
+  auto* em = ne ? reinterpret_cast<unsigned long long*>(w.tkey.p) : nullptr;
   if (ne)
-    hipLaunchKernelGGL(k_solo_insert, dim3(blocks(ne)), dim3(TB), 0, st, ekeys, nullptr, nullptr, eids, ne, tk, tm,
-                       mask, shift, 1u, nullptr);
-  hipLaunchKernelGGL(k_solo_insert, dim3(blocks(n)), dim3(TB), 0, st, keys, has_key, status, ids, n, tk, tm, mask,
-                     shift, 0u, w.tpos.p);
+    hipLaunchKernelGGL(k_solo_insert, dim3(blocks(ne)), dim3(TB), 0, st, ekeys, nullptr, nullptr, eids, ne, tab, em,
+                       mask, shift, nullptr);
+  hipLaunchKernelGGL(k_solo_insert, dim3(blocks(n)), dim3(TB), 0, st, keys, has_key, status, ids, n, tab,
+                     (unsigned long long*)nullptr, mask, shift, w.tpos.p);
   hipLaunchKernelGGL(k_solo_apply, dim3(blocks(n) < 1024 ? blocks(n) : 1024), dim3(TB), 0, st, ids, w.tpos.p, n,
-                     w.tmin.p, chunk_size ? chunk_size : 100, link, counts);
+                     w.tmin.p, ne ? w.tkey.p : nullptr, chunk_size ? chunk_size : 100, link, counts);
   return hipGetLastError();
 }
 
