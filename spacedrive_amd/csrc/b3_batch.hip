@@ -1319,7 +1319,7 @@ __global__ void __launch_bounds__(256) k_shape_scatter(const uint64_t* __restric
 // may arrive over many launches (streamed windows); k_bigfile_finish merges a
 // file's list once all of it is there.
 
-template <int PF, int MINW, int DIRECT = 0>
+template <int PF, int MINW, int DIRECT = 0, int ROT = 0>
 __global__ void __launch_bounds__(kWG, MINW) k_piece_tree(const uint8_t* __restrict__ blob,
                                                           const PieceDesc* __restrict__ pieces, uint32_t npieces,
                                                           uint32_t* __restrict__ file_nodes) {
@@ -1331,11 +1331,18 @@ __global__ void __launch_bounds__(kWG, MINW) k_piece_tree(const uint8_t* __restr
     const PieceDesc pd = pieces[pi];
     const uint32_t nchunks = (pd.len + CHUNK_LEN - 1) / CHUNK_LEN;
     if (tid < 16) ntask[tid] = 0;
+    // ROT: co-resident workgroups start at different 64-chunk offsets of
+    // their pieces, so the chip's concurrent reads do not all sit at the
+    // same offset of 1 MiB-aligned pieces
+    const uint32_t rot = ROT ? (uint32_t)((pi * 7u * 64u) % nchunks) & ~63u : 0u;
 #pragma unroll 1
-    for (uint32_t s = tid; s < nchunks; s += kWG) {
+    for (uint32_t s0 = tid; s0 < nchunks; s0 += kWG) {
+      uint32_t s = s0 + rot;
+      if (ROT && s >= nchunks) s -= nchunks;
       const uint32_t clen = min(CHUNK_LEN, pd.len - s * CHUNK_LEN);
       uint32_t cv[8];
       if (PF == 8) hash_chunk_ps(blob + pd.off + (uint64_t)s * CHUNK_LEN, clen, pd.j0 + s, false, cv);
+      else if (PF == 2) hash_chunk_diag(blob + pd.off + (uint64_t)s * CHUNK_LEN, clen, pd.j0 + s, false, cv, 2);
       else if (PF == 4) hash_chunk_pp(blob + pd.off + (uint64_t)s * CHUNK_LEN, clen, pd.j0 + s, false, cv);
       else if (PF) hash_chunk_pf(blob + pd.off + (uint64_t)s * CHUNK_LEN, clen, pd.j0 + s, false, cv);
       else hash_chunk(blob + pd.off + (uint64_t)s * CHUNK_LEN, clen, pd.j0 + s, false, cv);
@@ -1733,6 +1740,12 @@ hipError_t piece_hash(const uint8_t* blob, const PieceDesc* pieces, uint32_t npi
     hipLaunchKernelGGL((k_piece_tree<4, 8, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   else if (v == 6)  // 4 with both halves of a line loaded together
     hipLaunchKernelGGL((k_piece_tree<8, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
+  else if (v == 8)  // 4 with per-workgroup rotated chunk order
+    hipLaunchKernelGGL((k_piece_tree<4, 6, 1, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
+  else if (v == 9)  // 6 with per-workgroup rotated chunk order
+    hipLaunchKernelGGL((k_piece_tree<8, 6, 1, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
+  else if (v == 7)  // DIAGNOSTIC (wrong digests): 4's loop without memory reads
+    hipLaunchKernelGGL((k_piece_tree<2, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   else hipLaunchKernelGGL((k_piece_tree<1, 8>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   return hipGetLastError();
 }
