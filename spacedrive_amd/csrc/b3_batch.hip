@@ -1744,7 +1744,18 @@ hipError_t piece_hash(const uint8_t* blob, const PieceDesc* pieces, uint32_t npi
     hipLaunchKernelGGL((k_piece_tree<4, 6, 1, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   else if (v == 9)  // 6 with per-workgroup rotated chunk order
     hipLaunchKernelGGL((k_piece_tree<8, 6, 1, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
-  else if (v == 7)  // DIAGNOSTIC (wrong digests): 4's loop without memory reads
+  else if (v == 10) {  // 4 as a persistent grid (resident workgroups loop over the pieces)
+    static int grid = 0;
+    if (!grid) {
+      int dev = 0, cus = 0, per = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k_piece_tree<4, 6, 1>, kWG, 0);
+      grid = (cus > 0 ? cus : 256) * (per > 0 ? per : 1);
+    }
+    hipLaunchKernelGGL((k_piece_tree<4, 6, 1>), dim3(std::min<uint32_t>(npieces, (uint32_t)grid)), dim3(kWG), 0, st,
+                       blob, pieces, npieces, file_nodes);
+  } else if (v == 7)  // DIAGNOSTIC (wrong digests): 4's loop without memory reads
     hipLaunchKernelGGL((k_piece_tree<2, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   else hipLaunchKernelGGL((k_piece_tree<1, 8>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   return hipGetLastError();
