@@ -158,7 +158,6 @@ def identifier_dedup_distributed(stages, keys, has_key, status, ids, chunk_size=
         return link, int(c[0]), int(c[1])
     rec, slot, starts = stages.combine(keys, has_key, status, ids, world)
     counts = [starts[r + 1] - starts[r] for r in range(world)]
-    frecv, fcounts = (rec, counts) if solo else _exchange(rec, counts, group)
     if existing_keys is not None:
         # collective: every rank passes its (possibly empty) share, or none does
         if existing_keys.numel():
@@ -166,8 +165,21 @@ def identifier_dedup_distributed(stages, keys, has_key, status, ids, chunk_size=
             ecounts = [estarts[r + 1] - estarts[r] for r in range(world)]
         else:
             erec, ecounts = rec.new_empty((0, 2)), [0] * world
-        erecv = erec if solo else _exchange(erec, ecounts, group)[0]
+    if solo:
+        frecv, fcounts = rec, counts
+        erecv = erec if existing_keys is not None else rec.new_empty((0, 2))
+    elif existing_keys is not None:
+        # one counts exchange for both record streams: rank r's pair is
+        # (file records, existing records) bound for r -- one host sync, not two
+        sc = torch.tensor([c for r in range(world) for c in (counts[r], ecounts[r])],
+                          dtype=torch.int64, device=rec.device)
+        rc = torch.empty_like(sc)
+        dist.all_to_all_single(rc, sc, group=group)
+        pairs = rc.view(world, 2).tolist()
+        frecv, fcounts = _exchange(rec, counts, group, recv_counts=[int(a) for a, _ in pairs])
+        erecv = _exchange(erec, ecounts, group, recv_counts=[int(b) for _, b in pairs])[0]
     else:
+        frecv, fcounts = _exchange(rec, counts, group)
         erecv = rec.new_empty((0, 2))
     answer = stages.resolve(frecv, erecv)
     # the answers retrace the file records' route: this rank receives back

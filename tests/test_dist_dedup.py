@@ -29,32 +29,43 @@ def _free_port():
     return p
 
 
-def _gloo_worker(rank, world, port, outdir, seed, n, chunk_size):
+def _gloo_corpus(seed, n, existing_mode):
+    # "full": ~350 existing Objects; "sparse": one, so most ranks' shares are
+    # empty; "none": the caller passes no existing Objects at all
+    keys, has, status, existing = make_corpus(seed, n, n_existing=1 if existing_mode == "sparse" else 300)
+    if existing_mode == "none":
+        existing = existing[:0]
+    return keys, has, status, existing
+
+
+def _gloo_worker(rank, world, port, outdir, seed, n, chunk_size, existing_mode="full"):
     import torch.distributed as dist
 
     from spacedrive_amd.dist_dedup import identifier_dedup_distributed
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
-        keys, has, status, existing = make_corpus(seed, n)
+        keys, has, status, existing = _gloo_corpus(seed, n, existing_mode)
         shards, ex = shard(keys, has, status, existing, world)
         k, h, s, ids = shards[rank]
-        ek, eids = ex[rank]
+        ek, eids = ex[rank] if existing_mode != "none" else (None, None)
         link, created, linked = identifier_dedup_distributed(NumpyStages(), k, h, s, ids, chunk_size, ek, eids)
         np.savez(os.path.join(outdir, f"r{rank}.npz"), link=link.numpy(), created=created, linked=linked)
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,chunk_size", [(1, 100), (2, 100), (4, 7), (3, 1)])
-def test_gloo_protocol_vs_oracle(oracle, world, chunk_size):
+@pytest.mark.parametrize("world,chunk_size,existing_mode", [
+    (1, 100, "full"), (2, 100, "full"), (4, 7, "full"), (3, 1, "full"), (1, 100, "none"), (2, 100, "none"),
+    (3, 100, "sparse")])
+def test_gloo_protocol_vs_oracle(oracle, world, chunk_size, existing_mode):
     import torch.multiprocessing as mp
     seed, n = 1000 + world, 3000
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_gloo_worker, args=(world, _free_port(), d, seed, n, chunk_size), nprocs=world,
-                           join=True, start_method="spawn")
+        mp.start_processes(_gloo_worker, args=(world, _free_port(), d, seed, n, chunk_size, existing_mode),
+                           nprocs=world, join=True, start_method="spawn")
         parts = [np.load(os.path.join(d, f"r{r}.npz")) for r in range(world)]
     got = np.concatenate([p["link"] for p in parts])
-    keys, has, status, existing = make_corpus(seed, n)
+    keys, has, status, existing = _gloo_corpus(seed, n, existing_mode)
     want, wc, wl = oracle.identifier_dedup(keys, has, status, chunk_size, existing)
     assert np.array_equal(got, want)
     for p in parts:  # node-wide totals on every rank
