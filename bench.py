@@ -20,16 +20,21 @@ Other workloads (--workload; reported the same way):
       files); same step as c3 — the dedup shuffle under heavy hitters
 
 Multi-GPU (torchrun): files are sharded, rank r owns global files
-[r*n, (r+1)*n) (c5: files r, r+8, r+16, ... so every GPU sees the corpus'
-mix) — independent units for hashing (no collective), one
-all-to-all exchange for the c3/c5 dedup; value = all ranks'
-files / max-over-ranks time.
+[r*n, (r+1)*n) (c5: the contents of corpus files r, r+8, r+16, ... so every
+GPU sees the corpus' mix; orphan ordinals r*n .. (r+1)*n-1) — independent
+units for hashing (no collective), one all-to-all exchange for the c3/c5
+dedup; value = all ranks' files / max-over-ranks time.
 
 Extra fields: blake3_gbps, roofline (leaf/tree kernel, HIP events on its
 stream, vs HBM peak; plus the VALU roofline the kernel is actually bound by),
-cpu_baseline (rank 0, N=1, c2: the reference's shape — one hashing thread,
-SIMD BLAKE3 — over the whole C2 workload, via the oracle; its keys double as
-a parity check of every GPU key).
+cpu_baseline (rank 0, N=1: the reference's shape — one hashing thread,
+SIMD BLAKE3 — over the whole workload from RAM, via the oracle; its keys
+double as a parity check of every GPU key; plus `reference_faithful`: the
+identifier job's CPU shape over real files, 100-file steps in series with
+cas.rs's reads, on a 200 k-file subset), e2e (c2, rank 0, N=1: the host-facing
+C ABI from a pinned host buffer and from files, timed outside the on-device
+loop; never `value`), parity.dedup (c3/c5 at N=1: every link and both counts
+against the chunked oracle).
 """
 import argparse
 import ctypes
@@ -95,11 +100,12 @@ def files_of(workload, rank, n):
         s, k, _ = S.c3_files(rank * n, (rank + 1) * n)
         return s, k, np.arange(rank * n, (rank + 1) * n, dtype=np.int64)
     if workload == "c5":
-        # a strided share keeps each GPU's mix (40% first copies, 60% Zipf
-        # draws) equal to the whole corpus' at any N <= 8
-        ids = np.arange(n, dtype=np.int64) * C5_STRIDE + rank % C5_STRIDE + (rank // C5_STRIDE) * n * C5_STRIDE
-        cid = S.c5_content_ids_at(ids.astype(np.uint64))
-        return S.c5_sizes_of(cid), S.content_key(S.SEED_C5, cid), ids
+        # a strided share of the corpus keeps each GPU's mix (40% first
+        # copies, 60% Zipf draws) equal to the whole corpus' at any N <= 8;
+        # the orphan ordinals (the job's id order) are contiguous per rank
+        fi = np.arange(n, dtype=np.int64) * C5_STRIDE + rank % C5_STRIDE + (rank // C5_STRIDE) * n * C5_STRIDE
+        cid = S.c5_content_ids_at(fi.astype(np.uint64))
+        return S.c5_sizes_of(cid), S.content_key(S.SEED_C5, cid), np.arange(rank * n, (rank + 1) * n, dtype=np.int64)
     raise ValueError(workload)
 
 
@@ -219,6 +225,84 @@ def sample_parity(gpu_keys, sizes, ckeys, count, seed=1):
             "oracle": "scalar BLAKE3 restatement over the synthetic cas message (oracle/cas_ref.c)"}
 
 
+def e2e_c2(args, eng, torch, dev, d_blob, offs, lens, sizes, gpu_keys):
+    """End-to-end (PCIe- and I/O-inclusive) C2 throughput of the host-facing
+    C ABI on the first `--e2e-files` files, timed outside the on-device loop
+    (it is never `value`):
+      messages_pinned  sdcas_cas_ids_from_messages from a page-locked buffer
+                       (direct DMA per staging slot)
+      files            sdcas_cas_ids over the same files in the page cache
+                       (cas.rs's reads by the library's I/O threads)
+    and, on the same files, the reference-faithful CPU baseline: the
+    identifier job's shape (100-file steps in series; per step the reads on an
+    I/O pool, BLAKE3 on one thread; oracle/cpu_bench.c)."""
+    import shutil
+    import tempfile
+    m = min(int(args.e2e_files), int(lens.size))
+    msg_bytes = int(lens[:m].sum())
+    end = int(offs[m - 1] + lens[m - 1])
+    out = {"workload": f"C2 files [0,{m})", "files": m, "message_bytes": msg_bytes,
+           "io_threads": args.cpu_threads, "staging_bytes_per_slot": 256 << 20}
+    pin = torch.empty(end + 64, dtype=torch.uint8).pin_memory()
+    pin.copy_(d_blob[: end + 64])
+    host = pin.numpy()
+    want = gpu_keys[:m]
+    with type(eng)(device=dev.index, io_threads=args.cpu_threads, staging_bytes=256 << 20) as e:
+        probe = torch.empty(256 << 20, dtype=torch.uint8, device=dev)
+        probe.copy_(pin[: 256 << 20], non_blocking=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(4):
+            probe.copy_(pin[: 256 << 20], non_blocking=True)
+        torch.cuda.synchronize()
+        out["pcie_h2d_pinned_gbps"] = 4 * (256 << 20) / (time.perf_counter() - t0) / 1e9
+        del probe
+        best, got = None, None
+        for _ in range(3):
+            t0 = time.perf_counter()
+            got = e.cas_ids_from_messages(host, offs[:m], lens[:m])
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        out["messages_pinned"] = {"files_per_s": m / best, "gbps": msg_bytes / best / 1e9, "seconds": best,
+                                  "mismatches": int((got != want).sum())}
+        if args.no_faithful:
+            return out
+        root = tempfile.mkdtemp(prefix="sdcas_e2e_", dir=os.environ.get("TMPDIR", "/tmp"))
+        try:
+            paths = []
+            t0 = time.perf_counter()
+            for i in range(m):
+                p = os.path.join(root, f"{i:07d}")
+                o = int(offs[i])
+                with open(p, "wb") as f:
+                    f.write(host[o + 8:o + int(lens[i])])
+                paths.append(p)
+            out["files_written_s"] = time.perf_counter() - t0
+            best = None
+            for _ in range(2):
+                t0 = time.perf_counter()
+                got, st = e.generate_cas_ids(paths, sizes[:m])
+                dt = time.perf_counter() - t0
+                best = dt if best is None else min(best, dt)
+            out["files"] = {"files_per_s": m / best, "gbps": msg_bytes / best / 1e9, "seconds": best,
+                            "mismatches": int((got != want).sum()), "errors": int((st != 0).sum()),
+                            "storage": "page cache (files just written)"}
+            from tests._oracle import load_oracle
+            keys, st, secs, hasher = load_oracle().cpu_faithful(paths, sizes[:m], 100, args.cpu_threads)
+            out["reference_faithful"] = {
+                "value": m / secs, "unit": "files/s", "cores": 1, "io_threads": args.cpu_threads, "kind": "port",
+                "gbps": msg_bytes / secs / 1e9, "seconds": secs, "mismatches": int((keys != want).sum()),
+                "errors": int((st != 0).sum()),
+                "sample": f"C2 files [0,{m}) as files in the page cache: the identifier job's CPU shape — 100-file "
+                          f"steps in series (job/mod.rs:559-673), per step metadata + cas.rs reads on "
+                          f"{args.cpu_threads} I/O threads and {hasher} on ONE thread "
+                          f"(file_identifier/mod.rs:105-147); DB writes excluded",
+                "gpu_same_files_speedup": (m / out["files"]["seconds"]) / (m / secs)}
+        finally:
+            shutil.rmtree(root, ignore_errors=True)
+    return out
+
+
 def c4_assign(sizes, world):
     """largest-first greedy assignment of files to ranks"""
     load = [0] * world
@@ -267,6 +351,8 @@ def run_c4(args, torch, dist, dev, rank, world, distributed):
     window = int(args.window_gib) << 30
     wins = c4_windows(sizes, mine, window)
     eng = Engine(device=dev.index)
+    if args.piece_variant >= 0:
+        assert eng.dev_set_piece_variant(args.piece_variant), args.piece_variant
     s = torch.cuda.Stream(dev)
     sp = s.cuda_stream
     blob = torch.empty(window + (2 << 20), dtype=torch.uint8, device=dev)
@@ -371,6 +457,10 @@ def main():
     ap.add_argument("--c4-total-gib", type=int, default=256)
     ap.add_argument("--window-gib", type=int, default=64)
     ap.add_argument("--c4-cpu-gib", type=int, default=16, help="C4 CPU-baseline sample size")
+    ap.add_argument("--e2e-files", type=int, default=200_000, help="c2: files in the end-to-end / faithful leg")
+    ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-faithful", action="store_true", help="e2e without the page-cache files legs")
+    ap.add_argument("--piece-variant", type=int, default=-1, help="c4: piece kernel variant (-1 default)")
     args = ap.parse_args()
     W = WORKLOADS[args.workload]
 
@@ -534,14 +624,20 @@ def main():
             out["parity"] = parity
         else:
             out["parity"] = sample_parity(gk, sizes, keys, 2000)
-        if dd is not None and args.workload == "c3":
+        if dd is not None:
             from tests._oracle import load_oracle
             link = dd["last"][0].cpu().numpy()
-            # the oracle walks ordinals 0..n-1 in chunks of 100: a contiguous
-            # share only (c5's strided share is checked by tests/test_dist_dedup.py)
+            # the oracle walks ordinals 0..n-1 in chunks of 100 (rank 0's
+            # ordinals at N = 1), over the GPU's keys (checked above)
             want, wc, wl = load_oracle().identifier_dedup(gk, (sizes != 0).astype(np.uint8), None, 100)
             out["parity"]["dedup"] = {"files": n, "link_mismatches": int((link != want).sum()),
-                                      "counts_match": (wc, wl) == (dd["last"][1], dd["last"][2])}
+                                      "counts_match": (wc, wl) == (dd["last"][1], dd["last"][2]),
+                                      "oracle": "chunked restatement of file_identifier/mod.rs:149-254 "
+                                                "(oracle/cas_ref.c)"}
+        if args.workload == "c2" and not args.no_e2e:
+            out["e2e"] = e2e_c2(args, eng, torch, dev, d_blob, offs, lens, sizes, gk)
+            if "cpu_baseline" in out and out["e2e"].get("reference_faithful"):
+                out["cpu_baseline"]["reference_faithful"] = out["e2e"].pop("reference_faithful")
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()

@@ -39,9 +39,21 @@
  *   - Ownership: the caller owns every input and output array; the library
  *     owns device memory, pinned staging and streams inside the context and
  *     retains no caller pointer after a call returns.
- *   - Threading: a context is used by one thread at a time (calls on one
- *     context serialise internally); create one context per worker thread or
- *     wrap calls in spawn_blocking (the C calls block).
+ *   - Threading: calls on one context serialise internally (a mutex on the
+ *     host; on the device, a call's stream waits for the previous call's work
+ *     whatever stream either names, because they share the context's device
+ *     scratch). Use one context per concurrent job for parallelism; the path
+ *     calls block, so wrap them in spawn_blocking.
+ *   - Progress and cancellation (job/worker.rs:35-36,458-480 kill a job that
+ *     reports no progress for 10 minutes; job/mod.rs:862-960 pause/cancel):
+ *     the path calls (sdcas_cas_ids, sdcas_checksums, sdcas_hash_messages,
+ *     sdcas_cas_ids_from_messages) call the context's progress function after
+ *     every staging slot / 1 MiB-piece window completes, with bytes of input
+ *     whose results are final, and stop at the next such point once the
+ *     cancel flag reads nonzero: items already complete keep their results
+ *     and status, every other item gets SDCAS_STATUS_CANCELLED, and the call
+ *     returns SDCAS_E_CANCELLED.
+ *   - Limits: a batch holds at most SDCAS_MAX_BATCH (2^31 - 1) items.
  */
 #ifndef SDCAS_H
 #define SDCAS_H
@@ -59,8 +71,14 @@ extern "C" {
 #define SDCAS_E_OOM (-3)
 #define SDCAS_E_HIP (-4)
 #define SDCAS_E_CAPACITY (-5)
+#define SDCAS_E_CANCELLED (-6)
 
 #define SDCAS_STATUS_UNEXPECTED_EOF 100001
+/* per-item status of an item the call did not complete because it was
+ * cancelled (ECANCELED) */
+#define SDCAS_STATUS_CANCELLED 125
+
+#define SDCAS_MAX_BATCH 0x7FFFFFFF
 
 /* constants of core/src/object/cas.rs:10-15 and validation/hash.rs:9 */
 #define SDCAS_SAMPLE_COUNT 4
@@ -74,10 +92,17 @@ extern "C" {
 
 typedef struct sdcas_ctx sdcas_ctx;
 
+/* Progress report: `done` of `total` bytes of input have final results. Called
+ * on the thread that made the path call. */
+typedef void (*sdcas_progress_fn)(void *user, uint64_t done, uint64_t total);
+
 typedef struct sdcas_options {
   int32_t device;          /* HIP device ordinal (-1: current device) */
   uint32_t io_threads;     /* reader threads for the path APIs (0: 8) */
   uint64_t staging_bytes;  /* pinned host staging per batch (0: 256 MiB) */
+  sdcas_progress_fn progress;      /* may be NULL */
+  void *progress_user;             /* passed to progress */
+  const volatile int32_t *cancel;  /* may be NULL; caller-owned, read atomically: nonzero cancels */
 } sdcas_options;
 
 const char *sdcas_version(void);
@@ -87,6 +112,9 @@ int sdcas_init(const sdcas_options *opts, sdcas_ctx **out_ctx);
 void sdcas_destroy(sdcas_ctx *ctx);
 /* Text of the last library failure on this context ("" if none). */
 const char *sdcas_last_error(const sdcas_ctx *ctx);
+/* Re-bind the progress function and cancel flag (e.g. to the job now using
+ * the context); any of them may be NULL. */
+int sdcas_set_progress(sdcas_ctx *ctx, sdcas_progress_fn progress, void *user, const volatile int32_t *cancel);
 
 /* ---- the reference functions, batched --------------------------------- */
 
@@ -98,7 +126,12 @@ int sdcas_cas_ids(sdcas_ctx *ctx, const char *const *paths, const uint64_t *size
                   uint64_t *out_keys, int32_t *out_status);
 
 /* file_checksum of n files (hash.rs:11-25): BLAKE3 of the whole content.
- * out32 receives 32*n bytes. */
+ * out32 receives 32*n bytes. The content hashed is the file's first L bytes,
+ * L = its length when the call stats it (hash.rs reads to its first short
+ * read, which on a regular local file is EOF): a file that grows while it is
+ * read is hashed over L bytes, and one that shrinks below L before its bytes
+ * are read gets SDCAS_STATUS_UNEXPECTED_EOF (the reference would hash the
+ * shorter content). Neither happens to a file nobody writes meanwhile. */
 int sdcas_checksums(sdcas_ctx *ctx, const char *const *paths, size_t n, uint8_t *out32,
                     int32_t *out_status);
 
@@ -212,6 +245,24 @@ int sdcas_dev_dedup_resolve(sdcas_ctx *ctx, const uint64_t *d_frec, size_t nf, c
 int sdcas_dev_dedup_apply(sdcas_ctx *ctx, const uint64_t *d_ids, const uint32_t *d_slot, size_t n,
                           const int64_t *d_result, size_t chunk_size, int64_t *d_link, uint64_t *d_counts,
                           void *stream);
+/* The same two stages without any host synchronisation, for RCCL's
+ * all-to-all with equal splits (spacedrive_amd/dist_dedup.py): the combine
+ * writes owner r's records to bucket r of d_send (world x cap records of 16 B,
+ * record p of bucket r at d_send[2 * (r * cap + p)]), d_counts[r] (device
+ * int64) = its valid records, d_slot[i] = the bucket position r * cap + p of
+ * file i's record, and sets *d_overflow (device u32) to 1 when some owner has
+ * more than cap records (the buckets are then unusable: rerun the exact
+ * stages). resolve_buckets answers the received buckets (world x fcap file
+ * records, world x ecap existing records, the first d_fcounts[r] /
+ * d_ecounts[r] of bucket r valid) into d_result[world * fcap], bucket layout;
+ * apply then reads the answers returned in the same layout. */
+int sdcas_dev_dedup_combine_buckets(sdcas_ctx *ctx, const uint64_t *d_keys, const uint8_t *d_has_key,
+                                    const int32_t *d_status, const uint64_t *d_ids, size_t n, uint32_t world,
+                                    size_t cap, uint64_t *d_send, uint32_t *d_slot, int64_t *d_counts,
+                                    uint32_t *d_overflow, void *stream);
+int sdcas_dev_dedup_resolve_buckets(sdcas_ctx *ctx, const uint64_t *d_frec, size_t fcap, const int64_t *d_fcounts,
+                                    const uint64_t *d_erec, size_t ecap, const int64_t *d_ecounts, uint32_t world,
+                                    int64_t *d_result, void *stream);
 /* A world of one: the three stages without the combine (nothing is
  * exchanged, so files and existing Objects go straight into resolve's table):
  * the same d_link / d_counts as combine -> resolve -> apply. d_ekeys/d_eids

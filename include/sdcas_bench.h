@@ -22,7 +22,9 @@ int sdcas_dev_synth_cas_messages(sdcas_ctx *ctx, const uint64_t *d_keys, const u
 int sdcas_dev_synth_content(sdcas_ctx *ctx, const uint64_t *d_keys, const uint64_t *d_starts,
                             const uint64_t *d_lens, const uint64_t *d_offs, size_t n, uint8_t *d_blob,
                             void *stream);
-/* device-resident dedup (keys etc. are device pointers; d_counts: 2 x u64). */
+/* device-resident dedup of a whole job in file order, no existing Objects
+ * (keys etc. are device pointers; d_counts: 2 x u64, overwritten): the
+ * single-rank path of sdcas_dev_dedup_local with ids 0..n-1. */
 int sdcas_dev_dedup(sdcas_ctx *ctx, const uint64_t *d_keys, const uint8_t *d_has_key,
                     const int32_t *d_status, size_t n, size_t chunk_size, int64_t *d_out_link,
                     uint64_t *d_counts, void *stream);
@@ -34,9 +36,14 @@ int sdcas_dev_dedup(sdcas_ctx *ctx, const uint64_t *d_keys, const uint8_t *d_has
 int sdcas_dev_profile(sdcas_ctx *ctx, int enable);
 int sdcas_dev_last_kernel_ms(sdcas_ctx *ctx, float *leaf_ms, float *total_ms);
 
-/* Tuning: select the leaf/tree kernel variant (-1 = default). Returns the
- * number of variants. */
+/* Tuning: select the leaf/tree kernel variant (-1 = default). Returns
+ * SDCAS_OK, or SDCAS_E_INVALID (selection unchanged) for a variant this
+ * build does not hold: libsdcas.so holds only the bit-exact product kernels;
+ * the ablation build (libsdcas_ablate.so, tools only) holds all of them. */
 int sdcas_dev_set_leaf_variant(sdcas_ctx *ctx, int variant);
+/* Tuning: select the 1 MiB-piece kernel variant of the checksum path (-1 =
+ * default); same return convention. */
+int sdcas_dev_set_piece_variant(sdcas_ctx *ctx, int variant);
 /* Tuning: hash messages in length-sorted slot order (1, default) or in caller
  * order (0). Results are identical either way. */
 int sdcas_dev_set_sort(sdcas_ctx *ctx, int enable);

@@ -79,6 +79,12 @@ class Engine {
     int device = -1;             // HIP device ordinal, -1: current
     uint32_t io_threads = 0;     // reader threads (0: library default)
     uint64_t staging_bytes = 0;  // pinned staging per slot (0: library default)
+    // progress / cancellation of the batch calls (sdcas.h "Conventions"): the
+    // job's progress hook (job/worker.rs:458-480) and its cancel command
+    // (job/mod.rs:862-960)
+    sdcas_progress_fn progress = nullptr;
+    void* progress_user = nullptr;
+    const volatile int32_t* cancel = nullptr;
   };
   static std::unique_ptr<Engine> open(const Options& opts);
   static std::unique_ptr<Engine> open() { return open(Options{}); }

@@ -88,6 +88,18 @@ int oracle_cpu_bench_files(const uint64_t *keys, const uint64_t *sizes, size_t n
                            int prefer_upstream, uint64_t *out_keys, uint64_t *bytes, double *secs, int *kind,
                            char *version_out);
 
+/* every cas key of n synthetic files (the -m gpu corpus tests' checker), on
+ * `threads` threads; returns 1 if upstream SIMD BLAKE3 hashed, 0 scalar */
+int oracle_synth_cas_keys_mt(const uint64_t *keys, const uint64_t *sizes, size_t n, int threads, int prefer_upstream,
+                             uint64_t *out_keys);
+/* bench.py's reference-faithful CPU baseline: the identifier job's CPU shape
+ * over real files (steps of `chunk` files in series; per step an I/O pool of
+ * io_threads does metadata + cas.rs reads, one thread hashes in file order).
+ * secs[0] = wall time; out_status[i] = errno / UnexpectedEof or 0. */
+int oracle_cpu_faithful(const char *const *paths, const uint64_t *sizes, size_t n, size_t chunk, int io_threads,
+                        int prefer_upstream, uint64_t *out_keys, int32_t *out_status, double *secs, int *kind,
+                        char *version_out);
+
 /* periodic.c: BLAKE3 of messages whose content repeats with a period of 2^k
  * chunks (the >= 4 TiB checksum fixture); upstream = hash each period with
  * llvm_blake3_compress_subtree_wide (1.8.2) instead of the scalar oracle */

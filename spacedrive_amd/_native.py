@@ -3,12 +3,17 @@
 The library is the product: every hash and every dedup result comes from its
 HIP kernels. Importing this module without the built library, or calling it
 without a GPU, raises — there is no CPU fallback.
+
+`use_ablation_library()` (tools/ab_leaf.py only) binds libsdcas_ablate.so
+instead: the same sources built with every A/B kernel variant, including
+diagnostic ones that produce wrong digests. Nothing in the package calls it.
 """
 import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsdcas.so")
+ABLATION_LIB_PATH = os.path.join(_HERE, "libsdcas_ablate.so")
 
 SDCAS_OK = 0
 SDCAS_E_NO_DEVICE = -1
@@ -16,7 +21,10 @@ SDCAS_E_INVALID = -2
 SDCAS_E_OOM = -3
 SDCAS_E_HIP = -4
 SDCAS_E_CAPACITY = -5
+SDCAS_E_CANCELLED = -6
 SDCAS_STATUS_UNEXPECTED_EOF = 100001
+SDCAS_STATUS_CANCELLED = 125
+SDCAS_MAX_BATCH = 0x7FFFFFFF
 
 # every entry point include/sdcas.h and include/sdcas_bench.h declare
 ABI_SYMBOLS = [
@@ -24,10 +32,12 @@ ABI_SYMBOLS = [
     "sdcas_checksums", "sdcas_hash_messages", "sdcas_cas_ids_from_messages", "sdcas_dev_reserve",
     "sdcas_dev_hash_messages", "sdcas_dev_sync", "sdcas_dedup", "sdcas_key_to_hex",
     "sdcas_digest_to_hex", "sdcas_cas_message_len", "sdcas_dev_dedup_combine", "sdcas_dev_dedup_resolve",
-    "sdcas_dev_dedup_apply", "sdcas_dev_dedup_local", "sdcas_dev_stream_begin", "sdcas_dev_stream_update", "sdcas_dev_stream_finish",
+    "sdcas_dev_dedup_apply", "sdcas_dev_dedup_local", "sdcas_dev_dedup_combine_buckets",
+    "sdcas_dev_dedup_resolve_buckets", "sdcas_dev_stream_begin", "sdcas_dev_stream_update",
+    "sdcas_dev_stream_finish", "sdcas_set_progress",
     # bench / test plumbing
     "sdcas_dev_synth_cas_messages", "sdcas_dev_synth_content", "sdcas_dev_dedup", "sdcas_dev_profile",
-    "sdcas_dev_last_kernel_ms", "sdcas_dev_set_leaf_variant", "sdcas_dev_set_sort",
+    "sdcas_dev_last_kernel_ms", "sdcas_dev_set_leaf_variant", "sdcas_dev_set_piece_variant", "sdcas_dev_set_sort",
 ]
 
 
@@ -37,12 +47,37 @@ class SdcasError(RuntimeError):
         self.code = code
 
 
+class Cancelled(SdcasError):
+    """SDCAS_E_CANCELLED: the call stopped at the cancel flag. `partial` holds
+    what the call returns normally (results and per-item status); items with
+    status SDCAS_STATUS_CANCELLED were not completed, the others are final."""
+
+    def __init__(self, msg, partial=None):
+        super().__init__(SDCAS_E_CANCELLED, msg)
+        self.partial = partial
+
+
+# void (*)(void* user, uint64_t done, uint64_t total)
+PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64)
+
+
 class Options(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("io_threads", ctypes.c_uint32),
-                ("staging_bytes", ctypes.c_uint64)]
+                ("staging_bytes", ctypes.c_uint64), ("progress", PROGRESS_FN),
+                ("progress_user", ctypes.c_void_p), ("cancel", ctypes.POINTER(ctypes.c_int32))]
 
 
 _lib = None
+_lib_path = LIB_PATH
+
+
+def use_ablation_library():
+    """Bind libsdcas_ablate.so (A/B tools only; see the module docstring).
+    Must be called before the first load()."""
+    global _lib_path
+    if _lib is not None and _lib_path != ABLATION_LIB_PATH:
+        raise RuntimeError("libsdcas.so is already loaded in this process")
+    _lib_path = ABLATION_LIB_PATH
 
 _vp = ctypes.c_void_p
 _sz = ctypes.c_size_t
@@ -63,10 +98,10 @@ def load():
         import torch  # noqa: F401
     except ImportError:
         pass
-    if not os.path.exists(LIB_PATH):
-        raise ImportError(f"{LIB_PATH} is not built: run `make -C spacedrive_amd/csrc` "
+    if not os.path.exists(_lib_path):
+        raise ImportError(f"{_lib_path} is not built: run `make -C spacedrive_amd/csrc` "
                           "(or __graft_entry__.build()) — there is no CPU fallback")
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(_lib_path)
     L.sdcas_version.restype = ctypes.c_char_p
     L.sdcas_init.argtypes = [ctypes.POINTER(Options), ctypes.POINTER(_vp)]
     L.sdcas_destroy.argtypes = [_vp]
@@ -91,7 +126,12 @@ def load():
     L.sdcas_dev_last_kernel_ms.argtypes = [_vp, ctypes.POINTER(ctypes.c_float),
                                            ctypes.POINTER(ctypes.c_float)]
     L.sdcas_dev_set_leaf_variant.argtypes = [_vp, ctypes.c_int]
+    L.sdcas_dev_set_piece_variant.argtypes = [_vp, ctypes.c_int]
     L.sdcas_dev_set_sort.argtypes = [_vp, ctypes.c_int]
+    L.sdcas_set_progress.argtypes = [_vp, PROGRESS_FN, _vp, ctypes.POINTER(ctypes.c_int32)]
+    L.sdcas_dev_dedup_combine_buckets.argtypes = [_vp, _vp, _vp, _vp, _vp, _sz, ctypes.c_uint32, _sz, _vp, _vp,
+                                                  _vp, _vp, _vp]
+    L.sdcas_dev_dedup_resolve_buckets.argtypes = [_vp, _vp, _sz, _vp, _vp, _sz, _vp, ctypes.c_uint32, _vp, _vp]
     L.sdcas_dev_dedup_combine.argtypes = [_vp, _vp, _vp, _vp, _vp, _sz, ctypes.c_uint32, _vp, _vp, _vp, _vp]
     L.sdcas_dev_dedup_resolve.argtypes = [_vp, _vp, _sz, _vp, _sz, _vp, _vp]
     L.sdcas_dev_dedup_apply.argtypes = [_vp, _vp, _vp, _sz, _vp, _sz, _vp, _vp, _vp]

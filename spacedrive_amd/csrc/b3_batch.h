@@ -20,7 +20,7 @@ struct BatchWorkspace {
   uint32_t cap_msgs = 0;
   uint64_t cap_chunks = 0;  // chunks a batch of up to cap_msgs messages may hold
   uint64_t cap_slots = 0;   // slots the workspace holds (chunks + the quad layout's padding)
-  int variant = -1;  // leaf kernel variant (-1: default / SDCAS_LEAF_VARIANT)
+  int variant = -1;  // leaf kernel variant (-1: default / SDCAS_LEAF_VARIANT; unavailable ones: default)
   // length-sorted slot order (messages of equal length share waves, so the
   // lanes of a wave run the same number of blocks): perm[slot-order index] =
   // caller index; soffs/slens = offsets/lengths in slot order
@@ -34,6 +34,8 @@ struct BatchWorkspace {
 size_t batch_scan_temp_bytes(uint32_t max_msgs);
 int leaf_variant();
 int leaf_variant_count();
+bool leaf_variant_available(int v);  // compiled into this build (the diagnostic ones never are in libsdcas.so)
+bool piece_variant_available(int v);
 
 // Hash n messages (blob + offs[i], lens[i] bytes; offsets 16-byte aligned),
 // all pointers device pointers. Writes 32-byte digests to out32 and/or cas
@@ -59,8 +61,10 @@ struct FileDesc {
 inline uint64_t bigfile_node_count(uint64_t C) {
   return C / kTile + (uint64_t)__builtin_popcountll(C % kTile);
 }
+// ctr: one u32 of device scratch (the persistent variants' piece counter);
+// variant: piece kernel variant (-1: default / SDCAS_PIECE_VARIANT)
 hipError_t piece_hash(const uint8_t* blob, const PieceDesc* pieces, uint32_t npieces, uint32_t* file_nodes,
-                      hipStream_t st);
+                      uint32_t* ctr, int variant, hipStream_t st);
 hipError_t bigfile_finish(const FileDesc* files, uint32_t nfiles, const uint32_t* file_nodes, uint8_t* out32,
                           hipStream_t st);
 

@@ -31,6 +31,12 @@
 // aligned power-of-two subtrees are tree nodes, and the stack merge (merge
 // while the stack is longer than popcount(chunks so far), then fold
 // right-to-left) reassembles them in the crate's order.
+//
+// Only bit-exact, GPU-tested kernels are compiled into libsdcas.so. The
+// layouts and block loops that lost round 1's A/B runs (and two diagnostic
+// loops that skip memory reads or compressions, i.e. produce wrong digests)
+// live in b3_ablate_*.inc and are compiled only with -DSDCAS_ABLATIONS into
+// libsdcas_ablate.so, which only tools/ab_leaf.py loads.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
@@ -84,48 +90,6 @@ __global__ void k_tile_first(const uint64_t* __restrict__ lens, const uint64_t* 
   for (uint64_t t = (s0 + kTile - 1) / kTile; t * kTile < s0 + C && t * kTile < cap_chunks; ++t) tile_first[t] = m;
 }
 
-// Hash one chunk (`clen` bytes at p, 0 <= clen <= 1024) with chunk counter j.
-__device__ __forceinline__ void hash_chunk(const uint8_t* __restrict__ p, uint32_t clen, uint64_t j, bool root,
-                                           uint32_t (&cv)[8]) {
-  set_iv(cv);
-  const uint32_t nb = clen == 0 ? 1 : (clen + BLOCK_LEN - 1) / BLOCK_LEN;
-#pragma unroll 1
-  for (uint32_t b = 0; b < nb; ++b) {
-    const uint32_t blen = min(BLOCK_LEN, clen - b * BLOCK_LEN);
-    uint32_t m[16];
-    load_full_block(p + b * BLOCK_LEN, m);
-    if (blen < BLOCK_LEN) mask_tail(m, blen);
-    const uint32_t flags = (b == 0 ? CHUNK_START : 0u) | (b + 1 == nb ? (CHUNK_END | (root ? ROOT : 0u)) : 0u);
-    compress(cv, m, j, blen, flags);
-  }
-}
-
-// Same, with the next block's loads issued before the current block is
-// compressed (software pipelining: one 64-byte block per lane in flight while
-// the VALU works). The load address is clamped to the chunk's last block, so
-// the final iteration re-reads it harmlessly instead of running off the end.
-template <bool NT = false>
-__device__ __forceinline__ void hash_chunk_pf(const uint8_t* __restrict__ p, uint32_t clen, uint64_t j, bool root,
-                                              uint32_t (&cv)[8]) {
-  set_iv(cv);
-  const uint32_t nb = clen == 0 ? 1 : (clen + BLOCK_LEN - 1) / BLOCK_LEN;
-  uint32_t m[16];
-  if (NT) load_full_block_nt(p, m);
-  else load_full_block(p, m);
-#pragma unroll 1
-  for (uint32_t b = 0; b < nb; ++b) {
-    uint32_t nx[16];
-    if (NT) load_full_block_nt(p + min(b + 1, nb - 1) * BLOCK_LEN, nx);
-    else load_full_block(p + min(b + 1, nb - 1) * BLOCK_LEN, nx);
-    const uint32_t blen = min(BLOCK_LEN, clen - b * BLOCK_LEN);
-    if (blen < BLOCK_LEN) mask_tail(m, blen);
-    const uint32_t flags = (b == 0 ? CHUNK_START : 0u) | (b + 1 == nb ? (CHUNK_END | (root ? ROOT : 0u)) : 0u);
-    compress(cv, m, j, blen, flags);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) m[i] = nx[i];
-  }
-}
-
 // Same, unrolled by two blocks with ping-pong message registers (no
 // register copies between blocks; block b+1's loads fly while b compresses).
 __device__ __forceinline__ void hash_chunk_pp(const uint8_t* __restrict__ p, uint32_t clen, uint64_t j, bool root,
@@ -149,85 +113,6 @@ __device__ __forceinline__ void hash_chunk_pp(const uint8_t* __restrict__ p, uin
       if (blen < BLOCK_LEN) mask_tail(m1, blen);
       compress(cv, m1, j, blen, b + 2 == nb ? endf : 0u);
     }
-  }
-}
-
-// Same, two blocks of prefetch distance (three rotating message register
-// sets, unrolled by three): block b+2's loads fly while b compresses.
-#define B3_PF2_STEP(cur, nxt_blk)                                                              \
-  {                                                                                            \
-    const uint32_t blen = min(BLOCK_LEN, clen - b * BLOCK_LEN);                                \
-    if (blen < BLOCK_LEN) mask_tail(cur, blen);                                                \
-    compress(cv, cur, j, blen, (b == 0 ? CHUNK_START : 0u) | (b + 1 == nb ? endf : 0u));       \
-    if (++b >= nb) break;                                                                      \
-    load_full_block(p + min(nxt_blk, nb - 1) * BLOCK_LEN, cur);                                \
-  }
-__device__ __forceinline__ void hash_chunk_pf2(const uint8_t* __restrict__ p, uint32_t clen, uint64_t j, bool root,
-                                               uint32_t (&cv)[8]) {
-  set_iv(cv);
-  const uint32_t nb = clen == 0 ? 1 : (clen + BLOCK_LEN - 1) / BLOCK_LEN;
-  const uint32_t endf = CHUNK_END | (root ? ROOT : 0u);
-  uint32_t x[16], y[16], z[16];
-  load_full_block(p, x);
-  load_full_block(p + min(1u, nb - 1) * BLOCK_LEN, y);
-  load_full_block(p + min(2u, nb - 1) * BLOCK_LEN, z);
-  uint32_t b = 0;
-#pragma unroll 1
-  for (;;) {
-    B3_PF2_STEP(x, b + 2)
-    B3_PF2_STEP(y, b + 2)
-    B3_PF2_STEP(z, b + 2)
-  }
-}
-#undef B3_PF2_STEP
-
-// Same, loading 128 bytes (two blocks, one L2 line of a 128-byte aligned
-// chunk) per step into one register set while the previous pair compresses.
-// The pair load at an odd last block is cut to 64 bytes so nothing past the
-// guaranteed 64-byte tail is read.
-__device__ __forceinline__ void load_pair(const uint8_t* p, uint32_t b, uint32_t nb, uint32_t (&m)[32]) {
-  const uint4* q = reinterpret_cast<const uint4*>(p + b * BLOCK_LEN);
-  uint4 r[8];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) r[i] = q[i];
-  if (b + 1 < nb) {
-#pragma unroll
-    for (int i = 4; i < 8; ++i) r[i] = q[i];
-  } else {
-#pragma unroll
-    for (int i = 4; i < 8; ++i) r[i] = r[i - 4];
-  }
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    m[4 * i] = r[i].x; m[4 * i + 1] = r[i].y; m[4 * i + 2] = r[i].z; m[4 * i + 3] = r[i].w;
-  }
-}
-__device__ __forceinline__ void hash_chunk_pair(const uint8_t* __restrict__ p, uint32_t clen, uint64_t j, bool root,
-                                                uint32_t (&cv)[8]) {
-  set_iv(cv);
-  const uint32_t nb = clen == 0 ? 1 : (clen + BLOCK_LEN - 1) / BLOCK_LEN;
-  const uint32_t endf = CHUNK_END | (root ? ROOT : 0u);
-  uint32_t cur[32];
-  load_pair(p, 0, nb, cur);
-#pragma unroll 1
-  for (uint32_t b = 0; b < nb; b += 2) {
-    uint32_t nx[32];
-    load_pair(p, min(b + 2, (nb - 1) & ~1u), nb, nx);
-    uint32_t m[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) m[i] = cur[i];
-    uint32_t blen = min(BLOCK_LEN, clen - b * BLOCK_LEN);
-    if (blen < BLOCK_LEN) mask_tail(m, blen);
-    compress(cv, m, j, blen, (b == 0 ? CHUNK_START : 0u) | (b + 1 == nb ? endf : 0u));
-    if (b + 1 < nb) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) m[i] = cur[16 + i];
-      blen = min(BLOCK_LEN, clen - (b + 1) * BLOCK_LEN);
-      if (blen < BLOCK_LEN) mask_tail(m, blen);
-      compress(cv, m, j, blen, b + 2 == nb ? endf : 0u);
-    }
-#pragma unroll
-    for (int i = 0; i < 32; ++i) cur[i] = nx[i];
   }
 }
 
@@ -258,25 +143,30 @@ __device__ __forceinline__ void hash_chunk_ps(const uint8_t* __restrict__ p, uin
   }
 }
 
-// DIAGNOSTIC ONLY (wrong digests, never the default): PF=2 compresses
-// register-made blocks without touching memory (pure VALU rate); PF=3 streams
-// the chunk's blocks and folds them with XOR, no compression (pure load rate).
-__device__ __forceinline__ void hash_chunk_diag(const uint8_t* __restrict__ p, uint32_t clen, uint64_t j, bool root,
-                                                uint32_t (&cv)[8], int mode) {
-  set_iv(cv);
-  const uint32_t nb = clen == 0 ? 1 : (clen + BLOCK_LEN - 1) / BLOCK_LEN;
-#pragma unroll 1
-  for (uint32_t b = 0; b < nb; ++b) {
-    uint32_t m[16];
-    if (mode == 2) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) m[i] = (uint32_t)(uintptr_t)p + b * 64 + i;
-      compress(cv, m, j, 64, b == 0 ? CHUNK_START : 0u);
-    } else if (mode == 3) {
-      load_full_block(p + b * BLOCK_LEN, m);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) cv[i & 7] ^= m[i];
-    }
+#ifdef SDCAS_ABLATIONS
+#include "b3_ablate_loops.inc"
+#endif
+
+// Block loop of a leaf chunk: PF 8 = hash_chunk_ps (default), 4 =
+// hash_chunk_pp; any other PF names an ablation loop.
+template <int PF>
+__device__ __forceinline__ void leaf_hash(const uint8_t* __restrict__ p, uint32_t clen, uint64_t j, bool root,
+                                          uint32_t (&cv)[8]) {
+  if constexpr (PF == 8) {
+    hash_chunk_ps(p, clen, j, root, cv);
+  } else if constexpr (PF == 4) {
+    hash_chunk_pp(p, clen, j, root, cv);
+  } else {
+#ifdef SDCAS_ABLATIONS
+    if constexpr (PF == 6) hash_chunk_pf2(p, clen, j, root, cv);
+    else if constexpr (PF == 7) hash_chunk_pair(p, clen, j, root, cv);
+    else if constexpr (PF == 5) hash_chunk_pf<true>(p, clen, j, root, cv);
+    else if constexpr (PF >= 2) hash_chunk_diag(p, clen, j, root, cv, PF);
+    else if constexpr (PF == 1) hash_chunk_pf(p, clen, j, root, cv);
+    else hash_chunk(p, clen, j, root, cv);
+#else
+    static_assert(PF == 8 || PF == 4, "ablation block loops need -DSDCAS_ABLATIONS");
+#endif
   }
 }
 
@@ -370,7 +260,7 @@ __device__ __forceinline__ void leaf_order(uint32_t tid, const uint32_t (&bin)[k
   __syncthreads();
 }
 
-template <int WG, int PF, int TR = 1, int STAGGER = 0, int PRIO = 0, int ORD = 0, int DYN = 0>
+template <int WG, int PF, int TR = 1, int ORD = 0, int DYN = 0>
 __global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ offs,
                                                    const uint64_t* __restrict__ lens, uint32_t n,
                                                    const uint64_t* __restrict__ S,
@@ -390,16 +280,6 @@ __global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __
   if (total > cap_chunks) return;  // reported by sdcas_dev_sync
   const uint64_t ntiles = (total + kTile - 1) / kTile;
   const uint32_t tid = threadIdx.x;
-  if (STAGGER) {
-    // Co-resident workgroups run identical tiles in lockstep, so their
-    // barrier-bound tree phases coincide and leave the CU's SIMDs idle.
-    // Offset them once by a fraction of a tile (speed only).
-    const uint32_t phase = (blockIdx.x / (gridDim.x / (STAGGER ? STAGGER : 1))) % (STAGGER ? STAGGER : 1);
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    const uint64_t wait = (uint64_t)phase * 25000 / STAGGER;  // 100 MHz ticks: ~250 us per tile
-    while (__builtin_amdgcn_s_memrealtime() - t0 < wait) __builtin_amdgcn_s_sleep(100);
-  }
-
   // DYN: tiles after the first are handed out by a global counter (total_p[2],
   // zeroed by k_tile_first) instead of round-robin, so a workgroup that drew
   // cheap tiles takes more and the grid drains within about one tile; the
@@ -498,14 +378,7 @@ __global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __
       const uint32_t clen = len == 0 ? 0u : (uint32_t)min<uint64_t>(CHUNK_LEN, len - j * CHUNK_LEN);
       const bool root = (C == 1);
       uint32_t cv[8];
-      if (PF == 8) hash_chunk_ps(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
-      else if (PF == 6) hash_chunk_pf2(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
-      else if (PF == 7) hash_chunk_pair(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
-      else if (PF == 4) hash_chunk_pp(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
-      else if (PF == 5) hash_chunk_pf<true>(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
-      else if (PF >= 2) hash_chunk_diag(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv, PF);
-      else if (PF) hash_chunk_pf(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
-      else hash_chunk(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
+      leaf_hash<PF>(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
       if (root) {
         store_digest(perm ? perm[m] : m, cv, out32, out_keys);
       } else {
@@ -514,9 +387,12 @@ __global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __
       }
     }
     __syncthreads();
+    // the next tile, read between two barriers: thread 0 overwrites next_tile
+    // only after this tile's last barrier, which every thread has passed the
+    // read by then
+    const uint64_t nt = DYN ? next_tile : tile + gridDim.x;
 
     // (3) the tree, level by level: every task of a level is independent
-    if (PRIO) __builtin_amdgcn_s_setprio(PRIO);  // the few tree waves gate the barrier: let them issue first
     for (uint32_t k = 1; TR && k <= 10; ++k) {
       const uint32_t T = ntask[k];
       if (T == 0) continue;
@@ -542,7 +418,6 @@ __global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __
       }
       __syncthreads();
     }
-    if (PRIO) __builtin_amdgcn_s_setprio(0);
 
     // (4) messages crossing a tile boundary: their maximal in-tile nodes go to
     // HBM at their first slot, for k_finish
@@ -561,242 +436,9 @@ __global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __
       o[1] = make_uint4(cvs[s][4], cvs[s][5], cvs[s][6], cvs[s][7]);
     }
     __syncthreads();
-    tile = DYN ? next_tile : tile + gridDim.x;
+    tile = nt;
   }
 }
-
-// k_leaf_slim: k_leaf_tree's algorithm with a 39 KB LDS image, so four
-// 512-thread workgroups (8 waves per SIMD) fit in a CU's 160 KB when the
-// kernel also fits 64 VGPRs (__launch_bounds__ MINW = 8):
-//   * message starts relative to the tile as u16 (a message other than the
-//     tile's first starts inside it: 1..1024); the first message's start is
-//     the uniform S[m0];
-//   * tree tasks as u16 (left slot | ROOT << 15): the right child of a level-k
-//     task is always 2^(k-1) slots further and a root's message is the owner
-//     of its left slot; tasks are counted per level first, then written
-//     compacted (a tile holds at most kTile - 1 parent compressions).
-constexpr uint16_t kTaskRoot = 0x8000;
-
-template <int WG, int PF, int MINW, int ORD = 0, int DYN = 0>
-__global__ void __launch_bounds__(WG, MINW) k_leaf_slim(const uint8_t* __restrict__ blob,
-                                                        const uint64_t* __restrict__ offs,
-                                                        const uint64_t* __restrict__ lens, uint32_t n,
-                                                        const uint64_t* __restrict__ S,
-                                                        const uint32_t* __restrict__ tile_first,
-                                                        const uint64_t* __restrict__ total_p, uint64_t cap_chunks,
-                                                        uint32_t* __restrict__ nodes, uint8_t* __restrict__ out32,
-                                                        uint64_t* __restrict__ out_keys,
-                                                        const uint32_t* __restrict__ perm) {
-  __shared__ uint32_t cvs[kTile][8];
-  __shared__ uint16_t srel[kTile + 2];
-  __shared__ uint16_t smsg[kTile];
-  __shared__ uint16_t task[kTile];
-  __shared__ uint32_t ntask[12], tbase_k[12];
-  // ORD: leaf order by block count (slots whose chunks have the same number
-  // of blocks share waves, so a partial last chunk does not idle 63 lanes)
-  __shared__ uint16_t order[ORD ? kTile : 1];
-  __shared__ uint32_t obin[ORD ? 17 : 1];
-  __shared__ uint64_t next_tile;  // DYN: k_leaf_tree's global tile counter
-
-  const uint64_t total = *total_p;
-  if (total > cap_chunks) return;
-  const uint64_t ntiles = (total + kTile - 1) / kTile;
-  const uint32_t tid = threadIdx.x;
-  unsigned long long* tile_ctr = reinterpret_cast<unsigned long long*>(const_cast<uint64_t*>(total_p) + 2);
-
-  for (uint64_t tile = blockIdx.x; tile < ntiles;) {
-    const uint64_t tbase = tile * kTile;
-    const uint32_t m0 = tile_first[tile];
-    const uint32_t m1 = (tile + 1 < ntiles) ? tile_first[tile + 1] : n - 1;
-    const uint32_t cnt = m1 - m0 + 1;  // <= kTile + 1
-    const uint64_t lead = tbase - S[m0];  // chunks of the first message before this tile
-    for (uint32_t i = tid + 1; i < cnt; i += WG) srel[i] = (uint16_t)(S[m0 + i] - tbase);
-    if (tid < 12) ntask[tid] = 0;
-    if (ORD && tid < 17) obin[tid] = 0;
-    if (DYN && tid == 0) next_tile = gridDim.x + atomicAdd(tile_ctr, 1ull);
-    __syncthreads();
-
-    // (1a) slot -> message; count the tree tasks of every level
-#pragma unroll 1
-    for (uint32_t s = tid; s < kTile; s += WG) {
-      if (tbase + s >= total) {
-        smsg[s] = kNoMsg;
-        continue;
-      }
-      uint32_t lo = 0, hi = cnt - 1;  // last message starting at or before slot s
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi + 1) >> 1;
-        if (srel[mid] <= s) lo = mid;
-        else hi = mid - 1;
-      }
-      smsg[s] = (uint16_t)lo;
-      const uint64_t j = lo ? (uint64_t)(s - srel[lo]) : lead + s;
-      const uint64_t len = lens[m0 + lo];
-      const uint64_t C = chunk_count(len);
-      if (ORD) atomicAdd(&obin[leaf_bin(len, j)], 1u);
-      if (C == 1) continue;
-      const uint32_t K = node_level(j, C, s);
-      for (uint32_t k = 1; k <= K; ++k) atomicAdd(&ntask[k], 1u);
-      // a message lying wholly in the tile starts here: its spine steps
-      if (j == 0 && (lo || lead == 0) && s + C <= kTile) {
-        const uint32_t c = (uint32_t)C;
-        if (!(c & (c - 1))) {
-          atomicAdd(&ntask[31 - __clz(c)], 1u);
-        } else {
-          uint32_t rem = c & (c - 1);  // the lowest part is not a step of its own
-          while (rem) {
-            const uint32_t part = rem & (0u - rem);
-            atomicAdd(&ntask[32 - __clz(part)], 1u);
-            rem -= part;
-          }
-        }
-      }
-    }
-    __syncthreads();
-    if (tid == 0) {
-      uint32_t acc = 0;
-      for (int k = 1; k <= 10; ++k) {
-        tbase_k[k] = acc;
-        acc += ntask[k];
-        ntask[k] = 0;
-      }
-      tbase_k[11] = acc;
-      if (ORD) {
-        uint32_t o = 0;
-        for (int b = 0; b < 17; ++b) {
-          const uint32_t c = obin[b];
-          obin[b] = o;
-          o += c;
-        }
-      }
-    }
-    __syncthreads();
-    // (1b) write the tasks, compacted by level
-#pragma unroll 1
-    for (uint32_t s = tid; s < kTile; s += WG) {
-      const uint32_t mi = smsg[s];
-      if (mi == kNoMsg) continue;
-      const uint64_t j = mi ? (uint64_t)(s - srel[mi]) : lead + s;
-      const uint64_t len1 = lens[m0 + mi];
-      const uint64_t C = chunk_count(len1);
-      if (ORD) order[atomicAdd(&obin[leaf_bin(len1, j)], 1u)] = (uint16_t)s;
-      if (C == 1) continue;
-      const uint32_t K = node_level(j, C, s);
-      for (uint32_t k = 1; k <= K; ++k) task[tbase_k[k] + atomicAdd(&ntask[k], 1u)] = (uint16_t)s;
-      if (j == 0 && (mi || lead == 0) && s + C <= kTile) {
-        const uint32_t c = (uint32_t)C;
-        if (!(c & (c - 1))) {
-          const uint32_t k = 31 - __clz(c);
-          task[tbase_k[k] + atomicAdd(&ntask[k], 1u)] = (uint16_t)(s | kTaskRoot);
-        } else {
-          // right-to-left fold over the binary decomposition of c
-          uint32_t rem = c, part = rem & (0u - rem);
-          uint32_t pos = c - part;
-          rem -= part;
-          while (rem) {
-            part = rem & (0u - rem);
-            pos -= part;
-            const uint32_t k = 32 - __clz(part);
-            task[tbase_k[k] + atomicAdd(&ntask[k], 1u)] = (uint16_t)((s + pos) | (rem == part ? kTaskRoot : 0u));
-            rem -= part;
-          }
-        }
-      }
-    }
-
-    // (2) leaves
-    if (ORD) __syncthreads();  // order[] is complete
-    const uint32_t nleaf = ORD ? obin[16] : kTile;
-#pragma unroll 1
-    for (uint32_t i = tid; i < nleaf; i += WG) {
-      const uint32_t s = ORD ? order[i] : i;
-      const uint32_t mi = smsg[s];
-      if (mi == kNoMsg) continue;
-      const uint32_t m = m0 + mi;
-      const uint64_t j = mi ? (uint64_t)(s - srel[mi]) : lead + s;
-      const uint64_t len = lens[m];
-      const uint32_t clen = len == 0 ? 0u : (uint32_t)min<uint64_t>(CHUNK_LEN, len - j * CHUNK_LEN);
-      const bool root = len <= CHUNK_LEN;
-      uint32_t cv[8];
-      if (PF == 4) hash_chunk_pp(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
-      else if (PF) hash_chunk_pf(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
-      else hash_chunk(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
-      if (root) {
-        store_digest(perm ? perm[m] : m, cv, out32, out_keys);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) cvs[s][i] = cv[i];
-      }
-    }
-    __syncthreads();
-
-    // (3) the tree, level by level
-    for (uint32_t k = 1; k <= 10; ++k) {
-      const uint32_t T = ntask[k];
-      if (T == 0) continue;
-      const uint32_t base = tbase_k[k], half = 1u << (k - 1);
-#pragma unroll 1
-      for (uint32_t t = tid; t < T; t += WG) {
-        const uint32_t e = task[base + t];
-        const uint32_t l = e & 1023u, r = l + half;
-        const bool root = e & kTaskRoot;
-        uint32_t a[8], b[8], o[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          a[q] = cvs[l][q];
-          b[q] = cvs[r][q];
-        }
-        parent(a, b, root, o);
-        if (root) {
-          const uint32_t mm = m0 + smsg[l];
-          store_digest(perm ? perm[mm] : mm, o, out32, out_keys);
-        } else {
-#pragma unroll
-          for (int q = 0; q < 8; ++q) cvs[l][q] = o[q];
-        }
-      }
-      __syncthreads();
-    }
-
-    // (4) maximal in-tile nodes of messages crossing a tile boundary
-#pragma unroll 1
-    for (uint32_t s = tid; s < kTile; s += WG) {
-      const uint32_t mi = smsg[s];
-      if (mi == kNoMsg) continue;
-      const uint64_t C = chunk_count(lens[m0 + mi]);
-      if (C == 1) continue;
-      const bool inside = mi ? (srel[mi] + C <= kTile) : (lead == 0 && C <= kTile);
-      if (inside) continue;
-      const uint64_t j = mi ? (uint64_t)(s - srel[mi]) : lead + s;
-      const uint32_t k = node_level(j, C, s);
-      if (parent_in_tile(j, C, s, k)) continue;
-      uint4* o = reinterpret_cast<uint4*>(nodes + 8ull * (tbase + s));
-      o[0] = make_uint4(cvs[s][0], cvs[s][1], cvs[s][2], cvs[s][3]);
-      o[1] = make_uint4(cvs[s][4], cvs[s][5], cvs[s][6], cvs[s][7]);
-    }
-    __syncthreads();
-    tile = DYN ? next_tile : tile + gridDim.x;
-  }
-}
-
-// ---- quad layout: four consecutive chunks per lane ----------------------------
-//
-// The in-tile tree of k_leaf_tree parks a workgroup's waves at one barrier per
-// level while a few waves compress (profiles/r01_pmc_sq_variants_c2.json: 18 %
-// of wave time). Here every lane owns an aligned group of four chunk slots of
-// one message and reduces it in registers — P(P(c0,c1), P(c2,c3)), a BLAKE3
-// tree node because the group is aligned inside the message — so levels 1 and
-// 2 need no barrier, a tile holds 2048 slots for the same 32 KB of node LDS,
-// and the barrier-bound levels start at 3 (8 chunks). The leaf phase per lane
-// grows to 64 compressions + 3 parents, the tree phase keeps its length, so
-// the parked share of a tile halves.
-//
-// Slot layout (requires the shape-sorted order, single-chunk messages first):
-// a single-chunk message takes one slot; the last of them is padded so the
-// first multi-chunk message starts on a multiple of 4; a multi-chunk message
-// takes its chunk count rounded up to 4 (the padding slots are dead). Every
-// node starts on an even slot, so node CVs live at cvs[slot / 2].
-constexpr uint32_t kQTile = 2048;
 
 template <uint32_t TILE>
 __host__ __device__ inline uint32_t node_level_t(uint64_t j, uint64_t C, uint32_t s) {
@@ -815,264 +457,6 @@ __host__ __device__ inline bool parent_in_tile_t(uint64_t j, uint64_t C, uint32_
   if (!((j >> k) & 1)) return false;
   return j + w <= C && 2 * w < C && s >= w && (uint64_t)s + w <= TILE;
 }
-
-__host__ __device__ inline uint64_t quad_slots(const uint64_t* lens, uint32_t n, uint32_t i) {
-  const uint64_t C = chunk_count(lens[i]);
-  if (C > 1) return (C + 3) & ~3ull;
-  if (i + 1 < n && chunk_count(lens[i + 1]) > 1) return 1 + ((4 - ((i + 1) & 3)) & 3);
-  return 1;
-}
-
-struct QuadSlotsOp {
-  const uint64_t* lens;
-  uint32_t n;
-  __host__ __device__ uint64_t operator()(uint32_t i) const { return quad_slots(lens, n, i); }
-};
-
-__global__ void k_tile_first_q(const uint64_t* __restrict__ lens, const uint64_t* __restrict__ S, uint32_t n,
-                               uint64_t cap_slots, uint32_t* __restrict__ tile_first, uint64_t* __restrict__ total) {
-  uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= n) return;
-  const uint64_t s0 = S[m], Q = quad_slots(lens, n, m);
-  if (m == n - 1) *total = s0 + Q;
-  for (uint64_t t = (s0 + kQTile - 1) / kQTile; t * kQTile < s0 + Q && t * kQTile < cap_slots; ++t) tile_first[t] = m;
-}
-
-template <int PF>
-__device__ __forceinline__ void quad_chunk(const uint8_t* __restrict__ base, uint64_t len, uint64_t j, bool root,
-                                           uint32_t (&cv)[8]) {
-  const uint32_t clen = len == 0 ? 0u : (uint32_t)min<uint64_t>(CHUNK_LEN, len - j * CHUNK_LEN);
-  if (PF) hash_chunk_pf(base + j * CHUNK_LEN, clen, j, root, cv);
-  else hash_chunk(base + j * CHUNK_LEN, clen, j, root, cv);
-}
-
-__device__ __forceinline__ void lds_get(const uint32_t (*cvs)[8], uint32_t i, uint32_t (&o)[8]) {
-#pragma unroll
-  for (int q = 0; q < 8; ++q) o[q] = cvs[i][q];
-}
-__device__ __forceinline__ void lds_put(uint32_t (*cvs)[8], uint32_t i, const uint32_t (&v)[8]) {
-#pragma unroll
-  for (int q = 0; q < 8; ++q) cvs[i][q] = v[q];
-}
-
-template <int PF>
-__global__ void __launch_bounds__(512, 6) k_leaf_quad(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ offs,
-                                                   const uint64_t* __restrict__ lens, uint32_t n,
-                                                   const uint64_t* __restrict__ S,
-                                                   const uint32_t* __restrict__ tile_first,
-                                                   const uint64_t* __restrict__ total_p, uint64_t cap_slots,
-                                                   uint32_t* __restrict__ nodes, uint8_t* __restrict__ out32,
-                                                   uint64_t* __restrict__ out_keys,
-                                                   const uint32_t* __restrict__ perm) {
-  constexpr uint32_t T = kQTile, WG = 512;
-  __shared__ uint32_t cvs[T / 2][8];  // node CVs by first slot / 2
-  __shared__ uint16_t srel[T + 2];    // message starts relative to the tile (messages 1..)
-  __shared__ uint16_t smsg[T];        // slot -> message in the tile
-  __shared__ uint16_t task[T / 4];    // level >= 3 merges of group nodes: < T / 4
-  __shared__ uint32_t ntask[13], tbase_k[13];
-
-  const uint64_t total = *total_p;
-  if (total > cap_slots) return;
-  const uint64_t ntiles = (total + T - 1) / T;
-  const uint32_t tid = threadIdx.x;
-
-  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const uint64_t tbase = tile * T;
-    const uint32_t m0 = tile_first[tile];
-    const uint32_t m1 = (tile + 1 < ntiles) ? tile_first[tile + 1] : n - 1;
-    const uint32_t cnt = m1 - m0 + 1;
-    const uint64_t lead = tbase - S[m0];
-    for (uint32_t i = tid + 1; i < cnt; i += WG) srel[i] = (uint16_t)(S[m0 + i] - tbase);
-    if (tid < 13) ntask[tid] = 0;
-    __syncthreads();
-
-    // (1a) slot -> message; count the level >= 3 merges: regular nodes of 8+
-    // chunks, and the spine of every multi-group message lying in the tile
-#pragma unroll 1
-    for (uint32_t s = tid; s < T; s += WG) {
-      if (tbase + s >= total) {
-        smsg[s] = kNoMsg;
-        continue;
-      }
-      uint32_t lo = 0, hi = cnt - 1;
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi + 1) >> 1;
-        if (srel[mid] <= s) lo = mid;
-        else hi = mid - 1;
-      }
-      smsg[s] = (uint16_t)lo;
-      const uint64_t j = lo ? (uint64_t)(s - srel[lo]) : lead + s;
-      const uint64_t C = chunk_count(lens[m0 + lo]);
-      if (C <= 4 || j >= C) continue;
-      const uint32_t K = node_level_t<T>(j, C, s);
-      for (uint32_t k = 3; k <= K; ++k) atomicAdd(&ntask[k], 1u);
-      if (j == 0 && (lo || lead == 0) && s + C <= T) {
-        const uint32_t c = (uint32_t)C;
-        if (!(c & (c - 1))) {
-          atomicAdd(&ntask[31 - __clz(c)], 1u);
-        } else {
-          uint32_t rem = c & ~3u;
-          if (!(c & 3)) rem &= rem - 1;  // the lowest 4+ part is the fold's start, not a step
-          while (rem) {
-            const uint32_t part = rem & (0u - rem);
-            atomicAdd(&ntask[32 - __clz(part)], 1u);
-            rem -= part;
-          }
-        }
-      }
-    }
-    __syncthreads();
-    if (tid == 0) {
-      uint32_t acc = 0;
-      for (int k = 3; k <= 11; ++k) {
-        tbase_k[k] = acc;
-        acc += ntask[k];
-        ntask[k] = 0;
-      }
-    }
-    __syncthreads();
-    // (1b) write the merges, compacted by level
-#pragma unroll 1
-    for (uint32_t s = tid; s < T; s += WG) {
-      const uint32_t mi = smsg[s];
-      if (mi == kNoMsg) continue;
-      const uint64_t j = mi ? (uint64_t)(s - srel[mi]) : lead + s;
-      const uint64_t C = chunk_count(lens[m0 + mi]);
-      if (C <= 4 || j >= C) continue;
-      const uint32_t K = node_level_t<T>(j, C, s);
-      for (uint32_t k = 3; k <= K; ++k) task[tbase_k[k] + atomicAdd(&ntask[k], 1u)] = (uint16_t)s;
-      if (j == 0 && (mi || lead == 0) && s + C <= T) {
-        const uint32_t c = (uint32_t)C;
-        if (!(c & (c - 1))) {
-          const uint32_t k = 31 - __clz(c);
-          task[tbase_k[k] + atomicAdd(&ntask[k], 1u)] = (uint16_t)(s | kTaskRoot);
-        } else {
-          // right-to-left fold: the tail (< 4 chunks, folded in its group)
-          // or the lowest part is the accumulator; each higher part merges in
-          uint32_t rem = c & ~3u, pos;
-          if (c & 3) {
-            pos = c & ~3u;
-          } else {
-            pos = c - (rem & (0u - rem));
-            rem &= rem - 1;
-          }
-          while (rem) {
-            const uint32_t part = rem & (0u - rem);
-            pos -= part;
-            const uint32_t k = 32 - __clz(part);
-            task[tbase_k[k] + atomicAdd(&ntask[k], 1u)] = (uint16_t)((s + pos) | (rem == part ? kTaskRoot : 0u));
-            rem -= part;
-          }
-        }
-      }
-    }
-
-    // (2) groups: four chunk slots per lane, reduced in registers
-#pragma unroll 1
-    for (uint32_t g = tid; g < T / 4; g += WG) {
-      const uint32_t s = 4 * g;
-      const uint32_t mi = smsg[s];
-      if (mi == kNoMsg) continue;
-      const uint32_t m = m0 + mi;
-      const uint64_t len = lens[m];
-      const uint64_t C = chunk_count(len);
-      if (C == 1) {
-        // up to four single-chunk messages (or the padding after the last)
-#pragma unroll 1
-        for (uint32_t q = 0; q < 4; ++q) {
-          const uint32_t mq = smsg[s + q];
-          if (mq == kNoMsg) break;
-          const uint64_t jq = mq ? (uint64_t)(s + q - srel[mq]) : lead + s + q;
-          if (jq != 0) continue;
-          const uint32_t mm = m0 + mq;
-          uint32_t cv[8];
-          quad_chunk<PF>(blob + offs[mm], lens[mm], 0, true, cv);
-          store_digest(perm ? perm[mm] : mm, cv, out32, out_keys);
-        }
-        continue;
-      }
-      const uint64_t rel0 = mi ? srel[mi] : 0;
-      const uint64_t j0 = mi ? (uint64_t)s - rel0 : lead + s;
-      const uint32_t nv = (uint32_t)min<uint64_t>(4, C - j0);
-      // the last three chunks of a message lying in the tile are folded here
-      // (the spine's first step); a crossing message keeps P(c0,c1) and c2
-      const bool fold3 = nv == 3 && (C == 3 || ((mi || lead == 0) && rel0 + C <= T));
-      const uint8_t* base = blob + offs[m];
-      // chunks one by one; the group's nodes stack up in cvs[2g], cvs[2g+1]
-      // and merge as pairs complete (one hash and one parent call site keep
-      // the register footprint of a single chunk)
-      uint32_t depth = 0;
-#pragma unroll 1
-      for (uint32_t q = 0; q < nv; ++q) {
-        uint32_t cv[8];
-        quad_chunk<PF>(base, len, j0 + q, false, cv);
-        uint32_t merges = q == 1 ? 1u : (q == 3 ? 2u : 0u);
-        if (q == 2 && fold3) merges = 1;
-        bool root = false;
-#pragma unroll 1
-        for (uint32_t t = 0; t < merges; ++t) {
-          uint32_t a[8];
-          lds_get(cvs, 2 * g + depth - 1, a);
-          root = depth == 1 && j0 == 0 && q + 1 == C;  // the merge that completes the whole message
-          parent(a, cv, root, cv);
-          --depth;
-        }
-        if (root) {
-          store_digest(perm ? perm[m] : m, cv, out32, out_keys);
-          break;
-        }
-        lds_put(cvs, 2 * g + depth, cv);
-        ++depth;
-      }
-    }
-    __syncthreads();
-
-    // (3) the tree above the groups, level by level
-    for (uint32_t k = 3; k <= 11; ++k) {
-      const uint32_t Tk = ntask[k];
-      if (Tk == 0) continue;
-      const uint32_t base = tbase_k[k], half = 1u << (k - 1);
-#pragma unroll 1
-      for (uint32_t t = tid; t < Tk; t += WG) {
-        const uint32_t e = task[base + t];
-        const uint32_t l = e & (T - 1), r = l + half;
-        const bool root = e & kTaskRoot;
-        uint32_t a[8], b[8], o[8];
-        lds_get(cvs, l >> 1, a);
-        lds_get(cvs, r >> 1, b);
-        parent(a, b, root, o);
-        if (root) {
-          const uint32_t mm = m0 + smsg[l];
-          store_digest(perm ? perm[mm] : mm, o, out32, out_keys);
-        } else {
-          lds_put(cvs, l >> 1, o);
-        }
-      }
-      __syncthreads();
-    }
-
-    // (4) maximal in-tile nodes of messages crossing a tile boundary
-#pragma unroll 1
-    for (uint32_t s = tid; s < T; s += WG) {
-      const uint32_t mi = smsg[s];
-      if (mi == kNoMsg) continue;
-      const uint64_t C = chunk_count(lens[m0 + mi]);
-      if (C <= 4) continue;
-      const uint64_t rel0 = mi ? srel[mi] : 0;
-      if ((mi || lead == 0) && rel0 + C <= T) continue;
-      const uint64_t j = mi ? (uint64_t)s - rel0 : lead + s;
-      if (j >= C) continue;
-      const uint32_t k = node_level_t<T>(j, C, s);
-      if (parent_in_tile_t<T>(j, C, s, k)) continue;
-      uint4* o = reinterpret_cast<uint4*>(nodes + 8ull * (tbase + s));
-      const uint32_t i = s >> 1;
-      o[0] = make_uint4(cvs[i][0], cvs[i][1], cvs[i][2], cvs[i][3]);
-      o[1] = make_uint4(cvs[i][4], cvs[i][5], cvs[i][6], cvs[i][7]);
-    }
-    __syncthreads();
-  }
-}
-
 
 // Messages crossing tile boundaries: one lane per tile boundary t (the
 // message holding slot t*kTile, when it started in tile t-1 — its first
@@ -1242,6 +626,10 @@ __global__ void __launch_bounds__(kFinishWG) k_finish_t(const uint64_t* __restri
   store_digest(perm ? perm[m] : m, cv, out32, out_keys);
 }
 
+#ifdef SDCAS_ABLATIONS
+#include "b3_ablate_kernels.inc"
+#endif
+
 // Slot order by message shape: key = min(chunks, 15) << 4 | (blocks in the
 // last chunk - 1). Single-chunk messages — whose lanes otherwise run 1..16
 // blocks side by side in one wave — end up grouped by block count;
@@ -1341,11 +729,7 @@ __global__ void __launch_bounds__(kWG, MINW) k_piece_tree(const uint8_t* __restr
       if (ROT && s >= nchunks) s -= nchunks;
       const uint32_t clen = min(CHUNK_LEN, pd.len - s * CHUNK_LEN);
       uint32_t cv[8];
-      if (PF == 8) hash_chunk_ps(blob + pd.off + (uint64_t)s * CHUNK_LEN, clen, pd.j0 + s, false, cv);
-      else if (PF == 2) hash_chunk_diag(blob + pd.off + (uint64_t)s * CHUNK_LEN, clen, pd.j0 + s, false, cv, 2);
-      else if (PF == 4) hash_chunk_pp(blob + pd.off + (uint64_t)s * CHUNK_LEN, clen, pd.j0 + s, false, cv);
-      else if (PF) hash_chunk_pf(blob + pd.off + (uint64_t)s * CHUNK_LEN, clen, pd.j0 + s, false, cv);
-      else hash_chunk(blob + pd.off + (uint64_t)s * CHUNK_LEN, clen, pd.j0 + s, false, cv);
+      leaf_hash<PF>(blob + pd.off + (uint64_t)s * CHUNK_LEN, clen, pd.j0 + s, false, cv);
 #pragma unroll
       for (int i = 0; i < 8; ++i) cvs[s][i] = cv[i];
     }
@@ -1392,6 +776,120 @@ __global__ void __launch_bounds__(kWG, MINW) k_piece_tree(const uint8_t* __restr
       o[1] = make_uint4(cvs[s][4], cvs[s][5], cvs[s][6], cvs[s][7]);
     }
     __syncthreads();
+  }
+}
+
+// hash_chunk_ps whose first line (blocks 0 and min(1, nb-1)) the caller has
+// already loaded into m0 / m1
+__device__ __forceinline__ void hash_chunk_ps_loaded(const uint8_t* __restrict__ p, uint32_t clen, uint64_t j,
+                                                     uint32_t (&cv)[8], uint32_t (&m0)[16], uint32_t (&m1)[16]) {
+  set_iv(cv);
+  const uint32_t nb = clen == 0 ? 1 : (clen + BLOCK_LEN - 1) / BLOCK_LEN;
+#pragma unroll 1
+  for (uint32_t b = 0;; b += 2) {
+    {
+      const uint32_t blen = min(BLOCK_LEN, clen - b * BLOCK_LEN);
+      if (blen < BLOCK_LEN) mask_tail(m0, blen);
+      compress(cv, m0, j, blen, (b == 0 ? CHUNK_START : 0u) | (b + 1 == nb ? CHUNK_END : 0u));
+    }
+    if (b + 1 < nb) {
+      const uint32_t blen = min(BLOCK_LEN, clen - (b + 1) * BLOCK_LEN);
+      if (blen < BLOCK_LEN) mask_tail(m1, blen);
+      compress(cv, m1, j, blen, b + 2 == nb ? CHUNK_END : 0u);
+    }
+    if (b + 2 >= nb) break;
+    load_full_block(p + (b + 2) * BLOCK_LEN, m0);
+    load_full_block(p + min(b + 3, nb - 1) * BLOCK_LEN, m1);
+  }
+}
+
+// k_piece_tree on the leaf kernel's schedule: a persistent grid whose
+// workgroups claim pieces from a global counter (`ctr`, zeroed before the
+// launch; the next piece is claimed at the start of the current one, so the
+// atomic's latency hides behind it), and — PRE — each lane loads the first
+// line of its first chunk of the NEXT piece before the current piece's tree
+// levels, whose few active waves would otherwise leave the CU's load path
+// idle while the next piece starts cold. Full pieces only reduce to their
+// level-10 node; tail pieces to the binary decomposition of their chunks, as
+// in k_piece_tree.
+template <int MINW, int PRE>
+__global__ void __launch_bounds__(kWG, MINW) k_piece_dyn(const uint8_t* __restrict__ blob,
+                                                         const PieceDesc* __restrict__ pieces, uint32_t npieces,
+                                                         uint32_t* __restrict__ file_nodes,
+                                                         uint32_t* __restrict__ ctr) {
+  __shared__ uint32_t cvs[kTile][8];
+  __shared__ uint32_t next_piece;
+  const uint32_t tid = threadIdx.x;
+  uint32_t pm0[16], pm1[16];
+  bool have = false;  // PRE: pm0 / pm1 hold chunk `tid` of piece pi
+#pragma unroll 1
+  for (uint32_t pi = blockIdx.x; pi < npieces;) {
+    if (tid == 0) next_piece = gridDim.x + atomicAdd(ctr, 1u);
+    const PieceDesc pd = pieces[pi];
+    const uint32_t nchunks = (pd.len + CHUNK_LEN - 1) / CHUNK_LEN;
+#pragma unroll 1
+    for (uint32_t s = tid; s < nchunks; s += kWG) {
+      const uint32_t clen = min(CHUNK_LEN, pd.len - s * CHUNK_LEN);
+      const uint8_t* p = blob + pd.off + (uint64_t)s * CHUNK_LEN;
+      uint32_t cv[8];
+      if (PRE && have && s == tid) {
+        hash_chunk_ps_loaded(p, clen, pd.j0 + s, cv, pm0, pm1);
+      } else {
+        hash_chunk_ps(p, clen, pd.j0 + s, false, cv);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) cvs[s][i] = cv[i];
+    }
+    __syncthreads();
+    // read between two barriers: thread 0 rewrites it after this piece's last one
+    const uint32_t nx = next_piece;
+    if (PRE) {
+      have = false;
+      if (nx < npieces) {
+        const PieceDesc nd = pieces[nx];
+        if (tid * CHUNK_LEN < nd.len) {
+          const uint32_t clen = min(CHUNK_LEN, nd.len - tid * CHUNK_LEN);
+          const uint32_t nb = (clen + BLOCK_LEN - 1) / BLOCK_LEN;
+          const uint8_t* p = blob + nd.off + (uint64_t)tid * CHUNK_LEN;
+          load_full_block(p, pm0);
+          load_full_block(p + min(1u, nb - 1) * BLOCK_LEN, pm1);
+          have = true;
+        }
+      }
+    }
+    // the complete aligned level-k nodes of a piece are its first
+    // nchunks >> k multiples of 2^k
+#pragma unroll 1
+    for (uint32_t k = 1; k <= 10; ++k) {
+      const uint32_t T = nchunks >> k;
+      if (T == 0) break;
+      const uint32_t half = 1u << (k - 1);
+#pragma unroll 1
+      for (uint32_t t = tid; t < T; t += kWG) {
+        const uint32_t s = t << k;
+        uint32_t l[8], r[8], o[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          l[i] = cvs[s][i];
+          r[i] = cvs[s + half][i];
+        }
+        parent(l, r, false, o);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) cvs[s][i] = o[i];
+      }
+      __syncthreads();
+    }
+    // maximal nodes: the binary decomposition of nchunks (one node for a full piece)
+    for (uint32_t s = tid; s < nchunks; s += kWG) {
+      const uint32_t k = 31 - __clz(nchunks - s);
+      if ((s & ((1u << k) - 1)) || (s != (nchunks & ~((2u << k) - 1)))) continue;
+      const uint64_t idx = pd.node_base + (nchunks == kTile ? pd.j0 / kTile : pd.j0 / kTile + __popc(nchunks >> (k + 1)));
+      uint4* o = reinterpret_cast<uint4*>(file_nodes + 8ull * idx);
+      o[0] = make_uint4(cvs[s][0], cvs[s][1], cvs[s][2], cvs[s][3]);
+      o[1] = make_uint4(cvs[s][4], cvs[s][5], cvs[s][6], cvs[s][7]);
+    }
+    __syncthreads();
+    pi = nx;
   }
 }
 
@@ -1546,104 +1044,102 @@ __global__ void __launch_bounds__(kWG) k_bigfile_finish(const FileDesc* __restri
 
 // ---------------------------------------------------------------------------
 
+#ifdef SDCAS_ABLATIONS
 using QuadIt = hipcub::TransformInputIterator<uint64_t, QuadSlotsOp, hipcub::CountingInputIterator<uint32_t>>;
+#endif
 
 size_t batch_scan_temp_bytes(uint32_t max_msgs) {
   size_t bytes = 0, qbytes = 0;
   hipcub::TransformInputIterator<uint64_t, ChunkCountOp, const uint64_t*> it(nullptr, ChunkCountOp());
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, it, (uint64_t*)nullptr, (int)max_msgs);
+#ifdef SDCAS_ABLATIONS
   QuadIt qit(hipcub::CountingInputIterator<uint32_t>(0), QuadSlotsOp{nullptr, max_msgs});
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, qbytes, qit, (uint64_t*)nullptr, (int)max_msgs);
+#endif
   return std::max(bytes, qbytes);
 }
 
-// leaf/tree kernel variants (workgroup size x block prefetch); the default is
-// what bench measurements picked, SDCAS_LEAF_VARIANT overrides for A/B runs
+// Leaf/tree kernel variants, numbered as in round 1's A/B runs
+// so that profiles/ and tools/ keep their meaning. libsdcas.so holds only the
+// bit-exact, GPU-tested product kernels (the default, 43, and 36); every
+// other entry is compiled only into the ablation library (ABL), and the
+// stagger / priority experiments (8, 9, 11, 12, 37) are retired (RET).
 struct LeafVariant {
   const void* fn;
   int wg;
   int quad = 0;  // 1: quad slot layout (k_leaf_quad / k_finish_t<kQTile>, needs the shape-sorted order)
 };
+#define PROD(wg, ...) {(const void*)__VA_ARGS__, wg}
+#ifdef SDCAS_ABLATIONS
+#define ABL(wg, ...) {(const void*)__VA_ARGS__, wg}
+#define ABLQ(wg, ...) {(const void*)__VA_ARGS__, wg, 1}
+#else
+#define ABL(wg, ...) {nullptr, wg}
+#define ABLQ(wg, ...) {nullptr, wg, 1}
+#endif
+#define RET {nullptr, 512}
 static const LeafVariant kLeafVariants[] = {
-    {(const void*)k_leaf_tree<512, 0>, 512},
-    {(const void*)k_leaf_tree<512, 1>, 512},
-    {(const void*)k_leaf_tree<256, 1>, 256},
-    {(const void*)k_leaf_tree<1024, 1>, 1024},
-    // diagnostic (wrong results): 4 = no memory reads, 5 = no compression
-    {(const void*)k_leaf_tree<512, 2>, 512},
-    {(const void*)k_leaf_tree<512, 3>, 512},
-    // 6, 7 diagnostic (wrong results): no in-tile tree; no tree and no loads
-    {(const void*)k_leaf_tree<512, 1, 0>, 512},
-    {(const void*)k_leaf_tree<512, 2, 0>, 512},
-    // 8, 9: workgroups staggered by 1/3 and 1/2 of a tile
-    {(const void*)k_leaf_tree<512, 1, 1, 3>, 512},
-    {(const void*)k_leaf_tree<512, 1, 1, 2>, 512},
-    // 10: ping-pong block loop; 11: tree waves at priority 1; 12: both
-    {(const void*)k_leaf_tree<512, 4>, 512},
-    {(const void*)k_leaf_tree<512, 1, 1, 0, 1>, 512},
-    {(const void*)k_leaf_tree<512, 4, 1, 0, 1>, 512},
-    // 13: non-temporal (streaming) message loads
-    {(const void*)k_leaf_tree<512, 5>, 512},
-    // 14-16: compact LDS (4 workgroups per CU); min waves/SIMD 8, 6; 16: no prefetch
-    {(const void*)k_leaf_slim<512, 1, 8>, 512},
-    {(const void*)k_leaf_slim<512, 1, 6>, 512},
-    {(const void*)k_leaf_slim<512, 0, 8>, 512},
-    // 17: prefetch distance two blocks; 18: 128-byte pair loads
-    {(const void*)k_leaf_tree<512, 6>, 512},
-    {(const void*)k_leaf_tree<512, 7>, 512},
-    // 19, 20: compact LDS + leaf order by block count (6 waves/SIMD); the same without prefetch
-    {(const void*)k_leaf_slim<512, 1, 6, 1>, 512},
-    {(const void*)k_leaf_slim<512, 0, 6, 1>, 512},
-    // 21, 22: quad layout (four chunks per lane, 2048-slot tiles); without prefetch
-    {(const void*)k_leaf_quad<1>, 512, 1},
-    {(const void*)k_leaf_quad<0>, 512, 1},
-    // 23, 24: compact LDS + ping-pong message registers (no copies) under a
-    // 6- and 5-wave register cap
-    {(const void*)k_leaf_slim<512, 4, 6>, 512},
-    {(const void*)k_leaf_slim<512, 4, 5>, 512},
-    // 25: leaf order by block count (ballot ranks, no LDS atomics)
-    {(const void*)k_leaf_tree<512, 1, 1, 0, 0, 1>, 512},
-    // 26-28 diagnostic (wrong results), 25 with: no memory reads; no in-tile tree; neither
-    {(const void*)k_leaf_tree<512, 2, 1, 0, 0, 1>, 512},
-    {(const void*)k_leaf_tree<512, 1, 0, 0, 0, 1>, 512},
-    {(const void*)k_leaf_tree<512, 2, 0, 0, 0, 1>, 512},
-    // 29: 25 with tiles handed out by a global counter (dynamic schedule)
-    {(const void*)k_leaf_tree<512, 1, 1, 0, 0, 1, 1>, 512},
-    // 30-33: compact LDS with the dynamic schedule: 8 waves/SIMD; 6 + leaf
-    // order; 8 + leaf order; 30 without prefetch
-    {(const void*)k_leaf_slim<512, 1, 8, 0, 1>, 512},
-    {(const void*)k_leaf_slim<512, 1, 6, 1, 1>, 512},
-    {(const void*)k_leaf_slim<512, 1, 8, 1, 1>, 512},
-    {(const void*)k_leaf_slim<512, 0, 8, 0, 1>, 512},
-    // 34: 29 at 1024 threads per workgroup (one chunk per lane)
-    {(const void*)k_leaf_tree<1024, 1, 1, 0, 0, 1, 1>, 1024},
-    // 35-38: 29 without the leaf order; with ping-pong blocks; with tree
-    // waves at priority 1; with prefetch distance two
-    {(const void*)k_leaf_tree<512, 1, 1, 0, 0, 0, 1>, 512},
-    {(const void*)k_leaf_tree<512, 4, 1, 0, 0, 1, 1>, 512},
-    {(const void*)k_leaf_tree<512, 1, 1, 0, 1, 1, 1>, 512},
-    {(const void*)k_leaf_tree<512, 6, 1, 0, 0, 1, 1>, 512},
-    // 39-41 diagnostic (wrong results), 36 with: no in-tile tree; no memory
-    // reads (block loop of 29); neither
-    {(const void*)k_leaf_tree<512, 4, 0, 0, 0, 1, 1>, 512},
-    {(const void*)k_leaf_tree<512, 2, 1, 0, 0, 1, 1>, 512},
-    {(const void*)k_leaf_tree<512, 2, 0, 0, 0, 1, 1>, 512},
-    // 42: 29 with 128-byte pair loads (a lane reads a whole L2 line at once)
-    {(const void*)k_leaf_tree<512, 7, 1, 0, 0, 1, 1>, 512},
-    // 43: 36 with both halves of a line loaded together, no prefetch
-    {(const void*)k_leaf_tree<512, 8, 1, 0, 0, 1, 1>, 512},
+    ABL(512, k_leaf_tree<512, 0>),   // 0: plain block loop
+    ABL(512, k_leaf_tree<512, 1>),   // 1: next block prefetched
+    ABL(256, k_leaf_tree<256, 1>),   // 2, 3: 256 / 1024 threads per workgroup
+    ABL(1024, k_leaf_tree<1024, 1>),
+    ABL(512, k_leaf_tree<512, 2>),   // 4 DIAGNOSTIC (wrong digests): no memory reads
+    ABL(512, k_leaf_tree<512, 3>),   // 5 DIAGNOSTIC (wrong digests): no compression
+    ABL(512, k_leaf_tree<512, 1, 0>),  // 6, 7 DIAGNOSTIC (wrong digests): no in-tile tree; neither tree nor loads
+    ABL(512, k_leaf_tree<512, 2, 0>),
+    RET, RET,                          // 8, 9: workgroups staggered by a fraction of a tile
+    ABL(512, k_leaf_tree<512, 4>),   // 10: ping-pong block loop
+    RET, RET,                          // 11, 12: tree waves at priority 1
+    ABL(512, k_leaf_tree<512, 5>),   // 13: non-temporal message loads
+    ABL(512, k_leaf_slim<512, 1, 8>),  // 14-16: compact LDS (4 workgroups per CU)
+    ABL(512, k_leaf_slim<512, 1, 6>),
+    ABL(512, k_leaf_slim<512, 0, 8>),
+    ABL(512, k_leaf_tree<512, 6>),   // 17: prefetch distance two blocks
+    ABL(512, k_leaf_tree<512, 7>),   // 18: 128-byte pair loads
+    ABL(512, k_leaf_slim<512, 1, 6, 1>),  // 19, 20: compact LDS + leaf order by block count
+    ABL(512, k_leaf_slim<512, 0, 6, 1>),
+    ABLQ(512, k_leaf_quad<1>),        // 21, 22: quad layout (four chunks per lane)
+    ABLQ(512, k_leaf_quad<0>),
+    ABL(512, k_leaf_slim<512, 4, 6>),  // 23, 24: compact LDS + ping-pong under a 6 / 5 wave register cap
+    ABL(512, k_leaf_slim<512, 4, 5>),
+    ABL(512, k_leaf_tree<512, 1, 1, 1>),     // 25: leaf order by block count
+    ABL(512, k_leaf_tree<512, 2, 1, 1>),     // 26-28 DIAGNOSTIC (wrong digests): 25 without loads / tree / both
+    ABL(512, k_leaf_tree<512, 1, 0, 1>),
+    ABL(512, k_leaf_tree<512, 2, 0, 1>),
+    ABL(512, k_leaf_tree<512, 1, 1, 1, 1>),  // 29: 25 + tiles from a global counter (dynamic schedule)
+    ABL(512, k_leaf_slim<512, 1, 8, 0, 1>),  // 30-33: compact LDS with the dynamic schedule
+    ABL(512, k_leaf_slim<512, 1, 6, 1, 1>),
+    ABL(512, k_leaf_slim<512, 1, 8, 1, 1>),
+    ABL(512, k_leaf_slim<512, 0, 8, 0, 1>),
+    ABL(1024, k_leaf_tree<1024, 1, 1, 1, 1>),  // 34: 29 at 1024 threads
+    ABL(512, k_leaf_tree<512, 1, 1, 0, 1>),    // 35: 29 without the leaf order
+    PROD(512, k_leaf_tree<512, 4, 1, 1, 1>),   // 36: 29 with the ping-pong block loop
+    RET,                                        // 37: 29 with tree waves at priority 1
+    ABL(512, k_leaf_tree<512, 6, 1, 1, 1>),    // 38: 29 with prefetch distance two
+    ABL(512, k_leaf_tree<512, 4, 0, 1, 1>),    // 39-41 DIAGNOSTIC (wrong digests): 36 without tree / loads / both
+    ABL(512, k_leaf_tree<512, 2, 1, 1, 1>),
+    ABL(512, k_leaf_tree<512, 2, 0, 1, 1>),
+    ABL(512, k_leaf_tree<512, 7, 1, 1, 1>),    // 42: 29 with 128-byte pair loads
+    PROD(512, k_leaf_tree<512, 8, 1, 1, 1>),   // 43 (default): 36 with both halves of a line loaded together
 };
+#undef PROD
+#undef ABL
+#undef ABLQ
+#undef RET
 constexpr int kNumLeafVariants = sizeof(kLeafVariants) / sizeof(kLeafVariants[0]);
 constexpr int kDefaultLeafVariant = 43;
 
 int leaf_variant_count() { return kNumLeafVariants; }
+bool leaf_variant_available(int v) { return v >= 0 && v < kNumLeafVariants && kLeafVariants[v].fn != nullptr; }
 
+// SDCAS_LEAF_VARIANT selects a variant for A/B runs; a variant this build
+// does not hold (every diagnostic one in libsdcas.so) falls back to the default
 int leaf_variant() {
   static int v = -2;
   if (v == -2) {
     const char* e = getenv("SDCAS_LEAF_VARIANT");
     v = e ? atoi(e) : kDefaultLeafVariant;
-    if (v < 0 || v >= kNumLeafVariants) v = kDefaultLeafVariant;
+    if (!leaf_variant_available(v)) v = kDefaultLeafVariant;
   }
   return v;
 }
@@ -1679,15 +1175,20 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
     lens = ws.slens;
     perm = ws.perm;
   }
-  int v = ws.variant >= 0 && ws.variant < kNumLeafVariants ? ws.variant : leaf_variant();
-  const bool quad = kLeafVariants[v].quad && (perm || n == 1);
-  if (kLeafVariants[v].quad && !quad) v = 1;  // the quad layout needs the shape-sorted order
+  int v = leaf_variant_available(ws.variant) ? ws.variant : leaf_variant();
+  bool quad = false;
+#ifdef SDCAS_ABLATIONS
+  quad = kLeafVariants[v].quad && (perm || n == 1);
+  if (kLeafVariants[v].quad && !quad) v = kDefaultLeafVariant;  // the quad layout needs the shape-sorted order
+#endif
   size_t tmp = ws.scan_tmp_bytes;
   if (quad) {
+#ifdef SDCAS_ABLATIONS
     QuadIt qit(hipcub::CountingInputIterator<uint32_t>(0), QuadSlotsOp{lens, n});
     if ((e = hipcub::DeviceScan::ExclusiveSum(ws.scan_tmp, tmp, qit, ws.S, (int)n, st))) return e;
     hipLaunchKernelGGL(k_tile_first_q, dim3((n + tb - 1) / tb), dim3(tb), 0, st, lens, ws.S, n, ws.cap_slots,
                        ws.tile_first, ws.total);
+#endif
   } else {
     hipcub::TransformInputIterator<uint64_t, ChunkCountOp, const uint64_t*> it(lens, ChunkCountOp());
     if ((e = hipcub::DeviceScan::ExclusiveSum(ws.scan_tmp, tmp, it, ws.S, (int)n, st))) return e;
@@ -1707,9 +1208,11 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
   }
   if (ev1) (void)hipEventRecord(ev1, st);
   if (quad) {
+#ifdef SDCAS_ABLATIONS
     const uint64_t tiles = ws.cap_slots / kQTile + 1;
     hipLaunchKernelGGL(k_finish_t<kQTile>, dim3((uint32_t)((tiles + kFinishWG - 1) / kFinishWG)), dim3(kFinishWG), 0,
                        st, lens, n, ws.S, ws.tile_first, ws.total, ws.cap_slots, ws.nodes, perm, out32, out_keys);
+#endif
   } else {
     const uint64_t tiles = ws.cap_slots / kTile + 1;
     hipLaunchKernelGGL(k_finish_t<kTile>, dim3((uint32_t)((tiles + kFinishWG - 1) / kFinishWG)), dim3(kFinishWG), 0,
@@ -1718,46 +1221,86 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
   return hipGetLastError();
 }
 
-hipError_t piece_hash(const uint8_t* blob, const PieceDesc* pieces, uint32_t npieces, uint32_t* file_nodes,
-                      hipStream_t st) {
-  if (!npieces) return hipSuccess;
-  // SDCAS_PIECE_VARIANT (A/B): 0 = plain block loop, 1 = block prefetch at 8 waves/SIMD,
-  // 2 = 1 with tree tasks indexed directly (one barrier per level), 3 = 2 at 6 waves/SIMD,
-  // 4, 5 = 2 with the ping-pong block loop at 6 / 8 waves/SIMD (4: default, +2 % on C4)
-  static int v = -1;
-  if (v < 0) {
+// Piece kernel variants: 4 = one workgroup per piece, ping-pong block loop,
+// 6 waves/SIMD (round 1's default); 11 = persistent grid on a global piece
+// counter (k_piece_dyn); 12 = 11 with the next piece's first line loaded
+// before the current piece's tree levels; 13 = 11 at 8 waves/SIMD. The
+// others (plain / prefetch loops, rotated chunk order, a round-robin
+// persistent grid, and the DIAGNOSTIC 7 without memory reads) exist only in
+// the ablation library.
+constexpr int kDefaultPieceVariant = 4;
+
+bool piece_variant_available(int v) {
+  if (v == 4 || v == 11 || v == 12 || v == 13) return true;
+#ifdef SDCAS_ABLATIONS
+  if (v >= 0 && v <= 10) return true;
+#endif
+  return false;
+}
+
+int piece_variant() {
+  static int v = -2;
+  if (v == -2) {
     const char* e = getenv("SDCAS_PIECE_VARIANT");
-    v = e ? atoi(e) : 4;
+    v = e ? atoi(e) : kDefaultPieceVariant;
+    if (!piece_variant_available(v)) v = kDefaultPieceVariant;
   }
+  return v;
+}
+
+static int piece_grid(const void* fn) {
+  int dev = 0, cus = 0, per = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, kWG, 0);
+  return (cus > 0 ? cus : 256) * (per > 0 ? per : 1);
+}
+
+template <int MINW, int PRE>
+static hipError_t launch_piece_dyn(const uint8_t* blob, const PieceDesc* pieces, uint32_t npieces,
+                                   uint32_t* file_nodes, uint32_t* ctr, hipStream_t st) {
+  static int grid = 0;  // the same on every MI355X of the node
+  if (!grid) grid = piece_grid((const void*)k_piece_dyn<MINW, PRE>);
+  hipError_t e = hipMemsetAsync(ctr, 0, sizeof(uint32_t), st);
+  if (e) return e;
+  hipLaunchKernelGGL((k_piece_dyn<MINW, PRE>), dim3(std::min<uint32_t>(npieces, (uint32_t)grid)), dim3(kWG), 0, st,
+                     blob, pieces, npieces, file_nodes, ctr);
+  return hipGetLastError();
+}
+
+hipError_t piece_hash(const uint8_t* blob, const PieceDesc* pieces, uint32_t npieces, uint32_t* file_nodes,
+                      uint32_t* ctr, int variant, hipStream_t st) {
+  if (!npieces) return hipSuccess;
+  const int v = piece_variant_available(variant) ? variant : piece_variant();
+  if (v == 11) return launch_piece_dyn<6, 0>(blob, pieces, npieces, file_nodes, ctr, st);
+  if (v == 12) return launch_piece_dyn<6, 1>(blob, pieces, npieces, file_nodes, ctr, st);
+  if (v == 13) return launch_piece_dyn<8, 0>(blob, pieces, npieces, file_nodes, ctr, st);
+#ifdef SDCAS_ABLATIONS
   if (v == 0) hipLaunchKernelGGL((k_piece_tree<0, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
+  else if (v == 1)
+    hipLaunchKernelGGL((k_piece_tree<1, 8>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   else if (v == 2)
     hipLaunchKernelGGL((k_piece_tree<1, 8, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   else if (v == 3)
     hipLaunchKernelGGL((k_piece_tree<1, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
-  else if (v == 4)
-    hipLaunchKernelGGL((k_piece_tree<4, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   else if (v == 5)
     hipLaunchKernelGGL((k_piece_tree<4, 8, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   else if (v == 6)  // 4 with both halves of a line loaded together
     hipLaunchKernelGGL((k_piece_tree<8, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
+  else if (v == 7)  // DIAGNOSTIC (wrong digests): 4's loop without memory reads
+    hipLaunchKernelGGL((k_piece_tree<2, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   else if (v == 8)  // 4 with per-workgroup rotated chunk order
     hipLaunchKernelGGL((k_piece_tree<4, 6, 1, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   else if (v == 9)  // 6 with per-workgroup rotated chunk order
     hipLaunchKernelGGL((k_piece_tree<8, 6, 1, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
-  else if (v == 10) {  // 4 as a persistent grid (resident workgroups loop over the pieces)
+  else if (v == 10) {  // 4 as a persistent grid dealing pieces round-robin
     static int grid = 0;
-    if (!grid) {
-      int dev = 0, cus = 0, per = 0;
-      (void)hipGetDevice(&dev);
-      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k_piece_tree<4, 6, 1>, kWG, 0);
-      grid = (cus > 0 ? cus : 256) * (per > 0 ? per : 1);
-    }
+    if (!grid) grid = piece_grid((const void*)k_piece_tree<4, 6, 1>);
     hipLaunchKernelGGL((k_piece_tree<4, 6, 1>), dim3(std::min<uint32_t>(npieces, (uint32_t)grid)), dim3(kWG), 0, st,
                        blob, pieces, npieces, file_nodes);
-  } else if (v == 7)  // DIAGNOSTIC (wrong digests): 4's loop without memory reads
-    hipLaunchKernelGGL((k_piece_tree<2, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
-  else hipLaunchKernelGGL((k_piece_tree<1, 8>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
+  } else
+#endif
+    hipLaunchKernelGGL((k_piece_tree<4, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   return hipGetLastError();
 }
 
@@ -1767,5 +1310,6 @@ hipError_t bigfile_finish(const FileDesc* files, uint32_t nfiles, const uint32_t
   hipLaunchKernelGGL(k_bigfile_finish, dim3(nfiles), dim3(kWG), 0, st, files, nfiles, file_nodes, out32);
   return hipGetLastError();
 }
+
 
 }  // namespace sdcas

@@ -63,6 +63,23 @@ hipError_t dd_combine(DistWs& w, const uint64_t* keys, const uint8_t* has_key, c
                       const uint64_t* ids, uint32_t n, uint32_t world, uint64_t* rec, uint32_t* slot,
                       uint64_t* h_starts, uint64_t* h_u, hipStream_t st);
 
+// Stage 1 into fixed-capacity owner buckets, without a host synchronisation:
+// send[(r * cap + p) * 2 ..] = record p of owner r (p < counts[r] <= cap),
+// counts[world] (device int64), slot[i] = bucket position r * cap + p of file
+// i's record (or kSlotNoKey / kSlotDropped). *overflow (device) is set to 1
+// when an owner has more than cap records: the buckets are then incomplete
+// and the caller must use the exact path (dd_combine).
+hipError_t dd_combine_buckets(DistWs& w, const uint64_t* keys, const uint8_t* has_key, const int32_t* status,
+                              const uint64_t* ids, uint32_t n, uint32_t world, uint32_t cap, uint64_t* send,
+                              uint32_t* slot, int64_t* counts, uint32_t* overflow, hipStream_t st);
+
+// Stage 2 over received buckets: frec / erec hold world buckets of fcap / ecap
+// records, bucket r's first fcounts[r] / ecounts[r] valid (device int64).
+// result[r * fcap + p] answers file record p of bucket r (padding untouched).
+hipError_t dd_resolve_buckets(DistWs& w, const uint64_t* frec, uint32_t fcap, const int64_t* fcounts,
+                              const uint64_t* erec, uint32_t ecap, const int64_t* ecounts, uint32_t world,
+                              int64_t* result, hipStream_t st);
+
 // Stage 2 (owner). frec: nf received (key, min file id) records, erec: ne
 // received (key, min DB index) records of existing Objects. result[p] for
 // file record p = -(db+1) if an existing Object carries the key (the first in

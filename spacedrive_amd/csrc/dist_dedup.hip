@@ -185,16 +185,12 @@ void DistWs::release() {
   valid.release(); temp.release();
 }
 
-hipError_t dd_combine(DistWs& w, const uint64_t* keys, const uint8_t* has_key, const int32_t* status,
-                      const uint64_t* ids, uint32_t n, uint32_t world, uint64_t* rec, uint32_t* slot,
-                      uint64_t* h_starts, uint64_t* h_u, hipStream_t st) {
+// the combine up to its device outputs: rec, slot, w.starts[0..world] (n > 0)
+static hipError_t combine_core(DistWs& w, const uint64_t* keys, const uint8_t* has_key, const int32_t* status,
+                               const uint64_t* ids, uint32_t n, uint32_t world, uint64_t* rec, uint32_t* slot,
+                               hipStream_t st) {
   hipError_t e;
   if ((e = w.starts.ensure(world + 1))) return e;
-  if (n == 0) {
-    for (uint32_t r = 0; r <= world; ++r) h_starts[r] = 0;
-    *h_u = 0;
-    return hipSuccess;
-  }
   if ((e = ensure_n(w, n))) return e;
   if ((e = w.hi_a.ensure(n)) || (e = w.hi_b.ensure(n))) return e;
   hipLaunchKernelGGL(k_dd_prepare, dim3(blocks(n)), dim3(TB), 0, st, has_key, status, n, w.scan.p, slot);
@@ -220,6 +216,19 @@ hipError_t dd_combine(DistWs& w, const uint64_t* keys, const uint8_t* has_key, c
                      rec, slot);
   hipLaunchKernelGGL(k_dd_starts, dim3(blocks(world + 1)), dim3(TB), 0, st, rec, w.scan.p, w.nvalid.p, world,
                      w.starts.p);
+  return hipGetLastError();
+}
+
+hipError_t dd_combine(DistWs& w, const uint64_t* keys, const uint8_t* has_key, const int32_t* status,
+                      const uint64_t* ids, uint32_t n, uint32_t world, uint64_t* rec, uint32_t* slot,
+                      uint64_t* h_starts, uint64_t* h_u, hipStream_t st) {
+  hipError_t e;
+  if (n == 0) {
+    for (uint32_t r = 0; r <= world; ++r) h_starts[r] = 0;
+    *h_u = 0;
+    return hipSuccess;
+  }
+  if ((e = combine_core(w, keys, has_key, status, ids, n, world, rec, slot, st))) return e;
   uint32_t hs[1025];
   uint32_t* hp = world + 1 <= 1025 ? hs : new uint32_t[world + 1];
   e = hipMemcpyAsync(hp, w.starts.p, sizeof(uint32_t) * (world + 1), hipMemcpyDeviceToHost, st);
@@ -230,6 +239,75 @@ hipError_t dd_combine(DistWs& w, const uint64_t* keys, const uint8_t* has_key, c
   }
   if (hp != hs) delete[] hp;
   if (e) return e;
+  return hipGetLastError();
+}
+
+// ---- the combine into fixed-capacity owner buckets (no host sync) ---------------
+//
+// RCCL's all-to-all through torch needs every split size on the host, i.e.
+// a synchronisation to learn how many records go to each owner. With buckets
+// of a capacity the host picks in advance (dist_dedup.py: from the file
+// count and the previous call's fill), every exchange has equal splits and
+// nothing waits for the host; a bucket that would overflow raises a flag
+// that travels with the final counts, and the caller then reruns the exact
+// path. Record u of owner r goes to send[r * cap + (u - starts[r])].
+
+__global__ void k_dd_pack(const uint64_t* __restrict__ rec, const uint32_t* __restrict__ scan,
+                          const uint32_t* __restrict__ nv_p, const uint32_t* __restrict__ starts, uint32_t world,
+                          uint32_t cap, uint64_t* __restrict__ send, uint32_t* __restrict__ overflow) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t nv = *nv_p;
+  const uint32_t U = nv ? scan[nv - 1] : 0u;
+  if (u >= U) return;
+  const uint64_t key = rec[2 * (uint64_t)u];
+  const uint32_t r = dd_owner(key, world);
+  const uint32_t p = u - starts[r];
+  if (p >= cap) {
+    atomicOr(overflow, 1u);
+    return;
+  }
+  const uint64_t q = (uint64_t)r * cap + p;
+  send[2 * q] = key;
+  send[2 * q + 1] = rec[2 * (uint64_t)u + 1];
+}
+
+__global__ void k_dd_bucket_counts(const uint32_t* __restrict__ starts, uint32_t world, uint32_t cap,
+                                   int64_t* __restrict__ counts) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= world) return;
+  const uint32_t c = starts[r + 1] - starts[r];
+  counts[r] = c < cap ? c : cap;
+}
+
+// a file's record index -> its bucket position (codes of files without a
+// record are kept)
+__global__ void k_dd_slot_remap(const uint64_t* __restrict__ rec, const uint32_t* __restrict__ starts,
+                                uint32_t world, uint32_t cap, uint32_t n, uint32_t* __restrict__ slot) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t u = slot[i];
+  if (u >= kSlotDropped) return;
+  const uint32_t r = dd_owner(rec[2 * (uint64_t)u], world);
+  const uint32_t p = u - starts[r];
+  // a record past its bucket's capacity was not sent (k_dd_pack raised the
+  // overflow flag, the caller discards this pass): keep apply's reads in
+  // bounds by pointing the file nowhere
+  slot[i] = p < cap ? r * cap + p : kSlotNoKey;
+}
+
+hipError_t dd_combine_buckets(DistWs& w, const uint64_t* keys, const uint8_t* has_key, const int32_t* status,
+                              const uint64_t* ids, uint32_t n, uint32_t world, uint32_t cap, uint64_t* send,
+                              uint32_t* slot, int64_t* counts, uint32_t* overflow, hipStream_t st) {
+  hipError_t e;
+  if ((e = hipMemsetAsync(overflow, 0, sizeof(uint32_t), st))) return e;
+  if (n == 0) return hipMemsetAsync(counts, 0, sizeof(int64_t) * world, st);
+  if ((e = w.ukey.ensure(2 * (size_t)n))) return e;
+  if ((e = combine_core(w, keys, has_key, status, ids, n, world, w.ukey.p, slot, st))) return e;
+  hipLaunchKernelGGL(k_dd_pack, dim3(blocks(n)), dim3(TB), 0, st, w.ukey.p, w.scan.p, w.nvalid.p, w.starts.p, world,
+                     cap, send, overflow);
+  hipLaunchKernelGGL(k_dd_bucket_counts, dim3(blocks(world)), dim3(TB), 0, st, w.starts.p, world, cap, counts);
+  if (slot)
+    hipLaunchKernelGGL(k_dd_slot_remap, dim3(blocks(n)), dim3(TB), 0, st, w.ukey.p, w.starts.p, world, cap, n, slot);
   return hipGetLastError();
 }
 
@@ -305,6 +383,64 @@ hipError_t dd_resolve(DistWs& w, const uint64_t* frec, uint32_t nf, const uint64
   if (ne) hipLaunchKernelGGL(k_ht_insert, dim3(blocks(ne)), dim3(TB), 0, st, erec, ne, tk, tm, mask, shift, 1u, nullptr);
   hipLaunchKernelGGL(k_ht_insert, dim3(blocks(nf)), dim3(TB), 0, st, frec, nf, tk, tm, mask, shift, 0u, w.tpos.p);
   hipLaunchKernelGGL(k_ht_answer, dim3(blocks(nf)), dim3(TB), 0, st, w.tpos.p, nf, w.tmin.p, result);
+  return hipGetLastError();
+}
+
+// Resolve over received buckets: world buckets of `cap` records each, bucket
+// r holding counts[r] valid records (the rest is padding, skipped).
+constexpr uint32_t kNoEntry = 0xFFFFFFFFu;
+
+__global__ void k_ht_insert_b(const uint64_t* __restrict__ rec, uint32_t cap, const int64_t* __restrict__ counts,
+                              uint32_t total, unsigned long long* __restrict__ tkey,
+                              unsigned long long* __restrict__ tmin, uint32_t mask, uint32_t shift, uint32_t side,
+                              uint32_t* __restrict__ pos_out) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= total) return;
+  const uint32_t r = q / cap, p = q - r * cap;
+  if ((int64_t)p >= counts[r]) {
+    if (pos_out) pos_out[q] = kNoEntry;
+    return;
+  }
+  const uint32_t h = ht_find(tkey, rec[2 * (uint64_t)q], mask, shift);
+  const unsigned long long v = rec[2 * (uint64_t)q + 1];
+  unsigned long long* m = &tmin[2 * (uint64_t)h + side];
+  if (__hip_atomic_load(m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > v) atomicMin(m, v);
+  if (pos_out) pos_out[q] = h;
+}
+
+__global__ void k_ht_answer_b(const uint32_t* __restrict__ pos, uint32_t total, const uint64_t* __restrict__ tmin,
+                              int64_t* __restrict__ result) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= total) return;
+  const uint32_t h = pos[q];
+  if (h == kNoEntry) return;  // padding: nobody reads its answer
+  const uint64_t e = tmin[2 * (uint64_t)h + 1];
+  result[q] = e != ~0ull ? -(int64_t)e - 1 : (int64_t)tmin[2 * (uint64_t)h];
+}
+
+hipError_t dd_resolve_buckets(DistWs& w, const uint64_t* frec, uint32_t fcap, const int64_t* fcounts,
+                              const uint64_t* erec, uint32_t ecap, const int64_t* ecounts, uint32_t world,
+                              int64_t* result, hipStream_t st) {
+  hipError_t e;
+  const uint32_t nf = world * fcap, ne = world * ecap;
+  if (nf == 0) return hipSuccess;
+  uint64_t cap = 1024;
+  while (cap < 2 * ((uint64_t)nf + ne)) cap <<= 1;
+  if (cap > (1ull << 31)) return hipErrorInvalidValue;
+  if ((e = w.tkey.ensure(cap + 1)) || (e = w.tmin.ensure(2 * (cap + 1))) || (e = w.tpos.ensure(nf))) return e;
+  const uint32_t mask = (uint32_t)(cap - 1);
+  const uint32_t shift = 64u - (uint32_t)__builtin_ctzll(cap);
+  if ((e = hipMemsetAsync(w.tkey.p, 0xFF, sizeof(uint64_t) * (cap + 1), st)) ||
+      (e = hipMemsetAsync(w.tmin.p, 0xFF, sizeof(uint64_t) * 2 * (cap + 1), st)))
+    return e;
+  auto* tk = reinterpret_cast<unsigned long long*>(w.tkey.p);
+  auto* tm = reinterpret_cast<unsigned long long*>(w.tmin.p);
+  if (ne)
+    hipLaunchKernelGGL(k_ht_insert_b, dim3(blocks(ne)), dim3(TB), 0, st, erec, ecap, ecounts, ne, tk, tm, mask, shift,
+                       1u, nullptr);
+  hipLaunchKernelGGL(k_ht_insert_b, dim3(blocks(nf)), dim3(TB), 0, st, frec, fcap, fcounts, nf, tk, tm, mask, shift, 0u,
+                     w.tpos.p);
+  hipLaunchKernelGGL(k_ht_answer_b, dim3(blocks(nf)), dim3(TB), 0, st, w.tpos.p, nf, w.tmin.p, result);
   return hipGetLastError();
 }
 

@@ -26,7 +26,6 @@
 #include "../../include/sdcas.h"
 #include "../../include/sdcas_bench.h"
 #include "b3_batch.h"
-#include "dedup.h"
 #include "dist_dedup.h"
 #include "synth.h"
 
@@ -77,6 +76,7 @@ struct Slot {
   bool busy = false, res32 = false;
   size_t n = 0;
   uint64_t used = 0, chunks = 0;
+  uint64_t content = 0;  // input bytes whose results this slot's batch makes final (progress)
   std::vector<size_t> idx;  // caller index of message k
   const uint8_t* src = nullptr;  // message bytes DMA'd from here instead of h (a pinned caller buffer)
   uint64_t* offs() { return hm; }
@@ -105,11 +105,9 @@ struct sdcas_ctx {
   DevBuf<uint32_t> d_file_nodes;
   Slot slots[2];  // double-buffered pinned staging (host fills one, GPU hashes the other)
 
-  // dedup
-  DedupWorkspace dws;
-  DevBuf<uint64_t> dd_key_a, dd_key_b, dd_keys, dd_ekeys, dd_ekeys_sorted;
-  DevBuf<uint32_t> dd_idx_a, dd_idx_b, dd_head, dd_nvalid, dd_eidx;
-  DevBuf<uint8_t> dd_valid, dd_temp, dd_has;
+  // sdcas_dedup's device copies of the caller's host arrays
+  DevBuf<uint64_t> dd_keys, dd_ekeys, dd_ids;
+  DevBuf<uint8_t> dd_has;
   DevBuf<int32_t> dd_status;
   DevBuf<int64_t> dd_link;
   DevBuf<unsigned long long> dd_counts;
@@ -123,6 +121,23 @@ struct sdcas_ctx {
   DevBuf<uint32_t> sm_nodes;
   DevBuf<PieceDesc> sm_pieces;
   bool sm_active = false;
+  DevBuf<uint32_t> piece_ctr;  // the persistent piece kernels' work counter
+  int piece_variant = -1;
+
+  // Every call that enqueues work on the context's device scratch (the
+  // workspaces above) may name its own stream. The scratch is shared, so a
+  // call first makes its stream wait for the previous call's work (the event
+  // recorded at the end of that call), then records the event anew: calls on
+  // one context are ordered on the device as they are on the host, whatever
+  // streams they name.
+  hipEvent_t scratch_ev = nullptr;
+  hipStream_t scratch_st = nullptr;
+  bool scratch_pending = false;
+
+  // progress / cancellation of the path APIs (sdcas_options, sdcas_set_progress)
+  sdcas_progress_fn progress = nullptr;
+  void* progress_user = nullptr;
+  const volatile int32_t* cancel = nullptr;
 
   // profiling
   bool profile = false;
@@ -141,6 +156,24 @@ struct sdcas_ctx {
   int hip_fail(hipError_t e, const char* what) {
     return fail(e == hipErrorOutOfMemory ? SDCAS_E_OOM : SDCAS_E_HIP, "%s: %s", what, hipGetErrorString(e));
   }
+  // before enqueuing on st: wait for the previous call's use of the scratch
+  hipError_t fence_in(hipStream_t st) {
+    if (!scratch_pending || st == scratch_st) return hipSuccess;
+    return hipStreamWaitEvent(st, scratch_ev, 0);
+  }
+  // after enqueuing on st
+  hipError_t fence_out(hipStream_t st) {
+    hipError_t e = hipSuccess;
+    if (!scratch_ev && (e = hipEventCreateWithFlags(&scratch_ev, hipEventDisableTiming))) return e;
+    if ((e = hipEventRecord(scratch_ev, st))) return e;
+    scratch_st = st;
+    scratch_pending = true;
+    return hipSuccess;
+  }
+  bool cancelled() const { return cancel && __atomic_load_n(cancel, __ATOMIC_ACQUIRE) != 0; }
+  void report(uint64_t done, uint64_t total) {
+    if (progress) progress(progress_user, done, total);
+  }
   hipEvent_t event() {
     if (!ev_free.empty()) {
       hipEvent_t e = ev_free.back();
@@ -157,7 +190,8 @@ namespace {
 
 int reserve_ws(sdcas_ctx* c, size_t max_msgs, uint64_t max_chunks) {
   hipError_t e;
-  if (max_msgs > 0xFFFFFFF0ull) return c->fail(SDCAS_E_CAPACITY, "batch of %zu messages exceeds 2^32", max_msgs);
+  // the chunk scan takes an int count (hipcub)
+  if (max_msgs > SDCAS_MAX_BATCH) return c->fail(SDCAS_E_CAPACITY, "batch of %zu messages exceeds 2^31 - 1", max_msgs);
   if ((e = c->ws_S.ensure(max_msgs + 1))) return c->hip_fail(e, "workspace S");
   // room for the quad layout's padding too: < 4 dead slots per message (of
   // as many messages as the workspace takes)
@@ -298,14 +332,26 @@ int slot_submit(sdcas_ctx* c, Slot& s, bool res32) {
   return SDCAS_OK;
 }
 
-// Wait for the slot's batch and hand message k's result to sink(k, ptr).
+// Progress of one path call: bytes of input whose results are final.
+struct Progress {
+  sdcas_ctx* c;
+  uint64_t total = 0, done = 0;
+  void add(uint64_t bytes) {
+    done += bytes;
+    c->report(done, total);
+  }
+};
+
+// Wait for the slot's batch, hand message k's result to sink(k, ptr) and
+// report the slot's input bytes as done.
 template <class Sink>
-int slot_complete(sdcas_ctx* c, Slot& s, Sink sink) {
+int slot_complete(sdcas_ctx* c, Slot& s, Sink sink, Progress* pr = nullptr) {
   if (!s.busy) return SDCAS_OK;
   s.busy = false;
   hipError_t e = hipEventSynchronize(s.ev);
   if (e) return c->hip_fail(e, "batch");
   for (size_t k = 0; k < s.n; ++k) sink(k, s.res() + (s.res32 ? 32 : 8) * k);
+  if (pr) pr->add(s.content);
   return SDCAS_OK;
 }
 
@@ -313,13 +359,18 @@ int slot_complete(sdcas_ctx* c, Slot& s, Sink sink) {
 // two staging slots (one window filled by `fill` while the GPU hashes the
 // other); `fill(k, dst, off, len)` provides bytes [off, off+len) of item k
 // and returns a status (0 ok). Digests go to out32_host[32 * out_index].
+// Cancellation is checked once per window: items whose every piece was
+// submitted by then are finished, the rest get SDCAS_STATUS_CANCELLED and
+// *cancelled is set.
 struct BigItem {
   uint64_t len;
   uint64_t out_index;
 };
 
 template <class Fill>
-int run_big(sdcas_ctx* c, const std::vector<BigItem>& items, uint8_t* out32_host, Fill fill, int32_t* status) {
+int run_big(sdcas_ctx* c, const std::vector<BigItem>& items, uint8_t* out32_host, Fill fill, int32_t* status,
+            Progress& pr, bool* cancelled) {
+  *cancelled = false;
   if (items.empty()) return SDCAS_OK;
   hipError_t e;
   int rc;
@@ -339,15 +390,18 @@ int run_big(sdcas_ctx* c, const std::vector<BigItem>& items, uint8_t* out32_host
   if ((e = c->d_file_nodes.ensure(8 * nodes + 8))) return c->hip_fail(e, "file nodes");
   if ((e = c->d_files.ensure(items.size()))) return c->hip_fail(e, "file descs");
   if ((e = c->d_out32.ensure(32 * items.size()))) return c->hip_fail(e, "device digests");
+  if ((e = c->piece_ctr.ensure(1))) return c->hip_fail(e, "piece counter");
   hipStream_t st = c->stream;
   int cur = 0;
   size_t npieces = 0;
-  uint64_t used = 0;
+  uint64_t used = 0, content = 0;
   auto wait_slot = [&](Slot& s) -> int {
     if (!s.busy) return SDCAS_OK;
     s.busy = false;
     hipError_t ee = hipEventSynchronize(s.ev);
-    return ee ? c->hip_fail(ee, "piece window") : SDCAS_OK;
+    if (ee) return c->hip_fail(ee, "piece window");
+    pr.add(s.content);
+    return SDCAS_OK;
   };
   auto flush = [&]() -> int {
     if (!npieces) return SDCAS_OK;
@@ -358,21 +412,31 @@ int run_big(sdcas_ctx* c, const std::vector<BigItem>& items, uint8_t* out32_host
     if ((ee = hipMemcpyAsync(s.d_blob.p, s.h, used, hipMemcpyHostToDevice, st)) ||
         (ee = hipMemcpyAsync(dp, hp, sizeof(PieceDesc) * npieces, hipMemcpyHostToDevice, st)))
       return c->hip_fail(ee, "H2D pieces");
-    if ((ee = piece_hash(s.d_blob.p, dp, (uint32_t)npieces, c->d_file_nodes.p, st)))
+    if ((ee = piece_hash(s.d_blob.p, dp, (uint32_t)npieces, c->d_file_nodes.p, c->piece_ctr.p, c->piece_variant, st)))
       return c->hip_fail(ee, "piece_hash");
     if ((ee = hipEventRecord(s.ev, st))) return c->hip_fail(ee, "event");
     s.busy = true;
+    s.content = content;
     cur ^= 1;
     npieces = 0;
     used = 0;
+    content = 0;
     return wait_slot(c->slots[cur]);  // the next window's buffers are free again
   };
   if ((rc = wait_slot(c->slots[cur]))) return rc;
-  for (size_t i = 0; i < items.size(); ++i) {
+  size_t complete = items.size();  // items [0, complete) have every piece submitted
+  for (size_t i = 0; i < items.size() && !*cancelled; ++i) {
     const uint64_t len = items[i].len;
     for (uint64_t off = 0; off < len; off += piece_bytes) {
       const uint32_t pl = (uint32_t)std::min<uint64_t>(piece_bytes, len - off);
-      if (used + pl > window && (rc = flush())) return rc;
+      if (used + pl > window) {
+        if ((rc = flush())) return rc;
+        if (c->cancelled()) {
+          *cancelled = true;
+          complete = i;  // item i has pieces left (or none submitted yet): not complete
+          break;
+        }
+      }
       Slot& s = c->slots[cur];
       int st_i = fill(i, s.h + used, off, pl);
       if (st_i) {
@@ -386,21 +450,30 @@ int run_big(sdcas_ctx* c, const std::vector<BigItem>& items, uint8_t* out32_host
       pd.len = pl;
       reinterpret_cast<PieceDesc*>(s.hm)[npieces++] = pd;
       used += align16(pl);
+      content += pl;
     }
+  }
+  if (*cancelled) {
+    npieces = 0;  // pieces of an incomplete item are never hashed
+    used = content = 0;
   }
   if ((rc = flush())) return rc;
   for (Slot& s : c->slots)
     if ((rc = wait_slot(s))) return rc;
-  if ((e = hipMemcpyAsync(c->d_files.p, files.data(), sizeof(FileDesc) * files.size(), hipMemcpyHostToDevice,
-                          st)))
-    return c->hip_fail(e, "H2D files");
-  if ((e = bigfile_finish(c->d_files.p, (uint32_t)files.size(), c->d_file_nodes.p, c->d_out32.p, st)))
-    return c->hip_fail(e, "bigfile_finish");
-  std::vector<uint8_t> tmp(32 * items.size());
-  if ((e = hipMemcpyAsync(tmp.data(), c->d_out32.p, tmp.size(), hipMemcpyDeviceToHost, st)) ||
-      (e = hipStreamSynchronize(st)))
-    return c->hip_fail(e, "D2H big digests");
-  for (size_t i = 0; i < items.size(); ++i) memcpy(out32_host + 32 * items[i].out_index, &tmp[32 * i], 32);
+  const size_t nf = complete;
+  if (nf) {
+    if ((e = hipMemcpyAsync(c->d_files.p, files.data(), sizeof(FileDesc) * nf, hipMemcpyHostToDevice, st)))
+      return c->hip_fail(e, "H2D files");
+    if ((e = bigfile_finish(c->d_files.p, (uint32_t)nf, c->d_file_nodes.p, c->d_out32.p, st)))
+      return c->hip_fail(e, "bigfile_finish");
+    std::vector<uint8_t> tmp(32 * nf);
+    if ((e = hipMemcpyAsync(tmp.data(), c->d_out32.p, tmp.size(), hipMemcpyDeviceToHost, st)) ||
+        (e = hipStreamSynchronize(st)))
+      return c->hip_fail(e, "D2H big digests");
+    for (size_t i = 0; i < nf; ++i) memcpy(out32_host + 32 * items[i].out_index, &tmp[32 * i], 32);
+  }
+  for (size_t i = nf; i < items.size(); ++i)
+    if (status && !status[items[i].out_index]) status[items[i].out_index] = SDCAS_STATUS_CANCELLED;
   return SDCAS_OK;
 }
 
@@ -528,6 +601,9 @@ int sdcas_init(const sdcas_options* opts, sdcas_ctx** out) {
     dev = opts->device;
     if (opts->io_threads) c->io_threads = opts->io_threads;
     if (opts->staging_bytes) c->staging_bytes = std::max<uint64_t>(opts->staging_bytes, 1ull << 20);
+    c->progress = opts->progress;
+    c->progress_user = opts->progress_user;
+    c->cancel = opts->cancel;
   }
   if (dev < 0) (void)hipGetDevice(&dev);
   if (dev >= count) {
@@ -547,13 +623,12 @@ void sdcas_destroy(sdcas_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (auto* b : {&c->ws_S, &c->ws_total, &c->ws_soffs, &c->ws_slens, &c->dd_key_a, &c->dd_key_b,
-                  &c->dd_keys, &c->dd_ekeys, &c->dd_ekeys_sorted})
+  if (c->scratch_ev) (void)hipEventSynchronize(c->scratch_ev);
+  for (auto* b : {&c->ws_S, &c->ws_total, &c->ws_soffs, &c->ws_slens, &c->dd_keys, &c->dd_ekeys, &c->dd_ids})
     b->release();
-  for (auto* b : {&c->ws_tile_first, &c->ws_nodes, &c->ws_perm, &c->ws_sort_keys, &c->d_file_nodes, &c->dd_idx_a, &c->dd_idx_b, &c->dd_head,
-                  &c->dd_nvalid, &c->dd_eidx})
+  for (auto* b : {&c->ws_tile_first, &c->ws_nodes, &c->ws_perm, &c->ws_sort_keys, &c->d_file_nodes, &c->piece_ctr})
     b->release();
-  for (auto* b : {&c->ws_scan, &c->d_out32, &c->dd_valid, &c->dd_temp, &c->dd_has}) b->release();
+  for (auto* b : {&c->ws_scan, &c->d_out32, &c->dd_has}) b->release();
   c->d_files.release();
   c->dd_status.release();
   c->dd_link.release();
@@ -566,11 +641,21 @@ void sdcas_destroy(sdcas_ctx* c) {
   for (auto e : c->ev_free) (void)hipEventDestroy(e);
   for (auto& p : c->ev_leaf) (void)hipEventDestroy(p.first), (void)hipEventDestroy(p.second);
   for (auto& p : c->ev_all) (void)hipEventDestroy(p.first), (void)hipEventDestroy(p.second);
+  if (c->scratch_ev) (void)hipEventDestroy(c->scratch_ev);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
 
 const char* sdcas_last_error(const sdcas_ctx* c) { return c ? c->err.c_str() : "no context"; }
+
+int sdcas_set_progress(sdcas_ctx* c, sdcas_progress_fn progress, void* user, const volatile int32_t* cancel) {
+  if (!c) return SDCAS_E_INVALID;
+  std::lock_guard<std::mutex> g(c->mu);
+  c->progress = progress;
+  c->progress_user = user;
+  c->cancel = cancel;
+  return SDCAS_OK;
+}
 
 uint64_t sdcas_cas_message_len(uint64_t size) { return size <= kMin ? size + 8 : SDCAS_SAMPLED_MESSAGE_LEN; }
 
@@ -589,22 +674,43 @@ void sdcas_digest_to_hex(const uint8_t d[32], char out[65]) {
   out[64] = 0;
 }
 
+// A device-stream call: holds the context's mutex, orders its stream after
+// the previous call's use of the device scratch (sdcas_ctx::fence_in) and
+// marks its own use when it returns.
+struct DevCall {
+  sdcas_ctx* c;
+  std::lock_guard<std::mutex> g;
+  hipStream_t st;
+  int rc = SDCAS_OK;
+  DevCall(sdcas_ctx* cc, void* stream) : c(cc), g(cc->mu), st(stream ? (hipStream_t)stream : cc->stream) {
+    (void)hipSetDevice(c->device);
+    hipError_t e = c->fence_in(st);
+    if (e) rc = c->hip_fail(e, "stream wait");
+  }
+  ~DevCall() { (void)c->fence_out(st); }
+};
+
 int sdcas_dev_reserve(sdcas_ctx* c, size_t max_msgs, uint64_t max_chunks) {
   if (!c) return SDCAS_E_INVALID;
   std::lock_guard<std::mutex> g(c->mu);
   (void)hipSetDevice(c->device);
+  // the workspace is reallocated: no earlier call may still be using it
+  if (c->scratch_pending) {
+    hipError_t e = hipEventSynchronize(c->scratch_ev);
+    if (e) return c->hip_fail(e, "sync");
+  }
   return reserve_ws(c, max_msgs, max_chunks);
 }
 
 int sdcas_dev_hash_messages(sdcas_ctx* c, const uint8_t* d_blob, const uint64_t* d_offsets, const uint64_t* d_lens,
                             size_t n, uint8_t* d_out32, uint64_t* d_out_keys, void* stream) {
   if (!c || (n && (!d_blob || !d_offsets || !d_lens))) return SDCAS_E_INVALID;
-  std::lock_guard<std::mutex> g(c->mu);
   if (n == 0) return SDCAS_OK;
+  DevCall call(c, stream);
+  if (call.rc) return call.rc;
   if (n > c->ws.cap_msgs || !c->ws.S)
     return c->fail(SDCAS_E_CAPACITY, "dev_hash_messages: %zu messages > reserved %u", n, c->ws.cap_msgs);
-  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-  return launch_batch(c, d_blob, d_offsets, d_lens, (uint32_t)n, d_out32, d_out_keys, st);
+  return launch_batch(c, d_blob, d_offsets, d_lens, (uint32_t)n, d_out32, d_out_keys, call.st);
 }
 
 int sdcas_dev_sync(sdcas_ctx* c, void* stream) {
@@ -622,6 +728,7 @@ int sdcas_dev_sync(sdcas_ctx* c, void* stream) {
 
 int sdcas_dev_profile(sdcas_ctx* c, int enable) {
   if (!c) return SDCAS_E_INVALID;
+  std::lock_guard<std::mutex> g(c->mu);
   c->profile = enable != 0;
   for (auto* v : {&c->ev_all, &c->ev_leaf}) {
     for (auto& p : *v) c->ev_free.push_back(p.first), c->ev_free.push_back(p.second);
@@ -646,6 +753,7 @@ static float mean_ms(std::vector<std::pair<hipEvent_t, hipEvent_t>>& v) {
 
 int sdcas_dev_last_kernel_ms(sdcas_ctx* c, float* leaf_ms, float* total_ms) {
   if (!c) return SDCAS_E_INVALID;
+  std::lock_guard<std::mutex> g(c->mu);
   if (leaf_ms) *leaf_ms = mean_ms(c->ev_leaf);
   if (total_ms) *total_ms = mean_ms(c->ev_all);
   return SDCAS_OK;
@@ -665,16 +773,34 @@ static bool host_pinned(const void* p) {
   return a.type == hipMemoryTypeHost && a.hostPointer != nullptr;
 }
 
+// The path calls hold the context's mutex and run on its stream; they order
+// themselves after any device call that used the scratch on another stream,
+// and mark their own use when they return.
+struct PathCall {
+  sdcas_ctx* c;
+  std::lock_guard<std::mutex> g;
+  int rc = SDCAS_OK;
+  explicit PathCall(sdcas_ctx* cc) : c(cc), g(cc->mu) {
+    (void)hipSetDevice(c->device);
+    hipError_t e = c->fence_in(c->stream);
+    if (e) rc = c->hip_fail(e, "stream wait");
+  }
+  ~PathCall() { (void)c->fence_out(c->stream); }
+};
+
 static int hash_host_messages(sdcas_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* lens,
                               size_t n, uint8_t* out32, uint64_t* keys) {
   if (!c || (n && (!blob || !offsets || !lens))) return SDCAS_E_INVALID;
-  std::lock_guard<std::mutex> g(c->mu);
-  (void)hipSetDevice(c->device);
+  if (n > SDCAS_MAX_BATCH) return c->fail(SDCAS_E_CAPACITY, "batch of %zu messages exceeds 2^31 - 1", n);
+  PathCall call(c);
+  if (call.rc) return call.rc;
   const uint64_t big_cut = 1024ull * kTile;  // > 1 MiB: piece path
   const uint64_t cap = c->staging_bytes;
   const size_t cap_n = (size_t)(cap / 128) + 1;
   int rc;
   if ((rc = slots_prepare(c, cap, cap_n))) return rc;
+  Progress pr{c};
+  for (size_t i = 0; i < n; ++i) pr.total += lens[i];
   std::vector<BigItem> big;
   int cur = 0;
   // Direct DMA: a caller buffer in pinned (page-locked) host memory whose
@@ -686,19 +812,22 @@ static int hash_host_messages(sdcas_ctx* c, const uint8_t* blob, const uint64_t*
     if ((offsets[i] & 15) || (i && offsets[i] < offsets[i - 1] + lens[i - 1])) direct = false;
   uint64_t base = 0;  // caller offset of the current direct slot's first byte
   auto begin = [&](Slot& s) -> int {
-    const int r = slot_complete(c, s, [&](size_t k, const uint8_t* res) {
-      const size_t i = s.idx[k];
-      if (out32) memcpy(out32 + 32 * i, res, 32);
-      if (keys) {
-        uint64_t kk = 0;
-        if (s.res32)
-          for (int t = 0; t < 8; ++t) kk = (kk << 8) | res[t];
-        else
-          memcpy(&kk, res, 8);
-        keys[i] = kk;
-      }
-    });
-    s.n = 0, s.used = 0, s.chunks = 0;
+    const int r = slot_complete(
+        c, s,
+        [&](size_t k, const uint8_t* res) {
+          const size_t i = s.idx[k];
+          if (out32) memcpy(out32 + 32 * i, res, 32);
+          if (keys) {
+            uint64_t kk = 0;
+            if (s.res32)
+              for (int t = 0; t < 8; ++t) kk = (kk << 8) | res[t];
+            else
+              memcpy(&kk, res, 8);
+            keys[i] = kk;
+          }
+        },
+        &pr);
+    s.n = 0, s.used = 0, s.chunks = 0, s.content = 0;
     s.idx.clear();
     s.src = nullptr;
     return r;
@@ -715,6 +844,7 @@ static int hash_host_messages(sdcas_ctx* c, const uint8_t* blob, const uint64_t*
     }
     return slot_submit(c, s, out32 != nullptr);
   };
+  bool cancelled = false;
   if ((rc = begin(c->slots[cur]))) return rc;
   for (size_t i = 0; i < n; ++i) {
     const uint64_t L = lens[i];
@@ -729,6 +859,7 @@ static int hash_host_messages(sdcas_ctx* c, const uint8_t* blob, const uint64_t*
       cur ^= 1;
       s = &c->slots[cur];
       if ((rc = begin(*s))) return rc;
+      if ((cancelled = c->cancelled())) break;
     }
     if (direct && s->n == 0) base = offsets[i];
     s->offs()[s->n] = direct ? offsets[i] - base : s->used;
@@ -737,18 +868,19 @@ static int hash_host_messages(sdcas_ctx* c, const uint8_t* blob, const uint64_t*
     s->n++;
     s->used = direct ? offsets[i] + L - base : s->used + align16(L);
     s->chunks += chunks_of(L);
+    s->content += L;
   }
-  if ((rc = fill_submit(c->slots[cur]))) return rc;
+  if (!cancelled && (rc = fill_submit(c->slots[cur]))) return rc;
   for (Slot& s : c->slots)
     if ((rc = begin(s))) return rc;
-  if (!big.empty()) {
+  if (!cancelled && !big.empty()) {
     std::vector<uint8_t> d32(32 * n);
     rc = run_big(c, big, d32.data(),
                  [&](size_t k, uint8_t* dst, uint64_t off, uint32_t len) {
                    memcpy(dst, blob + offsets[big[k].out_index] + off, len);
                    return 0;
                  },
-                 nullptr);
+                 nullptr, pr, &cancelled);
     if (rc) return rc;
     for (auto& b : big) {
       if (out32) memcpy(out32 + 32 * b.out_index, &d32[32 * b.out_index], 32);
@@ -759,7 +891,7 @@ static int hash_host_messages(sdcas_ctx* c, const uint8_t* blob, const uint64_t*
       }
     }
   }
-  return SDCAS_OK;
+  return cancelled ? c->fail(SDCAS_E_CANCELLED, "cancelled") : SDCAS_OK;
 }
 
 int sdcas_hash_messages(sdcas_ctx* c, const uint8_t* blob, const uint64_t* offsets, const uint64_t* lens, size_t n,
@@ -777,8 +909,9 @@ int sdcas_cas_ids_from_messages(sdcas_ctx* c, const uint8_t* blob, const uint64_
 int sdcas_cas_ids(sdcas_ctx* c, const char* const* paths, const uint64_t* sizes, size_t n, uint64_t* out_keys,
                   int32_t* out_status) {
   if (!c || (n && (!paths || !sizes || !out_keys || !out_status))) return SDCAS_E_INVALID;
-  std::lock_guard<std::mutex> g(c->mu);
-  (void)hipSetDevice(c->device);
+  if (n > SDCAS_MAX_BATCH) return c->fail(SDCAS_E_CAPACITY, "batch of %zu files exceeds 2^31 - 1", n);
+  PathCall call(c);
+  if (call.rc) return call.rc;
   const uint64_t cap = c->staging_bytes;
   const size_t cap_n = (size_t)(cap / 128) + 1;
   int rc;
@@ -786,15 +919,20 @@ int sdcas_cas_ids(sdcas_ctx* c, const char* const* paths, const uint64_t* sizes,
   // slot sizes: the message the indexer's size predicts (cas.rs:27); a file
   // that grew is retried in a later batch with its actual size
   std::vector<uint64_t> want(n);
+  Progress pr{c};
   // (+1: room for the byte that tells a grown file from an unchanged one)
-  for (size_t i = 0; i < n; ++i) want[i] = sdcas_cas_message_len(sizes[i]) + (sizes[i] <= kMin ? 1 : 0);
+  for (size_t i = 0; i < n; ++i) {
+    want[i] = sdcas_cas_message_len(sizes[i]) + (sizes[i] <= kMin ? 1 : 0);
+    pr.total += sdcas_cas_message_len(sizes[i]) - 8;  // file bytes cas.rs reads
+  }
   std::vector<size_t> todo(n);
   for (size_t i = 0; i < n; ++i) todo[i] = i;
   int cur = 0;
   auto drain = [&](Slot& s) -> int {
-    return slot_complete(c, s, [&](size_t k, const uint8_t* r) { memcpy(&out_keys[s.idx[k]], r, 8); });
+    return slot_complete(c, s, [&](size_t k, const uint8_t* r) { memcpy(&out_keys[s.idx[k]], r, 8); }, &pr);
   };
-  for (int round = 0; round < 4 && !todo.empty(); ++round) {
+  bool cancelled = false;
+  for (int round = 0; round < 4 && !todo.empty() && !cancelled; ++round) {
     std::vector<size_t> retry;
     size_t p = 0;
     while (p < todo.size()) {
@@ -802,6 +940,12 @@ int sdcas_cas_ids(sdcas_ctx* c, const char* const* paths, const uint64_t* sizes,
       // — a whole-file cas message of a file grown past it — gets its own)
       Slot& s = c->slots[cur];
       if ((rc = drain(s))) return rc;
+      if ((cancelled = c->cancelled())) {
+        for (size_t k = p; k < todo.size(); ++k) out_status[todo[k]] = SDCAS_STATUS_CANCELLED;
+        for (size_t i : retry) out_status[i] = SDCAS_STATUS_CANCELLED;
+        retry.clear();
+        break;
+      }
       std::vector<uint64_t> slot_off;
       uint64_t used = 0;
       size_t q = p;
@@ -820,7 +964,7 @@ int sdcas_cas_ids(sdcas_ctx* c, const char* const* paths, const uint64_t* sizes,
         const size_t i = todo[p + k];
         st[k] = read_cas_message(paths[i], sizes[i], s.h + slot_off[k], align16(want[i]), &mlen[k], &retry_len[k]);
       });
-      s.n = 0, s.chunks = 0, s.used = used;
+      s.n = 0, s.chunks = 0, s.used = used, s.content = 0;
       s.idx.clear();
       for (size_t k = 0; k < m; ++k) {
         const size_t i = todo[p + k];
@@ -830,6 +974,7 @@ int sdcas_cas_ids(sdcas_ctx* c, const char* const* paths, const uint64_t* sizes,
           continue;
         }
         out_status[i] = st[k];
+        s.content += sdcas_cas_message_len(sizes[i]) - 8;
         if (st[k]) continue;
         s.offs()[s.n] = slot_off[k];
         s.lens()[s.n] = mlen[k];
@@ -838,6 +983,7 @@ int sdcas_cas_ids(sdcas_ctx* c, const char* const* paths, const uint64_t* sizes,
         s.chunks += chunks_of(mlen[k]);
       }
       if ((rc = slot_submit(c, s, false))) return rc;
+      if (!s.n) pr.add(s.content);  // nothing to hash: the slot's files are final now
       cur ^= 1;
       p = q;
     }
@@ -845,14 +991,15 @@ int sdcas_cas_ids(sdcas_ctx* c, const char* const* paths, const uint64_t* sizes,
       if ((rc = drain(s))) return rc;
     todo.swap(retry);
   }
-  for (size_t i : todo) out_status[i] = EAGAIN;  // kept growing while being read
-  return SDCAS_OK;
+  for (size_t i : todo) out_status[i] = cancelled ? SDCAS_STATUS_CANCELLED : EAGAIN;  // EAGAIN: kept growing
+  return cancelled ? c->fail(SDCAS_E_CANCELLED, "cancelled") : SDCAS_OK;
 }
 
 int sdcas_checksums(sdcas_ctx* c, const char* const* paths, size_t n, uint8_t* out32, int32_t* out_status) {
   if (!c || (n && (!paths || !out32 || !out_status))) return SDCAS_E_INVALID;
-  std::lock_guard<std::mutex> g(c->mu);
-  (void)hipSetDevice(c->device);
+  if (n > SDCAS_MAX_BATCH) return c->fail(SDCAS_E_CAPACITY, "batch of %zu files exceeds 2^31 - 1", n);
+  PathCall call(c);
+  if (call.rc) return call.rc;
   const uint64_t cap = c->staging_bytes, big_cut = 1024ull * kTile;
   const size_t cap_n = (size_t)(cap / 128) + 1;
   int rc;
@@ -868,20 +1015,24 @@ int sdcas_checksums(sdcas_ctx* c, const char* const* paths, size_t n, uint8_t* o
   });
   std::vector<size_t> small;
   std::vector<BigItem> big;
+  Progress pr{c};
   for (size_t i = 0; i < n; ++i) {
     out_status[i] = fst[i];
     if (fst[i]) continue;
+    pr.total += flen[i];
     if (flen[i] > big_cut) big.push_back({flen[i], i});
     else small.push_back(i);
   }
   int cur = 0;
   auto drain = [&](Slot& s) -> int {
-    return slot_complete(c, s, [&](size_t k, const uint8_t* r) { memcpy(out32 + 32 * s.idx[k], r, 32); });
+    return slot_complete(c, s, [&](size_t k, const uint8_t* r) { memcpy(out32 + 32 * s.idx[k], r, 32); }, &pr);
   };
+  bool cancelled = false;
   size_t p = 0;
   while (p < small.size()) {
     Slot& s = c->slots[cur];
     if ((rc = drain(s))) return rc;
+    if ((cancelled = c->cancelled())) break;
     std::vector<uint64_t> slot;
     uint64_t used = 0;
     size_t q = p;
@@ -902,16 +1053,17 @@ int sdcas_checksums(sdcas_ctx* c, const char* const* paths, size_t n, uint8_t* o
       }
       bool over = false;
       // hash.rs stops at its first short read; a file that grew since the
-      // stat above is hashed over its stat length
+      // stat above is hashed over its stat length (sdcas.h)
       st[k] = read_whole(fd, s.h + slot[k], flen[i] + 1, flen[i], &got[k], &over);
       if (over) got[k] = flen[i];
       close(fd);
     });
-    s.n = 0, s.chunks = 0, s.used = used;
+    s.n = 0, s.chunks = 0, s.used = used, s.content = 0;
     s.idx.clear();
     for (size_t k = 0; k < m; ++k) {
       const size_t i = small[p + k];
       out_status[i] = st[k];
+      s.content += flen[i];
       if (st[k]) continue;
       s.offs()[s.n] = slot[k];
       s.lens()[s.n] = got[k];
@@ -920,11 +1072,17 @@ int sdcas_checksums(sdcas_ctx* c, const char* const* paths, size_t n, uint8_t* o
       s.chunks += chunks_of(got[k]);
     }
     if ((rc = slot_submit(c, s, true))) return rc;
+    if (!s.n) pr.add(s.content);
     cur ^= 1;
     p = q;
   }
   for (Slot& s : c->slots)
     if ((rc = drain(s))) return rc;
+  if (cancelled) {
+    for (size_t k = p; k < small.size(); ++k) out_status[small[k]] = SDCAS_STATUS_CANCELLED;
+    for (auto& b : big) out_status[b.out_index] = SDCAS_STATUS_CANCELLED;
+    return c->fail(SDCAS_E_CANCELLED, "cancelled");
+  }
   if (!big.empty()) {
     std::vector<int> fds(big.size(), -1), oerr(big.size(), 0);
     for (size_t k = 0; k < big.size(); ++k) {
@@ -937,69 +1095,66 @@ int sdcas_checksums(sdcas_ctx* c, const char* const* paths, size_t n, uint8_t* o
                    if (fds[k] < 0) return oerr[k];
                    return pread_exact(fds[k], dst, len, off);  // hash.rs: 1 MiB reads to EOF
                  },
-                 out_status);
+                 out_status, pr, &cancelled);
     for (int fd : fds)
       if (fd >= 0) close(fd);
     if (rc) return rc;
     for (auto& b : big)
       if (!out_status[b.out_index]) memcpy(out32 + 32 * b.out_index, &d32[32 * b.out_index], 32);
   }
-  return SDCAS_OK;
+  return cancelled ? c->fail(SDCAS_E_CANCELLED, "cancelled") : SDCAS_OK;
 }
 
 
 // ---- dedup -----------------------------------------------------------------
+//
+// One implementation: the hash-table group-by of dist_dedup.hip. A single
+// rank (this call) runs it fused (dd_local: files and existing Objects go
+// straight into the resolve table; one insert pass per side, one apply
+// pass); a node of ranks runs the same stages split at the exchange
+// (sdcas_dev_dedup_combine / resolve / apply).
 
-static int dedup_reserve(sdcas_ctx* c, size_t n, size_t ne) {
-  hipError_t e;
-  const size_t m = std::max<size_t>(n, ne);
-  if ((e = c->dd_key_a.ensure(m)) || (e = c->dd_key_b.ensure(m)) || (e = c->dd_idx_a.ensure(m)) ||
-      (e = c->dd_idx_b.ensure(m)) || (e = c->dd_head.ensure(m)) || (e = c->dd_valid.ensure(m)) ||
-      (e = c->dd_nvalid.ensure(1)) || (e = c->dd_counts.ensure(2)) || (e = c->dd_ekeys_sorted.ensure(ne + 1)) ||
-      (e = c->dd_eidx.ensure(ne + 1)))
-    return c->hip_fail(e, "dedup workspace");
-  size_t tb = DedupWorkspace::temp_bytes_for((uint32_t)std::max<size_t>(m, 1));
-  if ((e = c->dd_temp.ensure(tb))) return c->hip_fail(e, "dedup temp");
-  DedupWorkspace& w = c->dws;
-  w.key_a = c->dd_key_a.p;
-  w.key_b = c->dd_key_b.p;
-  w.idx_a = c->dd_idx_a.p;
-  w.idx_b = c->dd_idx_b.p;
-  w.head = c->dd_head.p;
-  w.valid = c->dd_valid.p;
-  w.nvalid = c->dd_nvalid.p;
-  w.temp = c->dd_temp.p;
-  w.temp_bytes = c->dd_temp.cap;
-  w.cap = (uint32_t)c->dd_key_a.cap;
-  return SDCAS_OK;
+__global__ void k_iota64(uint64_t* __restrict__ p, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = i;
 }
+
+static hipError_t iota(DevBuf<uint64_t>& b, size_t n, hipStream_t st) {
+  hipError_t e = b.ensure(std::max<size_t>(n, 1));
+  if (e || !n) return e;
+  hipLaunchKernelGGL(k_iota64, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, b.p, (uint32_t)n);
+  return hipGetLastError();
+}
+
+// the resolve table holds 2 * (files + existing) entries, at most 2^31
+static bool dedup_fits(size_t n, size_t ne) { return (uint64_t)n + ne <= (1ull << 30); }
 
 int sdcas_dedup(sdcas_ctx* c, const uint64_t* keys, const uint8_t* has_key, const int32_t* status, size_t n,
                 size_t chunk_size, const uint64_t* existing_keys, size_t n_existing, int64_t* out_link,
                 int64_t* out_created, int64_t* out_linked) {
   if (!c || (n && (!keys || !has_key || !out_link)) || (n_existing && !existing_keys)) return SDCAS_E_INVALID;
-  if (n > 0xFFFFFFF0ull || n_existing > 0xFFFFFFF0ull) return SDCAS_E_CAPACITY;
-  std::lock_guard<std::mutex> g(c->mu);
-  (void)hipSetDevice(c->device);
+  if (!dedup_fits(n, n_existing))
+    return c->fail(SDCAS_E_CAPACITY, "dedup of %zu files + %zu Objects exceeds 2^30", n, n_existing);
+  PathCall call(c);
+  if (call.rc) return call.rc;
   if (chunk_size == 0) chunk_size = SDCAS_IDENTIFIER_CHUNK_SIZE;
-  int rc;
-  if ((rc = dedup_reserve(c, n, n_existing))) return rc;
   hipError_t e;
   hipStream_t st = c->stream;
   if ((e = c->dd_keys.ensure(n)) || (e = c->dd_has.ensure(n)) || (e = c->dd_link.ensure(n)) ||
-      (status && (e = c->dd_status.ensure(n))) || (e = c->dd_ekeys.ensure(n_existing + 1)))
+      (status && (e = c->dd_status.ensure(n))) || (e = c->dd_ekeys.ensure(n_existing + 1)) ||
+      (e = c->dd_counts.ensure(2)))
     return c->hip_fail(e, "dedup buffers");
   if ((e = hipMemcpyAsync(c->dd_keys.p, keys, 8 * n, hipMemcpyHostToDevice, st)) ||
       (e = hipMemcpyAsync(c->dd_has.p, has_key, n, hipMemcpyHostToDevice, st)) ||
       (status && (e = hipMemcpyAsync(c->dd_status.p, status, 4 * n, hipMemcpyHostToDevice, st))) ||
-      (n_existing && (e = hipMemcpyAsync(c->dd_ekeys.p, existing_keys, 8 * n_existing, hipMemcpyHostToDevice, st))))
+      (n_existing && (e = hipMemcpyAsync(c->dd_ekeys.p, existing_keys, 8 * n_existing, hipMemcpyHostToDevice, st))) ||
+      (e = hipMemsetAsync(c->dd_counts.p, 0, 2 * sizeof(unsigned long long), st)))
     return c->hip_fail(e, "dedup H2D");
-  if (n_existing &&
-      (e = dedup_sort_existing(c->dws, c->dd_ekeys.p, (uint32_t)n_existing, c->dd_ekeys_sorted.p, c->dd_eidx.p, st)))
-    return c->hip_fail(e, "dedup existing sort");
-  if ((e = dedup_run(c->dws, c->dd_keys.p, c->dd_has.p, status ? c->dd_status.p : nullptr, (uint32_t)n,
-                     (uint32_t)chunk_size, c->dd_ekeys_sorted.p, c->dd_eidx.p, (uint32_t)n_existing, c->dd_link.p,
-                     c->dd_counts.p, st)))
+  // files are ordinals 0..n-1 in orphan order, existing Objects 0..ne-1 in DB
+  // order: one iota serves both (ids of the first min(n, ne) coincide)
+  if ((e = iota(c->dd_ids, std::max(n, n_existing), st))) return c->hip_fail(e, "dedup ids");
+  if ((e = dd_local(c->dist, c->dd_keys.p, c->dd_has.p, status ? c->dd_status.p : nullptr, c->dd_ids.p, (uint32_t)n,
+                    c->dd_ekeys.p, c->dd_ids.p, (uint32_t)n_existing, chunk_size, c->dd_link.p, c->dd_counts.p, st)))
     return c->hip_fail(e, "dedup");
   unsigned long long cnt[2] = {0, 0};
   if (n && ((e = hipMemcpyAsync(out_link, c->dd_link.p, 8 * n, hipMemcpyDeviceToHost, st)) ||
@@ -1014,16 +1169,16 @@ int sdcas_dedup(sdcas_ctx* c, const uint64_t* keys, const uint8_t* has_key, cons
 int sdcas_dev_dedup(sdcas_ctx* c, const uint64_t* d_keys, const uint8_t* d_has_key, const int32_t* d_status,
                     size_t n, size_t chunk_size, int64_t* d_out_link, uint64_t* d_counts, void* stream) {
   if (!c || (n && (!d_keys || !d_has_key || !d_out_link))) return SDCAS_E_INVALID;
-  if (n > 0xFFFFFFF0ull) return SDCAS_E_CAPACITY;
-  std::lock_guard<std::mutex> g(c->mu);
+  if (!dedup_fits(n, 0)) return c->fail(SDCAS_E_CAPACITY, "dev_dedup of %zu files exceeds 2^30", n);
+  DevCall call(c, stream);
+  if (call.rc) return call.rc;
   if (chunk_size == 0) chunk_size = SDCAS_IDENTIFIER_CHUNK_SIZE;
-  int rc;
-  if (n > c->dws.cap && (rc = dedup_reserve(c, n, 0))) return rc;
-  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-  hipError_t e = dedup_run(c->dws, d_keys, d_has_key, d_status, (uint32_t)n, (uint32_t)chunk_size, nullptr, nullptr,
-                           0, d_out_link, (unsigned long long*)d_counts, st);
-  if (e) return c->hip_fail(e, "dev_dedup");
-  return SDCAS_OK;
+  hipError_t e;
+  if (d_counts && (e = hipMemsetAsync(d_counts, 0, 2 * sizeof(uint64_t), call.st))) return c->hip_fail(e, "counts");
+  if ((e = iota(c->dd_ids, n, call.st))) return c->hip_fail(e, "dev_dedup ids");
+  e = dd_local(c->dist, d_keys, d_has_key, d_status, c->dd_ids.p, (uint32_t)n, nullptr, nullptr, 0, chunk_size,
+               d_out_link, (unsigned long long*)d_counts, call.st);
+  return e ? c->hip_fail(e, "dev_dedup") : SDCAS_OK;
 }
 
 int sdcas_dev_set_sort(sdcas_ctx* c, int enable) {
@@ -1036,8 +1191,19 @@ int sdcas_dev_set_sort(sdcas_ctx* c, int enable) {
 int sdcas_dev_set_leaf_variant(sdcas_ctx* c, int variant) {
   if (!c) return SDCAS_E_INVALID;
   std::lock_guard<std::mutex> g(c->mu);
+  if (variant != -1 && !leaf_variant_available(variant))
+    return c->fail(SDCAS_E_INVALID, "leaf variant %d is not in this build", variant);
   c->ws.variant = variant;
-  return leaf_variant_count();
+  return SDCAS_OK;
+}
+
+int sdcas_dev_set_piece_variant(sdcas_ctx* c, int variant) {
+  if (!c) return SDCAS_E_INVALID;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (variant != -1 && !piece_variant_available(variant))
+    return c->fail(SDCAS_E_INVALID, "piece variant %d is not in this build", variant);
+  c->piece_variant = variant;
+  return SDCAS_OK;
 }
 
 // ---- synthetic corpora -------------------------------------------------------
@@ -1045,6 +1211,7 @@ int sdcas_dev_set_leaf_variant(sdcas_ctx* c, int variant) {
 int sdcas_dev_synth_cas_messages(sdcas_ctx* c, const uint64_t* d_keys, const uint64_t* d_sizes,
                                  const uint64_t* d_offs, size_t n, uint8_t* d_blob, void* stream) {
   if (!c) return SDCAS_E_INVALID;
+  (void)hipSetDevice(c->device);
   hipStream_t st = stream ? (hipStream_t)stream : c->stream;
   hipError_t e = synth_cas_messages(d_keys, d_sizes, d_offs, (uint32_t)n, d_blob, st);
   return e ? c->hip_fail(e, "synth") : SDCAS_OK;
@@ -1053,6 +1220,7 @@ int sdcas_dev_synth_cas_messages(sdcas_ctx* c, const uint64_t* d_keys, const uin
 int sdcas_dev_synth_content(sdcas_ctx* c, const uint64_t* d_keys, const uint64_t* d_starts, const uint64_t* d_lens,
                             const uint64_t* d_offs, size_t n, uint8_t* d_blob, void* stream) {
   if (!c) return SDCAS_E_INVALID;
+  (void)hipSetDevice(c->device);
   hipStream_t st = stream ? (hipStream_t)stream : c->stream;
   hipError_t e = synth_content(d_keys, d_starts, d_lens, d_offs, (uint32_t)n, d_blob, st);
   return e ? c->hip_fail(e, "synth") : SDCAS_OK;
@@ -1064,38 +1232,65 @@ int sdcas_dev_dedup_combine(sdcas_ctx* c, const uint64_t* d_keys, const uint8_t*
                             const uint64_t* d_ids, size_t n, uint32_t world, uint64_t* d_rec, uint32_t* d_slot,
                             uint64_t* out_starts, void* stream) {
   if (!c || world == 0 || !out_starts || (n && (!d_keys || !d_ids || !d_rec))) return SDCAS_E_INVALID;
-  if (n > 0xFFFFFFF0ull) return c->fail(SDCAS_E_CAPACITY, "dedup_combine: %zu records exceed 2^32", n);
-  std::lock_guard<std::mutex> g(c->mu);
-  (void)hipSetDevice(c->device);
-  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  // the combine's radix sort and scans take an int count (hipcub)
+  if (n > SDCAS_MAX_BATCH) return c->fail(SDCAS_E_CAPACITY, "dedup_combine: %zu records exceed 2^31 - 1", n);
+  DevCall call(c, stream);
+  if (call.rc) return call.rc;
   uint64_t u = 0;
   hipError_t e = dd_combine(c->dist, d_keys, d_has_key, d_status, d_ids, (uint32_t)n, world, d_rec, d_slot,
-                            out_starts, &u, st);
+                            out_starts, &u, call.st);
   return e ? c->hip_fail(e, "dedup_combine") : SDCAS_OK;
+}
+
+int sdcas_dev_dedup_combine_buckets(sdcas_ctx* c, const uint64_t* d_keys, const uint8_t* d_has_key,
+                                    const int32_t* d_status, const uint64_t* d_ids, size_t n, uint32_t world,
+                                    size_t cap, uint64_t* d_send, uint32_t* d_slot, int64_t* d_counts,
+                                    uint32_t* d_overflow, void* stream) {
+  if (!c || world == 0 || !d_counts || !d_overflow || (n && (!d_keys || !d_ids || !d_send))) return SDCAS_E_INVALID;
+  if (n > SDCAS_MAX_BATCH || (uint64_t)world * cap > SDCAS_MAX_BATCH)
+    return c->fail(SDCAS_E_CAPACITY, "dedup_combine_buckets: %zu records / %u x %zu buckets exceed 2^31 - 1", n,
+                   world, cap);
+  DevCall call(c, stream);
+  if (call.rc) return call.rc;
+  hipError_t e = dd_combine_buckets(c->dist, d_keys, d_has_key, d_status, d_ids, (uint32_t)n, world, (uint32_t)cap,
+                                    d_send, d_slot, d_counts, d_overflow, call.st);
+  return e ? c->hip_fail(e, "dedup_combine_buckets") : SDCAS_OK;
 }
 
 int sdcas_dev_dedup_resolve(sdcas_ctx* c, const uint64_t* d_frec, size_t nf, const uint64_t* d_erec, size_t ne,
                             int64_t* d_result, void* stream) {
   if (!c || (nf && (!d_frec || !d_result)) || (ne && !d_erec)) return SDCAS_E_INVALID;
-  if (nf > 0xFFFFFFF0ull || ne > 0xFFFFFFF0ull) return c->fail(SDCAS_E_CAPACITY, "dedup_resolve: > 2^32 records");
-  std::lock_guard<std::mutex> g(c->mu);
-  (void)hipSetDevice(c->device);
-  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-  hipError_t e = dd_resolve(c->dist, d_frec, (uint32_t)nf, d_erec, (uint32_t)ne, d_result, st);
+  if (!dedup_fits(nf, ne)) return c->fail(SDCAS_E_CAPACITY, "dedup_resolve: %zu + %zu records exceed 2^30", nf, ne);
+  DevCall call(c, stream);
+  if (call.rc) return call.rc;
+  hipError_t e = dd_resolve(c->dist, d_frec, (uint32_t)nf, d_erec, (uint32_t)ne, d_result, call.st);
   return e ? c->hip_fail(e, "dedup_resolve") : SDCAS_OK;
+}
+
+int sdcas_dev_dedup_resolve_buckets(sdcas_ctx* c, const uint64_t* d_frec, size_t fcap, const int64_t* d_fcounts,
+                                    const uint64_t* d_erec, size_t ecap, const int64_t* d_ecounts, uint32_t world,
+                                    int64_t* d_result, void* stream) {
+  if (!c || world == 0 || (fcap && (!d_frec || !d_fcounts || !d_result)) || (ecap && (!d_erec || !d_ecounts)))
+    return SDCAS_E_INVALID;
+  if (!dedup_fits((uint64_t)world * fcap, (uint64_t)world * ecap))
+    return c->fail(SDCAS_E_CAPACITY, "dedup_resolve_buckets: %u x (%zu + %zu) records exceed 2^30", world, fcap, ecap);
+  DevCall call(c, stream);
+  if (call.rc) return call.rc;
+  hipError_t e = dd_resolve_buckets(c->dist, d_frec, (uint32_t)fcap, d_fcounts, d_erec, (uint32_t)ecap, d_ecounts,
+                                    world, d_result, call.st);
+  return e ? c->hip_fail(e, "dedup_resolve_buckets") : SDCAS_OK;
 }
 
 int sdcas_dev_dedup_local(sdcas_ctx* c, const uint64_t* d_keys, const uint8_t* d_has_key, const int32_t* d_status,
                           const uint64_t* d_ids, size_t n, const uint64_t* d_ekeys, const uint64_t* d_eids, size_t ne,
                           size_t chunk_size, int64_t* d_link, uint64_t* d_counts, void* stream) {
   if (!c || (n && (!d_keys || !d_ids || !d_link)) || (ne && (!d_ekeys || !d_eids))) return SDCAS_E_INVALID;
-  if (n > 0xFFFFFFF0ull || ne > 0xFFFFFFF0ull) return c->fail(SDCAS_E_CAPACITY, "dedup_local: > 2^32 records");
-  std::lock_guard<std::mutex> g(c->mu);
-  (void)hipSetDevice(c->device);
-  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  if (!dedup_fits(n, ne)) return c->fail(SDCAS_E_CAPACITY, "dedup_local: %zu + %zu records exceed 2^30", n, ne);
+  DevCall call(c, stream);
+  if (call.rc) return call.rc;
   hipError_t e = dd_local(c->dist, d_keys, d_has_key, d_status, d_ids, (uint32_t)n, d_ekeys, d_eids, (uint32_t)ne,
                           chunk_size ? chunk_size : SDCAS_IDENTIFIER_CHUNK_SIZE, d_link,
-                          (unsigned long long*)d_counts, st);
+                          (unsigned long long*)d_counts, call.st);
   return e ? c->hip_fail(e, "dedup_local") : SDCAS_OK;
 }
 
@@ -1103,12 +1298,11 @@ int sdcas_dev_dedup_apply(sdcas_ctx* c, const uint64_t* d_ids, const uint32_t* d
                           const int64_t* d_result, size_t chunk_size, int64_t* d_link, uint64_t* d_counts,
                           void* stream) {
   if (!c || (n && (!d_ids || !d_slot || !d_link))) return SDCAS_E_INVALID;
-  if (n > 0xFFFFFFF0ull) return c->fail(SDCAS_E_CAPACITY, "dedup_apply: %zu files exceed 2^32", n);
-  std::lock_guard<std::mutex> g(c->mu);
-  (void)hipSetDevice(c->device);
-  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  if (n > SDCAS_MAX_BATCH) return c->fail(SDCAS_E_CAPACITY, "dedup_apply: %zu files exceed 2^31 - 1", n);
+  DevCall call(c, stream);
+  if (call.rc) return call.rc;
   hipError_t e = dd_apply(d_ids, d_slot, (uint32_t)n, d_result, chunk_size ? chunk_size : SDCAS_IDENTIFIER_CHUNK_SIZE,
-                          d_link, (unsigned long long*)d_counts, st);
+                          d_link, (unsigned long long*)d_counts, call.st);
   return e ? c->hip_fail(e, "dedup_apply") : SDCAS_OK;
 }
 
@@ -1118,6 +1312,12 @@ int sdcas_dev_stream_begin(sdcas_ctx* c, const uint64_t* lens, size_t nfiles) {
   if (!c || (nfiles && !lens)) return SDCAS_E_INVALID;
   std::lock_guard<std::mutex> g(c->mu);
   (void)hipSetDevice(c->device);
+  // the session's descriptors and node list are rewritten below: the previous
+  // session's kernels must be done with them
+  if (c->scratch_pending) {
+    hipError_t e = hipEventSynchronize(c->scratch_ev);
+    if (e) return c->hip_fail(e, "sync");
+  }
   c->sm_files.assign(nfiles, FileDesc{});
   uint64_t nodes = 0;
   for (size_t i = 0; i < nfiles; ++i) {
@@ -1130,7 +1330,7 @@ int sdcas_dev_stream_begin(sdcas_ctx* c, const uint64_t* lens, size_t nfiles) {
     nodes += bigfile_node_count(C);
   }
   hipError_t e;
-  if ((e = c->sm_nodes.ensure(8 * nodes + 8)) || (e = c->sm_d_files.ensure(nfiles + 1)))
+  if ((e = c->sm_nodes.ensure(8 * nodes + 8)) || (e = c->sm_d_files.ensure(nfiles + 1)) || (e = c->piece_ctr.ensure(1)))
     return c->hip_fail(e, "stream workspace");
   if (nfiles && (e = hipMemcpy(c->sm_d_files.p, c->sm_files.data(), sizeof(FileDesc) * nfiles,
                                hipMemcpyHostToDevice)))
@@ -1142,9 +1342,9 @@ int sdcas_dev_stream_begin(sdcas_ctx* c, const uint64_t* lens, size_t nfiles) {
 int sdcas_dev_stream_update(sdcas_ctx* c, size_t nseg, const uint64_t* h_file, const uint64_t* h_msg_off,
                             const uint64_t* h_len, const uint64_t* h_dev_addr, void* stream) {
   if (!c || (nseg && (!h_file || !h_msg_off || !h_len || !h_dev_addr))) return SDCAS_E_INVALID;
-  std::lock_guard<std::mutex> g(c->mu);
+  DevCall call(c, stream);
+  if (call.rc) return call.rc;
   if (!c->sm_active) return c->fail(SDCAS_E_INVALID, "stream_update without stream_begin");
-  (void)hipSetDevice(c->device);
   const uint64_t piece_bytes = 1024ull * kTile;
   uint64_t base = ~0ull;
   for (size_t k = 0; k < nseg; ++k) base = std::min(base, h_dev_addr[k]);
@@ -1167,7 +1367,8 @@ int sdcas_dev_stream_update(sdcas_ctx* c, size_t nseg, const uint64_t* h_file, c
     }
   }
   if (pieces.empty()) return SDCAS_OK;
-  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  if (pieces.size() > SDCAS_MAX_BATCH) return c->fail(SDCAS_E_CAPACITY, "stream_update: %zu pieces", pieces.size());
+  hipStream_t st = call.st;
   hipError_t e;
   if ((e = c->sm_pieces.ensure(pieces.size()))) return c->hip_fail(e, "piece descs");
   // stream-ordered: a previous update's kernel on `st` has finished reading
@@ -1182,7 +1383,8 @@ int sdcas_dev_stream_update(sdcas_ctx* c, size_t nseg, const uint64_t* h_file, c
     b = c->event();
     (void)hipEventRecord(a, st);
   }
-  e = piece_hash(reinterpret_cast<const uint8_t*>(base), c->sm_pieces.p, (uint32_t)pieces.size(), c->sm_nodes.p, st);
+  e = piece_hash(reinterpret_cast<const uint8_t*>(base), c->sm_pieces.p, (uint32_t)pieces.size(), c->sm_nodes.p,
+                 c->piece_ctr.p, c->piece_variant, st);
   if (c->profile) {
     (void)hipEventRecord(b, st);
     c->ev_leaf.push_back({a, b});
@@ -1195,10 +1397,10 @@ int sdcas_dev_stream_update(sdcas_ctx* c, size_t nseg, const uint64_t* h_file, c
 
 int sdcas_dev_stream_finish(sdcas_ctx* c, uint8_t* d_out32, void* stream) {
   if (!c || !d_out32) return SDCAS_E_INVALID;
-  std::lock_guard<std::mutex> g(c->mu);
+  DevCall call(c, stream);
+  if (call.rc) return call.rc;
   if (!c->sm_active) return c->fail(SDCAS_E_INVALID, "stream_finish without stream_begin");
-  (void)hipSetDevice(c->device);
-  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  hipStream_t st = call.st;
   c->sm_active = false;
   hipError_t e = bigfile_finish(c->sm_d_files.p, (uint32_t)c->sm_files.size(), c->sm_nodes.p, d_out32, st);
   return e ? c->hip_fail(e, "bigfile_finish") : SDCAS_OK;

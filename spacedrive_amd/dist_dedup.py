@@ -25,6 +25,16 @@ torch.distributed all_to_all_single (backend "nccl" = RCCL over xGMI). The
 `stages` object is pluggable only so that the collective protocol can be
 exercised with gloo on CPU by the test-suite's numpy stages
 (tests/_dist_stages.py); the product path is `DeviceStages`.
+
+Host synchronisations. all_to_all_single needs its split sizes on the host,
+so the exact protocol waits for the host three times (the combine's owner
+ranges, the received counts, the final totals). The bucket protocol sends
+every owner a fixed-capacity bucket instead (equal splits, nothing for the
+host to learn) and carries the valid counts on the device; its only host
+synchronisation is the final totals, which also carry an overflow flag.
+Capacities are agreed from the previous call's largest bucket (all ranks see
+the same all-reduced maximum); the first call of a `stages` object, and any
+call whose buckets overflow, takes the exact protocol.
 """
 from __future__ import annotations
 
@@ -103,6 +113,33 @@ class DeviceStages:
         self.eng._check(rc, "sdcas_dev_dedup_local")
         return link[:n], counts
 
+    def combine_buckets(self, keys, has_key, status, ids, world, cap, need_slot=True):
+        """-> (send int64[world * cap, 2], slot int32[n] or None, counts int64[world],
+        overflow int32[1]), all on the device, no host synchronisation"""
+        n = int(ids.numel())
+        dev = ids.device
+        send = torch.empty((max(world * cap, 1), 2), dtype=torch.int64, device=dev)
+        slot = torch.empty(max(n, 1), dtype=torch.int32, device=dev) if need_slot else None
+        counts = torch.empty(world, dtype=torch.int64, device=dev)
+        overflow = torch.empty(1, dtype=torch.int32, device=dev)
+        p = lambda t: t.data_ptr() if t is not None and t.numel() else None
+        rc = self.eng.L.sdcas_dev_dedup_combine_buckets(self.eng.ctx, p(keys), p(has_key), p(status), p(ids), n,
+                                                        world, cap, p(send), p(slot), p(counts), p(overflow),
+                                                        self._enter())
+        self._leave(keys, has_key, status, ids, send, slot, counts, overflow)
+        self.eng._check(rc, "sdcas_dev_dedup_combine_buckets")
+        return send[: world * cap], (slot[:n] if slot is not None else None), counts, overflow
+
+    def resolve_buckets(self, frecv, fcap, fcounts, erecv, ecap, ecounts, world):
+        """-> result int64[world * fcap] in the received buckets' layout"""
+        result = torch.empty(max(world * fcap, 1), dtype=torch.int64, device=frecv.device)
+        p = lambda t: t.data_ptr() if t is not None and t.numel() else None
+        rc = self.eng.L.sdcas_dev_dedup_resolve_buckets(self.eng.ctx, p(frecv), fcap, p(fcounts), p(erecv),
+                                                        ecap, p(ecounts), world, p(result), self._enter())
+        self._leave(frecv, fcounts, erecv, ecounts, result)
+        self.eng._check(rc, "sdcas_dev_dedup_resolve_buckets")
+        return result[: world * fcap]
+
     def apply(self, ids, slot, result, chunk_size):
         """-> (link int64[n], counts int64[2] = (created, linked)) on the device"""
         n = int(ids.numel())
@@ -151,20 +188,47 @@ def identifier_dedup_distributed(stages, keys, has_key, status, ids, chunk_size=
     # the collectives would deliver them, so the exchanges are skipped, and
     # without an exchange the combine has nothing to shrink or group: stages
     # that offer the fused single-rank path take it
-    solo = world == 1
-    if solo and hasattr(stages, "local"):
+    if world == 1 and hasattr(stages, "local"):
+        stages.last_protocol = "local"
         link, cnt = stages.local(keys, has_key, status, ids, chunk_size, existing_keys, existing_ids)
         c = cnt.tolist()
         return link, int(c[0]), int(c[1])
+    caps = getattr(stages, "bucket_caps", None)
+    if world > 1 and caps is not None and hasattr(stages, "combine_buckets"):
+        stages.last_protocol = "buckets"
+        out = _dedup_buckets(stages, world, caps, keys, has_key, status, ids, chunk_size, existing_keys,
+                             existing_ids, group)
+        if out is not None:
+            return out
+        stages.last_protocol = "buckets-overflow"
+    else:
+        stages.last_protocol = "exact"
+    return _dedup_exact(stages, world, keys, has_key, status, ids, chunk_size, existing_keys, existing_ids, group)
+
+
+def _next_caps(stages, fill_f, fill_e):
+    """bucket capacities for the next call from the node's largest buckets of
+    this one (identical on every rank: the fills are all-reduced maxima)"""
+    def cap(fill, old):
+        want = int(fill * 1.125) + 256
+        # keep the old capacity unless it overflowed or is more than twice too big
+        return old if old and fill <= old and old <= 2 * want else want
+    old = getattr(stages, "bucket_caps", None) or (0, 0)
+    stages.bucket_caps = (cap(fill_f, old[0]), cap(fill_e, old[1]) if fill_e >= 0 else 0)
+
+
+def _dedup_exact(stages, world, keys, has_key, status, ids, chunk_size, existing_keys, existing_ids, group):
+    solo = world == 1
     rec, slot, starts = stages.combine(keys, has_key, status, ids, world)
     counts = [starts[r + 1] - starts[r] for r in range(world)]
+    ecounts = [0] * world
     if existing_keys is not None:
         # collective: every rank passes its (possibly empty) share, or none does
         if existing_keys.numel():
             erec, _, estarts = stages.combine(existing_keys, None, None, existing_ids, world)
             ecounts = [estarts[r + 1] - estarts[r] for r in range(world)]
         else:
-            erec, ecounts = rec.new_empty((0, 2)), [0] * world
+            erec = rec.new_empty((0, 2))
     if solo:
         frecv, fcounts = rec, counts
         erecv = erec if existing_keys is not None else rec.new_empty((0, 2))
@@ -186,10 +250,65 @@ def identifier_dedup_distributed(stages, keys, has_key, status, ids, chunk_size=
     # exactly what it sent
     back = answer if solo else _exchange(answer, fcounts, group, recv_counts=counts)[0]
     link, cnt = stages.apply(ids, slot, back, chunk_size)
-    if not solo:
-        dist.all_reduce(cnt, group=group)
-    c = cnt.tolist()
+    if solo:
+        c = cnt.tolist()
+        return link, int(c[0]), int(c[1])
+    # totals, and the node's largest buckets for the next call's capacities
+    fills = torch.tensor([max(counts), max(ecounts) if existing_keys is not None else -1],
+                         dtype=torch.int64, device=cnt.device)
+    dist.all_reduce(cnt, group=group)
+    dist.all_reduce(fills, op=dist.ReduceOp.MAX, group=group)
+    c, f = cnt.tolist(), fills.tolist()
+    if hasattr(stages, "combine_buckets"):
+        _next_caps(stages, int(f[0]), int(f[1]))
     return link, int(c[0]), int(c[1])
+
+
+def _dedup_buckets(stages, world, caps, keys, has_key, status, ids, chunk_size, existing_keys, existing_ids,
+                   group):
+    """the exchange in fixed-capacity buckets: one host synchronisation (the
+    totals); None when a bucket overflowed (the caller reruns the exact path)"""
+    fcap, ecap = caps
+    has_ex = existing_keys is not None
+    if has_ex and ecap == 0:
+        return None  # the previous call had no existing Objects: no capacity agreed
+    send, slot, fcnt, ovf = stages.combine_buckets(keys, has_key, status, ids, world, fcap)
+    dev = fcnt.device
+    if has_ex:
+        if existing_keys.numel():
+            esend, _, ecnt, eovf = stages.combine_buckets(existing_keys, None, None, existing_ids, world, ecap,
+                                                          need_slot=False)
+        else:
+            esend = torch.zeros((world * ecap, 2), dtype=torch.int64, device=dev)
+            ecnt = torch.zeros(world, dtype=torch.int64, device=dev)
+            eovf = torch.zeros(1, dtype=torch.int32, device=dev)
+        sc = torch.stack([fcnt, ecnt], 1).contiguous()
+    else:
+        sc = fcnt.view(world, 1).contiguous()
+    rc = torch.empty_like(sc)
+    dist.all_to_all_single(rc, sc, group=group)  # equal splits: no host sizes
+    frecv = torch.empty_like(send)
+    dist.all_to_all_single(frecv, send.contiguous(), group=group)
+    if has_ex:
+        erecv = torch.empty_like(esend)
+        dist.all_to_all_single(erecv, esend.contiguous(), group=group)
+        ercnt = rc[:, 1].contiguous()
+    else:
+        erecv, ercnt = None, None
+    answer = stages.resolve_buckets(frecv, fcap, rc[:, 0].contiguous(), erecv, ecap if has_ex else 0, ercnt, world)
+    back = torch.empty_like(answer)
+    dist.all_to_all_single(back, answer.contiguous(), group=group)
+    link, cnt = stages.apply(ids, slot, back, chunk_size)
+    over = ovf.to(torch.int64) + (eovf.to(torch.int64) if has_ex else 0)
+    tot = torch.cat([cnt.to(torch.int64), over])
+    fills = torch.stack([fcnt.max(), ecnt.max() if has_ex else torch.full((), -1, dtype=torch.int64, device=dev)])
+    dist.all_reduce(tot, group=group)
+    dist.all_reduce(fills, op=dist.ReduceOp.MAX, group=group)
+    t, f = tot.tolist(), fills.tolist()  # the one host synchronisation
+    _next_caps(stages, int(f[0]), int(f[1]))
+    if t[2]:
+        return None
+    return link, int(t[0]), int(t[1])
 
 
 def owner_of(keys: np.ndarray, world: int) -> np.ndarray:

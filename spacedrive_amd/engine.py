@@ -52,16 +52,41 @@ def io_error(status: int, path=None) -> OSError:
 
 
 class Engine:
-    """One libsdcas context bound to one GPU."""
+    """One libsdcas context bound to one GPU.
 
-    def __init__(self, device: int = 0, io_threads: int = 0, staging_bytes: int = 0):
+    progress: optional callable(done_bytes, total_bytes), called on the
+    calling thread after every staging slot of a path call (the job's
+    progress report, job/worker.rs:458-480). cancel: optional
+    ``ctypes.c_int32`` the caller may set nonzero from any thread to stop a
+    path call (job/mod.rs:862-960); the call then raises ``Cancelled`` whose
+    ``partial`` holds the completed items.
+    """
+
+    def __init__(self, device: int = 0, io_threads: int = 0, staging_bytes: int = 0, progress=None, cancel=None):
         self.L = N.load()
-        opts = N.Options(device, io_threads, staging_bytes)
+        self._cb = self._progress_fn(progress)
+        self._cancel = cancel
+        opts = N.Options(device, io_threads, staging_bytes, self._cb, None,
+                         ctypes.pointer(cancel) if cancel is not None else None)
         ctx = ctypes.c_void_p()
         rc = self.L.sdcas_init(ctypes.byref(opts), ctypes.byref(ctx))
         if rc != N.SDCAS_OK:
             raise N.SdcasError(rc, "sdcas_init failed (no HIP device?)")
         self.ctx = ctx
+
+    @staticmethod
+    def _progress_fn(progress):
+        if progress is None:
+            return N.PROGRESS_FN()
+        return N.PROGRESS_FN(lambda _user, done, total: progress(int(done), int(total)))
+
+    def set_progress(self, progress=None, cancel=None):
+        """re-bind the progress callable and cancel flag (sdcas_set_progress)"""
+        cb = self._progress_fn(progress)
+        self._check(self.L.sdcas_set_progress(self.ctx, cb, None,
+                                              ctypes.pointer(cancel) if cancel is not None else None),
+                    "sdcas_set_progress")
+        self._cb, self._cancel = cb, cancel
 
     # -- lifetime -------------------------------------------------------------
     def close(self):
@@ -81,9 +106,11 @@ class Engine:
         except Exception:
             pass
 
-    def _check(self, rc, what):
+    def _check(self, rc, what, partial=None):
         if rc != N.SDCAS_OK:
             msg = self.L.sdcas_last_error(self.ctx).decode(errors="replace")
+            if rc == N.SDCAS_E_CANCELLED:
+                raise N.Cancelled(f"{what}: {msg}", partial)
             raise N.SdcasError(rc, f"{what}: {msg}")
 
     # -- reference functions, batched ------------------------------------------
@@ -96,7 +123,7 @@ class Engine:
         keys = np.zeros(n, np.uint64)
         st = np.zeros(n, np.int32)
         self._check(self.L.sdcas_cas_ids(self.ctx, parr, _ptr(sizes), n, _ptr(keys), _ptr(st)),
-                    "sdcas_cas_ids")
+                    "sdcas_cas_ids", (keys, st))
         return keys, st
 
     def file_checksums(self, paths):
@@ -105,7 +132,7 @@ class Engine:
         parr = (ctypes.c_char_p * max(n, 1))(*[os.fsencode(p) for p in paths])
         out = np.zeros((n, 32), np.uint8)
         st = np.zeros(n, np.int32)
-        self._check(self.L.sdcas_checksums(self.ctx, parr, n, _ptr(out), _ptr(st)), "sdcas_checksums")
+        self._check(self.L.sdcas_checksums(self.ctx, parr, n, _ptr(out), _ptr(st)), "sdcas_checksums", (out, st))
         return out, st
 
     def generate_cas_id(self, path, size) -> str:
@@ -205,8 +232,13 @@ class Engine:
         self._check(self.L.sdcas_dev_profile(self.ctx, 1 if enable else 0), "dev_profile")
 
     def dev_set_leaf_variant(self, v):
-        """tuning knob: leaf/tree kernel variant (-1 = default); returns the variant count"""
-        return self.L.sdcas_dev_set_leaf_variant(self.ctx, int(v))
+        """tuning knob: leaf/tree kernel variant (-1 = default); False (and the
+        selection unchanged) for a variant this build does not hold"""
+        return self.L.sdcas_dev_set_leaf_variant(self.ctx, int(v)) == N.SDCAS_OK
+
+    def dev_set_piece_variant(self, v):
+        """tuning knob: 1 MiB-piece kernel variant of the checksum path (-1 = default)"""
+        return self.L.sdcas_dev_set_piece_variant(self.ctx, int(v)) == N.SDCAS_OK
 
     def dev_set_sort(self, enable):
         """tuning knob: length-sorted slot order (default on); results identical"""

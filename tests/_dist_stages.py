@@ -119,6 +119,48 @@ class NumpyStages:
             res[p] = -emin[key] - 1 if key in emin else fmin[key]
         return torch.from_numpy(res)
 
+    def combine_buckets(self, keys, has_key, status, ids, world, cap, need_slot=True):
+        """the combine into world fixed-capacity buckets (dist_dedup.h
+        dd_combine_buckets): record p of owner r at row r * cap + p"""
+        rec, slot, starts = self.combine(keys, has_key, status, ids, world)
+        r64 = _u64(rec).reshape(-1, 2)
+        send = np.zeros((world * cap, 2), np.uint64)
+        counts = np.zeros(world, np.int64)
+        over = 0
+        for r in range(world):
+            c = starts[r + 1] - starts[r]
+            over |= int(c > cap)
+            c = min(c, cap)
+            counts[r] = c
+            send[r * cap: r * cap + c] = r64[starts[r]: starts[r] + c]
+        if slot is not None and need_slot:
+            s = slot.numpy().view(np.uint32).copy()
+            v = s < DROPPED
+            own = owner_of(r64[s[v], 0], world)
+            st = np.array(starts, np.int64)
+            pos = s[v].astype(np.int64) - st[own]
+            s[v] = np.where(pos < cap, own * cap + pos, np.int64(NOKEY)).astype(np.uint32)
+            slot = torch.from_numpy(s.view(np.int32))
+        else:
+            slot = None
+        return (_t64(send).reshape(-1, 2), slot, torch.from_numpy(counts),
+                torch.tensor([over], dtype=torch.int32))
+
+    def resolve_buckets(self, frecv, fcap, fcounts, erecv, ecap, ecounts, world):
+        f = frecv.reshape(-1, 2)
+        fsel = np.concatenate([np.arange(r * fcap, r * fcap + int(fcounts[r])) for r in range(world)]).astype(np.int64)
+        if erecv is not None and ecap:
+            e = erecv.reshape(-1, 2)
+            esel = np.concatenate([np.arange(r * ecap, r * ecap + int(ecounts[r]))
+                                   for r in range(world)]).astype(np.int64)
+            ev = e[torch.from_numpy(esel)]
+        else:
+            ev = f[:0]
+        ans = self.resolve(f[torch.from_numpy(fsel)], ev).numpy()
+        out = np.full(world * fcap, -7, np.int64)  # padding: never read
+        out[fsel] = ans
+        return torch.from_numpy(out)
+
     def apply(self, ids, slot, result, chunk_size):
         ids_np = _u64(ids).astype(np.int64)
         s = slot.numpy().view(np.uint32)
@@ -166,3 +208,51 @@ def shard(keys, has, status, existing, R, device="cpu", contiguous=True):
         idx = np.arange(r, existing.size, R, dtype=np.int64)
         ex.append((torch.from_numpy(existing[idx].view(np.int64)).to(device), torch.from_numpy(idx).to(device)))
     return out, ex
+
+
+def dedup_virtual_buckets(stages_for, shards, chunk_size, existing_shards, caps):
+    """The bucket protocol of identifier_dedup_distributed (fixed-capacity
+    owner buckets, equal-split exchanges, no host synchronisation inside) for
+    R virtual ranks in one process. caps = (file bucket capacity, existing
+    bucket capacity). Returns (per-rank links, created, linked, overflowed)."""
+    R = len(shards)
+    fcap, ecap = caps
+    st = [stages_for(r) for r in range(R)]
+    sends, slots, fcnts, over = [], [], [], 0
+    for r, (k, h, s, ids) in enumerate(shards):
+        send, slot, cnt, ovf = st[r].combine_buckets(k, h, s, ids, R, fcap)
+        sends.append(send)
+        slots.append(slot)
+        fcnts.append(cnt.cpu().numpy())
+        over |= int(ovf.cpu()[0])
+    esends, ecnts = [], []
+    for r in range(R):
+        if existing_shards is not None and existing_shards[r][0].numel():
+            ek, eids = existing_shards[r]
+            es, _, ec, eo = st[r].combine_buckets(ek, None, None, eids, R, ecap, need_slot=False)
+            over |= int(eo.cpu()[0])
+        else:
+            es = sends[r].new_zeros((R * ecap, 2))
+            ec = np.zeros(R, np.int64)
+        esends.append(es)
+        ecnts.append(ec if isinstance(ec, np.ndarray) else ec.cpu().numpy())
+
+    def xchg(bufs, cap):  # equal splits: destination d gets bucket d of every source, in source order
+        return [torch.cat([bufs[s][d * cap:(d + 1) * cap] for s in range(R)]) for d in range(R)]
+
+    dev = sends[0].device
+    frecv, erecv = xchg(sends, fcap), xchg(esends, ecap)
+    answers = []
+    for d in range(R):
+        fc = torch.tensor([int(fcnts[s][d]) for s in range(R)], dtype=torch.int64, device=dev)
+        ec = torch.tensor([int(ecnts[s][d]) for s in range(R)], dtype=torch.int64, device=dev)
+        answers.append(st[d].resolve_buckets(frecv[d], fcap, fc, erecv[d] if ecap else None, ecap, ec, R))
+    back = xchg(answers, fcap)
+    links, created, linked = [], 0, 0
+    for r, (k, h, s, ids) in enumerate(shards):
+        link, cnt = st[r].apply(ids, slots[r], back[r], chunk_size)
+        links.append(link)
+        c = cnt.cpu().tolist()
+        created += int(c[0])
+        linked += int(c[1])
+    return links, created, linked, over

@@ -42,6 +42,14 @@ class Oracle:
                                         ctypes.c_void_p]
         L.oracle_periodic_checksum.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int,
                                                ctypes.c_int, ctypes.c_void_p]
+        L.oracle_synth_cas_keys_mt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                               ctypes.c_int, ctypes.c_void_p]
+        L.oracle_synth_cas_keys_mt.restype = ctypes.c_int
+        L.oracle_cpu_faithful.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
+                                          ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
+                                          ctypes.c_char_p]
+        L.oracle_cpu_faithful.restype = ctypes.c_int
 
     def hash(self, data: bytes) -> str:
         buf = np.frombuffer(bytes(data), dtype=np.uint8)
@@ -96,6 +104,33 @@ class Oracle:
         rc = self.lib.oracle_periodic_checksum(period.ctypes.data, period.size, total, threads, int(upstream), out)
         assert rc == 0, rc
         return out.raw.hex()
+
+    def synth_cas_keys(self, content_keys, sizes, threads=16, upstream=True):
+        """every cas key of synthetic files (content key, size), multi-threaded
+        -> (keys uint64[n], hasher) with hasher 'upstream' (BLAKE3 C SIMD) or 'scalar'"""
+        ck = np.ascontiguousarray(content_keys, dtype=np.uint64)
+        sz = np.ascontiguousarray(sizes, dtype=np.uint64)
+        out = np.zeros(ck.size, np.uint64)
+        up = self.lib.oracle_synth_cas_keys_mt(ck.ctypes.data, sz.ctypes.data, ck.size, threads, int(upstream),
+                                               out.ctypes.data)
+        return out, ("upstream" if up else "scalar")
+
+    def cpu_faithful(self, paths, sizes, chunk=100, io_threads=16, upstream=True):
+        """the identifier job's CPU shape over real files (oracle/cpu_bench.c
+        oracle_cpu_faithful) -> (keys, status, seconds, hasher)"""
+        n = len(paths)
+        parr = (ctypes.c_char_p * max(n, 1))(*[os.fsencode(p) for p in paths])
+        sz = np.ascontiguousarray(sizes, dtype=np.uint64)
+        keys = np.zeros(n, np.uint64)
+        st = np.zeros(n, np.int32)
+        secs = ctypes.c_double(0)
+        kind = ctypes.c_int(0)
+        ver = ctypes.create_string_buffer(32)
+        rc = self.lib.oracle_cpu_faithful(parr, sz.ctypes.data, n, chunk, io_threads, int(upstream), keys.ctypes.data,
+                                          st.ctypes.data, ctypes.byref(secs), ctypes.byref(kind), ver)
+        assert rc == 0, rc
+        hasher = f"upstream BLAKE3 C {ver.value.decode()} SIMD" if kind.value else "scalar BLAKE3 restatement"
+        return keys, st, secs.value, hasher
 
     def identifier_dedup(self, keys, has_key, status=None, chunk_size=100, existing_keys=()):
         keys = np.ascontiguousarray(keys, dtype=np.uint64)

@@ -62,3 +62,30 @@ def test_init_fails_loudly_without_gpu():
     from spacedrive_amd import Engine
     with pytest.raises(N.SdcasError):
         Engine()
+
+
+def _kernel_stubs(path):
+    out = subprocess.run(["nm", "-C", path], capture_output=True, text=True).stdout
+    return sorted(set(re.findall(r"sdcas::__device_stub__(k_\w+(?:<[^>]*>)?)", out)))
+
+
+def test_product_library_holds_only_product_kernels():
+    """libsdcas.so carries the default leaf kernel (43), one bit-exact,
+    GPU-tested alternative (36), and no ablation or DIAGNOSTIC variant (those
+    produce wrong digests and live only in libsdcas_ablate.so)"""
+    stubs = _kernel_stubs(N.LIB_PATH)
+    leaf = [s for s in stubs if s.startswith("k_leaf")]
+    assert leaf == ["k_leaf_tree<512, 4, 1, 1, 1>", "k_leaf_tree<512, 8, 1, 1, 1>"], leaf
+    assert not [s for s in stubs if "slim" in s or "quad" in s]
+    pieces = [s for s in stubs if s.startswith("k_piece")]
+    assert sorted(pieces) == ["k_piece_dyn<6, 0>", "k_piece_dyn<6, 1>", "k_piece_dyn<8, 0>",
+                              "k_piece_tree<4, 6, 1, 0>"], pieces
+
+
+def test_ablation_build_is_separate():
+    """the A/B library is a different file that no product module names"""
+    assert N.ABLATION_LIB_PATH != N.LIB_PATH
+    pkg = os.path.join(ROOT, "spacedrive_amd")
+    for f in os.listdir(pkg):
+        if f.endswith(".py") and f != "_native.py":
+            assert "ablat" not in open(os.path.join(pkg, f)).read(), f

@@ -38,7 +38,7 @@ def _gloo_corpus(seed, n, existing_mode):
     return keys, has, status, existing
 
 
-def _gloo_worker(rank, world, port, outdir, seed, n, chunk_size, existing_mode="full"):
+def _gloo_worker(rank, world, port, outdir, seed, n, chunk_size, existing_mode="full", caps=None):
     import torch.distributed as dist
 
     from spacedrive_amd.dist_dedup import identifier_dedup_distributed
@@ -48,8 +48,18 @@ def _gloo_worker(rank, world, port, outdir, seed, n, chunk_size, existing_mode="
         shards, ex = shard(keys, has, status, existing, world)
         k, h, s, ids = shards[rank]
         ek, eids = ex[rank] if existing_mode != "none" else (None, None)
-        link, created, linked = identifier_dedup_distributed(NumpyStages(), k, h, s, ids, chunk_size, ek, eids)
-        np.savez(os.path.join(outdir, f"r{rank}.npz"), link=link.numpy(), created=created, linked=linked)
+        st = NumpyStages()
+        if caps is not None:
+            st.bucket_caps = caps
+        # the same stages object twice: the first call agrees bucket capacities
+        # (exact protocol, or the given caps), the second uses them
+        out = {}
+        for call in range(2):
+            link, created, linked = identifier_dedup_distributed(st, k, h, s, ids, chunk_size, ek, eids)
+            out[f"link{call}"] = link.numpy()
+            out[f"count{call}"] = np.array([created, linked])
+            out[f"proto{call}"] = np.array(st.last_protocol)
+        np.savez(os.path.join(outdir, f"r{rank}.npz"), **out)
     finally:
         dist.destroy_process_group()
 
@@ -58,18 +68,42 @@ def _gloo_worker(rank, world, port, outdir, seed, n, chunk_size, existing_mode="
     (1, 100, "full"), (2, 100, "full"), (4, 7, "full"), (3, 1, "full"), (1, 100, "none"), (2, 100, "none"),
     (3, 100, "sparse")])
 def test_gloo_protocol_vs_oracle(oracle, world, chunk_size, existing_mode):
+    """exact protocol on the first call, fixed-capacity buckets on the second"""
     import torch.multiprocessing as mp
     seed, n = 1000 + world, 3000
     with tempfile.TemporaryDirectory() as d:
         mp.start_processes(_gloo_worker, args=(world, _free_port(), d, seed, n, chunk_size, existing_mode),
                            nprocs=world, join=True, start_method="spawn")
         parts = [np.load(os.path.join(d, f"r{r}.npz")) for r in range(world)]
-    got = np.concatenate([p["link"] for p in parts])
     keys, has, status, existing = _gloo_corpus(seed, n, existing_mode)
     want, wc, wl = oracle.identifier_dedup(keys, has, status, chunk_size, existing)
-    assert np.array_equal(got, want)
-    for p in parts:  # node-wide totals on every rank
-        assert (int(p["created"]), int(p["linked"])) == (wc, wl)
+    for call in range(2):
+        got = np.concatenate([p[f"link{call}"] for p in parts])
+        assert np.array_equal(got, want)
+        for p in parts:  # node-wide totals on every rank
+            assert tuple(int(x) for x in p[f"count{call}"]) == (wc, wl)
+    if world > 1:
+        assert [str(p["proto0"]) for p in parts] == ["exact"] * world
+        assert [str(p["proto1"]) for p in parts] == ["buckets"] * world
+
+
+def test_gloo_bucket_overflow_falls_back(oracle):
+    """buckets too small for the records: the overflow flag travels with the
+    totals, every rank reruns the exact protocol, links still exact"""
+    import torch.multiprocessing as mp
+    world, seed, n = 3, 77, 3000
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_gloo_worker, args=(world, _free_port(), d, seed, n, 100, "full", (8, 8)),
+                           nprocs=world, join=True, start_method="spawn")
+        parts = [np.load(os.path.join(d, f"r{r}.npz")) for r in range(world)]
+    keys, has, status, existing = _gloo_corpus(seed, n, "full")
+    want, wc, wl = oracle.identifier_dedup(keys, has, status, 100, existing)
+    for call in range(2):
+        assert np.array_equal(np.concatenate([p[f"link{call}"] for p in parts]), want)
+        for p in parts:
+            assert tuple(int(x) for x in p[f"count{call}"]) == (wc, wl)
+    assert [str(p["proto0"]) for p in parts] == ["buckets-overflow"] * world
+    assert [str(p["proto1"]) for p in parts] == ["buckets"] * world
 
 
 @pytest.mark.parametrize("R", [1, 2, 5, 8])

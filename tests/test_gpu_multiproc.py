@@ -1,0 +1,132 @@
+"""The multi-rank dedup path as real device code in real processes
+(SURVEY.md §8e): two processes, one Engine and DeviceStages each (libsdcas's
+HIP kernels on cuda:0), exchanging through torch.distributed. Two RCCL ranks
+on one GPU are refused by RCCL, so the processes use gloo, whose collectives
+take the same device tensors (staged through the host); the protocol code is
+the one bench.py runs over RCCL. Each rank's links are compared with the
+chunked oracle of file_identifier/mod.rs:149-254, for the exact protocol
+(first call) and the one-synchronisation bucket protocol (second call),
+with and without existing Objects.
+
+Also: two streams sharing one context's device scratch (sdcas.h "Threading").
+"""
+import os
+import socket
+import tempfile
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from tests._dist_stages import make_corpus, shard
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _corpus(existing_mode):
+    keys, has, status, existing = make_corpus(4242, 60000, pool=9000, n_existing=1 if existing_mode == "sparse"
+                                              else 400)
+    if existing_mode == "none":
+        existing = existing[:0]
+    return keys, has, status, existing
+
+
+def _worker(rank, world, port, outdir, existing_mode):
+    import torch.distributed as dist
+
+    from spacedrive_amd import Engine
+    from spacedrive_amd.dist_dedup import DeviceStages, identifier_dedup_distributed
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    eng = Engine(device=0)
+    try:
+        keys, has, status, existing = _corpus(existing_mode)
+        shards, ex = shard(keys, has, status, existing, world, device="cuda")
+        k, h, s, ids = shards[rank]
+        ek, eids = ex[rank] if existing_mode != "none" else (None, None)
+        st = DeviceStages(eng, 0)
+        out = {}
+        for call in range(2):
+            link, c, l = identifier_dedup_distributed(st, k, h, s, ids, 100, ek, eids)
+            out[f"link{call}"] = link.cpu().numpy()
+            out[f"count{call}"] = np.array([c, l])
+            out[f"proto{call}"] = np.array(st.last_protocol)
+        np.savez(os.path.join(outdir, f"r{rank}.npz"), **out)
+    finally:
+        eng.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("existing_mode", ["full", "none", "sparse"])
+def test_two_process_device_dedup(oracle, existing_mode):
+    import torch.multiprocessing as mp
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        ctx = mp.start_processes(_worker, args=(world, _free_port(), d, existing_mode), nprocs=world, join=False,
+                                 start_method="spawn")
+        deadline = time.time() + 100
+        try:
+            while not ctx.join(timeout=5):
+                assert time.time() < deadline, "ranks did not finish"
+        finally:
+            for p in ctx.processes:
+                if p.is_alive():
+                    p.terminate()
+        parts = [np.load(os.path.join(d, f"r{r}.npz")) for r in range(world)]
+    keys, has, status, existing = _corpus(existing_mode)
+    want, wc, wl = oracle.identifier_dedup(keys, has, status, 100, existing)
+    for call in range(2):
+        assert np.array_equal(np.concatenate([p[f"link{call}"] for p in parts]), want), call
+        for p in parts:
+            assert tuple(int(x) for x in p[f"count{call}"]) == (wc, wl)
+    assert [str(p["proto0"]) for p in parts] == ["exact"] * world
+    assert [str(p["proto1"]) for p in parts] == ["buckets"] * world
+
+
+def test_two_streams_share_one_context(oracle):
+    """dedup_local on two raw streams of one context, enqueued back to back
+    with no ordering between the streams on the caller's side: the second
+    call clears the shared resolve table while the first may still run, so
+    the library must order them (sdcas_ctx::fence_in). Both results exact."""
+    from spacedrive_amd import Engine
+    eng = Engine()
+    try:
+        corpora = [make_corpus(s, 400_000, pool=50_000) for s in (1, 2)]
+        dev = torch.device("cuda", 0)
+        s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        bufs = []
+        for keys, has, status, existing in corpora:
+            t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+            bufs.append(dict(k=t(keys.view(np.int64)), h=t(has), s=t(status),
+                             ids=torch.arange(keys.size, dtype=torch.int64, device=dev),
+                             ek=t(existing.view(np.int64)),
+                             eids=torch.arange(existing.size, dtype=torch.int64, device=dev),
+                             link=torch.empty(keys.size, dtype=torch.int64, device=dev),
+                             cnt=torch.zeros(2, dtype=torch.int64, device=dev)))
+        torch.cuda.synchronize()
+        for rep in range(3):
+            for b in bufs:
+                b["cnt"].zero_()
+            torch.cuda.synchronize()
+            for b, s in zip(bufs, (s1, s2)):
+                rc = eng.L.sdcas_dev_dedup_local(eng.ctx, b["k"].data_ptr(), b["h"].data_ptr(), b["s"].data_ptr(),
+                                                 b["ids"].data_ptr(), b["k"].numel(), b["ek"].data_ptr(),
+                                                 b["eids"].data_ptr(), b["ek"].numel(), 100, b["link"].data_ptr(),
+                                                 b["cnt"].data_ptr(), s.cuda_stream)
+                eng._check(rc, "sdcas_dev_dedup_local")
+            torch.cuda.synchronize()
+            for (keys, has, status, existing), b in zip(corpora, bufs):
+                want, wc, wl = oracle.identifier_dedup(keys, has, status, 100, existing)
+                assert np.array_equal(b["link"].cpu().numpy(), want), rep
+                assert tuple(b["cnt"].tolist()) == (wc, wl)
+    finally:
+        eng.close()

@@ -132,3 +132,109 @@ def test_stream_over_4tib_golden(eng):
         eng.dev_stream_finish(out.data_ptr())
         eng.dev_sync()
         assert bytes(out.cpu().numpy()[0]).hex() == c["checksum"], n
+
+
+@pytest.mark.parametrize("variant", [4, 11, 12, 13])
+def test_piece_variants_vs_oracle(oracle, variant):
+    """every product piece kernel (4: one workgroup per piece; 11-13: the
+    persistent grid on a piece counter, with / without the next piece's first
+    line preloaded, at 6 / 8 waves per SIMD) over multi-window files whose
+    windows hold many pieces and a ragged tail, against the oracle"""
+    from spacedrive_amd import Engine
+    rng = np.random.default_rng(40 + variant)
+    sizes = [MiB + 1, 5 * MiB + 17, 16 * MiB, 9 * MiB + 4095, 2 * MiB - 1, 40 * MiB + 3]
+    keys = [content_key(0x5D0004, 300 + i) for i in range(len(sizes))]
+    with Engine(staging_bytes=8 * MiB) as e:
+        assert e.dev_set_piece_variant(variant)
+        from tests._oracle import content
+        blob, offs = [], []
+        pos = 0
+        for k, n in zip(keys, sizes):
+            offs.append(pos)
+            blob.append(content("synth", 0, n, k))
+            pos += n
+        host = np.concatenate(blob)
+        out = e.hash_messages(host, np.array(offs, np.uint64), np.array(sizes, np.uint64))
+    for i, (k, n) in enumerate(zip(keys, sizes)):
+        assert bytes(out[i]).hex() == oracle.synth_checksum(k, n), (variant, n)
+
+
+def test_checksums_progress_and_cancel(oracle, tmp_path):
+    """a 1 GiB validator batch (eight 128 MiB files, 1 MiB-piece windows of
+    16 MiB) reports progress window by window and is cancelled midway
+    (job/mod.rs:862-960): files whose every piece was submitted keep exact
+    digests and status 0, the rest get SDCAS_STATUS_CANCELLED, the call
+    raises Cancelled; a second batch with the flag cleared completes"""
+    import ctypes
+    from spacedrive_amd import Engine
+    from spacedrive_amd import _native as N
+    from tests._oracle import content
+    sizes = [128 * MiB] * 7 + [128 * MiB + 777]
+    keys = [content_key(0x5D0004, 900 + i) for i in range(len(sizes))]
+    paths = []
+    for i, (k, n) in enumerate(zip(keys, sizes)):
+        p = tmp_path / f"big{i}"
+        p.write_bytes(content("synth", 0, n, k).tobytes())
+        paths.append(str(p))
+    flag = ctypes.c_int32(0)
+    seen = []
+
+    def progress(done, total):
+        seen.append((done, total))
+        if done >= 0.4 * total:
+            flag.value = 1
+
+    with Engine(staging_bytes=16 * MiB, io_threads=4, progress=progress, cancel=flag) as e:
+        with pytest.raises(N.Cancelled) as ex:
+            e.file_checksums(paths)
+        out, st = ex.value.partial
+        assert set(int(x) for x in st) <= {0, N.SDCAS_STATUS_CANCELLED}
+        done_files = [i for i in range(len(paths)) if st[i] == 0]
+        assert 0 < len(done_files) < len(paths), st
+        for i in done_files:
+            assert bytes(out[i]).hex() == oracle.synth_checksum(keys[i], sizes[i]), i
+        assert len(seen) >= 8 and all(t == sum(sizes) for _, t in seen)
+        assert all(a[0] <= b[0] for a, b in zip(seen, seen[1:]))
+        # cleared flag: the same context completes the whole batch
+        flag.value = 0
+        seen.clear()
+        e.set_progress(lambda d, t: seen.append((d, t)), flag)
+        out, st = e.file_checksums(paths[:3])
+        assert not st.any()
+        for i in range(3):
+            assert bytes(out[i]).hex() == oracle.synth_checksum(keys[i], sizes[i])
+        assert seen[-1][0] == seen[-1][1] == sum(sizes[:3])
+
+
+def test_cas_ids_cancel_per_slot(oracle, tmp_path):
+    """sdcas_cas_ids over 3000 small files in 1 MiB staging slots, cancelled
+    after about a third: completed files keep exact keys, the others are
+    SDCAS_STATUS_CANCELLED; a flag set before the call cancels every file"""
+    import ctypes
+    from spacedrive_amd import Engine
+    from spacedrive_amd import _native as N
+    rng = np.random.default_rng(8)
+    paths, sizes = [], []
+    for i in range(3000):
+        n = int(rng.integers(1, 60000))
+        p = tmp_path / f"s{i}"
+        p.write_bytes(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+        paths.append(str(p))
+        sizes.append(n)
+    flag = ctypes.c_int32(0)
+
+    def progress(done, total):
+        if done >= total // 3:
+            flag.value = 1
+
+    with Engine(staging_bytes=1 * MiB, io_threads=4, progress=progress, cancel=flag) as e:
+        with pytest.raises(N.Cancelled) as ex:
+            e.generate_cas_ids(paths, sizes)
+        keys, st = ex.value.partial
+        ok = np.nonzero(st == 0)[0]
+        assert 0 < ok.size < len(paths) and set(st.tolist()) <= {0, N.SDCAS_STATUS_CANCELLED}
+        for i in ok[:: max(1, ok.size // 200)]:
+            assert f"{int(keys[i]):016x}" == oracle.generate_cas_id(paths[i], sizes[i])
+        with pytest.raises(N.Cancelled) as ex:
+            e.generate_cas_ids(paths[:50], sizes[:50])  # still set: nothing is read
+        assert (ex.value.partial[1] == N.SDCAS_STATUS_CANCELLED).all()

@@ -177,3 +177,44 @@ def test_periodic_golden_is_large():
     """the periodic fixture reaches chunk counters >= 2^32"""
     cases = golden("checksums_periodic.json")
     assert cases and all(c["size"] > (4 << 40) for c in cases)
+
+
+def test_synth_cas_keys_mt_matches_per_file(oracle):
+    """the multi-threaded checker of the -m gpu corpus tests equals the
+    per-file scalar oracle, with upstream SIMD BLAKE3 and with the scalar
+    restatement"""
+    from spacedrive_amd import synth as S
+    sizes, ckeys, _ = S.c3_files(0, 400)
+    want = np.array([oracle.synth_cas_key(int(k), int(s)) for k, s in zip(ckeys, sizes)], np.uint64)
+    for up in (True, False):
+        got, _ = oracle.synth_cas_keys(ckeys, sizes, threads=3, upstream=up)
+        assert np.array_equal(got, want)
+
+
+def test_cpu_faithful_matches_generate_cas_id(oracle, tmp_path):
+    """bench.py's reference-faithful CPU leg reads real files with cas.rs's
+    pattern in 100-file steps: its keys and statuses equal the per-file oracle
+    (whole files, sampled sparse files, a short file, a missing one), over
+    several steps and with ragged last steps"""
+    from tests._oracle import cas_windows, write_sparse_file
+    rng = np.random.default_rng(5)
+    sizes = [int(x) for x in rng.integers(0, 102400, 180)] + [102401, 5 << 20, 1 << 30, 0, 1]
+    paths = []
+    for i, s in enumerate(sizes):
+        p = tmp_path / f"f{i}"
+        write_sparse_file(p, "synth", 1000 + i, s, cas_windows(s))
+        paths.append(str(p))
+    short = tmp_path / "short"
+    short.write_bytes(b"y" * 50000)
+    paths += [str(short), str(tmp_path / "missing")]
+    sizes += [300000, 10]
+    for chunk in (100, 7):
+        keys, st, secs, _ = oracle.cpu_faithful(paths, sizes, chunk=chunk, io_threads=4)
+        assert secs > 0
+        for i, (p, s) in enumerate(zip(paths, sizes)):
+            try:
+                want = oracle.generate_cas_id(p, s)
+            except OSError as e:
+                assert st[i] == e.errno, (i, st[i])
+                continue
+            assert st[i] == 0 and f"{int(keys[i]):016x}" == want, i

@@ -1,7 +1,11 @@
 #!/usr/bin/env python3
 """A/B the leaf/tree kernel variants on the C2 workload, interleaved rounds in
 ONE process (cdna_hip_programming.md §5.4 rule 24). Prints per-variant median
-and min leaf-kernel ms (HIP events) and checks all variants agree bit-exactly."""
+and min leaf-kernel ms (HIP events) and checks all variants agree bit-exactly.
+
+Binds the ablation library (libsdcas_ablate.so: `make -C spacedrive_amd/csrc
+ablate`), which holds every variant of round 1's A/B runs, the DIAGNOSTIC ones
+(wrong digests) included; --product binds libsdcas.so (product variants only)."""
 import argparse
 import os
 import sys
@@ -22,9 +26,13 @@ def main():
     ap.add_argument("--align", type=int, default=128, help="message start alignment in HBM")
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c5"])
     ap.add_argument("--sorts", default="1", help="comma list of slot orders to try: 1 length-sorted, 0 caller order")
+    ap.add_argument("--product", action="store_true", help="bind libsdcas.so instead of the ablation library")
     a = ap.parse_args()
     import torch
     from spacedrive_amd import Engine
+    from spacedrive_amd import _native as N
+    if not a.product:
+        N.use_ablation_library()
     dev = torch.device("cuda", 0)
     n = a.files
     sizes, keys, _ = bench.files_of(a.workload, 0, n)
@@ -42,8 +50,9 @@ def main():
     eng.dev_reserve(n, chunks)
     sp = torch.cuda.current_stream().cuda_stream
     eng.dev_synth_cas_messages(dk.data_ptr(), ds.data_ptr(), do.data_ptr(), n, d_blob.data_ptr(), sp)
-    nv = eng.dev_set_leaf_variant(-1)
-    vl = [int(v) for v in a.variants.split(",")] if a.variants else list(range(nv))
+    vl = [int(v) for v in a.variants.split(",")] if a.variants else [v for v in range(64) if eng.dev_set_leaf_variant(v)]
+    for v in vl:
+        assert eng.dev_set_leaf_variant(v), f"variant {v} is not in {N.ABLATION_LIB_PATH if not a.product else N.LIB_PATH}"
     vs = [(v, int(so)) for v in vl for so in a.sorts.split(",")]
     outs = {}
     res = {v: [] for v in vs}
