@@ -125,9 +125,10 @@ def compressions(lens):
     return 16 * (C - 1) + np.maximum(1, (last + 63) // 64) + (C - 1)
 
 
-def load_traffic(workload):
-    """HBM bytes per launch of the leaf kernel from the committed rocprofv3
-    PMC pass (profiles/*pmc*.json, written by tools/pmc_summarize.py), if any."""
+def load_traffic(workload, kernel="k_leaf_tree"):
+    """HBM bytes per launch of the dominant kernel from the committed
+    rocprofv3 PMC passes (profiles/*pmc*.json, written by
+    tools/pmc_summarize.py), the latest round's if several; None if none."""
     import glob
     best = None
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
@@ -135,7 +136,7 @@ def load_traffic(workload):
             d = json.load(open(p))
         except Exception:
             continue
-        if d.get("workload") == workload.upper() and d.get("kernel", "").startswith("k_leaf_tree"):
+        if d.get("workload") == workload.upper() and d.get("kernel", "").startswith(kernel):
             best = d
     return best
 
@@ -340,16 +341,25 @@ def c4_windows(sizes, files, window):
     return wins
 
 
-def run_c4(args, torch, dist, dev, rank, world, distributed):
+def run_c4(args, torch, dist, dev, rank, world, distributed, out_f):
     """C4: file_checksum of 256 GiB of 1-4 GiB files (strong scaling: the node
-    hashes the whole corpus, files assigned largest-first). Each window's
-    bytes are generated in HBM (untimed), then hashed as 1 MiB pieces; value
-    = bytes / summed hash time (HIP events on the hashing stream)."""
+    hashes the whole corpus, files assigned largest-first), hashed as 1 MiB
+    pieces; value = bytes / summed hash time (HIP events on the hashing
+    stream). A rank's share is generated in HBM once, before the timed
+    region, whenever it fits (the whole 256 GiB does, in one MI355X's 288 GB);
+    otherwise it is cut into windows regenerated (untimed) inside each pass."""
     from spacedrive_amd import Engine
     sizes, ckeys = S.c4_files(int(args.c4_total_gib) << 30)
     mine = c4_assign(sizes, world)[rank]
-    window = int(args.window_gib) << 30
+    MiB = 1 << 20
+    need = int(sum((int(sizes[f]) + MiB - 1) // MiB * MiB for f in mine))
+    if args.window_gib > 0:
+        window = int(args.window_gib) << 30
+    else:
+        free, _ = torch.cuda.mem_get_info(dev)
+        window = need if need + (6 << 30) < free else 64 << 30
     wins = c4_windows(sizes, mine, window)
+    resident = len(wins) == 1
     eng = Engine(device=dev.index)
     if args.piece_variant >= 0:
         assert eng.dev_set_piece_variant(args.piece_variant), args.piece_variant
@@ -369,13 +379,21 @@ def run_c4(args, torch, dist, dev, rank, world, distributed):
                  np.array([x[2] for x in w], np.uint64), np.array([base + x[3] for x in w], np.uint64))))
     my_bytes = int(sum(int(sizes[f]) for f in mine))
 
+    def generate(a):
+        eng.dev_synth_content(a["keys"].data_ptr(), a["starts"].data_ptr(), a["lens"].data_ptr(),
+                              a["offs"].data_ptr(), a["keys"].numel(), base, sp)
+
     def one_pass():
         eng.dev_stream_begin(sizes[mine])
         for a in win_args:
-            eng.dev_synth_content(a["keys"].data_ptr(), a["starts"].data_ptr(), a["lens"].data_ptr(),
-                                  a["offs"].data_ptr(), a["keys"].numel(), base, sp)
+            if not resident:
+                generate(a)
             eng.dev_stream_update(*a["seg"], stream=sp)
         eng.dev_stream_finish(out32.data_ptr(), sp)
+
+    torch.cuda.synchronize()  # the argument tensors are on the device before the side stream reads them
+    if resident:
+        generate(win_args[0])
 
     for _ in range(args.warmup):
         one_pass()
@@ -403,16 +421,17 @@ def run_c4(args, torch, dist, dev, rank, world, distributed):
         "metric": METRIC, "value": gbs, "unit": "GB/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": hash_s / args.steps * 1e3, "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "u32",
-        "data": "synthetic: C4 corpus (seed 0x5D0004) generated in HBM window by window",
+        "data": "synthetic: C4 corpus (seed 0x5D0004) generated in HBM " +
+                ("once, before the timed region" if resident else "window by window (untimed)"),
         "config": {"workload": WORKLOADS["c4"]["desc"], "files": int(sizes.size), "bytes": int(sizes.sum()),
-                   "window_bytes": window, "windows_per_pass_rank0": len(win_args),
+                   "window_bytes": window, "windows_per_pass_rank0": len(win_args), "resident": resident,
                    "parallelism": f"files assigned largest-first over {world} GPU(s), no collective"},
         "blake3_gbps": gbs,
         "wall_incl_generation_gbps": total / wall / 1e9,
         "roofline": {
             "bound": "hbm", "kernel": "k_piece_tree (1 MiB pieces -> level-10 nodes)",
             "achieved": my_bytes * args.steps / (hash_s) / 1e9 if hash_s > 0 else None, "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "traffic": None,
+            "unit": "GB/s", "traffic": None, "algorithmic_bytes_per_launch": my_bytes,
             "valu": {"compressions_per_s_node": comp / hash_s,
                      "peak_compressions_per_s_isa": VALU_PEAK_ISA,
                      "frac_of_isa_peak_per_gpu": comp / hash_s / world / VALU_PEAK_ISA,
@@ -423,6 +442,12 @@ def run_c4(args, torch, dist, dev, rank, world, distributed):
                            "tests/test_gpu_stream.py (multi-piece messages up to 4 GiB + 1)"},
     }
     out["roofline"]["frac"] = out["roofline"]["achieved"] / HBM_PEAK_GBS if out["roofline"]["achieved"] else None
+    # PMC traffic of the kernel this run launched (the default piece kernel
+    # unless --piece-variant chose another)
+    tr = load_traffic("c4", "k_piece_tree<8, 6, 1, 0>") if args.piece_variant in (-1, 6) else None
+    if tr and resident and tr.get("algorithmic_bytes_per_launch") == my_bytes:
+        out["roofline"]["traffic"] = tr["hbm_bytes_per_launch"]
+        out["roofline"]["traffic_source"] = tr.get("source")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # bounded sample: the first files (in corpus order) up to c4_cpu_gib
         pick, acc = [], 0
@@ -440,11 +465,28 @@ def run_c4(args, torch, dist, dev, rank, world, distributed):
         out["cpu_baseline"] = base
         out["parity"]["cpu_baseline_sample"] = parity
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out_f, out)
     eng.close()
 
 
+def _json_stdout():
+    """The contract's ONE JSON line goes to the process's stdout; everything
+    else that C libraries print there (RCCL's version banner at communicator
+    setup) is moved to stderr: fd 1 becomes a copy of fd 2, and the JSON is
+    written to the saved original."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    return os.fdopen(saved, "w")
+
+
+def emit(out_f, obj):
+    out_f.write(json.dumps(obj) + "\n")
+    out_f.flush()
+
+
 def main():
+    out_f = _json_stdout()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -455,7 +497,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--c4-total-gib", type=int, default=256)
-    ap.add_argument("--window-gib", type=int, default=64)
+    ap.add_argument("--window-gib", type=int, default=0, help="c4: HBM window (0: the whole share when it fits)")
     ap.add_argument("--c4-cpu-gib", type=int, default=16, help="C4 CPU-baseline sample size")
     ap.add_argument("--e2e-files", type=int, default=200_000, help="c2: files in the end-to-end / faithful leg")
     ap.add_argument("--no-e2e", action="store_true")
@@ -487,7 +529,7 @@ def main():
         dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=dev)
 
     if args.workload == "c4":
-        run_c4(args, torch, dist, dev, rank, world, distributed)
+        run_c4(args, torch, dist, dev, rank, world, distributed, out_f)
         if dist.is_initialized():
             dist.destroy_process_group()
         return
@@ -639,7 +681,7 @@ def main():
             if "cpu_baseline" in out and out["e2e"].get("reference_faithful"):
                 out["cpu_baseline"]["reference_faithful"] = out["e2e"].pop("reference_faithful")
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out_f, out)
     eng.close()
     if dist.is_initialized():
         dist.destroy_process_group()

@@ -280,11 +280,13 @@ __global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __
   if (total > cap_chunks) return;  // reported by sdcas_dev_sync
   const uint64_t ntiles = (total + kTile - 1) / kTile;
   const uint32_t tid = threadIdx.x;
-  // DYN: tiles after the first are handed out by a global counter (total_p[2],
-  // zeroed by k_tile_first) instead of round-robin, so a workgroup that drew
-  // cheap tiles takes more and the grid drains within about one tile; the
-  // next tile is claimed at the start of the current one (the atomic's
-  // latency hides behind the tile) and read after its last barrier
+  // DYN 1: tiles after the first are handed out by a global counter
+  // (total_p[2], zeroed by k_tile_first) instead of round-robin, so a
+  // workgroup that drew cheap tiles takes more and the grid drains within
+  // about one tile; the next tile is claimed at the start of the current one
+  // (the atomic's latency hides behind the tile) and read after its last
+  // barrier. DYN 2: one tile per workgroup (the grid covers every tile the
+  // workspace can hold; the hardware dispatcher is the schedule).
   unsigned long long* tile_ctr = reinterpret_cast<unsigned long long*>(const_cast<uint64_t*>(total_p) + 2);
   for (uint64_t tile = blockIdx.x; tile < ntiles;) {
     const uint64_t tbase = tile * kTile;
@@ -293,7 +295,7 @@ __global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __
     const uint32_t cnt = m1 - m0 + 1;  // <= kTile + 1
     for (uint32_t i = tid; i < cnt; i += WG) sS[i] = S[m0 + i];
     if (tid < 12) ntask[tid] = 0;
-    if (DYN && tid == 0) next_tile = gridDim.x + atomicAdd(tile_ctr, 1ull);
+    if (DYN == 1 && tid == 0) next_tile = gridDim.x + atomicAdd(tile_ctr, 1ull);
     __syncthreads();
 
     // (1) slot -> message, and the tree schedule: every aligned complete
@@ -390,7 +392,7 @@ __global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __
     // the next tile, read between two barriers: thread 0 overwrites next_tile
     // only after this tile's last barrier, which every thread has passed the
     // read by then
-    const uint64_t nt = DYN ? next_tile : tile + gridDim.x;
+    const uint64_t nt = DYN == 2 ? ntiles : (DYN ? next_tile : tile + gridDim.x);
 
     // (3) the tree, level by level: every task of a level is independent
     for (uint32_t k = 1; TR && k <= 10; ++k) {
@@ -1067,7 +1069,8 @@ size_t batch_scan_temp_bytes(uint32_t max_msgs) {
 struct LeafVariant {
   const void* fn;
   int wg;
-  int quad = 0;  // 1: quad slot layout (k_leaf_quad / k_finish_t<kQTile>, needs the shape-sorted order)
+  int quad = 0;      // 1: quad slot layout (k_leaf_quad / k_finish_t<kQTile>, needs the shape-sorted order)
+  int one_tile = 0;  // 1: one tile per workgroup (DYN 2): the grid covers the workspace's tiles
 };
 #define PROD(wg, ...) {(const void*)__VA_ARGS__, wg}
 #ifdef SDCAS_ABLATIONS
@@ -1078,6 +1081,11 @@ struct LeafVariant {
 #define ABLQ(wg, ...) {nullptr, wg, 1}
 #endif
 #define RET {nullptr, 512}
+#ifdef SDCAS_ABLATIONS
+#define ABL1(wg, ...) {(const void*)__VA_ARGS__, wg, 0, 1}
+#else
+#define ABL1(wg, ...) {nullptr, wg, 0, 1}
+#endif
 static const LeafVariant kLeafVariants[] = {
     ABL(512, k_leaf_tree<512, 0>),   // 0: plain block loop
     ABL(512, k_leaf_tree<512, 1>),   // 1: next block prefetched
@@ -1121,8 +1129,11 @@ static const LeafVariant kLeafVariants[] = {
     ABL(512, k_leaf_tree<512, 2, 0, 1, 1>),
     ABL(512, k_leaf_tree<512, 7, 1, 1, 1>),    // 42: 29 with 128-byte pair loads
     PROD(512, k_leaf_tree<512, 8, 1, 1, 1>),   // 43 (default): 36 with both halves of a line loaded together
+    ABL1(512, k_leaf_tree<512, 8, 1, 1, 2>),   // 44: 43 with one tile per workgroup (hardware dispatch)
+    ABL1(512, k_leaf_tree<512, 4, 1, 1, 2>),   // 45: 36 with one tile per workgroup
 };
 #undef PROD
+#undef ABL1
 #undef ABL
 #undef ABLQ
 #undef RET
@@ -1199,7 +1210,8 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
   {
     int dev = 0;
     (void)hipGetDevice(&dev);
-    const int grid = batch_grid(dev, v);
+    const int grid = kLeafVariants[v].one_tile ? (int)std::min<uint64_t>(ws.cap_slots / kTile + 1, 0x7FFFFFFF)
+                                               : batch_grid(dev, v);
     void* args[] = {(void*)&blob,     (void*)&offs,          (void*)&lens,       (void*)&n,
                     (void*)&ws.S,     (void*)&ws.tile_first, (void*)&ws.total,   (void*)&ws.cap_slots,
                     (void*)&ws.nodes, (void*)&out32,         (void*)&out_keys,   (void*)&perm};
@@ -1222,16 +1234,19 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
 }
 
 // Piece kernel variants: 4 = one workgroup per piece, ping-pong block loop,
-// 6 waves/SIMD (round 1's default); 11 = persistent grid on a global piece
+// 6 waves/SIMD (round 1's default); 6 (default) = 4 with the leaf kernel's
+// line-pair loads: the same time on resident C4 (3.15 TB/s), HBM reads 1.007x
+// the file bytes instead of 1.074x (profiles/r02_pmc_c4*.json); 11 =
+// persistent grid on a global piece
 // counter (k_piece_dyn); 12 = 11 with the next piece's first line loaded
 // before the current piece's tree levels; 13 = 11 at 8 waves/SIMD. The
 // others (plain / prefetch loops, rotated chunk order, a round-robin
 // persistent grid, and the DIAGNOSTIC 7 without memory reads) exist only in
 // the ablation library.
-constexpr int kDefaultPieceVariant = 4;
+constexpr int kDefaultPieceVariant = 6;
 
 bool piece_variant_available(int v) {
-  if (v == 4 || v == 11 || v == 12 || v == 13) return true;
+  if (v == 4 || v == 6 || v == 11 || v == 12 || v == 13) return true;
 #ifdef SDCAS_ABLATIONS
   if (v >= 0 && v <= 10) return true;
 #endif
@@ -1275,6 +1290,10 @@ hipError_t piece_hash(const uint8_t* blob, const PieceDesc* pieces, uint32_t npi
   if (v == 11) return launch_piece_dyn<6, 0>(blob, pieces, npieces, file_nodes, ctr, st);
   if (v == 12) return launch_piece_dyn<6, 1>(blob, pieces, npieces, file_nodes, ctr, st);
   if (v == 13) return launch_piece_dyn<8, 0>(blob, pieces, npieces, file_nodes, ctr, st);
+  if (v == 6) {  // 4 with both halves of a 128-byte line loaded together (the leaf kernel's loop)
+    hipLaunchKernelGGL((k_piece_tree<8, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
+    return hipGetLastError();
+  }
 #ifdef SDCAS_ABLATIONS
   if (v == 0) hipLaunchKernelGGL((k_piece_tree<0, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   else if (v == 1)
@@ -1285,8 +1304,6 @@ hipError_t piece_hash(const uint8_t* blob, const PieceDesc* pieces, uint32_t npi
     hipLaunchKernelGGL((k_piece_tree<1, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   else if (v == 5)
     hipLaunchKernelGGL((k_piece_tree<4, 8, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
-  else if (v == 6)  // 4 with both halves of a line loaded together
-    hipLaunchKernelGGL((k_piece_tree<8, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   else if (v == 7)  // DIAGNOSTIC (wrong digests): 4's loop without memory reads
     hipLaunchKernelGGL((k_piece_tree<2, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   else if (v == 8)  // 4 with per-workgroup rotated chunk order

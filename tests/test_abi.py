@@ -79,7 +79,7 @@ def test_product_library_holds_only_product_kernels():
     assert not [s for s in stubs if "slim" in s or "quad" in s]
     pieces = [s for s in stubs if s.startswith("k_piece")]
     assert sorted(pieces) == ["k_piece_dyn<6, 0>", "k_piece_dyn<6, 1>", "k_piece_dyn<8, 0>",
-                              "k_piece_tree<4, 6, 1, 0>"], pieces
+                              "k_piece_tree<4, 6, 1, 0>", "k_piece_tree<8, 6, 1, 0>"], pieces
 
 
 def test_ablation_build_is_separate():

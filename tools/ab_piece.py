@@ -35,9 +35,13 @@ def main():
     t = lambda x: torch.from_numpy(np.ascontiguousarray(x, dtype=np.uint64).view(np.int64)).to(dev)
     eng = Engine()
     z = np.zeros(sizes.size, np.uint64)
-    eng.dev_synth_content(t(keys).data_ptr(), t(z).data_ptr(), t(sizes).data_ptr(), t(offs).data_ptr(), sizes.size,
-                          blob.data_ptr())
+    # keep every argument tensor alive until the kernel has run (a temporary's
+    # block returns to torch's cache at once and the next one may reuse it)
+    args = [t(keys), t(z), t(sizes), t(offs)]
+    torch.cuda.synchronize()
+    eng.dev_synth_content(*(x.data_ptr() for x in args), sizes.size, blob.data_ptr())
     eng.dev_sync()
+    del args
     out = torch.zeros((sizes.size, 32), dtype=torch.uint8, device=dev)
     files = np.arange(sizes.size, dtype=np.uint64)
     addrs = np.uint64(blob.data_ptr()) + offs

@@ -1,17 +1,19 @@
 #!/bin/bash
-# HBM traffic of the C2 leaf kernel from PMC counters (separate passes, as
-# MI355X_MICROARCH.md prescribes). Usage: tools/pmc_traffic.sh <outdir> [variant]
+# HBM traffic of one kernel from PMC counters, each counter group in a run of
+# its own (MI355X_MICROARCH.md, HBM / rocprofv3 section).
+# Usage: tools/pmc_traffic.sh <outdir> [-- program args...]
+# (default program: the C2 leaf kernel through tools/ab_leaf.py, variant 43)
 set -u
 OUT=${1:-gpurun_out/pmc_traffic}
-VAR=${2:-43}  # the default leaf variant (kDefaultLeafVariant)
+shift || true
 R=$(pwd)
+if [ "${1:-}" = "--" ]; then shift; PROG="$*"; else PROG="python $R/tools/ab_leaf.py --product --rounds 1 --reps 2 --variants 43"; fi
 mkdir -p $OUT
 export TMPDIR=/tmp
-PROG="python $R/tools/ab_leaf.py --rounds 1 --reps 2 --variants $VAR"
 pass() {
   local name=$1; shift
   echo "== pass $name: $*"
-  (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc "$@" -d $R/$OUT/$name -o $name --output-format csv -- $PROG \
+  (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc "$@" -d $R/$OUT/$name -o $name --output-format csv -- $PROG \
      > $R/$OUT/$name.log 2>&1)
   local rc=$?
   echo "rc=$rc"
