@@ -25,6 +25,7 @@
 
 #include "../../include/sdcas.h"
 #include "../../include/sdcas_bench.h"
+#include "../host/cas_io.hpp"
 #include "b3_batch.h"
 #include "dist_dedup.h"
 #include "synth.h"
@@ -33,12 +34,11 @@ using namespace sdcas;
 
 namespace {
 
-constexpr uint64_t kSample = SDCAS_SAMPLE_SIZE, kHF = SDCAS_HEADER_OR_FOOTER_SIZE;
-constexpr uint64_t kMin = SDCAS_MINIMUM_FILE_SIZE, kSampleCount = SDCAS_SAMPLE_COUNT;
+constexpr uint64_t kMin = SDCAS_MINIMUM_FILE_SIZE;  // cas.rs:15 (the reads themselves: host/cas_io.cpp)
 constexpr uint64_t kSlack = 64;  // readable bytes kept after every message
 
 // staged messages start on 128-byte (L2/HBM line) boundaries
-inline uint64_t align16(uint64_t x) { return (x + 127) & ~127ull; }
+inline uint64_t align16(uint64_t x) { return sdcas_io::align_line(x); }
 inline uint64_t chunks_of(uint64_t len) { return len == 0 ? 1 : (len + 1023) / 1024; }
 
 template <class T>
@@ -479,108 +479,13 @@ int run_big(sdcas_ctx* c, const std::vector<BigItem>& items, uint8_t* out32_host
 
 
 // ---- file I/O with the reference's read pattern ---------------------------
-
-// read_exact at `off` (tokio AsyncReadExt::read_exact): fill n bytes or fail
-// with UnexpectedEof
-int pread_exact(int fd, uint8_t* dst, uint64_t n, uint64_t off) {
-  uint64_t got = 0;
-  while (got < n) {
-    ssize_t r = pread(fd, dst + got, n - got, (off_t)(off + got));
-    if (r < 0) {
-      if (errno == EINTR) continue;
-      return errno;
-    }
-    if (r == 0) return SDCAS_STATUS_UNEXPECTED_EOF;
-    got += (uint64_t)r;
-  }
-  return 0;
-}
-
-// whole file into dst (capacity cap > expect, the size the indexer or a
-// stat just saw); returns status, *len = bytes read; sets *overflow when the
-// file holds at least cap bytes (it grew). A read that stops short exactly at
-// `expect` is taken as EOF — one pread per unchanged file instead of a second
-// one returning 0; shorter reads keep reading to EOF as fs::read does.
-int read_whole(int fd, uint8_t* dst, uint64_t cap, uint64_t expect, uint64_t* len, bool* overflow) {
-  uint64_t got = 0;
-  *overflow = false;
-  for (;;) {
-    if (got == cap) {
-      *overflow = true;
-      break;
-    }
-    ssize_t r = pread(fd, dst + got, cap - got, (off_t)got);
-    if (r < 0) {
-      if (errno == EINTR) continue;
-      return errno;
-    }
-    if (r == 0) break;
-    got += (uint64_t)r;
-    if (got == expect) break;
-  }
-  *len = got;
-  return 0;
-}
-
-// cas.rs:23-62 message of one file into dst (capacity >= expected length).
-// Returns status; *len = message length. *retry_len != 0 asks the caller to
-// retry with a bigger slot (the file grew past `size` since it was indexed).
-int read_cas_message(const char* path, uint64_t size, uint8_t* dst, uint64_t cap, uint64_t* len,
-                     uint64_t* retry_len) {
-  *retry_len = 0;
-  int fd = open(path, O_RDONLY | O_CLOEXEC);
-  if (fd < 0) return errno;
-  for (int i = 0; i < 8; ++i) dst[i] = (uint8_t)(size >> (8 * i));  // cas.rs:25
-  int st = 0;
-  if (size <= kMin) {
-    // cas.rs:27-29: fs::read of the file as it is now
-    uint64_t got = 0;
-    bool over = false;
-    st = read_whole(fd, dst + 8, cap - 8, size, &got, &over);
-    if (!st && over) {
-      struct stat sb;
-      if (fstat(fd, &sb) == 0) *retry_len = 8 + (uint64_t)sb.st_size + 4096;
-      else st = errno;
-    }
-    *len = 8 + got;
-  } else {
-    // cas.rs:35-58: header, 4 samples at 8192 + k*seek_jump, footer at EOF-8192
-    uint8_t* p = dst + 8;
-    st = pread_exact(fd, p, kHF, 0);
-    p += kHF;
-    const uint64_t seek_jump = (size - kHF * 2) / kSampleCount;
-    for (uint64_t k = 0; !st && k < kSampleCount; ++k) {
-      st = pread_exact(fd, p, kSample, kHF + k * seek_jump);
-      p += kSample;
-    }
-    if (!st) {
-      struct stat sb;
-      if (fstat(fd, &sb) != 0) st = errno;
-      else if ((uint64_t)sb.st_size < kHF) st = EINVAL;  // seek(End(-8192)) before byte 0
-      else st = pread_exact(fd, p, kHF, (uint64_t)sb.st_size - kHF);
-    }
-    *len = SDCAS_SAMPLED_MESSAGE_LEN;
-  }
-  close(fd);
-  return st;
-}
-
-template <class F>
-void parallel_for(uint32_t threads, size_t n, F f) {
-  if (n == 0) return;
-  threads = (uint32_t)std::max<size_t>(1, std::min<size_t>(threads, n));
-  if (threads == 1) {
-    for (size_t i = 0; i < n; ++i) f(i);
-    return;
-  }
-  std::atomic<size_t> next{0};
-  std::vector<std::thread> pool;
-  for (uint32_t t = 0; t < threads; ++t)
-    pool.emplace_back([&] {
-      for (size_t i; (i = next.fetch_add(1)) < n;) f(i);
-    });
-  for (auto& th : pool) th.join();
-}
+// (GPU-free, in spacedrive_amd/host/cas_io.cpp: tested under ASan / UBSan /
+// TSan by tests/cpp/test_cas_io.cpp)
+using sdcas_io::parallel_for;
+using sdcas_io::plan_batch;
+using sdcas_io::pread_exact;
+using sdcas_io::read_cas_message;
+using sdcas_io::read_whole;
 
 }  // namespace
 
@@ -948,14 +853,7 @@ int sdcas_cas_ids(sdcas_ctx* c, const char* const* paths, const uint64_t* sizes,
       }
       std::vector<uint64_t> slot_off;
       uint64_t used = 0;
-      size_t q = p;
-      while (q < todo.size() && q - p < cap_n) {
-        const uint64_t need = align16(want[todo[q]]);
-        if (q > p && used + need > cap) break;
-        slot_off.push_back(used);
-        used += need;
-        ++q;
-      }
+      const size_t q = plan_batch(want.data(), todo.data(), p, todo.size(), cap, cap_n, slot_off, &used);
       if ((rc = slot_prepare(c, s, std::max<uint64_t>(used, cap), cap_n))) return rc;
       const size_t m = q - p;
       std::vector<uint64_t> mlen(m), retry_len(m);
@@ -1015,9 +913,11 @@ int sdcas_checksums(sdcas_ctx* c, const char* const* paths, size_t n, uint8_t* o
   });
   std::vector<size_t> small;
   std::vector<BigItem> big;
+  std::vector<uint64_t> fneed(n);  // staging bytes: the stat length + the byte that tells a grown file
   Progress pr{c};
   for (size_t i = 0; i < n; ++i) {
     out_status[i] = fst[i];
+    fneed[i] = flen[i] + 1;
     if (fst[i]) continue;
     pr.total += flen[i];
     if (flen[i] > big_cut) big.push_back({flen[i], i});
@@ -1035,12 +935,7 @@ int sdcas_checksums(sdcas_ctx* c, const char* const* paths, size_t n, uint8_t* o
     if ((cancelled = c->cancelled())) break;
     std::vector<uint64_t> slot;
     uint64_t used = 0;
-    size_t q = p;
-    while (q < small.size() && q - p < cap_n && (q == p || used + align16(flen[small[q]] + 1) <= cap)) {
-      slot.push_back(used);
-      used += align16(flen[small[q]] + 1);
-      ++q;
-    }
+    const size_t q = plan_batch(fneed.data(), small.data(), p, small.size(), cap, cap_n, slot, &used);
     const size_t m = q - p;
     std::vector<uint64_t> got(m);
     std::vector<int32_t> st(m);

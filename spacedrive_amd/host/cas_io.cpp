@@ -1,0 +1,109 @@
+// cas_io.cpp — see cas_io.hpp. GPU-free; linked into libsdcas.so and into the
+// sanitizer test builds of tests/cpp.
+#include "cas_io.hpp"
+
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cerrno>
+
+namespace sdcas_io {
+
+// constants of core/src/object/cas.rs:10-15
+constexpr uint64_t kSampleCount = 4, kSample = 10240, kHF = 8192, kMin = 102400;
+constexpr uint64_t kSampledLen = 8 + 2 * kHF + kSampleCount * kSample;  // 57352
+
+int pread_exact(int fd, uint8_t* dst, uint64_t n, uint64_t off) {
+  uint64_t got = 0;
+  while (got < n) {
+    ssize_t r = pread(fd, dst + got, n - got, (off_t)(off + got));
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      return errno;
+    }
+    if (r == 0) return kUnexpectedEof;
+    got += (uint64_t)r;
+  }
+  return 0;
+}
+
+int read_whole(int fd, uint8_t* dst, uint64_t cap, uint64_t expect, uint64_t* len, bool* overflow) {
+  uint64_t got = 0;
+  *overflow = false;
+  for (;;) {
+    if (got == cap) {
+      *overflow = true;
+      break;
+    }
+    ssize_t r = pread(fd, dst + got, cap - got, (off_t)got);
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      return errno;
+    }
+    if (r == 0) break;
+    got += (uint64_t)r;
+    if (got == expect) break;
+  }
+  *len = got;
+  return 0;
+}
+
+int read_cas_message(const char* path, uint64_t size, uint8_t* dst, uint64_t cap, uint64_t* len,
+                     uint64_t* retry_len) {
+  *retry_len = 0;
+  *len = 0;
+  int fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return errno;
+  for (int i = 0; i < 8; ++i) dst[i] = (uint8_t)(size >> (8 * i));  // cas.rs:25
+  int st = 0;
+  if (size <= kMin) {
+    // cas.rs:27-29: fs::read of the file as it is now
+    uint64_t got = 0;
+    bool over = false;
+    st = read_whole(fd, dst + 8, cap - 8, size, &got, &over);
+    if (!st && over) {
+      struct stat sb;
+      if (fstat(fd, &sb) == 0) *retry_len = 8 + (uint64_t)sb.st_size + 4096;
+      else st = errno;
+    }
+    *len = 8 + got;
+  } else {
+    // cas.rs:35-58: header, 4 samples at 8192 + k*seek_jump, footer at EOF-8192
+    uint8_t* p = dst + 8;
+    st = pread_exact(fd, p, kHF, 0);
+    p += kHF;
+    const uint64_t seek_jump = (size - kHF * 2) / kSampleCount;
+    for (uint64_t k = 0; !st && k < kSampleCount; ++k) {
+      st = pread_exact(fd, p, kSample, kHF + k * seek_jump);
+      p += kSample;
+    }
+    if (!st) {
+      struct stat sb;
+      if (fstat(fd, &sb) != 0) st = errno;
+      else if ((uint64_t)sb.st_size < kHF) st = EINVAL;  // seek(End(-8192)) before byte 0
+      else st = pread_exact(fd, p, kHF, (uint64_t)sb.st_size - kHF);
+    }
+    *len = kSampledLen;
+  }
+  close(fd);
+  return st;
+}
+
+size_t plan_batch(const uint64_t* need, const size_t* order, size_t p, size_t end, uint64_t cap, size_t cap_n,
+                  std::vector<uint64_t>& offs, uint64_t* used) {
+  offs.clear();
+  uint64_t u = 0;
+  size_t q = p;
+  while (q < end && q - p < cap_n) {
+    const uint64_t nb = align_line(need[order ? order[q] : q]);
+    if (q > p && u + nb > cap) break;
+    offs.push_back(u);
+    u += nb;
+    ++q;
+  }
+  *used = u;
+  return q;
+}
+
+}  // namespace sdcas_io

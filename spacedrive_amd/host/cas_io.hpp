@@ -1,0 +1,72 @@
+// cas_io.hpp — the host file I/O of libsdcas's path calls, GPU-free so that it
+// is tested under ASan/UBSan and TSan on the CPU (tests/cpp/test_cas_io.cpp).
+//
+// The reads follow the reference exactly: generate_cas_id's
+// (core/src/object/cas.rs:23-62 — fs::read of a file up to 100 KiB; else an
+// 8 KiB header, four 10 KiB samples at 8192 + k * ((size - 16384) / 4) and
+// an 8 KiB footer at EOF - 8192, each with read_exact's UnexpectedEof), and
+// file_checksum's whole-content read (core/src/object/validation/hash.rs:15-21).
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <atomic>
+#include <thread>
+#include <vector>
+
+namespace sdcas_io {
+
+// per-item status of read_exact running out of file (tokio's UnexpectedEof;
+// include/sdcas.h SDCAS_STATUS_UNEXPECTED_EOF)
+constexpr int32_t kUnexpectedEof = 100001;
+
+// staged messages start on 128-byte (L2/HBM line) boundaries
+inline uint64_t align_line(uint64_t x) { return (x + 127) & ~127ull; }
+
+// read_exact at `off` (tokio AsyncReadExt::read_exact): fill n bytes or fail
+// with UnexpectedEof; returns 0 or a status
+int pread_exact(int fd, uint8_t* dst, uint64_t n, uint64_t off);
+
+// Whole file into dst (capacity cap > expect, the size the indexer or a stat
+// just saw); returns status, *len = bytes read; sets *overflow when the file
+// holds at least cap bytes (it grew). A read that stops short exactly at
+// `expect` is taken as EOF — one pread per unchanged file instead of a second
+// one returning 0; shorter reads keep reading to EOF as fs::read does.
+int read_whole(int fd, uint8_t* dst, uint64_t cap, uint64_t expect, uint64_t* len, bool* overflow);
+
+// cas.rs:23-62 message of one file into dst (capacity cap >= the message
+// length `size` predicts + 1). Returns status; *len = message length.
+// *retry_len != 0 asks the caller to retry with a slot of that capacity (the
+// file grew past `size` since it was indexed).
+int read_cas_message(const char* path, uint64_t size, uint8_t* dst, uint64_t cap, uint64_t* len,
+                     uint64_t* retry_len);
+
+// The next staging batch: items order[p], order[p+1], ... of `need` bytes
+// each (line-aligned here) go to offsets in one slot of `cap` bytes and at
+// most cap_n items; the first item always fits (a message larger than the
+// slot gets a slot of its own). Returns q (items [p, q) taken) and fills
+// offs[0 .. q-p) and *used.
+size_t plan_batch(const uint64_t* need, const size_t* order, size_t p, size_t end, uint64_t cap, size_t cap_n,
+                  std::vector<uint64_t>& offs, uint64_t* used);
+
+// f(i) for i in [0, n) on up to `threads` threads (items claimed from a
+// shared counter)
+template <class F>
+void parallel_for(uint32_t threads, size_t n, F f) {
+  if (n == 0) return;
+  threads = (uint32_t)std::max<size_t>(1, std::min<size_t>(threads, n));
+  if (threads == 1) {
+    for (size_t i = 0; i < n; ++i) f(i);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  std::vector<std::thread> pool;
+  for (uint32_t t = 0; t < threads; ++t)
+    pool.emplace_back([&] {
+      for (size_t i; (i = next.fetch_add(1)) < n;) f(i);
+    });
+  for (auto& th : pool) th.join();
+}
+
+}  // namespace sdcas_io

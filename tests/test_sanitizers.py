@@ -1,0 +1,39 @@
+"""Sanitizer runs of the host code (race detection /
+sanitizers). GPU sanitizers are not available on this pool, so the host side
+is checked on the CPU:
+
+* test_cas_io (plain, ASan + UBSan, TSan): libsdcas's GPU-free file I/O
+  (spacedrive_amd/host/cas_io.cpp — cas.rs's reads, the slot packing) on 8
+  threads against the oracle's generate_cas_id, over whole / sampled / grown /
+  shrunk / missing / directory paths;
+* test_sdcore_db_asan: the C++ host mirror (libsdcore: the identifier and
+  validator jobs over MemoryLibrary and SqliteLibrary, the indexer walk and
+  kind detection) built with ASan + UBSan, running the DB-side tests.
+
+A sanitizer report makes the binary fail (-fno-sanitize-recover, LSan at exit).
+"""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CPP = os.path.join(ROOT, "tests", "cpp")
+
+
+@pytest.fixture(scope="module")
+def built():
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    r = subprocess.run(["make", "-s", "-C", CPP, "sanitize"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    return os.path.join(CPP, "build")
+
+
+@pytest.mark.parametrize("binary", ["test_cas_io", "test_cas_io_asan", "test_cas_io_tsan", "test_sdcore_db_asan"])
+def test_sanitized_host_code(built, binary):
+    env = dict(os.environ, ASAN_OPTIONS="abort_on_error=0:detect_leaks=1", TSAN_OPTIONS="halt_on_error=1")
+    r = subprocess.run([os.path.join(built, binary)], capture_output=True, text=True, timeout=600, env=env)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0 and "ALL OK" in r.stdout, out[-4000:]
+    for marker in ("AddressSanitizer", "LeakSanitizer", "ThreadSanitizer", "runtime error:"):
+        assert marker not in out, out[-4000:]
