@@ -57,15 +57,21 @@ __host__ __device__ inline uint64_t chunk_count(uint64_t len) { return len == 0 
 // Highest level k such that the node of 2^k chunks starting at chunk j is
 // (a) an aligned complete block of the message, (b) not the whole message and
 // (c) inside the tile that holds chunk j at slot `s`.
-__host__ __device__ inline uint32_t node_level(uint64_t j, uint64_t C, uint32_t s) {
-  uint32_t k = 0;
-  for (;;) {
-    uint64_t w = 2ull << k;
-    if ((j & (w - 1)) || j + w > C || w >= C || (uint64_t)s + w > kTile) break;
-    ++k;
-  }
-  return k;
+// Closed form (checked against the defining loop — grow k while the node of
+// 2^(k+1) chunks at j is aligned, fits the message, is not the whole message
+// and fits the tile — on 2 M random cases): the largest k with 2^k dividing j,
+// 2^k <= C - j, 2^k < C and 2^k <= TILE - s.
+__host__ __device__ inline uint32_t floor_log2(uint64_t x) { return 63u - (uint32_t)__builtin_clzll(x); }  // x > 0
+
+template <uint32_t TILE>
+__host__ __device__ inline uint32_t node_level_t(uint64_t j, uint64_t C, uint32_t s) {
+  if (C <= 1) return 0;
+  const uint32_t a = j ? (uint32_t)__builtin_ctzll(j) : 63u;
+  const uint32_t b = min(floor_log2(C - j), floor_log2(C - 1));
+  return min(min(a, b), floor_log2((uint64_t)TILE - s));
 }
+
+__host__ __device__ inline uint32_t node_level(uint64_t j, uint64_t C, uint32_t s) { return node_level_t<kTile>(j, C, s); }
 
 // Is the level-k node at (j, s) consumed by a parent computed in the same tile?
 __host__ __device__ inline bool parent_in_tile(uint64_t j, uint64_t C, uint32_t s, uint32_t k) {
@@ -143,17 +149,50 @@ __device__ __forceinline__ void hash_chunk_ps(const uint8_t* __restrict__ p, uin
   }
 }
 
+// The line-pair loop with its per-block bookkeeping cut to compares against
+// the chunk's last block index (computed once): a full block's length and
+// flags are constants selected by one compare, the tail mask runs only on
+// the last block, the second half of a line is loaded only if the chunk has
+// it (no clamped address), and the block pointer advances by one add.
+__device__ __forceinline__ void hash_chunk_pl(const uint8_t* __restrict__ p, uint32_t clen, uint64_t j, bool root,
+                                              uint32_t (&cv)[8]) {
+  set_iv(cv);
+  const uint32_t lb = clen <= BLOCK_LEN ? 0u : (clen - 1) / BLOCK_LEN;  // last block index
+  const uint32_t lblen = clen - lb * BLOCK_LEN;                          // its length (0 only for an empty message)
+  const uint32_t endf = CHUNK_END | (root ? ROOT : 0u);
+  uint32_t m0[16], m1[16];
+  const uint8_t* q = p;
+#pragma unroll 1
+  for (uint32_t b = 0; b <= lb; b += 2, q += 2 * BLOCK_LEN) {
+    const bool two = b + 1 <= lb;
+    load_full_block(q, m0);
+    if (two) load_full_block(q + BLOCK_LEN, m1);
+    {
+      const bool last = b == lb;
+      if (last && lblen < BLOCK_LEN) mask_tail(m0, lblen);
+      compress(cv, m0, j, last ? lblen : BLOCK_LEN, (b == 0 ? CHUNK_START : 0u) | (last ? endf : 0u));
+    }
+    if (two) {
+      const bool last = b + 1 == lb;
+      if (last && lblen < BLOCK_LEN) mask_tail(m1, lblen);
+      compress(cv, m1, j, last ? lblen : BLOCK_LEN, last ? endf : 0u);
+    }
+  }
+}
+
 #ifdef SDCAS_ABLATIONS
 #include "b3_ablate_loops.inc"
 #endif
 
-// Block loop of a leaf chunk: PF 8 = hash_chunk_ps (default), 4 =
-// hash_chunk_pp; any other PF names an ablation loop.
+// Block loop of a leaf chunk: PF 8 = hash_chunk_ps (default), 9 =
+// hash_chunk_pl, 4 = hash_chunk_pp; any other PF names an ablation loop.
 template <int PF>
 __device__ __forceinline__ void leaf_hash(const uint8_t* __restrict__ p, uint32_t clen, uint64_t j, bool root,
                                           uint32_t (&cv)[8]) {
   if constexpr (PF == 8) {
     hash_chunk_ps(p, clen, j, root, cv);
+  } else if constexpr (PF == 9) {
+    hash_chunk_pl(p, clen, j, root, cv);
   } else if constexpr (PF == 4) {
     hash_chunk_pp(p, clen, j, root, cv);
   } else {
@@ -165,7 +204,7 @@ __device__ __forceinline__ void leaf_hash(const uint8_t* __restrict__ p, uint32_
     else if constexpr (PF == 1) hash_chunk_pf(p, clen, j, root, cv);
     else hash_chunk(p, clen, j, root, cv);
 #else
-    static_assert(PF == 8 || PF == 4, "ablation block loops need -DSDCAS_ABLATIONS");
+    static_assert(PF == 8 || PF == 9 || PF == 4, "ablation block loops need -DSDCAS_ABLATIONS");
 #endif
   }
 }
@@ -260,7 +299,7 @@ __device__ __forceinline__ void leaf_order(uint32_t tid, const uint32_t (&bin)[k
   __syncthreads();
 }
 
-template <int WG, int PF, int TR = 1, int ORD = 0, int DYN = 0>
+template <int WG, int PF, int TR = 1, int ORD = 0, int DYN = 0, int CA = 0>
 __global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ offs,
                                                    const uint64_t* __restrict__ lens, uint32_t n,
                                                    const uint64_t* __restrict__ S,
@@ -303,7 +342,19 @@ __global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __
     // the spine of each message lying wholly in the tile — the right-to-left
     // fold over its binary decomposition, one step per part, scheduled in the
     // level after that part's node is complete; the last step is the ROOT.
-#pragma unroll 1
+    // CA: the leaf phase takes the same two slots per lane as this loop (unless
+    // the leaf order permutes them), so their chunk's address, length and
+    // counter are kept in registers from here — the message's offset is
+    // loaded now, its latency hidden behind the schedule and the barrier,
+    // instead of on the leaf phase's critical path
+    constexpr uint32_t R = kTile / WG;
+    const uint8_t* c_p[R];
+    uint64_t c_j[R];
+    uint32_t c_clen[R], c_m[R];
+    bool c_ok[R], c_root[R];
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) c_ok[r] = false;
+#pragma unroll(CA ? R : 1)
     for (uint32_t s = tid; s < kTile; s += WG) {
       const uint64_t g = tbase + s;
       if (g >= total) {
@@ -317,10 +368,20 @@ __global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __
         else hi = mid - 1;
       }
       smsg[s] = (uint16_t)lo;
-      if (!TR) continue;
+      if (!TR && !CA) continue;
       const uint64_t j = g - sS[lo];
-      const uint64_t C = chunk_count(lens[m0 + lo]);
-      if (C == 1) continue;
+      const uint64_t len = lens[m0 + lo];
+      const uint64_t C = chunk_count(len);
+      if (CA) {
+        const uint32_t r = (s - tid) / WG;
+        c_ok[r] = true;
+        c_m[r] = m0 + lo;
+        c_j[r] = j;
+        c_clen[r] = len == 0 ? 0u : (uint32_t)min<uint64_t>(CHUNK_LEN, len - j * CHUNK_LEN);
+        c_root[r] = C == 1;
+        c_p[r] = blob + offs[m0 + lo] + j * CHUNK_LEN;
+      }
+      if (!TR || C == 1) continue;
       const uint32_t K = node_level(j, C, s);
       for (uint32_t k = 1; k <= K; ++k)
         task[task_base(k) + atomicAdd(&ntask[k], 1u)] = enc_task(s, s + (1u << (k - 1)), 0, false);
@@ -368,8 +429,23 @@ __global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __
       // between the previous tile's last barrier and this tile's leaves
       leaf_order<WG>(tid, bin, order, reinterpret_cast<uint16_t*>(&cvs[0][0]));
     }
+    if (CA && !ord) {
+#pragma unroll
+      for (uint32_t r = 0; r < R; ++r) {
+        if (!c_ok[r]) continue;
+        uint32_t cv[8];
+        leaf_hash<PF>(c_p[r], c_clen[r], c_j[r], c_root[r], cv);
+        if (c_root[r]) {
+          store_digest(perm ? perm[c_m[r]] : c_m[r], cv, out32, out_keys);
+        } else {
+          const uint32_t s = tid + r * WG;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) cvs[s][i] = cv[i];
+        }
+      }
+    }
 #pragma unroll 1
-    for (uint32_t i = tid; i < kTile; i += WG) {
+    for (uint32_t i = tid; (!CA || ord) && i < kTile; i += WG) {
       const uint32_t s = ord ? order[i] : i;
       const uint32_t mi = smsg[s];
       if (mi == kNoMsg) continue;
@@ -440,17 +516,6 @@ __global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __
     __syncthreads();
     tile = nt;
   }
-}
-
-template <uint32_t TILE>
-__host__ __device__ inline uint32_t node_level_t(uint64_t j, uint64_t C, uint32_t s) {
-  uint32_t k = 0;
-  for (;;) {
-    uint64_t w = 2ull << k;
-    if ((j & (w - 1)) || j + w > C || w >= C || (uint64_t)s + w > TILE) break;
-    ++k;
-  }
-  return k;
 }
 
 template <uint32_t TILE>
@@ -1061,11 +1126,12 @@ size_t batch_scan_temp_bytes(uint32_t max_msgs) {
   return std::max(bytes, qbytes);
 }
 
-// Leaf/tree kernel variants, numbered as in round 1's A/B runs
-// so that profiles/ and tools/ keep their meaning. libsdcas.so holds only the
-// bit-exact, GPU-tested product kernels (the default, 43, and 36); every
-// other entry is compiled only into the ablation library (ABL), and the
-// stagger / priority experiments (8, 9, 11, 12, 37) are retired (RET).
+// Leaf/tree kernel variants, numbered as in the A/B runs of rounds 1-2
+//  so that profiles/ and tools/ keep their meaning. libsdcas.so
+// holds only the bit-exact, GPU-tested product kernels (the default, 49, and
+// round 1's default, 43); every other entry is compiled only into the
+// ablation library (ABL), and the stagger / priority experiments (8, 9, 11,
+// 12, 37) are retired (RET).
 struct LeafVariant {
   const void* fn;
   int wg;
@@ -1073,6 +1139,7 @@ struct LeafVariant {
   int one_tile = 0;  // 1: one tile per workgroup (DYN 2): the grid covers the workspace's tiles
 };
 #define PROD(wg, ...) {(const void*)__VA_ARGS__, wg}
+#define PROD1(wg, ...) {(const void*)__VA_ARGS__, wg, 0, 1}
 #ifdef SDCAS_ABLATIONS
 #define ABL(wg, ...) {(const void*)__VA_ARGS__, wg}
 #define ABLQ(wg, ...) {(const void*)__VA_ARGS__, wg, 1}
@@ -1121,24 +1188,29 @@ static const LeafVariant kLeafVariants[] = {
     ABL(512, k_leaf_slim<512, 0, 8, 0, 1>),
     ABL(1024, k_leaf_tree<1024, 1, 1, 1, 1>),  // 34: 29 at 1024 threads
     ABL(512, k_leaf_tree<512, 1, 1, 0, 1>),    // 35: 29 without the leaf order
-    PROD(512, k_leaf_tree<512, 4, 1, 1, 1>),   // 36: 29 with the ping-pong block loop
+    ABL(512, k_leaf_tree<512, 4, 1, 1, 1>),    // 36: 29 with the ping-pong block loop
     RET,                                        // 37: 29 with tree waves at priority 1
     ABL(512, k_leaf_tree<512, 6, 1, 1, 1>),    // 38: 29 with prefetch distance two
     ABL(512, k_leaf_tree<512, 4, 0, 1, 1>),    // 39-41 DIAGNOSTIC (wrong digests): 36 without tree / loads / both
     ABL(512, k_leaf_tree<512, 2, 1, 1, 1>),
     ABL(512, k_leaf_tree<512, 2, 0, 1, 1>),
     ABL(512, k_leaf_tree<512, 7, 1, 1, 1>),    // 42: 29 with 128-byte pair loads
-    PROD(512, k_leaf_tree<512, 8, 1, 1, 1>),   // 43 (default): 36 with both halves of a line loaded together
+    PROD(512, k_leaf_tree<512, 8, 1, 1, 1>),   // 43 (round 1's default): 36 with both halves of a line loaded together
     ABL1(512, k_leaf_tree<512, 8, 1, 1, 2>),   // 44: 43 with one tile per workgroup (hardware dispatch)
     ABL1(512, k_leaf_tree<512, 4, 1, 1, 2>),   // 45: 36 with one tile per workgroup
+    ABL1(512, k_leaf_tree<512, 9, 1, 1, 2>),   // 46: 44 with the last-block-index loop (hash_chunk_pl)
+    ABL(512, k_leaf_tree<512, 9, 1, 1, 1>),    // 47: 43 with the last-block-index loop
+    ABL(512, k_leaf_tree<512, 9, 1, 1, 1, 1>),    // 48: 47 with the leaf's chunk kept in registers from phase 1
+    PROD1(512, k_leaf_tree<512, 9, 1, 1, 2, 1>),  // 49 (default): 46 with the same
 };
 #undef PROD
+#undef PROD1
 #undef ABL1
 #undef ABL
 #undef ABLQ
 #undef RET
 constexpr int kNumLeafVariants = sizeof(kLeafVariants) / sizeof(kLeafVariants[0]);
-constexpr int kDefaultLeafVariant = 43;
+constexpr int kDefaultLeafVariant = 49;
 
 int leaf_variant_count() { return kNumLeafVariants; }
 bool leaf_variant_available(int v) { return v >= 0 && v < kNumLeafVariants && kLeafVariants[v].fn != nullptr; }
