@@ -344,7 +344,7 @@ __global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __
     // level after that part's node is complete; the last step is the ROOT.
     // CA: the leaf phase takes the same two slots per lane as this loop (unless
     // the leaf order permutes them), so their chunk's address, length and
-    // counter are kept in registers from here — the message's offset is
+    // counter (CA 2: the first slot's only) are kept in registers from here — the message's offset is
     // loaded now, its latency hidden behind the schedule and the barrier,
     // instead of on the leaf phase's critical path
     constexpr uint32_t R = kTile / WG;
@@ -372,7 +372,7 @@ __global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __
       const uint64_t j = g - sS[lo];
       const uint64_t len = lens[m0 + lo];
       const uint64_t C = chunk_count(len);
-      if (CA) {
+      if (CA && (CA == 1 || s == tid)) {
         const uint32_t r = (s - tid) / WG;
         c_ok[r] = true;
         c_m[r] = m0 + lo;
@@ -431,7 +431,7 @@ __global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __
     }
     if (CA && !ord) {
 #pragma unroll
-      for (uint32_t r = 0; r < R; ++r) {
+      for (uint32_t r = 0; r < (CA == 1 ? R : 1); ++r) {
         if (!c_ok[r]) continue;
         uint32_t cv[8];
         leaf_hash<PF>(c_p[r], c_clen[r], c_j[r], c_root[r], cv);
@@ -444,8 +444,10 @@ __global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __
         }
       }
     }
+    // (CA 2 keeps the first slot only: the second one's state would live in
+    // registers across the first one's block loop, where they spill)
 #pragma unroll 1
-    for (uint32_t i = tid; (!CA || ord) && i < kTile; i += WG) {
+    for (uint32_t i = (CA == 2 && !ord) ? tid + WG : tid; (CA != 1 || ord) && i < kTile; i += WG) {
       const uint32_t s = ord ? order[i] : i;
       const uint32_t mi = smsg[s];
       if (mi == kNoMsg) continue;
@@ -1128,7 +1130,7 @@ size_t batch_scan_temp_bytes(uint32_t max_msgs) {
 
 // Leaf/tree kernel variants, numbered as in the A/B runs of rounds 1-2
 //  so that profiles/ and tools/ keep their meaning. libsdcas.so
-// holds only the bit-exact, GPU-tested product kernels (the default, 49, and
+// holds only the bit-exact, GPU-tested product kernels (the default, 50, and
 // round 1's default, 43); every other entry is compiled only into the
 // ablation library (ABL), and the stagger / priority experiments (8, 9, 11,
 // 12, 37) are retired (RET).
@@ -1201,7 +1203,8 @@ static const LeafVariant kLeafVariants[] = {
     ABL1(512, k_leaf_tree<512, 9, 1, 1, 2>),   // 46: 44 with the last-block-index loop (hash_chunk_pl)
     ABL(512, k_leaf_tree<512, 9, 1, 1, 1>),    // 47: 43 with the last-block-index loop
     ABL(512, k_leaf_tree<512, 9, 1, 1, 1, 1>),    // 48: 47 with the leaf's chunk kept in registers from phase 1
-    PROD1(512, k_leaf_tree<512, 9, 1, 1, 2, 1>),  // 49 (default): 46 with the same
+    ABL1(512, k_leaf_tree<512, 9, 1, 1, 2, 1>),   // 49: 46 with the same
+    PROD1(512, k_leaf_tree<512, 9, 1, 1, 2, 2>),  // 50 (default): 49 keeping only the first slot's chunk (no spills)
 };
 #undef PROD
 #undef PROD1
@@ -1210,7 +1213,7 @@ static const LeafVariant kLeafVariants[] = {
 #undef ABLQ
 #undef RET
 constexpr int kNumLeafVariants = sizeof(kLeafVariants) / sizeof(kLeafVariants[0]);
-constexpr int kDefaultLeafVariant = 49;
+constexpr int kDefaultLeafVariant = 50;
 
 int leaf_variant_count() { return kNumLeafVariants; }
 bool leaf_variant_available(int v) { return v >= 0 && v < kNumLeafVariants && kLeafVariants[v].fn != nullptr; }

@@ -70,13 +70,13 @@ def _kernel_stubs(path):
 
 
 def test_product_library_holds_only_product_kernels():
-    """libsdcas.so carries the default leaf kernel (49), round 1's default
+    """libsdcas.so carries the default leaf kernel (50), round 1's default
     (43) as the one bit-exact, GPU-tested alternative, and no ablation or
     DIAGNOSTIC variant (those produce wrong digests and live only in
     libsdcas_ablate.so)"""
     stubs = _kernel_stubs(N.LIB_PATH)
     leaf = [s for s in stubs if s.startswith("k_leaf")]
-    assert leaf == ["k_leaf_tree<512, 8, 1, 1, 1, 0>", "k_leaf_tree<512, 9, 1, 1, 2, 1>"], leaf
+    assert leaf == ["k_leaf_tree<512, 8, 1, 1, 1, 0>", "k_leaf_tree<512, 9, 1, 1, 2, 2>"], leaf
     assert not [s for s in stubs if "slim" in s or "quad" in s]
     pieces = [s for s in stubs if s.startswith("k_piece")]
     assert sorted(pieces) == ["k_piece_dyn<6, 0>", "k_piece_dyn<6, 1>", "k_piece_dyn<8, 0>",
