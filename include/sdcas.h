@@ -187,6 +187,16 @@ int sdcas_dev_stream_begin(sdcas_ctx *ctx, const uint64_t *lens, size_t nfiles);
 int sdcas_dev_stream_update(sdcas_ctx *ctx, size_t nseg, const uint64_t *h_file, const uint64_t *h_msg_off,
                             const uint64_t *h_len, const uint64_t *h_dev_addr, void *stream);
 int sdcas_dev_stream_finish(sdcas_ctx *ctx, uint8_t *d_out32, void *stream);
+/* One message's pieces split over several GPUs (a file larger
+ * than one GPU's share): every rank opens the same session (same lens),
+ * updates with its own disjoint segments, exports its node list (32 B per
+ * node: one per full 1 MiB piece, then the tail piece's nodes; entries it did
+ * not hash are zero), the ranks sum the lists (an all-reduce over int64 words:
+ * each entry is nonzero on one rank only), import the sum, and finish. Bytes
+ * must equal sdcas_dev_stream_node_bytes(); device pointers; on `stream`. */
+size_t sdcas_dev_stream_node_bytes(sdcas_ctx *ctx);
+int sdcas_dev_stream_export(sdcas_ctx *ctx, uint8_t *d_dst, size_t bytes, void *stream);
+int sdcas_dev_stream_import(sdcas_ctx *ctx, const uint8_t *d_src, size_t bytes, void *stream);
 
 /* ---- dedup / link (file_identifier/mod.rs:149-254) --------------------- */
 

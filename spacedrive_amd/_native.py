@@ -34,7 +34,8 @@ ABI_SYMBOLS = [
     "sdcas_digest_to_hex", "sdcas_cas_message_len", "sdcas_dev_dedup_combine", "sdcas_dev_dedup_resolve",
     "sdcas_dev_dedup_apply", "sdcas_dev_dedup_local", "sdcas_dev_dedup_combine_buckets",
     "sdcas_dev_dedup_resolve_buckets", "sdcas_dev_stream_begin", "sdcas_dev_stream_update",
-    "sdcas_dev_stream_finish", "sdcas_set_progress",
+    "sdcas_dev_stream_finish", "sdcas_dev_stream_node_bytes", "sdcas_dev_stream_export", "sdcas_dev_stream_import",
+    "sdcas_set_progress",
     # bench / test plumbing
     "sdcas_dev_synth_cas_messages", "sdcas_dev_synth_content", "sdcas_dev_dedup", "sdcas_dev_profile",
     "sdcas_dev_last_kernel_ms", "sdcas_dev_set_leaf_variant", "sdcas_dev_set_piece_variant", "sdcas_dev_set_sort",
@@ -139,5 +140,9 @@ def load():
     L.sdcas_dev_stream_begin.argtypes = [_vp, _vp, _sz]
     L.sdcas_dev_stream_update.argtypes = [_vp, _sz, _vp, _vp, _vp, _vp, _vp]
     L.sdcas_dev_stream_finish.argtypes = [_vp, _vp, _vp]
+    L.sdcas_dev_stream_node_bytes.argtypes = [_vp]
+    L.sdcas_dev_stream_node_bytes.restype = _sz
+    L.sdcas_dev_stream_export.argtypes = [_vp, _vp, _sz, _vp]
+    L.sdcas_dev_stream_import.argtypes = [_vp, _vp, _sz, _vp]
     _lib = L
     return L

@@ -121,6 +121,7 @@ struct sdcas_ctx {
   DevBuf<uint32_t> sm_nodes;
   DevBuf<PieceDesc> sm_pieces;
   bool sm_active = false;
+  uint64_t sm_node_bytes = 0;
   DevBuf<uint32_t> piece_ctr;  // the persistent piece kernels' work counter
   int piece_variant = -1;
 
@@ -1230,8 +1231,37 @@ int sdcas_dev_stream_begin(sdcas_ctx* c, const uint64_t* lens, size_t nfiles) {
   if (nfiles && (e = hipMemcpy(c->sm_d_files.p, c->sm_files.data(), sizeof(FileDesc) * nfiles,
                                hipMemcpyHostToDevice)))
     return c->hip_fail(e, "stream descs");
+  // node entries no segment of this session writes stay zero, so that the
+  // node lists of ranks that hashed disjoint pieces of the same messages add
+  // up to the complete list (sdcas_dev_stream_import)
+  c->sm_node_bytes = 32 * nodes;
+  if (nodes && (e = hipMemset(c->sm_nodes.p, 0, c->sm_node_bytes))) return c->hip_fail(e, "stream nodes");
   c->sm_active = true;
   return SDCAS_OK;
+}
+
+size_t sdcas_dev_stream_node_bytes(sdcas_ctx* c) { return c && c->sm_active ? (size_t)c->sm_node_bytes : 0; }
+
+int sdcas_dev_stream_export(sdcas_ctx* c, uint8_t* d_dst, size_t bytes, void* stream) {
+  if (!c || (bytes && !d_dst)) return SDCAS_E_INVALID;
+  DevCall call(c, stream);
+  if (call.rc) return call.rc;
+  if (!c->sm_active || bytes != c->sm_node_bytes)
+    return c->fail(SDCAS_E_INVALID, "stream_export: %zu bytes, the session's node list holds %llu", bytes,
+                   (unsigned long long)c->sm_node_bytes);
+  hipError_t e = bytes ? hipMemcpyAsync(d_dst, c->sm_nodes.p, bytes, hipMemcpyDeviceToDevice, call.st) : hipSuccess;
+  return e ? c->hip_fail(e, "stream_export") : SDCAS_OK;
+}
+
+int sdcas_dev_stream_import(sdcas_ctx* c, const uint8_t* d_src, size_t bytes, void* stream) {
+  if (!c || (bytes && !d_src)) return SDCAS_E_INVALID;
+  DevCall call(c, stream);
+  if (call.rc) return call.rc;
+  if (!c->sm_active || bytes != c->sm_node_bytes)
+    return c->fail(SDCAS_E_INVALID, "stream_import: %zu bytes, the session's node list holds %llu", bytes,
+                   (unsigned long long)c->sm_node_bytes);
+  hipError_t e = bytes ? hipMemcpyAsync(c->sm_nodes.p, d_src, bytes, hipMemcpyDeviceToDevice, call.st) : hipSuccess;
+  return e ? c->hip_fail(e, "stream_import") : SDCAS_OK;
 }
 
 int sdcas_dev_stream_update(sdcas_ctx* c, size_t nseg, const uint64_t* h_file, const uint64_t* h_msg_off,

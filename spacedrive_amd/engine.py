@@ -225,6 +225,15 @@ class Engine:
         self._check(self.L.sdcas_dev_stream_update(self.ctx, f.size, _ptr(f), _ptr(o), _ptr(l), _ptr(a),
                                                    stream or None), "dev_stream_update")
 
+    def dev_stream_node_bytes(self):
+        return int(self.L.sdcas_dev_stream_node_bytes(self.ctx))
+
+    def dev_stream_export(self, dst, nbytes, stream=0):
+        self._check(self.L.sdcas_dev_stream_export(self.ctx, dst, int(nbytes), stream or None), "dev_stream_export")
+
+    def dev_stream_import(self, src, nbytes, stream=0):
+        self._check(self.L.sdcas_dev_stream_import(self.ctx, src, int(nbytes), stream or None), "dev_stream_import")
+
     def dev_stream_finish(self, out32, stream=0):
         self._check(self.L.sdcas_dev_stream_finish(self.ctx, out32, stream or None), "dev_stream_finish")
 

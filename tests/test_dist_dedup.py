@@ -316,3 +316,25 @@ def test_device_local_vs_oracle(eng, oracle, corpus, chunk_size):
     want, wc, wl = oracle.identifier_dedup(np.array([5, 5, 6], np.uint64), np.array([0, 1, 1], np.uint8),
                                            np.array([0, 3, 3], np.int32), 100, np.zeros(0, np.uint64))
     assert np.array_equal(link.cpu().numpy(), want) and tuple(cnt.tolist()) == (wc, wl)
+
+
+# ---- the piece split of big-file checksums (spacedrive_amd/dist_checksum.py) ----
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_split_pieces_covers_every_piece_once(world):
+    from spacedrive_amd.dist_checksum import MiB, split_pieces
+    rng = np.random.default_rng(world)
+    sizes = [int(x) for x in rng.integers(MiB + 1, 40 * MiB, 13)] + [4 * MiB, MiB + 1]
+    parts = split_pieces(sizes, world)
+    seen = {}
+    for r, segs in enumerate(parts):
+        for f, off, ln in segs:
+            assert off % MiB == 0 and ln > 0 and off + ln <= sizes[f]
+            assert ln % MiB == 0 or off + ln == sizes[f]  # whole pieces, or the file's tail
+            for q in range(off // MiB, (off + ln + MiB - 1) // MiB):
+                assert (f, q) not in seen
+                seen[(f, q)] = r
+    total = sum((s + MiB - 1) // MiB for s in sizes)
+    assert len(seen) == total
+    counts = [sum((ln + MiB - 1) // MiB for _, _, ln in segs) for segs in parts]
+    assert max(counts) - min(counts) <= 1

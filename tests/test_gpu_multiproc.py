@@ -130,3 +130,109 @@ def test_two_streams_share_one_context(oracle):
                 assert tuple(b["cnt"].tolist()) == (wc, wl)
     finally:
         eng.close()
+
+
+# ---- big-file checksums with the pieces split over ranks (dist_checksum.py) ----
+
+MiB = 1 << 20
+SPLIT_SIZES = [5 * MiB + 3, 17 * MiB, 2 * MiB + 1, 33 * MiB - 1, 9 * MiB + 4095]
+
+
+def _split_keys():
+    from tests._oracle import content_key
+    return [content_key(0x5D0004, 500 + i) for i in range(len(SPLIT_SIZES))]
+
+
+def _rank_blob(segments, keys, dev):
+    """this rank's segments' bytes generated in HBM -> (blob, device addresses)"""
+    from tests._oracle import content
+    offs, parts, pos = [], [], 0
+    for f, off, ln in segments:
+        offs.append(pos)
+        parts.append(content("synth", off, ln, keys[f]))
+        pos += (ln + MiB - 1) // MiB * MiB
+    blob = torch.zeros(pos + 4096, dtype=torch.uint8, device=dev)
+    for o, p in zip(offs, parts):
+        blob[o:o + p.size].copy_(torch.from_numpy(p))
+    return blob, [blob.data_ptr() + o for o in offs]
+
+
+def test_split_checksum_virtual_ranks(oracle):
+    """three contexts hash disjoint piece ranges of the same files; their node
+    lists, summed, finish to the oracle's digests on every context"""
+    from spacedrive_amd import Engine
+    from spacedrive_amd.dist_checksum import split_pieces
+    keys = _split_keys()
+    R = 3
+    parts = split_pieces(SPLIT_SIZES, R)
+    engs = [Engine() for _ in range(R)]
+    try:
+        lists, blobs = [], []
+        for r in range(R):
+            blob, addrs = _rank_blob(parts[r], keys, "cuda")
+            blobs.append(blob)
+            torch.cuda.synchronize()
+            e = engs[r]
+            e.dev_stream_begin(SPLIT_SIZES)
+            seg = parts[r]
+            e.dev_stream_update([x[0] for x in seg], [x[1] for x in seg], [x[2] for x in seg], addrs)
+            nb = e.dev_stream_node_bytes()
+            t = torch.empty(nb // 8, dtype=torch.int64, device="cuda")
+            e.dev_stream_export(t.data_ptr(), nb)
+            e.dev_sync()
+            lists.append(t)
+        total = sum(lists)
+        torch.cuda.synchronize()
+        for r in range(R):
+            out = torch.zeros((len(SPLIT_SIZES), 32), dtype=torch.uint8, device="cuda")
+            engs[r].dev_stream_import(total.data_ptr(), total.numel() * 8)
+            engs[r].dev_stream_finish(out.data_ptr())
+            engs[r].dev_sync()
+            got = out.cpu().numpy()
+            for i, (k, n) in enumerate(zip(keys, SPLIT_SIZES)):
+                assert bytes(got[i]).hex() == oracle.synth_checksum(k, n), (r, n)
+    finally:
+        for e in engs:
+            e.close()
+
+
+def _split_worker(rank, world, port, outdir):
+    import torch.distributed as dist
+
+    from spacedrive_amd import Engine
+    from spacedrive_amd.dist_checksum import checksums_split, split_pieces
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    eng = Engine(device=0)
+    try:
+        keys = _split_keys()
+        seg = split_pieces(SPLIT_SIZES, world)[rank]
+        blob, addrs = _rank_blob(seg, keys, "cuda")
+        out = torch.zeros((len(SPLIT_SIZES), 32), dtype=torch.uint8, device="cuda")
+        checksums_split(eng, SPLIT_SIZES, seg, addrs, out)
+        np.save(os.path.join(outdir, f"r{rank}.npy"), out.cpu().numpy())
+    finally:
+        eng.close()
+        dist.destroy_process_group()
+
+
+def test_split_checksum_two_processes(oracle):
+    """two processes (gloo, the collective bench.py runs over RCCL) split the
+    files' pieces; both end with every file's exact digest"""
+    import torch.multiprocessing as mp
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        ctx = mp.start_processes(_split_worker, args=(world, _free_port(), d), nprocs=world, join=False,
+                                 start_method="spawn")
+        deadline = time.time() + 100
+        try:
+            while not ctx.join(timeout=5):
+                assert time.time() < deadline, "ranks did not finish"
+        finally:
+            for p in ctx.processes:
+                if p.is_alive():
+                    p.terminate()
+        outs = [np.load(os.path.join(d, f"r{r}.npy")) for r in range(world)]
+    for got in outs:
+        for i, (k, n) in enumerate(zip(_split_keys(), SPLIT_SIZES)):
+            assert bytes(got[i]).hex() == oracle.synth_checksum(k, n), n
