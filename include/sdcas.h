@@ -96,10 +96,16 @@ typedef struct sdcas_ctx sdcas_ctx;
  * on the thread that made the path call. */
 typedef void (*sdcas_progress_fn)(void *user, uint64_t done, uint64_t total);
 
+/* sdcas_options.flags */
+#define SDCAS_OPT_DIRECT_IO 1u /* file_checksum of files > 1 MiB reads with O_DIRECT (cold storage;
+                                   falls back to the page cache where the filesystem refuses it) */
+
 typedef struct sdcas_options {
   int32_t device;          /* HIP device ordinal (-1: current device) */
   uint32_t io_threads;     /* reader threads for the path APIs (0: 8) */
   uint64_t staging_bytes;  /* pinned host staging per batch (0: 256 MiB) */
+  uint32_t flags;          /* SDCAS_OPT_* */
+  uint32_t reserved;
   sdcas_progress_fn progress;      /* may be NULL */
   void *progress_user;             /* passed to progress */
   const volatile int32_t *cancel;  /* may be NULL; caller-owned, read atomically: nonzero cancels */

@@ -79,6 +79,7 @@ class Engine {
     int device = -1;             // HIP device ordinal, -1: current
     uint32_t io_threads = 0;     // reader threads (0: library default)
     uint64_t staging_bytes = 0;  // pinned staging per slot (0: library default)
+    uint32_t flags = 0;          // SDCAS_OPT_* (SDCAS_OPT_DIRECT_IO: big-file checksums bypass the page cache)
     // progress / cancellation of the batch calls (sdcas.h "Conventions"): the
     // job's progress hook (job/worker.rs:458-480) and its cancel command
     // (job/mod.rs:862-960)

@@ -25,6 +25,7 @@ SDCAS_E_CANCELLED = -6
 SDCAS_STATUS_UNEXPECTED_EOF = 100001
 SDCAS_STATUS_CANCELLED = 125
 SDCAS_MAX_BATCH = 0x7FFFFFFF
+SDCAS_OPT_DIRECT_IO = 1
 
 # every entry point include/sdcas.h and include/sdcas_bench.h declare
 ABI_SYMBOLS = [
@@ -64,7 +65,8 @@ PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_
 
 class Options(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("io_threads", ctypes.c_uint32),
-                ("staging_bytes", ctypes.c_uint64), ("progress", PROGRESS_FN),
+                ("staging_bytes", ctypes.c_uint64), ("flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("progress", PROGRESS_FN),
                 ("progress_user", ctypes.c_void_p), ("cancel", ctypes.POINTER(ctypes.c_int32))]
 
 

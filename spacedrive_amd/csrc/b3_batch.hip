@@ -354,7 +354,8 @@ __global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __
     bool c_ok[R], c_root[R];
 #pragma unroll
     for (uint32_t r = 0; r < R; ++r) c_ok[r] = false;
-#pragma unroll(CA ? R : 1)
+    constexpr uint32_t kPhase1Unroll = CA ? R : 1;
+#pragma unroll kPhase1Unroll
     for (uint32_t s = tid; s < kTile; s += WG) {
       const uint64_t g = tbase + s;
       if (g >= total) {

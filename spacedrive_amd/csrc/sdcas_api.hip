@@ -34,6 +34,17 @@ using namespace sdcas;
 
 namespace {
 
+// file I/O with the reference's read pattern (GPU-free, in
+// spacedrive_amd/host/cas_io.cpp: tested under ASan / UBSan / TSan by
+// tests/cpp/test_cas_io.cpp)
+using sdcas_io::open_for_read;
+using sdcas_io::parallel_for;
+using sdcas_io::plan_batch;
+using sdcas_io::pread_direct;
+using sdcas_io::pread_exact;
+using sdcas_io::read_cas_message;
+using sdcas_io::read_whole;
+
 constexpr uint64_t kMin = SDCAS_MINIMUM_FILE_SIZE;  // cas.rs:15 (the reads themselves: host/cas_io.cpp)
 constexpr uint64_t kSlack = 64;  // readable bytes kept after every message
 
@@ -93,6 +104,7 @@ struct sdcas_ctx {
   std::mutex mu;
   uint32_t io_threads = 8;
   uint64_t staging_bytes = 256ull << 20;
+  bool direct_io = false;  // SDCAS_OPT_DIRECT_IO: big-file checksum reads bypass the page cache
 
   BatchWorkspace ws;
   DevBuf<uint64_t> ws_S, ws_total, ws_soffs, ws_slens;
@@ -357,16 +369,21 @@ int slot_complete(sdcas_ctx* c, Slot& s, Sink sink, Progress* pr = nullptr) {
 }
 
 // Big messages (> 1 MiB) from host memory: 1 MiB pieces streamed through the
-// two staging slots (one window filled by `fill` while the GPU hashes the
-// other); `fill(k, dst, off, len)` provides bytes [off, off+len) of item k
-// and returns a status (0 ok). Digests go to out32_host[32 * out_index].
-// Cancellation is checked once per window: items whose every piece was
-// submitted by then are finished, the rest get SDCAS_STATUS_CANCELLED and
-// *cancelled is set.
+// two staging slots (one window filled while the GPU hashes the other). A
+// window's pieces are filled by the I/O threads in parallel (several reads in
+// flight: what cold storage needs, and page-cache copies scale with threads
+// too); `fill(k, dst, off, len)` provides bytes [off, off+len) of item k and
+// returns a status (0 ok). Pieces sit at 4 KiB-aligned window offsets (the
+// O_DIRECT rule; the device needs 16 B). Digests go to
+// out32_host[32 * out_index]. Cancellation is checked once per window: items
+// whose every piece was submitted by then are finished, the rest get
+// SDCAS_STATUS_CANCELLED and *cancelled is set.
 struct BigItem {
   uint64_t len;
   uint64_t out_index;
 };
+
+inline uint64_t align_page(uint64_t x) { return (x + sdcas_io::kDirectAlign - 1) & ~(sdcas_io::kDirectAlign - 1); }
 
 template <class Fill>
 int run_big(sdcas_ctx* c, const std::vector<BigItem>& items, uint8_t* out32_host, Fill fill, int32_t* status,
@@ -394,8 +411,15 @@ int run_big(sdcas_ctx* c, const std::vector<BigItem>& items, uint8_t* out32_host
   if ((e = c->piece_ctr.ensure(1))) return c->hip_fail(e, "piece counter");
   hipStream_t st = c->stream;
   int cur = 0;
-  size_t npieces = 0;
+  struct Job {
+    size_t item;
+    uint64_t off, dst;
+    uint32_t len;
+  };
+  std::vector<Job> jobs;
+  std::vector<int32_t> jst;
   uint64_t used = 0, content = 0;
+  std::vector<int32_t> item_st(items.size(), 0);
   auto wait_slot = [&](Slot& s) -> int {
     if (!s.busy) return SDCAS_OK;
     s.busy = false;
@@ -404,22 +428,38 @@ int run_big(sdcas_ctx* c, const std::vector<BigItem>& items, uint8_t* out32_host
     pr.add(s.content);
     return SDCAS_OK;
   };
+  // fill the window's pieces (in parallel), then copy and hash them
   auto flush = [&]() -> int {
-    if (!npieces) return SDCAS_OK;
+    if (jobs.empty()) return SDCAS_OK;
     Slot& s = c->slots[cur];
+    jst.assign(jobs.size(), 0);
+    parallel_for(c->io_threads, jobs.size(), [&](size_t k) {
+      const Job& jb = jobs[k];
+      jst[k] = fill(jb.item, s.h + jb.dst, jb.off, jb.len);
+    });
     PieceDesc* hp = reinterpret_cast<PieceDesc*>(s.hm);
+    for (size_t k = 0; k < jobs.size(); ++k) {
+      if (jst[k] && !item_st[jobs[k].item]) item_st[jobs[k].item] = jst[k];
+      PieceDesc pd{};
+      pd.off = jobs[k].dst;
+      pd.j0 = jobs[k].off / 1024;
+      pd.node_base = files[jobs[k].item].node_base;
+      pd.len = jobs[k].len;
+      hp[k] = pd;  // a failed item's pieces are hashed too: its digest is never returned
+    }
     PieceDesc* dp = reinterpret_cast<PieceDesc*>(s.d_meta.p);
     hipError_t ee;
     if ((ee = hipMemcpyAsync(s.d_blob.p, s.h, used, hipMemcpyHostToDevice, st)) ||
-        (ee = hipMemcpyAsync(dp, hp, sizeof(PieceDesc) * npieces, hipMemcpyHostToDevice, st)))
+        (ee = hipMemcpyAsync(dp, hp, sizeof(PieceDesc) * jobs.size(), hipMemcpyHostToDevice, st)))
       return c->hip_fail(ee, "H2D pieces");
-    if ((ee = piece_hash(s.d_blob.p, dp, (uint32_t)npieces, c->d_file_nodes.p, c->piece_ctr.p, c->piece_variant, st)))
+    if ((ee = piece_hash(s.d_blob.p, dp, (uint32_t)jobs.size(), c->d_file_nodes.p, c->piece_ctr.p, c->piece_variant,
+                         st)))
       return c->hip_fail(ee, "piece_hash");
     if ((ee = hipEventRecord(s.ev, st))) return c->hip_fail(ee, "event");
     s.busy = true;
     s.content = content;
     cur ^= 1;
-    npieces = 0;
+    jobs.clear();
     used = 0;
     content = 0;
     return wait_slot(c->slots[cur]);  // the next window's buffers are free again
@@ -428,9 +468,9 @@ int run_big(sdcas_ctx* c, const std::vector<BigItem>& items, uint8_t* out32_host
   size_t complete = items.size();  // items [0, complete) have every piece submitted
   for (size_t i = 0; i < items.size() && !*cancelled; ++i) {
     const uint64_t len = items[i].len;
-    for (uint64_t off = 0; off < len; off += piece_bytes) {
+    for (uint64_t off = 0; off < len && !item_st[i]; off += piece_bytes) {
       const uint32_t pl = (uint32_t)std::min<uint64_t>(piece_bytes, len - off);
-      if (used + pl > window) {
+      if (used + align_page(pl) > window) {
         if ((rc = flush())) return rc;
         if (c->cancelled()) {
           *cancelled = true;
@@ -438,29 +478,20 @@ int run_big(sdcas_ctx* c, const std::vector<BigItem>& items, uint8_t* out32_host
           break;
         }
       }
-      Slot& s = c->slots[cur];
-      int st_i = fill(i, s.h + used, off, pl);
-      if (st_i) {
-        if (status) status[items[i].out_index] = st_i;
-        break;
-      }
-      PieceDesc pd{};
-      pd.off = used;
-      pd.j0 = off / 1024;
-      pd.node_base = files[i].node_base;
-      pd.len = pl;
-      reinterpret_cast<PieceDesc*>(s.hm)[npieces++] = pd;
-      used += align16(pl);
+      jobs.push_back({i, off, used, pl});
+      used += align_page(pl);
       content += pl;
     }
   }
   if (*cancelled) {
-    npieces = 0;  // pieces of an incomplete item are never hashed
+    jobs.clear();  // pieces of an incomplete item are never hashed
     used = content = 0;
   }
   if ((rc = flush())) return rc;
   for (Slot& s : c->slots)
     if ((rc = wait_slot(s))) return rc;
+  for (size_t i = 0; i < items.size(); ++i)
+    if (status && item_st[i] && !status[items[i].out_index]) status[items[i].out_index] = item_st[i];
   const size_t nf = complete;
   if (nf) {
     if ((e = hipMemcpyAsync(c->d_files.p, files.data(), sizeof(FileDesc) * nf, hipMemcpyHostToDevice, st)))
@@ -479,14 +510,6 @@ int run_big(sdcas_ctx* c, const std::vector<BigItem>& items, uint8_t* out32_host
 }
 
 
-// ---- file I/O with the reference's read pattern ---------------------------
-// (GPU-free, in spacedrive_amd/host/cas_io.cpp: tested under ASan / UBSan /
-// TSan by tests/cpp/test_cas_io.cpp)
-using sdcas_io::parallel_for;
-using sdcas_io::plan_batch;
-using sdcas_io::pread_exact;
-using sdcas_io::read_cas_message;
-using sdcas_io::read_whole;
 
 }  // namespace
 
@@ -507,6 +530,7 @@ int sdcas_init(const sdcas_options* opts, sdcas_ctx** out) {
     dev = opts->device;
     if (opts->io_threads) c->io_threads = opts->io_threads;
     if (opts->staging_bytes) c->staging_bytes = std::max<uint64_t>(opts->staging_bytes, 1ull << 20);
+    c->direct_io = (opts->flags & SDCAS_OPT_DIRECT_IO) != 0;
     c->progress = opts->progress;
     c->progress_user = opts->progress_user;
     c->cancel = opts->cancel;
@@ -980,16 +1004,21 @@ int sdcas_checksums(sdcas_ctx* c, const char* const* paths, size_t n, uint8_t* o
     return c->fail(SDCAS_E_CANCELLED, "cancelled");
   }
   if (!big.empty()) {
+    // hash.rs reads the file to EOF in 1 MiB blocks; here a window's 1 MiB
+    // pieces are read in parallel, with O_DIRECT when asked for and accepted
     std::vector<int> fds(big.size(), -1), oerr(big.size(), 0);
+    std::vector<uint8_t> direct(big.size(), 0);
     for (size_t k = 0; k < big.size(); ++k) {
-      fds[k] = open(paths[big[k].out_index], O_RDONLY | O_CLOEXEC);
-      if (fds[k] < 0) oerr[k] = errno ? errno : EIO;
+      bool d = false;
+      fds[k] = open_for_read(paths[big[k].out_index], c->direct_io, &d);
+      if (fds[k] < 0) oerr[k] = -fds[k];
+      direct[k] = d;
     }
     std::vector<uint8_t> d32(32 * n);
     rc = run_big(c, big, d32.data(),
                  [&](size_t k, uint8_t* dst, uint64_t off, uint32_t len) -> int {
                    if (fds[k] < 0) return oerr[k];
-                   return pread_exact(fds[k], dst, len, off);  // hash.rs: 1 MiB reads to EOF
+                   return direct[k] ? pread_direct(fds[k], dst, len, off) : pread_exact(fds[k], dst, len, off);
                  },
                  out_status, pr, &cancelled);
     for (int fd : fds)

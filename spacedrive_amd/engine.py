@@ -59,15 +59,17 @@ class Engine:
     progress report, job/worker.rs:458-480). cancel: optional
     ``ctypes.c_int32`` the caller may set nonzero from any thread to stop a
     path call (job/mod.rs:862-960); the call then raises ``Cancelled`` whose
-    ``partial`` holds the completed items.
+    ``partial`` holds the completed items. direct_io: file_checksum of files
+    over 1 MiB reads with O_DIRECT (cold storage).
     """
 
-    def __init__(self, device: int = 0, io_threads: int = 0, staging_bytes: int = 0, progress=None, cancel=None):
+    def __init__(self, device: int = 0, io_threads: int = 0, staging_bytes: int = 0, progress=None, cancel=None,
+                 direct_io=False):
         self.L = N.load()
         self._cb = self._progress_fn(progress)
         self._cancel = cancel
-        opts = N.Options(device, io_threads, staging_bytes, self._cb, None,
-                         ctypes.pointer(cancel) if cancel is not None else None)
+        opts = N.Options(device, io_threads, staging_bytes, N.SDCAS_OPT_DIRECT_IO if direct_io else 0, 0, self._cb,
+                         None, ctypes.pointer(cancel) if cancel is not None else None)
         ctx = ctypes.c_void_p()
         rc = self.L.sdcas_init(ctypes.byref(opts), ctypes.byref(ctx))
         if rc != N.SDCAS_OK:

@@ -2,6 +2,9 @@
 // sanitizer test builds of tests/cpp.
 #include "cas_io.hpp"
 
+#ifndef _GNU_SOURCE
+#define _GNU_SOURCE  // O_DIRECT
+#endif
 #include <fcntl.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -26,6 +29,36 @@ int pread_exact(int fd, uint8_t* dst, uint64_t n, uint64_t off) {
     got += (uint64_t)r;
   }
   return 0;
+}
+
+int pread_direct(int fd, uint8_t* dst, uint64_t n, uint64_t off) {
+  const uint64_t want = (n + kDirectAlign - 1) & ~(kDirectAlign - 1);
+  uint64_t got = 0;
+  while (got < want) {
+    ssize_t r = pread(fd, dst + got, want - got, (off_t)(off + got));
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      return errno;
+    }
+    if (r == 0) break;
+    got += (uint64_t)r;
+    if (got % kDirectAlign) break;  // short of a block: the file ends here (another read would be unaligned)
+  }
+  return got >= n ? 0 : kUnexpectedEof;
+}
+
+int open_for_read(const char* path, bool direct, bool* is_direct) {
+  *is_direct = false;
+  if (direct) {
+    int fd = open(path, O_RDONLY | O_CLOEXEC | O_DIRECT);
+    if (fd >= 0) {
+      *is_direct = true;
+      return fd;
+    }
+    if (errno != EINVAL) return -errno;
+  }
+  int fd = open(path, O_RDONLY | O_CLOEXEC);
+  return fd >= 0 ? fd : -errno;
 }
 
 int read_whole(int fd, uint8_t* dst, uint64_t cap, uint64_t expect, uint64_t* len, bool* overflow) {

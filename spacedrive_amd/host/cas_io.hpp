@@ -28,6 +28,18 @@ inline uint64_t align_line(uint64_t x) { return (x + 127) & ~127ull; }
 // with UnexpectedEof; returns 0 or a status
 int pread_exact(int fd, uint8_t* dst, uint64_t n, uint64_t off);
 
+// The O_DIRECT form of pread_exact for the big-file checksum path: `off`
+// and `dst` 4 KiB aligned, the length read is n rounded up to 4 KiB (dst must
+// have room), a read shorter than that ends at EOF; fails with UnexpectedEof
+// when fewer than n bytes were there.
+constexpr uint64_t kDirectAlign = 4096;
+int pread_direct(int fd, uint8_t* dst, uint64_t n, uint64_t off);
+
+// open(path) for reading, with O_DIRECT when `direct` and the filesystem
+// accepts it (tmpfs and some overlays refuse it: then the page cache is
+// used); *is_direct says which. Returns the fd or -errno.
+int open_for_read(const char* path, bool direct, bool* is_direct);
+
 // Whole file into dst (capacity cap > expect, the size the indexer or a stat
 // just saw); returns status, *len = bytes read; sets *overflow when the file
 // holds at least cap bytes (it grew). A read that stops short exactly at

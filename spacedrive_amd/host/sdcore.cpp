@@ -25,7 +25,7 @@ void Engine::fail(int rc, const char* what) const {
 }
 
 std::unique_ptr<Engine> Engine::open(const Options& o) {
-  sdcas_options opts{o.device, o.io_threads, o.staging_bytes, o.progress, o.progress_user, o.cancel};
+  sdcas_options opts{o.device, o.io_threads, o.staging_bytes, o.flags, 0, o.progress, o.progress_user, o.cancel};
   sdcas_ctx* c = nullptr;
   const int rc = sdcas_init(&opts, &c);
   if (rc != SDCAS_OK) {

@@ -14,6 +14,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <cstdio>
 #include <cstdlib>
@@ -141,6 +142,43 @@ int main() {
   }
   CHECK(want_st[cases.size() - 3] == ENOENT, "missing path: %d", want_st[cases.size() - 3]);
   CHECK(want_st[cases.size() - 2] == EISDIR, "directory: %d", want_st[cases.size() - 2]);
+
+  // the big-file checksum reads: 1 MiB pieces with O_DIRECT (4 KiB-aligned
+  // destination, the tail piece's length rounded up) where the filesystem
+  // takes it, the page cache where it refuses; both give the file's bytes
+  {
+    const std::string bp = path("big_direct");
+    const uint64_t n = (5ull << 20) + 123;
+    write_file(bp, n, rng);
+    std::vector<uint8_t> want(n);
+    FILE* f = std::fopen(bp.c_str(), "rb");
+    CHECK(std::fread(want.data(), 1, n, f) == n, "read back");
+    std::fclose(f);
+    for (bool direct : {false, true}) {
+      bool is_direct = false;
+      const int fd = sdcas_io::open_for_read(bp.c_str(), direct, &is_direct);
+      CHECK(fd >= 0, "open_for_read %d", fd);
+      CHECK(direct || !is_direct, "O_DIRECT without asking");
+      if (direct && !is_direct) std::printf("(O_DIRECT refused by this filesystem: page-cache fallback)\n");
+      void* buf = nullptr;
+      if (posix_memalign(&buf, 4096, (1u << 20) + 4096) != 0) return 2;
+      for (uint64_t off = 0; off < n; off += 1u << 20) {
+        const uint64_t len = std::min<uint64_t>(1u << 20, n - off);
+        const int st = is_direct ? sdcas_io::pread_direct(fd, (uint8_t*)buf, len, off)
+                                 : sdcas_io::pread_exact(fd, (uint8_t*)buf, len, off);
+        CHECK(st == 0 && std::memcmp(buf, want.data() + off, len) == 0, "piece at %llu (direct %d): %d",
+              (unsigned long long)off, (int)is_direct, st);
+      }
+      // one piece more than the file holds: UnexpectedEof either way
+      const int st = is_direct ? sdcas_io::pread_direct(fd, (uint8_t*)buf, 1u << 20, 5ull << 20)
+                               : sdcas_io::pread_exact(fd, (uint8_t*)buf, 1u << 20, 5ull << 20);
+      CHECK(st == sdcas_io::kUnexpectedEof, "past EOF: %d", st);
+      std::free(buf);
+      close(fd);
+    }
+    bool d = false;
+    CHECK(sdcas_io::open_for_read(path("nope").c_str(), true, &d) == -ENOENT, "missing file");
+  }
 
   // plan_batch: items in order, line-aligned ascending offsets, within the
   // slot (the first item of a batch always taken), at most cap_n per batch

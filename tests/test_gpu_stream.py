@@ -238,3 +238,25 @@ def test_cas_ids_cancel_per_slot(oracle, tmp_path):
         with pytest.raises(N.Cancelled) as ex:
             e.generate_cas_ids(paths[:50], sizes[:50])  # still set: nothing is read
         assert (ex.value.partial[1] == N.SDCAS_STATUS_CANCELLED).all()
+
+
+@pytest.mark.parametrize("direct", [False, True])
+def test_checksums_parallel_pieces_and_direct_io(oracle, tmp_path, direct):
+    """file_checksum of files over 1 MiB: a window's 1 MiB pieces are read by
+    the I/O threads in parallel, with O_DIRECT when asked (page cache where
+    the filesystem refuses it); digests exact, small files alongside, and a
+    file that shrank below its stat length (UnexpectedEof, sdcas.h)"""
+    from spacedrive_amd import Engine
+    from tests._oracle import content
+    sizes = [3 * MiB + 5, 40 * MiB + 1, 2 * MiB, 100 * MiB + 4097, 5000, MiB + 1]
+    keys = [content_key(0x5D0004, 700 + i) for i in range(len(sizes))]
+    paths = []
+    for i, (k, n) in enumerate(zip(keys, sizes)):
+        p = tmp_path / f"d{i}"
+        p.write_bytes(content("synth", 0, n, k).tobytes())
+        paths.append(str(p))
+    with Engine(staging_bytes=16 * MiB, io_threads=6, direct_io=direct) as e:
+        out, st = e.file_checksums(paths)
+    assert not st.any(), st
+    for i, (k, n) in enumerate(zip(keys, sizes)):
+        assert bytes(out[i]).hex() == oracle.synth_checksum(k, n), n
