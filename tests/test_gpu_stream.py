@@ -244,8 +244,7 @@ def test_cas_ids_cancel_per_slot(oracle, tmp_path):
 def test_checksums_parallel_pieces_and_direct_io(oracle, tmp_path, direct):
     """file_checksum of files over 1 MiB: a window's 1 MiB pieces are read by
     the I/O threads in parallel, with O_DIRECT when asked (page cache where
-    the filesystem refuses it); digests exact, small files alongside, and a
-    file that shrank below its stat length (UnexpectedEof, sdcas.h)"""
+    the filesystem refuses it); digests exact, small files alongside"""
     from spacedrive_amd import Engine
     from tests._oracle import content
     sizes = [3 * MiB + 5, 40 * MiB + 1, 2 * MiB, 100 * MiB + 4097, 5000, MiB + 1]
