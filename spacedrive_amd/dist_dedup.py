@@ -304,7 +304,8 @@ def _dedup_buckets(stages, world, caps, keys, has_key, status, ids, chunk_size, 
     fills = torch.stack([fcnt.max(), ecnt.max() if has_ex else torch.full((), -1, dtype=torch.int64, device=dev)])
     dist.all_reduce(tot, group=group)
     dist.all_reduce(fills, op=dist.ReduceOp.MAX, group=group)
-    t, f = tot.tolist(), fills.tolist()  # the one host synchronisation
+    tf = torch.cat([tot, fills]).tolist()  # the one host synchronisation
+    t, f = tf[:3], tf[3:]
     _next_caps(stages, int(f[0]), int(f[1]))
     if t[2]:
         return None
