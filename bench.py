@@ -125,6 +125,12 @@ def compressions(lens):
     return 16 * (C - 1) + np.maximum(1, (last + 63) // 64) + (C - 1)
 
 
+# the library's default kernels (spacedrive_amd/csrc/b3_batch.hip
+# kDefaultLeafVariant / kDefaultPieceVariant): the PMC traffic files are per kernel
+DEFAULT_LEAF_KERNEL = "k_leaf_tree<512, 109, 1, 1, 2, 2>"
+DEFAULT_PIECE_VARIANT = 14
+
+
 def load_traffic(workload, kernel="k_leaf_tree"):
     """HBM bytes per launch of the dominant kernel from the committed
     rocprofv3 PMC passes (profiles/*pmc*.json, written by
@@ -488,7 +494,9 @@ def run_c4(args, torch, dist, dev, rank, world, distributed, out_f):
     out["roofline"]["frac"] = out["roofline"]["achieved"] / HBM_PEAK_GBS if out["roofline"]["achieved"] else None
     # PMC traffic of the kernel this run launched (the default piece kernel
     # unless --piece-variant chose another)
-    tr = load_traffic("c4", "k_piece_tree<8, 6, 1, 0>") if args.piece_variant in (-1, 6) else None
+    piece_kernels = {6: "k_piece_tree<8, 6, 1, 0>", 14: "k_piece_tree<108, 6, 1, 0>"}
+    pv = DEFAULT_PIECE_VARIANT if args.piece_variant < 0 else args.piece_variant
+    tr = load_traffic("c4", piece_kernels[pv]) if pv in piece_kernels else None
     if tr and resident and tr.get("algorithmic_bytes_per_launch") == my_bytes:
         out["roofline"]["traffic"] = tr["hbm_bytes_per_launch"]
         out["roofline"]["traffic_source"] = tr.get("source")
@@ -651,7 +659,7 @@ def main():
     gbps = msg_bytes * world * args.steps / dt / 1e9
     leaf_s = leaf_ms / 1e3
     achieved_gbs = msg_bytes / leaf_s / 1e9 if leaf_s > 0 else None
-    traffic = load_traffic(args.workload)
+    traffic = load_traffic(args.workload, DEFAULT_LEAF_KERNEL)
     valu_rate = comp / leaf_s if leaf_s > 0 else None
     roof = {
         "bound": "hbm", "kernel": "k_leaf_tree (leaf chunks + in-tile tree)",

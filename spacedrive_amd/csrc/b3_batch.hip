@@ -98,6 +98,7 @@ __global__ void k_tile_first(const uint64_t* __restrict__ lens, const uint64_t* 
 
 // Same, unrolled by two blocks with ping-pong message registers (no
 // register copies between blocks; block b+1's loads fly while b compresses).
+template <int GA = 0>
 __device__ __forceinline__ void hash_chunk_pp(const uint8_t* __restrict__ p, uint32_t clen, uint64_t j, bool root,
                                               uint32_t (&cv)[8]) {
   set_iv(cv);
@@ -111,13 +112,13 @@ __device__ __forceinline__ void hash_chunk_pp(const uint8_t* __restrict__ p, uin
     {
       const uint32_t blen = min(BLOCK_LEN, clen - b * BLOCK_LEN);
       if (blen < BLOCK_LEN) mask_tail(m0, blen);
-      compress(cv, m0, j, blen, (b == 0 ? CHUNK_START : 0u) | (b + 1 == nb ? endf : 0u));
+      compress<GA>(cv, m0, j, blen, (b == 0 ? CHUNK_START : 0u) | (b + 1 == nb ? endf : 0u));
     }
     if (b + 1 < nb) {
       load_full_block(p + min(b + 2, nb - 1) * BLOCK_LEN, m0);
       const uint32_t blen = min(BLOCK_LEN, clen - (b + 1) * BLOCK_LEN);
       if (blen < BLOCK_LEN) mask_tail(m1, blen);
-      compress(cv, m1, j, blen, b + 2 == nb ? endf : 0u);
+      compress<GA>(cv, m1, j, blen, b + 2 == nb ? endf : 0u);
     }
   }
 }
@@ -126,6 +127,7 @@ __device__ __forceinline__ void hash_chunk_pp(const uint8_t* __restrict__ p, uin
 // 128-byte line are requested together (no prefetch across lines): the second
 // half never waits in L2 for a compression and cannot be evicted before it is
 // read; the load latency is left to the other waves of the SIMD.
+template <int GA = 0>
 __device__ __forceinline__ void hash_chunk_ps(const uint8_t* __restrict__ p, uint32_t clen, uint64_t j, bool root,
                                               uint32_t (&cv)[8]) {
   set_iv(cv);
@@ -139,12 +141,12 @@ __device__ __forceinline__ void hash_chunk_ps(const uint8_t* __restrict__ p, uin
     {
       const uint32_t blen = min(BLOCK_LEN, clen - b * BLOCK_LEN);
       if (blen < BLOCK_LEN) mask_tail(m0, blen);
-      compress(cv, m0, j, blen, (b == 0 ? CHUNK_START : 0u) | (b + 1 == nb ? endf : 0u));
+      compress<GA>(cv, m0, j, blen, (b == 0 ? CHUNK_START : 0u) | (b + 1 == nb ? endf : 0u));
     }
     if (b + 1 < nb) {
       const uint32_t blen = min(BLOCK_LEN, clen - (b + 1) * BLOCK_LEN);
       if (blen < BLOCK_LEN) mask_tail(m1, blen);
-      compress(cv, m1, j, blen, b + 2 == nb ? endf : 0u);
+      compress<GA>(cv, m1, j, blen, b + 2 == nb ? endf : 0u);
     }
   }
 }
@@ -154,6 +156,7 @@ __device__ __forceinline__ void hash_chunk_ps(const uint8_t* __restrict__ p, uin
 // flags are constants selected by one compare, the tail mask runs only on
 // the last block, the second half of a line is loaded only if the chunk has
 // it (no clamped address), and the block pointer advances by one add.
+template <int GA = 0>
 __device__ __forceinline__ void hash_chunk_pl(const uint8_t* __restrict__ p, uint32_t clen, uint64_t j, bool root,
                                               uint32_t (&cv)[8]) {
   set_iv(cv);
@@ -170,12 +173,12 @@ __device__ __forceinline__ void hash_chunk_pl(const uint8_t* __restrict__ p, uin
     {
       const bool last = b == lb;
       if (last && lblen < BLOCK_LEN) mask_tail(m0, lblen);
-      compress(cv, m0, j, last ? lblen : BLOCK_LEN, (b == 0 ? CHUNK_START : 0u) | (last ? endf : 0u));
+      compress<GA>(cv, m0, j, last ? lblen : BLOCK_LEN, (b == 0 ? CHUNK_START : 0u) | (last ? endf : 0u));
     }
     if (two) {
       const bool last = b + 1 == lb;
       if (last && lblen < BLOCK_LEN) mask_tail(m1, lblen);
-      compress(cv, m1, j, last ? lblen : BLOCK_LEN, last ? endf : 0u);
+      compress<GA>(cv, m1, j, last ? lblen : BLOCK_LEN, last ? endf : 0u);
     }
   }
 }
@@ -184,17 +187,21 @@ __device__ __forceinline__ void hash_chunk_pl(const uint8_t* __restrict__ p, uin
 #include "b3_ablate_loops.inc"
 #endif
 
-// Block loop of a leaf chunk: PF 8 = hash_chunk_ps (default), 9 =
-// hash_chunk_pl, 4 = hash_chunk_pp; any other PF names an ablation loop.
+// Block loop of a leaf chunk: PF 8 = hash_chunk_ps, 9 = hash_chunk_pl, 4 =
+// hash_chunk_pp; PF + 100 = the same loop with the asm G blocks (B3_G_ASM,
+// b3_device.h); any other PF names an ablation loop.
+template <int PF>
+constexpr int kGA = PF >= 100 ? 1 : 0;
 template <int PF>
 __device__ __forceinline__ void leaf_hash(const uint8_t* __restrict__ p, uint32_t clen, uint64_t j, bool root,
                                           uint32_t (&cv)[8]) {
-  if constexpr (PF == 8) {
-    hash_chunk_ps(p, clen, j, root, cv);
-  } else if constexpr (PF == 9) {
-    hash_chunk_pl(p, clen, j, root, cv);
-  } else if constexpr (PF == 4) {
-    hash_chunk_pp(p, clen, j, root, cv);
+  constexpr int L = PF % 100, GA = kGA<PF>;
+  if constexpr (L == 8) {
+    hash_chunk_ps<GA>(p, clen, j, root, cv);
+  } else if constexpr (L == 9) {
+    hash_chunk_pl<GA>(p, clen, j, root, cv);
+  } else if constexpr (L == 4) {
+    hash_chunk_pp<GA>(p, clen, j, root, cv);
   } else {
 #ifdef SDCAS_ABLATIONS
     if constexpr (PF == 6) hash_chunk_pf2(p, clen, j, root, cv);
@@ -204,7 +211,7 @@ __device__ __forceinline__ void leaf_hash(const uint8_t* __restrict__ p, uint32_
     else if constexpr (PF == 1) hash_chunk_pf(p, clen, j, root, cv);
     else hash_chunk(p, clen, j, root, cv);
 #else
-    static_assert(PF == 8 || PF == 9 || PF == 4, "ablation block loops need -DSDCAS_ABLATIONS");
+    static_assert(L == 8 || L == 9 || L == 4, "ablation block loops need -DSDCAS_ABLATIONS");
 #endif
   }
 }
@@ -488,7 +495,7 @@ __global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __
           a[q] = cvs[l][q];
           b[q] = cvs[r][q];
         }
-        parent(a, b, root, o);
+        parent<kGA<PF>>(a, b, root, o);
         if (root) {
           const uint32_t mm = m0 + ((e >> 20) & 2047u);
           store_digest(perm ? perm[mm] : mm, o, out32, out_keys);
@@ -828,7 +835,7 @@ __global__ void __launch_bounds__(kWG, MINW) k_piece_tree(const uint8_t* __restr
           l[i] = cvs[s][i];
           r[i] = cvs[s + (w >> 1)][i];
         }
-        parent(l, r, false, o);
+        parent<kGA<PF>>(l, r, false, o);
 #pragma unroll
         for (int i = 0; i < 8; ++i) cvs[s][i] = o[i];
       }
@@ -1205,7 +1212,8 @@ static const LeafVariant kLeafVariants[] = {
     ABL(512, k_leaf_tree<512, 9, 1, 1, 1>),    // 47: 43 with the last-block-index loop
     ABL(512, k_leaf_tree<512, 9, 1, 1, 1, 1>),    // 48: 47 with the leaf's chunk kept in registers from phase 1
     ABL1(512, k_leaf_tree<512, 9, 1, 1, 2, 1>),   // 49: 46 with the same
-    PROD1(512, k_leaf_tree<512, 9, 1, 1, 2, 2>),  // 50 (default): 49 keeping only the first slot's chunk (no spills)
+    PROD1(512, k_leaf_tree<512, 9, 1, 1, 2, 2>),  // 50: 49 keeping only the first slot's chunk (no spills)
+    PROD1(512, k_leaf_tree<512, 109, 1, 1, 2, 2>),  // 51 (default): 50 with the asm G blocks (B3_G_ASM)
 };
 #undef PROD
 #undef PROD1
@@ -1214,7 +1222,7 @@ static const LeafVariant kLeafVariants[] = {
 #undef ABLQ
 #undef RET
 constexpr int kNumLeafVariants = sizeof(kLeafVariants) / sizeof(kLeafVariants[0]);
-constexpr int kDefaultLeafVariant = 50;
+constexpr int kDefaultLeafVariant = 51;
 
 int leaf_variant_count() { return kNumLeafVariants; }
 bool leaf_variant_available(int v) { return v >= 0 && v < kNumLeafVariants && kLeafVariants[v].fn != nullptr; }
@@ -1310,19 +1318,20 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
 }
 
 // Piece kernel variants: 4 = one workgroup per piece, ping-pong block loop,
-// 6 waves/SIMD (round 1's default); 6 (default) = 4 with the leaf kernel's
+// 6 waves/SIMD (round 1's default); 6 = 4 with the leaf kernel's
 // line-pair loads: the same time on resident C4 (3.15 TB/s), HBM reads 1.007x
 // the file bytes instead of 1.074x (profiles/r02_pmc_c4*.json); 11 =
 // persistent grid on a global piece
 // counter (k_piece_dyn); 12 = 11 with the next piece's first line loaded
-// before the current piece's tree levels; 13 = 11 at 8 waves/SIMD. The
+// before the current piece's tree levels; 13 = 11 at 8 waves/SIMD; 14
+// (default) = 6 with the asm G blocks (B3_G_ASM, b3_device.h). The
 // others (plain / prefetch loops, rotated chunk order, a round-robin
 // persistent grid, and the DIAGNOSTIC 7 without memory reads) exist only in
 // the ablation library.
-constexpr int kDefaultPieceVariant = 6;
+constexpr int kDefaultPieceVariant = 14;
 
 bool piece_variant_available(int v) {
-  if (v == 4 || v == 6 || v == 11 || v == 12 || v == 13) return true;
+  if (v == 4 || v == 6 || v == 11 || v == 12 || v == 13 || v == 14) return true;
 #ifdef SDCAS_ABLATIONS
   if (v >= 0 && v <= 10) return true;
 #endif
@@ -1368,6 +1377,10 @@ hipError_t piece_hash(const uint8_t* blob, const PieceDesc* pieces, uint32_t npi
   if (v == 13) return launch_piece_dyn<8, 0>(blob, pieces, npieces, file_nodes, ctr, st);
   if (v == 6) {  // 4 with both halves of a 128-byte line loaded together (the leaf kernel's loop)
     hipLaunchKernelGGL((k_piece_tree<8, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
+    return hipGetLastError();
+  }
+  if (v == 14) {  // 6 with the asm G blocks (B3_G_ASM)
+    hipLaunchKernelGGL((k_piece_tree<108, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
     return hipGetLastError();
   }
 #ifdef SDCAS_ABLATIONS

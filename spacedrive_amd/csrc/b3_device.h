@@ -38,36 +38,67 @@ __device__ __forceinline__ uint32_t rotr(uint32_t x, uint32_t n) {
     b = rotr(b ^ c, 7);        \
   } while (0)
 
-// one round; s0..s15 = this round's message schedule (compile-time)
-#define B3_ROUND(s0, s1, s2, s3, s4, s5, s6, s7, s8, s9, s10, s11, s12, s13, s14, s15) \
-  do {                                                                                \
-    B3_G(v0, v4, v8, v12, m[s0], m[s1]);                                              \
-    B3_G(v1, v5, v9, v13, m[s2], m[s3]);                                              \
-    B3_G(v2, v6, v10, v14, m[s4], m[s5]);                                             \
-    B3_G(v3, v7, v11, v15, m[s6], m[s7]);                                             \
-    B3_G(v0, v5, v10, v15, m[s8], m[s9]);                                             \
-    B3_G(v1, v6, v11, v12, m[s10], m[s11]);                                           \
-    B3_G(v2, v7, v8, v13, m[s12], m[s13]);                                            \
-    B3_G(v3, v4, v9, v14, m[s14], m[s15]);                                            \
+// The same G as ONE inline-asm block: its twelve instructions issue in
+// dependence order, and each v_alignbit_b32 is followed by "s_nop 0", which
+// parks the issuing wave for one cycle so that the SIMD's other waves take the
+// VALU. Measured on gfx950 with a register-only compression loop
+// (tools/ubench_compress.hip, profiles/r02_ubench_compress.txt): the
+// compiler's schedule of B3_G (the four G's of a half-round interleaved)
+// sustains 58 G compressions/s, this block 67 G/s at 8 waves per SIMD, the
+// block without the nops 58 G/s. Plain VALU ops on VGPRs, so no hazard needs a
+// wait state inside the block.
+#define B3_G_ASM(a, b, c, d, x, y)                                                           \
+  asm volatile(                                                                              \
+      "v_add3_u32 %0, %0, %1, %4\n v_xor_b32 %3, %3, %0\n v_alignbit_b32 %3, %3, %3, 16\n"   \
+      " s_nop 0\n v_add_u32 %2, %2, %3\n v_xor_b32 %1, %1, %2\n"                             \
+      " v_alignbit_b32 %1, %1, %1, 12\n s_nop 0\n v_add3_u32 %0, %0, %1, %5\n"               \
+      " v_xor_b32 %3, %3, %0\n v_alignbit_b32 %3, %3, %3, 8\n s_nop 0\n"                     \
+      " v_add_u32 %2, %2, %3\n v_xor_b32 %1, %1, %2\n v_alignbit_b32 %1, %1, %1, 7\n"        \
+      " s_nop 0\n"                                                                          \
+      : "+v"(a), "+v"(b), "+v"(c), "+v"(d)                                                   \
+      : "v"(x), "v"(y))
+
+// one round; s0..s15 = this round's message schedule (compile-time); G = the
+// G step (B3_G or B3_G_ASM)
+#define B3_ROUND_G(G, s0, s1, s2, s3, s4, s5, s6, s7, s8, s9, s10, s11, s12, s13, s14, s15) \
+  do {                                                                                     \
+    G(v0, v4, v8, v12, m[s0], m[s1]);                                                      \
+    G(v1, v5, v9, v13, m[s2], m[s3]);                                                      \
+    G(v2, v6, v10, v14, m[s4], m[s5]);                                                     \
+    G(v3, v7, v11, v15, m[s6], m[s7]);                                                     \
+    G(v0, v5, v10, v15, m[s8], m[s9]);                                                     \
+    G(v1, v6, v11, v12, m[s10], m[s11]);                                                   \
+    G(v2, v7, v8, v13, m[s12], m[s13]);                                                    \
+    G(v3, v4, v9, v14, m[s14], m[s15]);                                                    \
   } while (0)
+#define B3_ROUND(...) B3_ROUND_G(B3_G, __VA_ARGS__)
+
+#define B3_SEVEN_ROUNDS(G)                                                 \
+  B3_ROUND_G(G, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);    \
+  B3_ROUND_G(G, 2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8);    \
+  B3_ROUND_G(G, 3, 4, 10, 12, 13, 2, 7, 14, 6, 5, 9, 0, 11, 15, 8, 1);    \
+  B3_ROUND_G(G, 10, 7, 12, 9, 14, 3, 13, 15, 4, 0, 11, 2, 5, 8, 1, 6);    \
+  B3_ROUND_G(G, 12, 13, 9, 11, 15, 10, 14, 8, 7, 2, 5, 3, 0, 1, 6, 4);    \
+  B3_ROUND_G(G, 9, 14, 11, 5, 8, 12, 15, 1, 13, 3, 0, 10, 2, 6, 4, 7);    \
+  B3_ROUND_G(G, 11, 15, 5, 0, 1, 9, 8, 6, 14, 10, 2, 12, 3, 4, 7, 13)
 
 // cv <- first 8 words of compress(cv, m, counter, block_len, flags).
 // For a ROOT compression these 8 words are the 32 digest bytes (LE words),
 // because the root's output-block counter is 0 and every root on this path
 // (a single chunk, or a parent) has counter 0 as well.
+// GA = 0: compiler-scheduled G steps; GA = 1: B3_G_ASM blocks.
+template <int GA = 0>
 __device__ __forceinline__ void compress(uint32_t (&cv)[8], const uint32_t (&m)[16], uint64_t counter,
                                          uint32_t block_len, uint32_t flags) {
   uint32_t v0 = cv[0], v1 = cv[1], v2 = cv[2], v3 = cv[3];
   uint32_t v4 = cv[4], v5 = cv[5], v6 = cv[6], v7 = cv[7];
   uint32_t v8 = IV0, v9 = IV1, v10 = IV2, v11 = IV3;
   uint32_t v12 = (uint32_t)counter, v13 = (uint32_t)(counter >> 32), v14 = block_len, v15 = flags;
-  B3_ROUND(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
-  B3_ROUND(2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8);
-  B3_ROUND(3, 4, 10, 12, 13, 2, 7, 14, 6, 5, 9, 0, 11, 15, 8, 1);
-  B3_ROUND(10, 7, 12, 9, 14, 3, 13, 15, 4, 0, 11, 2, 5, 8, 1, 6);
-  B3_ROUND(12, 13, 9, 11, 15, 10, 14, 8, 7, 2, 5, 3, 0, 1, 6, 4);
-  B3_ROUND(9, 14, 11, 5, 8, 12, 15, 1, 13, 3, 0, 10, 2, 6, 4, 7);
-  B3_ROUND(11, 15, 5, 0, 1, 9, 8, 6, 14, 10, 2, 12, 3, 4, 7, 13);
+  if constexpr (GA) {
+    B3_SEVEN_ROUNDS(B3_G_ASM);
+  } else {
+    B3_SEVEN_ROUNDS(B3_G);
+  }
   cv[0] = v0 ^ v8;
   cv[1] = v1 ^ v9;
   cv[2] = v2 ^ v10;
@@ -84,6 +115,7 @@ __device__ __forceinline__ void set_iv(uint32_t (&cv)[8]) {
 }
 
 // parent node: message = left CV || right CV, counter 0, 64-byte block
+template <int GA = 0>
 __device__ __forceinline__ void parent(const uint32_t (&l)[8], const uint32_t (&r)[8], bool root,
                                        uint32_t (&out)[8]) {
   uint32_t m[16];
@@ -93,7 +125,7 @@ __device__ __forceinline__ void parent(const uint32_t (&l)[8], const uint32_t (&
     m[8 + i] = r[i];
   }
   set_iv(out);
-  compress(out, m, 0, BLOCK_LEN, PARENT | (root ? ROOT : 0u));
+  compress<GA>(out, m, 0, BLOCK_LEN, PARENT | (root ? ROOT : 0u));
 }
 
 // 64 message bytes, 16-byte aligned, fully inside the message

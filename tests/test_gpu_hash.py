@@ -146,7 +146,7 @@ def test_tile_straddles_vs_oracle(eng, oracle):
         assert bytes(d).hex() == oracle.hash(m), len(m)
 
 
-@pytest.mark.parametrize("variant", [43, 50])
+@pytest.mark.parametrize("variant", [43, 50, 51])
 def test_tile_straddles_per_variant(oracle, variant):
     """the straddle corpus through each product leaf variant, in caller
     order (shape sort off) so messages straddle tiles at every level"""
@@ -170,7 +170,7 @@ def test_tile_straddles_per_variant(oracle, variant):
     assert not bad, [len(msgs[i]) for i in bad[:10]]
 
 
-@pytest.mark.parametrize("variant", [43, 50])
+@pytest.mark.parametrize("variant", [43, 50, 51])
 def test_many_short_multichunk_messages(oracle, variant):
     """C5-shaped batches — mostly 2..5-chunk messages, so tiles hold far more
     partial last chunks than a wave has lanes and the leaf kernel's block-count

@@ -2,7 +2,7 @@
 # SQ instruction / wave-state counters and HBM read bytes of the default leaf
 # kernel (product library) on each leaf workload, one counter group per run:
 #   tools/pmc_sq_workloads.sh OUTDIR "c2:1000000 c3:1250000 c5:6250000"
-# Summarise with tools/pmc_sq_summary.py.
+# Summarise with tools/pmc_sq_workloads_summary.py.
 set -u
 OUT=${1:-gpurun_out/pmc_sq_workloads}
 R=$(pwd)
@@ -10,7 +10,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 for WN in ${2:-c2:1000000 c3:1250000 c5:6250000}; do
   W=${WN%%:*}; N=${WN##*:}
-  PROG="python $R/tools/ab_leaf.py --product --rounds 1 --reps 2 --variants 50 --workload $W --files $N"
+  PROG="python $R/tools/ab_leaf.py --product --rounds 1 --reps 2 --variants ${VARIANT:-51} --workload $W --files $N"
   (cd /tmp && timeout -s KILL 180 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
      SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD -d $R/$OUT/s_$W -o s_$W --output-format csv \
      -- $PROG > $R/$OUT/s_$W.log 2>&1) || exit 1

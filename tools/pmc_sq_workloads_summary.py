@@ -28,7 +28,7 @@ XCDS = 8
 def main():
     src, dst = sys.argv[1], sys.argv[2]
     out = {"source": "rocprofv3 --pmc passes (tools/pmc_sq_workloads.sh) over tools/ab_leaf.py --product "
-                     "--variants 50, one counter group per run; FETCH_SIZE x2 per MI355X_MICROARCH.md",
+                     "--variants <VARIANT> (51 unless noted), one counter group per run; FETCH_SIZE x2 per MI355X_MICROARCH.md",
            "workloads": {}}
     for w, n in WORKLOADS:
         sizes, _, _ = bench.files_of(w, 0, n)

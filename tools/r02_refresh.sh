@@ -19,4 +19,7 @@ timeout -k 10 400 python -u bench.py --workload c4 --steps 3 --warmup 1 > $OUT/b
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$OUT/prof_c4 -o c4 --output-format csv -- \
    python $R/bench.py --workload c4 --steps 2 --warmup 1 --no-cpu-baseline > $R/$OUT/prof_c4.log 2>&1) || exit 6
 bash tools/pmc_traffic.sh $OUT/pmc_c2 > $OUT/pmc_c2.log 2>&1 || exit 7
+bash tools/pmc_traffic.sh $OUT/pmc_c4 -- python $R/bench.py --workload c4 --steps 1 --warmup 0 --no-cpu-baseline \
+  > $OUT/pmc_c4.log 2>&1 || exit 8
+VARIANT=51 bash tools/pmc_sq_workloads.sh $OUT/sqw > $OUT/sqw.log 2>&1 || exit 9
 echo done
