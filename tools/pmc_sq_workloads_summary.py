@@ -4,6 +4,9 @@ kernel's VALU / SALU / LDS / VMEM instructions per compression, VALU issue per
 SIMD per cycle, HBM read bytes over the algorithmic message bytes, and the
 clock the kernel ran at (GRBM_GUI_ACTIVE per XCD over the kernel time the same
 run printed).
+Also writes profiles/r02_pmc_<w>.json for C3 and C5 (the HBM traffic per
+launch in tools/pmc_summarize.py's format, which bench.py reads); C2's comes
+from tools/pmc_traffic.sh's dedicated passes.
 usage: pmc_sq_workloads_summary.py SRC DST"""
 import collections
 import csv
@@ -70,6 +73,19 @@ def main():
             "counters_median": m,
         }
     json.dump(out, open(dst, "w"), indent=1)
+    kernel = "k_leaf_tree<512, 109, 1, 1, 2, 2>"
+    for w in ("c3", "c5"):
+        d = out["workloads"].get(w)
+        if not d:
+            continue
+        m = d["counters_median"]
+        rd = m["FETCH_SIZE"] * 1024 * 2
+        tr = {"workload": w.upper(), "kernel": kernel, "hbm_bytes_per_launch": rd + m["WRITE_SIZE"] * 1024,
+              "read_bytes_fetch_size_x2": rd, "write_bytes": m["WRITE_SIZE"] * 1024,
+              "algorithmic_bytes_per_launch": d["message_bytes"],
+              "traffic_over_algorithmic": (rd + m["WRITE_SIZE"] * 1024) / d["message_bytes"],
+              "source": out["source"] + f"; {w.upper()} {d['files']} files"}
+        json.dump(tr, open(os.path.join(os.path.dirname(dst), f"r02_pmc_{w}.json"), "w"), indent=1)
     for w, d in out["workloads"].items():
         print(w, {k: round(v, 4) if isinstance(v, float) else v for k, v in d.items() if k != "counters_median"})
 
