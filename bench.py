@@ -57,10 +57,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # issues over 2 cycles) = 7.86e13 int32 lane-ops/s
 VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9
 OPS_PER_COMPRESSION = 680  # 7 rounds x 8 G x 12 (add3, xor, alignbit) + 8 feed-forward xor
-# tools/ubench_valu.hip on MI355X: the 3-operand VOP3 ops BLAKE3 needs
-# (v_alignbit_b32, v_add3_u32) issue at half the VOP2 rate, and a
-# register-only compression loop saturates at 58.5 G compressions/s
-VALU_ROOF_MEASURED = 58.5e9
+# tools/ubench_compress.hip on MI355X (profiles/r02_ubench_compress.txt): the
+# best register-only compression loop (each G one asm block with s_nop 0
+# after every v_alignbit_b32, the leaf kernels' B3_G_ASM) sustains 67 G
+# compressions/s at 8 waves/SIMD (the compiler-scheduled G: 58.5 G/s)
+VALU_ROOF_MEASURED = 67.0e9
 # the VALU roofline of this instruction mix at the spec clock: one compression
 # is 56 G x (2 v_add3_u32 + 4 v_alignbit_b32, 4 issue cycles each per wave64)
 # + 56 G x (4 v_xor_b32 + 2 v_add_u32) + 8 feed-forward v_xor_b32 (2 cycles
