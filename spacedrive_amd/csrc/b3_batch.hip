@@ -189,9 +189,10 @@ __device__ __forceinline__ void hash_chunk_pl(const uint8_t* __restrict__ p, uin
 
 // Block loop of a leaf chunk: PF 8 = hash_chunk_ps, 9 = hash_chunk_pl, 4 =
 // hash_chunk_pp; PF + 100 = the same loop with the asm G blocks (B3_G_ASM,
-// b3_device.h); any other PF names an ablation loop.
+// b3_device.h), PF + 200 = with the copy-free first column steps too
+// (compress<2>); any other PF names an ablation loop.
 template <int PF>
-constexpr int kGA = PF >= 100 ? 1 : 0;
+constexpr int kGA = PF / 100;
 template <int PF>
 __device__ __forceinline__ void leaf_hash(const uint8_t* __restrict__ p, uint32_t clen, uint64_t j, bool root,
                                           uint32_t (&cv)[8]) {
@@ -1205,15 +1206,16 @@ static const LeafVariant kLeafVariants[] = {
     ABL(512, k_leaf_tree<512, 2, 1, 1, 1>),
     ABL(512, k_leaf_tree<512, 2, 0, 1, 1>),
     ABL(512, k_leaf_tree<512, 7, 1, 1, 1>),    // 42: 29 with 128-byte pair loads
-    PROD(512, k_leaf_tree<512, 8, 1, 1, 1>),   // 43 (round 1's default): 36 with both halves of a line loaded together
+    ABL(512, k_leaf_tree<512, 8, 1, 1, 1>),    // 43 (round 1's default): 36 with both halves of a line loaded together
     ABL1(512, k_leaf_tree<512, 8, 1, 1, 2>),   // 44: 43 with one tile per workgroup (hardware dispatch)
     ABL1(512, k_leaf_tree<512, 4, 1, 1, 2>),   // 45: 36 with one tile per workgroup
     ABL1(512, k_leaf_tree<512, 9, 1, 1, 2>),   // 46: 44 with the last-block-index loop (hash_chunk_pl)
     ABL(512, k_leaf_tree<512, 9, 1, 1, 1>),    // 47: 43 with the last-block-index loop
     ABL(512, k_leaf_tree<512, 9, 1, 1, 1, 1>),    // 48: 47 with the leaf's chunk kept in registers from phase 1
     ABL1(512, k_leaf_tree<512, 9, 1, 1, 2, 1>),   // 49: 46 with the same
-    PROD1(512, k_leaf_tree<512, 9, 1, 1, 2, 2>),  // 50: 49 keeping only the first slot's chunk (no spills)
+    ABL1(512, k_leaf_tree<512, 9, 1, 1, 2, 2>),   // 50: 49 keeping only the first slot's chunk (no spills)
     PROD1(512, k_leaf_tree<512, 109, 1, 1, 2, 2>),  // 51 (default): 50 with the asm G blocks (B3_G_ASM)
+    PROD1(512, k_leaf_tree<512, 209, 1, 1, 2, 2>),  // 52: 51 with copy-free first column steps (compress<2>)
 };
 #undef PROD
 #undef PROD1
@@ -1317,23 +1319,23 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
   return hipGetLastError();
 }
 
-// Piece kernel variants: 4 = one workgroup per piece, ping-pong block loop,
-// 6 waves/SIMD (round 1's default); 6 = 4 with the leaf kernel's
-// line-pair loads: the same time on resident C4 (3.15 TB/s), HBM reads 1.007x
-// the file bytes instead of 1.074x (profiles/r02_pmc_c4*.json); 11 =
-// persistent grid on a global piece
-// counter (k_piece_dyn); 12 = 11 with the next piece's first line loaded
-// before the current piece's tree levels; 13 = 11 at 8 waves/SIMD; 14
-// (default) = 6 with the asm G blocks (B3_G_ASM, b3_device.h). The
-// others (plain / prefetch loops, rotated chunk order, a round-robin
-// persistent grid, and the DIAGNOSTIC 7 without memory reads) exist only in
-// the ablation library.
+// Piece kernel variants. Product: 14 (default) = one workgroup per 1 MiB
+// piece, the leaf kernel's line-pair block loop, 6 waves/SIMD, every G step a
+// B3_G_ASM block (b3_device.h); 15 = 14 with the copy-free first column steps
+// (compress<2>; same time within noise, profiles/r02_ab_asm_g.txt). Ablation
+// library only: 4 = ping-pong block loop (round 1's default), 6 = 14 with the
+// compiler-scheduled G (round 2's default before B3_G_ASM: 10 % slower), 11
+// = persistent grid on a global piece counter (k_piece_dyn), 12 = 11 with the
+// next piece's first line loaded before the current piece's tree levels, 13
+// = 11 at 8 waves/SIMD (11-13 lost to the hardware dispatcher), and the older
+// plain / prefetch loops, rotated chunk orders, a round-robin persistent grid
+// and the DIAGNOSTIC 7 without memory reads.
 constexpr int kDefaultPieceVariant = 14;
 
 bool piece_variant_available(int v) {
-  if (v == 4 || v == 6 || v == 11 || v == 12 || v == 13 || v == 14) return true;
+  if (v == 14 || v == 15) return true;
 #ifdef SDCAS_ABLATIONS
-  if (v >= 0 && v <= 10) return true;
+  if (v >= 0 && v <= 13) return true;
 #endif
   return false;
 }
@@ -1348,6 +1350,7 @@ int piece_variant() {
   return v;
 }
 
+#ifdef SDCAS_ABLATIONS
 static int piece_grid(const void* fn) {
   int dev = 0, cus = 0, per = 0;
   (void)hipGetDevice(&dev);
@@ -1368,22 +1371,11 @@ static hipError_t launch_piece_dyn(const uint8_t* blob, const PieceDesc* pieces,
   return hipGetLastError();
 }
 
-hipError_t piece_hash(const uint8_t* blob, const PieceDesc* pieces, uint32_t npieces, uint32_t* file_nodes,
-                      uint32_t* ctr, int variant, hipStream_t st) {
-  if (!npieces) return hipSuccess;
-  const int v = piece_variant_available(variant) ? variant : piece_variant();
+static hipError_t piece_hash_ablation(int v, const uint8_t* blob, const PieceDesc* pieces, uint32_t npieces,
+                                      uint32_t* file_nodes, uint32_t* ctr, hipStream_t st) {
   if (v == 11) return launch_piece_dyn<6, 0>(blob, pieces, npieces, file_nodes, ctr, st);
   if (v == 12) return launch_piece_dyn<6, 1>(blob, pieces, npieces, file_nodes, ctr, st);
   if (v == 13) return launch_piece_dyn<8, 0>(blob, pieces, npieces, file_nodes, ctr, st);
-  if (v == 6) {  // 4 with both halves of a 128-byte line loaded together (the leaf kernel's loop)
-    hipLaunchKernelGGL((k_piece_tree<8, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
-    return hipGetLastError();
-  }
-  if (v == 14) {  // 6 with the asm G blocks (B3_G_ASM)
-    hipLaunchKernelGGL((k_piece_tree<108, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
-    return hipGetLastError();
-  }
-#ifdef SDCAS_ABLATIONS
   if (v == 0) hipLaunchKernelGGL((k_piece_tree<0, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   else if (v == 1)
     hipLaunchKernelGGL((k_piece_tree<1, 8>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
@@ -1393,6 +1385,8 @@ hipError_t piece_hash(const uint8_t* blob, const PieceDesc* pieces, uint32_t npi
     hipLaunchKernelGGL((k_piece_tree<1, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   else if (v == 5)
     hipLaunchKernelGGL((k_piece_tree<4, 8, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
+  else if (v == 6)
+    hipLaunchKernelGGL((k_piece_tree<8, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   else if (v == 7)  // DIAGNOSTIC (wrong digests): 4's loop without memory reads
     hipLaunchKernelGGL((k_piece_tree<2, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   else if (v == 8)  // 4 with per-workgroup rotated chunk order
@@ -1404,9 +1398,26 @@ hipError_t piece_hash(const uint8_t* blob, const PieceDesc* pieces, uint32_t npi
     if (!grid) grid = piece_grid((const void*)k_piece_tree<4, 6, 1>);
     hipLaunchKernelGGL((k_piece_tree<4, 6, 1>), dim3(std::min<uint32_t>(npieces, (uint32_t)grid)), dim3(kWG), 0, st,
                        blob, pieces, npieces, file_nodes);
-  } else
-#endif
+  } else  // 4
     hipLaunchKernelGGL((k_piece_tree<4, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
+  return hipGetLastError();
+}
+#endif
+
+hipError_t piece_hash(const uint8_t* blob, const PieceDesc* pieces, uint32_t npieces, uint32_t* file_nodes,
+                      uint32_t* ctr, int variant, hipStream_t st) {
+  if (!npieces) return hipSuccess;
+  const int v = piece_variant_available(variant) ? variant : piece_variant();
+  if (v == 15) {
+    hipLaunchKernelGGL((k_piece_tree<208, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
+    return hipGetLastError();
+  }
+#ifdef SDCAS_ABLATIONS
+  if (v != 14) return piece_hash_ablation(v, blob, pieces, npieces, file_nodes, ctr, st);
+#else
+  (void)ctr;
+#endif
+  hipLaunchKernelGGL((k_piece_tree<108, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   return hipGetLastError();
 }
 

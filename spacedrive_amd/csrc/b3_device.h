@@ -58,6 +58,21 @@ __device__ __forceinline__ uint32_t rotr(uint32_t x, uint32_t n) {
       : "+v"(a), "+v"(b), "+v"(c), "+v"(d)                                                   \
       : "v"(x), "v"(y))
 
+// The first round's four column steps read c = an IV word and d = a word of
+// (counter, block length, flags) only once, so they take them as inputs: c
+// from an SGPR, d from the caller's VGPR, and write fresh c, d (no copies of
+// the inputs into the state registers).
+#define B3_G_ASM_FIRST(a, b, c, d, cin, din, x, y)                                           \
+  asm volatile(                                                                              \
+      "v_add3_u32 %0, %0, %1, %6\n v_xor_b32 %3, %5, %0\n v_alignbit_b32 %3, %3, %3, 16\n"   \
+      " s_nop 0\n v_add_u32 %2, %4, %3\n v_xor_b32 %1, %1, %2\n"                             \
+      " v_alignbit_b32 %1, %1, %1, 12\n s_nop 0\n v_add3_u32 %0, %0, %1, %7\n"               \
+      " v_xor_b32 %3, %3, %0\n v_alignbit_b32 %3, %3, %3, 8\n s_nop 0\n"                     \
+      " v_add_u32 %2, %2, %3\n v_xor_b32 %1, %1, %2\n v_alignbit_b32 %1, %1, %1, 7\n"        \
+      " s_nop 0\n"                                                                          \
+      : "+v"(a), "+v"(b), "=&v"(c), "=&v"(d)                                                 \
+      : "s"(cin), "v"(din), "v"(x), "v"(y))
+
 // one round; s0..s15 = this round's message schedule (compile-time); G = the
 // G step (B3_G or B3_G_ASM)
 #define B3_ROUND_G(G, s0, s1, s2, s3, s4, s5, s6, s7, s8, s9, s10, s11, s12, s13, s14, s15) \
@@ -73,8 +88,7 @@ __device__ __forceinline__ uint32_t rotr(uint32_t x, uint32_t n) {
   } while (0)
 #define B3_ROUND(...) B3_ROUND_G(B3_G, __VA_ARGS__)
 
-#define B3_SEVEN_ROUNDS(G)                                                 \
-  B3_ROUND_G(G, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);    \
+#define B3_SIX_ROUNDS(G)                                                   \
   B3_ROUND_G(G, 2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8);    \
   B3_ROUND_G(G, 3, 4, 10, 12, 13, 2, 7, 14, 6, 5, 9, 0, 11, 15, 8, 1);    \
   B3_ROUND_G(G, 10, 7, 12, 9, 14, 3, 13, 15, 4, 0, 11, 2, 5, 8, 1, 6);    \
@@ -86,18 +100,44 @@ __device__ __forceinline__ uint32_t rotr(uint32_t x, uint32_t n) {
 // For a ROOT compression these 8 words are the 32 digest bytes (LE words),
 // because the root's output-block counter is 0 and every root on this path
 // (a single chunk, or a parent) has counter 0 as well.
-// GA = 0: compiler-scheduled G steps; GA = 1: B3_G_ASM blocks.
+// GA = 0: compiler-scheduled G steps; GA = 1: B3_G_ASM blocks; GA = 2:
+// B3_G_ASM with the first column steps as B3_G_ASM_FIRST.
+#define B3_ROUND0(G) B3_ROUND_G(G, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15)
 template <int GA = 0>
 __device__ __forceinline__ void compress(uint32_t (&cv)[8], const uint32_t (&m)[16], uint64_t counter,
                                          uint32_t block_len, uint32_t flags) {
   uint32_t v0 = cv[0], v1 = cv[1], v2 = cv[2], v3 = cv[3];
   uint32_t v4 = cv[4], v5 = cv[5], v6 = cv[6], v7 = cv[7];
+  if constexpr (GA == 2) {
+    uint32_t v8, v9, v10, v11, v12, v13, v14, v15;
+    const uint32_t c_lo = (uint32_t)counter, c_hi = (uint32_t)(counter >> 32);
+    B3_G_ASM_FIRST(v0, v4, v8, v12, IV0, c_lo, m[0], m[1]);
+    B3_G_ASM_FIRST(v1, v5, v9, v13, IV1, c_hi, m[2], m[3]);
+    B3_G_ASM_FIRST(v2, v6, v10, v14, IV2, block_len, m[4], m[5]);
+    B3_G_ASM_FIRST(v3, v7, v11, v15, IV3, flags, m[6], m[7]);
+    B3_G_ASM(v0, v5, v10, v15, m[8], m[9]);
+    B3_G_ASM(v1, v6, v11, v12, m[10], m[11]);
+    B3_G_ASM(v2, v7, v8, v13, m[12], m[13]);
+    B3_G_ASM(v3, v4, v9, v14, m[14], m[15]);
+    B3_SIX_ROUNDS(B3_G_ASM);
+    cv[0] = v0 ^ v8;
+    cv[1] = v1 ^ v9;
+    cv[2] = v2 ^ v10;
+    cv[3] = v3 ^ v11;
+    cv[4] = v4 ^ v12;
+    cv[5] = v5 ^ v13;
+    cv[6] = v6 ^ v14;
+    cv[7] = v7 ^ v15;
+    return;
+  }
   uint32_t v8 = IV0, v9 = IV1, v10 = IV2, v11 = IV3;
   uint32_t v12 = (uint32_t)counter, v13 = (uint32_t)(counter >> 32), v14 = block_len, v15 = flags;
   if constexpr (GA) {
-    B3_SEVEN_ROUNDS(B3_G_ASM);
+    B3_ROUND0(B3_G_ASM);
+    B3_SIX_ROUNDS(B3_G_ASM);
   } else {
-    B3_SEVEN_ROUNDS(B3_G);
+    B3_ROUND0(B3_G);
+    B3_SIX_ROUNDS(B3_G);
   }
   cv[0] = v0 ^ v8;
   cv[1] = v1 ^ v9;

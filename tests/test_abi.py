@@ -70,20 +70,17 @@ def _kernel_stubs(path):
 
 
 def test_product_library_holds_only_product_kernels():
-    """libsdcas.so carries the product leaf kernels (50, 51 = 50 with the asm
-    G blocks) and round 1's default (43), all bit-exact and GPU-tested, and
-    no ablation or
+    """libsdcas.so carries only the product kernels — leaf 51 (default) and
+    52, piece 14 (default) and 15, all bit-exact and GPU-tested — and no
+    ablation or
     DIAGNOSTIC variant (those produce wrong digests and live only in
     libsdcas_ablate.so)"""
     stubs = _kernel_stubs(N.LIB_PATH)
     leaf = [s for s in stubs if s.startswith("k_leaf")]
-    assert leaf == ["k_leaf_tree<512, 109, 1, 1, 2, 2>", "k_leaf_tree<512, 8, 1, 1, 1, 0>",
-                    "k_leaf_tree<512, 9, 1, 1, 2, 2>"], leaf
+    assert leaf == ["k_leaf_tree<512, 109, 1, 1, 2, 2>", "k_leaf_tree<512, 209, 1, 1, 2, 2>"], leaf
     assert not [s for s in stubs if "slim" in s or "quad" in s]
     pieces = [s for s in stubs if s.startswith("k_piece")]
-    assert sorted(pieces) == ["k_piece_dyn<6, 0>", "k_piece_dyn<6, 1>", "k_piece_dyn<8, 0>",
-                              "k_piece_tree<108, 6, 1, 0>", "k_piece_tree<4, 6, 1, 0>",
-                              "k_piece_tree<8, 6, 1, 0>"], pieces
+    assert sorted(pieces) == ["k_piece_tree<108, 6, 1, 0>", "k_piece_tree<208, 6, 1, 0>"], pieces
 
 
 def test_ablation_build_is_separate():

@@ -134,7 +134,7 @@ def test_stream_over_4tib_golden(eng):
         assert bytes(out.cpu().numpy()[0]).hex() == c["checksum"], n
 
 
-@pytest.mark.parametrize("variant", [4, 6, 11, 12, 13, 14])
+@pytest.mark.parametrize("variant", [14, 15])
 def test_piece_variants_vs_oracle(oracle, variant):
     """every product piece kernel (4: one workgroup per piece; 11-13: the
     persistent grid on a piece counter, with / without the next piece's first

@@ -18,12 +18,17 @@ def main():
     ap.add_argument("--gib", type=int, default=16, help="window size (GiB of file bytes)")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--variants", default="4,11,12,13")
+    ap.add_argument("--variants", default="14,15")
+    ap.add_argument("--ablation", action="store_true",
+                    help="bind libsdcas_ablate.so (variants 0-13: round 1/2's losing and DIAGNOSTIC kernels)")
     a = ap.parse_args()
     import torch
 
     from spacedrive_amd import Engine
     from spacedrive_amd import synth as S
+    if a.ablation:
+        from spacedrive_amd import _native as N
+        N.use_ablation_library()
     MiB = 1 << 20
     sizes, keys = S.c4_files(int(a.gib) << 30)
     dev = torch.device("cuda", 0)
