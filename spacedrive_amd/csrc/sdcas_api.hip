@@ -21,6 +21,8 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <chrono>
+#include <memory>
 #include <vector>
 
 #include "../../include/sdcas.h"
@@ -38,7 +40,6 @@ namespace {
 // spacedrive_amd/host/cas_io.cpp: tested under ASan / UBSan / TSan by
 // tests/cpp/test_cas_io.cpp)
 using sdcas_io::open_for_read;
-using sdcas_io::parallel_for;
 using sdcas_io::plan_batch;
 using sdcas_io::pread_direct;
 using sdcas_io::pread_exact;
@@ -103,6 +104,7 @@ struct sdcas_ctx {
   std::string err;
   std::mutex mu;
   uint32_t io_threads = 8;
+  std::unique_ptr<sdcas_io::WorkerPool> pool;  // io_threads readers (the calling thread is one)
   uint64_t staging_bytes = 256ull << 20;
   bool direct_io = false;  // SDCAS_OPT_DIRECT_IO: big-file checksum reads bypass the page cache
 
@@ -433,7 +435,7 @@ int run_big(sdcas_ctx* c, const std::vector<BigItem>& items, uint8_t* out32_host
     if (jobs.empty()) return SDCAS_OK;
     Slot& s = c->slots[cur];
     jst.assign(jobs.size(), 0);
-    parallel_for(c->io_threads, jobs.size(), [&](size_t k) {
+    c->pool->run(jobs.size(), [&](size_t k) {
       const Job& jb = jobs[k];
       jst[k] = fill(jb.item, s.h + jb.dst, jb.off, jb.len);
     });
@@ -535,6 +537,7 @@ int sdcas_init(const sdcas_options* opts, sdcas_ctx** out) {
     c->progress_user = opts->progress_user;
     c->cancel = opts->cancel;
   }
+  c->pool.reset(new sdcas_io::WorkerPool(c->io_threads));
   if (dev < 0) (void)hipGetDevice(&dev);
   if (dev >= count) {
     delete c;
@@ -768,7 +771,7 @@ static int hash_host_messages(sdcas_ctx* c, const uint8_t* blob, const uint64_t*
     if (direct) {
       s.src = blob + base;
     } else {
-      parallel_for(c->io_threads, s.n, [&](size_t k) {
+      c->pool->run(s.n, [&](size_t k) {
         memcpy(s.h + s.offs()[k], blob + offsets[s.idx[k]], s.lens()[k]);
       });
     }
@@ -836,6 +839,25 @@ int sdcas_cas_ids_from_messages(sdcas_ctx* c, const uint8_t* blob, const uint64_
   return hash_host_messages(c, blob, offsets, lens, n, nullptr, out_keys);
 }
 
+// SDCAS_TRACE_IO=1: per-call wall time of sdcas_cas_ids' phases on stderr
+// (measurement aid for the page-cache path; no effect otherwise)
+struct IoTrace {
+  bool on = getenv("SDCAS_TRACE_IO") != nullptr;
+  double t[5] = {0, 0, 0, 0, 0};  // drain, plan, read, bookkeeping, submit
+  std::chrono::steady_clock::time_point m = std::chrono::steady_clock::now();
+  void lap(int k) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    t[k] += std::chrono::duration<double, std::milli>(now - m).count();
+    m = now;
+  }
+  ~IoTrace() {
+    if (on)
+      fprintf(stderr, "sdcas_cas_ids trace ms: drain %.1f plan %.1f read %.1f book %.1f submit %.1f\n", t[0], t[1],
+              t[2], t[3], t[4]);
+  }
+};
+
 int sdcas_cas_ids(sdcas_ctx* c, const char* const* paths, const uint64_t* sizes, size_t n, uint64_t* out_keys,
                   int32_t* out_status) {
   if (!c || (n && (!paths || !sizes || !out_keys || !out_status))) return SDCAS_E_INVALID;
@@ -862,6 +884,7 @@ int sdcas_cas_ids(sdcas_ctx* c, const char* const* paths, const uint64_t* sizes,
     return slot_complete(c, s, [&](size_t k, const uint8_t* r) { memcpy(&out_keys[s.idx[k]], r, 8); }, &pr);
   };
   bool cancelled = false;
+  IoTrace tr;
   for (int round = 0; round < 4 && !todo.empty() && !cancelled; ++round) {
     std::vector<size_t> retry;
     size_t p = 0;
@@ -869,7 +892,9 @@ int sdcas_cas_ids(sdcas_ctx* c, const char* const* paths, const uint64_t* sizes,
       // batch [p, q) fitting one staging slot (a message larger than the slot
       // — a whole-file cas message of a file grown past it — gets its own)
       Slot& s = c->slots[cur];
+      tr.lap(4);
       if ((rc = drain(s))) return rc;
+      tr.lap(0);
       if ((cancelled = c->cancelled())) {
         for (size_t k = p; k < todo.size(); ++k) out_status[todo[k]] = SDCAS_STATUS_CANCELLED;
         for (size_t i : retry) out_status[i] = SDCAS_STATUS_CANCELLED;
@@ -883,10 +908,12 @@ int sdcas_cas_ids(sdcas_ctx* c, const char* const* paths, const uint64_t* sizes,
       const size_t m = q - p;
       std::vector<uint64_t> mlen(m), retry_len(m);
       std::vector<int32_t> st(m);
-      parallel_for(c->io_threads, m, [&](size_t k) {
+      tr.lap(1);
+      c->pool->run(m, [&](size_t k) {
         const size_t i = todo[p + k];
         st[k] = read_cas_message(paths[i], sizes[i], s.h + slot_off[k], align16(want[i]), &mlen[k], &retry_len[k]);
       });
+      tr.lap(2);
       s.n = 0, s.chunks = 0, s.used = used, s.content = 0;
       s.idx.clear();
       for (size_t k = 0; k < m; ++k) {
@@ -905,6 +932,7 @@ int sdcas_cas_ids(sdcas_ctx* c, const char* const* paths, const uint64_t* sizes,
         s.n++;
         s.chunks += chunks_of(mlen[k]);
       }
+      tr.lap(3);
       if ((rc = slot_submit(c, s, false))) return rc;
       if (!s.n) pr.add(s.content);  // nothing to hash: the slot's files are final now
       cur ^= 1;
@@ -930,7 +958,7 @@ int sdcas_checksums(sdcas_ctx* c, const char* const* paths, size_t n, uint8_t* o
   // file lengths first (hash.rs reads to EOF; a regular file's EOF is its length)
   std::vector<uint64_t> flen(n);
   std::vector<int32_t> fst(n);
-  parallel_for(c->io_threads, n, [&](size_t i) {
+  c->pool->run(n, [&](size_t i) {
     struct stat sb;
     if (stat(paths[i], &sb) != 0) fst[i] = errno;
     else if (S_ISDIR(sb.st_mode)) fst[i] = EISDIR;
@@ -964,7 +992,7 @@ int sdcas_checksums(sdcas_ctx* c, const char* const* paths, size_t n, uint8_t* o
     const size_t m = q - p;
     std::vector<uint64_t> got(m);
     std::vector<int32_t> st(m);
-    parallel_for(c->io_threads, m, [&](size_t k) {
+    c->pool->run(m, [&](size_t k) {
       const size_t i = small[p + k];
       int fd = open(paths[i], O_RDONLY | O_CLOEXEC);
       if (fd < 0) {

@@ -19,10 +19,35 @@ chunk instead of per file. Everything runs on the GPU; there is no CPU path.
 """
 import ctypes
 import os
+import sys
 
 import numpy as np
 
 from . import _native as N
+
+
+def _cpaths(paths):
+    """(buffer, pointers) for a `const char* const*` argument: the paths
+    NUL-terminated in ONE bytes buffer and a uint64 array of their addresses
+    (one numpy pass instead of a ctypes object per path — the per-path form
+    cost more than the library's reads of 200 K files). Keep `buffer` alive
+    for the call."""
+    n = len(paths)
+    if n == 0:
+        return None, np.zeros(1, np.uint64)
+    try:  # the common case, a list of str: one join, one encode
+        enc = ("\0".join(paths) + "\0").encode(sys.getfilesystemencoding(), "surrogateescape")
+    except TypeError:  # bytes or os.PathLike items
+        enc = b"\0".join(os.fsencode(p) for p in paths) + b"\0"
+    buf = np.frombuffer(enc, np.uint8)
+    ends = np.flatnonzero(buf == 0)
+    if len(ends) != n:
+        raise ValueError("a path contains a NUL byte")
+    ptrs = np.empty(n, np.uint64)
+    ptrs[0] = 0
+    ptrs[1:] = ends[:-1] + 1
+    ptrs += np.uint64(buf.ctypes.data)
+    return buf, ptrs
 
 
 def _arr(a, dtype):
@@ -119,22 +144,24 @@ class Engine:
     def generate_cas_ids(self, paths, sizes):
         """cas.rs:23-62 for many files -> (keys uint64[n], status int32[n])"""
         n = len(paths)
-        bpaths = [os.fsencode(p) for p in paths]
-        parr = (ctypes.c_char_p * max(n, 1))(*bpaths)
+        buf, parr = _cpaths(paths)
         sizes = _arr(sizes, np.uint64)
         keys = np.zeros(n, np.uint64)
         st = np.zeros(n, np.int32)
-        self._check(self.L.sdcas_cas_ids(self.ctx, parr, _ptr(sizes), n, _ptr(keys), _ptr(st)),
+        self._check(self.L.sdcas_cas_ids(self.ctx, _ptr(parr), _ptr(sizes), n, _ptr(keys), _ptr(st)),
                     "sdcas_cas_ids", (keys, st))
+        del buf
         return keys, st
 
     def file_checksums(self, paths):
         """hash.rs:11-25 for many files -> (digests uint8[n, 32], status int32[n])"""
         n = len(paths)
-        parr = (ctypes.c_char_p * max(n, 1))(*[os.fsencode(p) for p in paths])
+        buf, parr = _cpaths(paths)
         out = np.zeros((n, 32), np.uint8)
         st = np.zeros(n, np.int32)
-        self._check(self.L.sdcas_checksums(self.ctx, parr, n, _ptr(out), _ptr(st)), "sdcas_checksums", (out, st))
+        self._check(self.L.sdcas_checksums(self.ctx, _ptr(parr), n, _ptr(out), _ptr(st)), "sdcas_checksums",
+                    (out, st))
+        del buf
         return out, st
 
     def generate_cas_id(self, path, size) -> str:

@@ -139,4 +139,51 @@ size_t plan_batch(const uint64_t* need, const size_t* order, size_t p, size_t en
   return q;
 }
 
+WorkerPool::WorkerPool(uint32_t threads) {
+  for (uint32_t t = 1; t < threads; ++t) workers_.emplace_back([this] { loop(); });
+}
+
+WorkerPool::~WorkerPool() {
+  {
+    std::lock_guard<std::mutex> g(m_);
+    stop_ = true;
+  }
+  go_.notify_all();
+  for (auto& t : workers_) t.join();
+}
+
+void WorkerPool::drain() {
+  for (size_t i; (i = next_.fetch_add(1, std::memory_order_relaxed)) < n_;) (*fn_)(i);
+}
+
+void WorkerPool::dispatch(size_t n, const std::function<void(size_t)>* fn) {
+  {
+    std::lock_guard<std::mutex> g(m_);
+    fn_ = fn;
+    n_ = n;
+    next_.store(0, std::memory_order_relaxed);
+    active_ = workers_.size();
+    ++gen_;
+  }
+  go_.notify_all();
+  drain();  // the calling thread is one of the workers
+  std::unique_lock<std::mutex> g(m_);
+  done_.wait(g, [this] { return active_ == 0; });
+  fn_ = nullptr;
+}
+
+void WorkerPool::loop() {
+  uint64_t seen = 0;
+  std::unique_lock<std::mutex> g(m_);
+  for (;;) {
+    go_.wait(g, [&] { return stop_ || gen_ != seen; });
+    if (stop_) return;
+    seen = gen_;
+    g.unlock();
+    drain();
+    g.lock();
+    if (--active_ == 0) done_.notify_one();
+  }
+}
+
 }  // namespace sdcas_io

@@ -12,6 +12,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -80,5 +83,41 @@ void parallel_for(uint32_t threads, size_t n, F f) {
     });
   for (auto& th : pool) th.join();
 }
+
+// The same on a pool of threads kept for the life of a context: `threads`
+// workers in all, the calling thread being one of them (no thread is created
+// per batch). run() is not reentrant; a context serialises its calls.
+class WorkerPool {
+ public:
+  explicit WorkerPool(uint32_t threads);
+  ~WorkerPool();
+  WorkerPool(const WorkerPool&) = delete;
+  WorkerPool& operator=(const WorkerPool&) = delete;
+  uint32_t threads() const { return (uint32_t)workers_.size() + 1; }
+  template <class F>
+  void run(size_t n, F f) {
+    if (n == 0) return;
+    if (workers_.empty() || n == 1) {
+      for (size_t i = 0; i < n; ++i) f(i);
+      return;
+    }
+    std::function<void(size_t)> fn(f);
+    dispatch(n, &fn);
+  }
+
+ private:
+  void dispatch(size_t n, const std::function<void(size_t)>* fn);
+  void drain();
+  void loop();
+  std::vector<std::thread> workers_;
+  std::mutex m_;
+  std::condition_variable go_, done_;
+  const std::function<void(size_t)>* fn_ = nullptr;
+  size_t n_ = 0;
+  std::atomic<size_t> next_{0};
+  size_t active_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
 
 }  // namespace sdcas_io

@@ -21,6 +21,7 @@
 #include <cstring>
 #include <random>
 #include <string>
+#include <atomic>
 #include <vector>
 
 #include "../../oracle/oracle.h"
@@ -119,11 +120,15 @@ int main() {
     want_st[i] = oracle_generate_cas_id(cases[i].path.c_str(), cases[i].size, hex);
     want_hex[i] = hex;
   }
-  // the library's reads, 8 threads at once, five times over
-  for (int rep = 0; rep < 5; ++rep) {
+  // the library's reads, 8 threads at once, five times over: through
+  // parallel_for, then through one WorkerPool reused for every run (as a
+  // context reuses its pool for every staging slot)
+  sdcas_io::WorkerPool pool(8);
+  CHECK(pool.threads() == 8, "pool threads %u", pool.threads());
+  for (int rep = 0; rep < 10; ++rep) {
     std::vector<int> st(cases.size());
     std::vector<std::string> hex(cases.size());
-    sdcas_io::parallel_for(8, cases.size(), [&](size_t i) {
+    auto one = [&](size_t i) {
       std::vector<uint8_t> buf;
       uint64_t len = 0;
       st[i] = library_read(cases[i], buf, &len);
@@ -132,13 +137,27 @@ int main() {
         std::snprintf(h, sizeof h, "%016llx", (unsigned long long)oracle_cas_key_of_message(buf.data(), len));
         hex[i] = h;
       }
-    });
+    };
+    if (rep < 5) sdcas_io::parallel_for(8, cases.size(), one);
+    else pool.run(cases.size(), one);
     for (size_t i = 0; i < cases.size(); ++i) {
       CHECK(st[i] == want_st[i], "%s: status %d, oracle %d", cases[i].path.c_str(), st[i], want_st[i]);
       if (!st[i] && !want_st[i])
         CHECK(hex[i] == want_hex[i], "%s: %s, oracle %s", cases[i].path.c_str(), hex[i].c_str(),
               want_hex[i].c_str());
     }
+  }
+  {  // many small jobs back to back on one pool: every item exactly once per job
+    std::vector<std::atomic<int>> hits(1000);
+    for (int job = 0; job < 300; ++job) {
+      const size_t n = 1 + (size_t)(job * 37 % 1000);
+      pool.run(n, [&](size_t i) { hits[i].fetch_add(1, std::memory_order_relaxed); });
+    }
+    long total = 0;
+    for (auto& h : hits) total += h.load();
+    long want = 0;
+    for (int job = 0; job < 300; ++job) want += 1 + (job * 37 % 1000);
+    CHECK(total == want, "pool ran %ld items, want %ld", total, want);
   }
   CHECK(want_st[cases.size() - 3] == ENOENT, "missing path: %d", want_st[cases.size() - 3]);
   CHECK(want_st[cases.size() - 2] == EISDIR, "directory: %d", want_st[cases.size() - 2]);
