@@ -97,8 +97,11 @@ typedef struct sdcas_ctx sdcas_ctx;
 typedef void (*sdcas_progress_fn)(void *user, uint64_t done, uint64_t total);
 
 /* sdcas_options.flags */
-#define SDCAS_OPT_DIRECT_IO 1u /* file_checksum of files > 1 MiB reads with O_DIRECT (cold storage;
-                                   falls back to the page cache where the filesystem refuses it) */
+#define SDCAS_OPT_DIRECT_IO 1u /* the path calls (sdcas_cas_ids, sdcas_checksums) read files with
+                                   O_DIRECT (cold storage: no page-cache copy; small and unaligned
+                                   reads go through an aligned per-thread buffer); a file whose
+                                   filesystem refuses O_DIRECT is read through the page cache.
+                                   Same bytes, same statuses. */
 
 typedef struct sdcas_options {
   int32_t device;          /* HIP device ordinal (-1: current device) */

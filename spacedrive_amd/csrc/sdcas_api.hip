@@ -45,6 +45,7 @@ using sdcas_io::pread_direct;
 using sdcas_io::pread_exact;
 using sdcas_io::read_cas_message;
 using sdcas_io::read_whole;
+using sdcas_io::read_whole_any;
 
 constexpr uint64_t kMin = SDCAS_MINIMUM_FILE_SIZE;  // cas.rs:15 (the reads themselves: host/cas_io.cpp)
 constexpr uint64_t kSlack = 64;  // readable bytes kept after every message
@@ -911,7 +912,8 @@ int sdcas_cas_ids(sdcas_ctx* c, const char* const* paths, const uint64_t* sizes,
       tr.lap(1);
       c->pool->run(m, [&](size_t k) {
         const size_t i = todo[p + k];
-        st[k] = read_cas_message(paths[i], sizes[i], s.h + slot_off[k], align16(want[i]), &mlen[k], &retry_len[k]);
+        st[k] = read_cas_message(paths[i], sizes[i], s.h + slot_off[k], align16(want[i]), &mlen[k], &retry_len[k],
+                                 c->direct_io);
       });
       tr.lap(2);
       s.n = 0, s.chunks = 0, s.used = used, s.content = 0;
@@ -994,15 +996,16 @@ int sdcas_checksums(sdcas_ctx* c, const char* const* paths, size_t n, uint8_t* o
     std::vector<int32_t> st(m);
     c->pool->run(m, [&](size_t k) {
       const size_t i = small[p + k];
-      int fd = open(paths[i], O_RDONLY | O_CLOEXEC);
+      bool isd = false;
+      const int fd = open_for_read(paths[i], c->direct_io, &isd);
       if (fd < 0) {
-        st[k] = errno;
+        st[k] = -fd;
         return;
       }
       bool over = false;
       // hash.rs stops at its first short read; a file that grew since the
       // stat above is hashed over its stat length (sdcas.h)
-      st[k] = read_whole(fd, s.h + slot[k], flen[i] + 1, flen[i], &got[k], &over);
+      st[k] = read_whole_any(fd, isd, s.h + slot[k], flen[i] + 1, flen[i], &got[k], &over);
       if (over) got[k] = flen[i];
       close(fd);
     });

@@ -10,6 +10,8 @@
 #include <unistd.h>
 
 #include <cerrno>
+#include <cstdlib>
+#include <cstring>
 
 namespace sdcas_io {
 
@@ -82,19 +84,79 @@ int read_whole(int fd, uint8_t* dst, uint64_t cap, uint64_t expect, uint64_t* le
   return 0;
 }
 
-int read_cas_message(const char* path, uint64_t size, uint8_t* dst, uint64_t cap, uint64_t* len,
-                     uint64_t* retry_len) {
+namespace {
+// a 4 KiB-aligned buffer per reader thread for O_DIRECT reads, grown on demand
+struct Bounce {
+  uint8_t* p = nullptr;
+  size_t n = 0;
+  ~Bounce() { free(p); }
+};
+uint8_t* bounce(size_t need) {
+  thread_local Bounce b;
+  if (b.n < need) {
+    free(b.p);
+    b.p = nullptr;
+    b.n = 0;
+    void* q = nullptr;
+    if (posix_memalign(&q, kDirectAlign, need)) return nullptr;
+    b.p = static_cast<uint8_t*>(q);
+    b.n = need;
+  }
+  return b.p;
+}
+
+// read_exact (tokio) with either kind of read
+int read_exact_any(int fd, bool aligned, uint8_t* dst, uint64_t n, uint64_t off) {
+  if (!aligned) return pread_exact(fd, dst, n, off);
+  uint64_t got = 0;
+  const int st = read_span_direct(fd, dst, n, off, &got);
+  return st ? st : (got < n ? kUnexpectedEof : 0);
+}
+}  // namespace
+
+int read_span_direct(int fd, uint8_t* dst, uint64_t n, uint64_t off, uint64_t* got) {
+  *got = 0;
+  const uint64_t a = off & ~(kDirectAlign - 1), head = off - a;
+  const uint64_t span = (head + n + kDirectAlign - 1) & ~(kDirectAlign - 1);
+  uint8_t* b = bounce(span);
+  if (!b) return ENOMEM;
+  uint64_t r_total = 0;
+  while (r_total < span) {
+    ssize_t r = pread(fd, b + r_total, span - r_total, (off_t)(a + r_total));
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      return errno;
+    }
+    if (r == 0) break;
+    r_total += (uint64_t)r;
+    if (r_total % kDirectAlign) break;  // short of a block: the file ends here
+  }
+  const uint64_t avail = r_total > head ? std::min<uint64_t>(r_total - head, n) : 0;
+  if (avail) memcpy(dst, b + head, avail);
+  *got = avail;
+  return 0;
+}
+
+int read_whole_any(int fd, bool aligned, uint8_t* dst, uint64_t cap, uint64_t expect, uint64_t* len,
+                   bool* overflow) {
+  if (!aligned) return read_whole(fd, dst, cap, expect, len, overflow);
+  *overflow = false;
+  const int st = read_span_direct(fd, dst, cap, 0, len);
+  if (!st && *len == cap) *overflow = true;  // the file holds at least cap bytes
+  return st;
+}
+
+int read_cas_message_fd(int fd, bool aligned, uint64_t size, uint8_t* dst, uint64_t cap, uint64_t* len,
+                        uint64_t* retry_len) {
   *retry_len = 0;
   *len = 0;
-  int fd = open(path, O_RDONLY | O_CLOEXEC);
-  if (fd < 0) return errno;
   for (int i = 0; i < 8; ++i) dst[i] = (uint8_t)(size >> (8 * i));  // cas.rs:25
   int st = 0;
   if (size <= kMin) {
     // cas.rs:27-29: fs::read of the file as it is now
     uint64_t got = 0;
     bool over = false;
-    st = read_whole(fd, dst + 8, cap - 8, size, &got, &over);
+    st = read_whole_any(fd, aligned, dst + 8, cap - 8, size, &got, &over);
     if (!st && over) {
       struct stat sb;
       if (fstat(fd, &sb) == 0) *retry_len = 8 + (uint64_t)sb.st_size + 4096;
@@ -104,21 +166,32 @@ int read_cas_message(const char* path, uint64_t size, uint8_t* dst, uint64_t cap
   } else {
     // cas.rs:35-58: header, 4 samples at 8192 + k*seek_jump, footer at EOF-8192
     uint8_t* p = dst + 8;
-    st = pread_exact(fd, p, kHF, 0);
+    st = read_exact_any(fd, aligned, p, kHF, 0);
     p += kHF;
     const uint64_t seek_jump = (size - kHF * 2) / kSampleCount;
     for (uint64_t k = 0; !st && k < kSampleCount; ++k) {
-      st = pread_exact(fd, p, kSample, kHF + k * seek_jump);
+      st = read_exact_any(fd, aligned, p, kSample, kHF + k * seek_jump);
       p += kSample;
     }
     if (!st) {
       struct stat sb;
       if (fstat(fd, &sb) != 0) st = errno;
       else if ((uint64_t)sb.st_size < kHF) st = EINVAL;  // seek(End(-8192)) before byte 0
-      else st = pread_exact(fd, p, kHF, (uint64_t)sb.st_size - kHF);
+      else st = read_exact_any(fd, aligned, p, kHF, (uint64_t)sb.st_size - kHF);
     }
     *len = kSampledLen;
   }
+  return st;
+}
+
+int read_cas_message(const char* path, uint64_t size, uint8_t* dst, uint64_t cap, uint64_t* len,
+                     uint64_t* retry_len, bool direct) {
+  *retry_len = 0;
+  *len = 0;
+  bool is_direct = false;
+  const int fd = open_for_read(path, direct, &is_direct);
+  if (fd < 0) return -fd;
+  const int st = read_cas_message_fd(fd, is_direct, size, dst, cap, len, retry_len);
   close(fd);
   return st;
 }

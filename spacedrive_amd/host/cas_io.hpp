@@ -50,12 +50,26 @@ int open_for_read(const char* path, bool direct, bool* is_direct);
 // one returning 0; shorter reads keep reading to EOF as fs::read does.
 int read_whole(int fd, uint8_t* dst, uint64_t cap, uint64_t expect, uint64_t* len, bool* overflow);
 
+// Bytes [off, off + n) of an O_DIRECT descriptor (any off and n): the 4 KiB
+// blocks holding them are read into a per-thread aligned bounce buffer and
+// the span copied to dst; *got = the bytes there were (fewer at EOF).
+int read_span_direct(int fd, uint8_t* dst, uint64_t n, uint64_t off, uint64_t* got);
+
+// read_whole with aligned (O_DIRECT) reads when `aligned`
+int read_whole_any(int fd, bool aligned, uint8_t* dst, uint64_t cap, uint64_t expect, uint64_t* len,
+                   bool* overflow);
+
 // cas.rs:23-62 message of one file into dst (capacity cap >= the message
 // length `size` predicts + 1). Returns status; *len = message length.
 // *retry_len != 0 asks the caller to retry with a slot of that capacity (the
-// file grew past `size` since it was indexed).
+// file grew past `size` since it was indexed). `direct`: open with O_DIRECT
+// (cold storage) where the filesystem takes it, every read then aligned
+// through read_span_direct; the bytes and statuses are the same.
 int read_cas_message(const char* path, uint64_t size, uint8_t* dst, uint64_t cap, uint64_t* len,
-                     uint64_t* retry_len);
+                     uint64_t* retry_len, bool direct = false);
+// the same read pattern on an open descriptor (`aligned`: O_DIRECT reads)
+int read_cas_message_fd(int fd, bool aligned, uint64_t size, uint8_t* dst, uint64_t cap, uint64_t* len,
+                        uint64_t* retry_len);
 
 // The next staging batch: items order[p], order[p+1], ... of `need` bytes
 // each (line-aligned here) go to offsets in one slot of `cap` bytes and at

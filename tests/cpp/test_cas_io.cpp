@@ -68,13 +68,24 @@ static void write_sparse(const std::string& p, uint64_t n, std::mt19937_64& rng)
 
 // sdcas_cas_ids' use of read_cas_message: the slot the indexer's size
 // predicts (+1 byte to tell a grown file), a retry in a bigger one
-static int library_read(const Case& c, std::vector<uint8_t>& buf, uint64_t* len) {
+// mode 0: page-cache reads; 1: SDCAS_OPT_DIRECT_IO (O_DIRECT where the
+// filesystem takes it); 2: the aligned (O_DIRECT) read logic on a plain
+// descriptor, so that it is exercised whatever the filesystem
+static int library_read(const Case& c, std::vector<uint8_t>& buf, uint64_t* len, int mode = 0) {
   const uint64_t want = (c.size <= 102400 ? c.size + 8 + 1 : 57352);
   uint64_t cap = sdcas_io::align_line(want);
   for (int round = 0; round < 4; ++round) {
     buf.assign(cap + 64, 0);
     uint64_t retry = 0;
-    const int st = sdcas_io::read_cas_message(c.path.c_str(), c.size, buf.data(), cap, len, &retry);
+    int st;
+    if (mode == 2) {
+      const int fd = open(c.path.c_str(), O_RDONLY | O_CLOEXEC);
+      if (fd < 0) return errno;
+      st = sdcas_io::read_cas_message_fd(fd, true, c.size, buf.data(), cap, len, &retry);
+      close(fd);
+    } else {
+      st = sdcas_io::read_cas_message(c.path.c_str(), c.size, buf.data(), cap, len, &retry, mode == 1);
+    }
     if (st || !retry) return st;
     cap = sdcas_io::align_line(retry);
   }
@@ -120,9 +131,10 @@ int main() {
     want_st[i] = oracle_generate_cas_id(cases[i].path.c_str(), cases[i].size, hex);
     want_hex[i] = hex;
   }
-  // the library's reads, 8 threads at once, five times over: through
-  // parallel_for, then through one WorkerPool reused for every run (as a
-  // context reuses its pool for every staging slot)
+  // the library's reads, 8 threads at once, ten times over (page cache,
+  // O_DIRECT, aligned logic in turn): through parallel_for, then through one
+  // WorkerPool reused for every run (as a context reuses its pool for every
+  // staging slot)
   sdcas_io::WorkerPool pool(8);
   CHECK(pool.threads() == 8, "pool threads %u", pool.threads());
   for (int rep = 0; rep < 10; ++rep) {
@@ -131,7 +143,7 @@ int main() {
     auto one = [&](size_t i) {
       std::vector<uint8_t> buf;
       uint64_t len = 0;
-      st[i] = library_read(cases[i], buf, &len);
+      st[i] = library_read(cases[i], buf, &len, rep % 3);
       if (!st[i]) {
         char h[17];
         std::snprintf(h, sizeof h, "%016llx", (unsigned long long)oracle_cas_key_of_message(buf.data(), len));
@@ -233,6 +245,6 @@ int main() {
     std::printf("%d FAILURES\n", failures);
     return 1;
   }
-  std::printf("ALL OK (%zu files x 5 reps on 8 threads)\n", cases.size());
+  std::printf("ALL OK (%zu files x 10 reps on 8 threads: page cache, O_DIRECT, aligned reads)\n", cases.size());
   return 0;
 }

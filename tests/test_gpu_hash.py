@@ -63,6 +63,41 @@ def test_generate_cas_id_files(eng, tmp_path):
     assert eng.generate_cas_id(paths[3], sizes[3]) == cases[3]["cas_id"]
 
 
+def test_generate_cas_id_files_direct_io(tmp_path):
+    """SDCAS_OPT_DIRECT_IO on the cas_id path: every golden file (whole-file
+    and sampled windows, sparse) read with O_DIRECT where the filesystem takes
+    it — unaligned sample windows through the aligned bounce buffer — gives
+    the same cas_ids; small checksums alongside, and a missing path keeps its
+    errno"""
+    import errno
+    from spacedrive_amd import Engine
+    cases = golden("cas_ids.json")
+    paths, sizes = [], []
+    for c in cases:
+        kind, key = spec_content(c["content"])
+        p = tmp_path / f"f_{c['content'].replace(':', '_')}_{c['size']}"
+        write_sparse_file(p, kind, key, c["size"], cas_windows(c["size"]))
+        paths.append(str(p))
+        sizes.append(c["size"])
+    with Engine(direct_io=True, staging_bytes=8 << 20) as e:
+        keys, st = e.generate_cas_ids(paths + [str(tmp_path / "missing")], sizes + [10])
+        assert st[-1] == errno.ENOENT
+        assert (st[:-1] == 0).all()
+        for c, k in zip(cases, keys):
+            assert f"{int(k):016x}" == c["cas_id"], c
+        small = [(p, n) for p, n in zip(paths, sizes) if n <= (1 << 20)]
+        d_direct, s1 = e.file_checksums([p for p, _ in small])
+    d_plain, s2 = eng_plain_checksums([p for p, _ in small])
+    assert not s1.any() and not s2.any()
+    assert (d_direct == d_plain).all()
+
+
+def eng_plain_checksums(paths):
+    from spacedrive_amd import Engine
+    with Engine() as e:
+        return e.file_checksums(paths)
+
+
 def test_file_checksums_golden(eng, tmp_path):
     cases = [c for c in golden("checksums.json") if c["size"] < (64 << 20)]
     paths = []

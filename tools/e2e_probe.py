@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--dir", default=os.path.join(os.environ.get("TMPDIR", "/tmp"), "sdcas_probe"))
     ap.add_argument("--threads", default="8,16,24,32")
     ap.add_argument("--staging-mib", default="64,256")
+    ap.add_argument("--direct", action="store_true", help="also time SDCAS_OPT_DIRECT_IO (O_DIRECT reads)")
     a = ap.parse_args()
     from spacedrive_amd import Engine
     import bench
@@ -47,20 +48,21 @@ def main():
             r = subprocess.run([ub, a.dir, str(n), str(t), "32", "2"], capture_output=True, text=True, timeout=300)
             print(json.dumps({"ubench_read_threads": t, "out": r.stdout.strip().splitlines()[-4:]}), flush=True)
     ref = None
-    for mib in [int(x) for x in a.staging_mib.split(",")]:
-        for t in [int(x) for x in a.threads.split(",")]:
-            with Engine(io_threads=t, staging_bytes=mib << 20) as e:
-                best = None
-                for _ in range(3):
-                    t0 = time.perf_counter()
-                    got, st = e.generate_cas_ids(paths, sizes)
-                    dt = time.perf_counter() - t0
-                    best = dt if best is None else min(best, dt)
-                if ref is None:
-                    ref = got
-                print(json.dumps({"io_threads": t, "staging_mib": mib, "files_per_s": n / best,
-                                  "same_as_first": bool(np.array_equal(got, ref)), "errors": int((st != 0).sum())}),
-                      flush=True)
+    configs = [(d, mib, t) for d in ([False, True] if a.direct else [False])
+               for mib in [int(x) for x in a.staging_mib.split(",")] for t in [int(x) for x in a.threads.split(",")]]
+    for direct, mib, t in configs:
+        with Engine(io_threads=t, staging_bytes=mib << 20, direct_io=direct) as e:
+            best = None
+            for _ in range(3):
+                t0 = time.perf_counter()
+                got, st = e.generate_cas_ids(paths, sizes)
+                dt = time.perf_counter() - t0
+                best = dt if best is None else min(best, dt)
+            if ref is None:
+                ref = got
+            print(json.dumps({"io_threads": t, "staging_mib": mib, "direct": direct, "files_per_s": n / best,
+                              "same_as_first": bool(np.array_equal(got, ref)), "errors": int((st != 0).sum())}),
+                  flush=True)
     shutil.rmtree(a.dir, ignore_errors=True)
 
 
