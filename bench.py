@@ -630,10 +630,13 @@ def main():
             # host wait in between); its share of the step from HIP events
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            link, created, linked = identifier_dedup_distributed(stages, d_out, d_has, None, d_ids, 100)
+            # a world of one leaves the counts on the device (read after the
+            # timed steps): the step enqueues without a host wait
+            res = identifier_dedup_distributed(stages, d_out, d_has, None, d_ids, 100,
+                                               counts_on_device=not distributed)
             e1.record(stream)
             dd["ev"].append((e0, e1))
-            dd["last"] = (link, created, linked)
+            dd["last"] = res
 
     for _ in range(args.warmup):
         step()
@@ -707,7 +710,12 @@ def main():
         ms, med = float(np.mean(dms)), float(np.median(dms))
         if distributed:
             ms, med = max_over_ranks(torch, dist, dev, [ms, med])
-        _, created, linked = dd["last"]
+        last = dd["last"]
+        if len(last) == 2:  # (link, counts on the device)
+            c = last[1].tolist()
+            last = (last[0], int(c[0]), int(c[1]))
+            dd["last"] = last
+        _, created, linked = last
         out["dedup"] = {"ms_per_step": ms, "ms_median": med, "objects_created": created, "files_linked": linked,
                         "records_per_gpu": n, "timing": "HIP events around the dedup stages, inside the step"}
     if rank == 0 and world == 1:

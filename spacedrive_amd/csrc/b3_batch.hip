@@ -156,7 +156,7 @@ __device__ __forceinline__ void hash_chunk_ps(const uint8_t* __restrict__ p, uin
 // flags are constants selected by one compare, the tail mask runs only on
 // the last block, the second half of a line is loaded only if the chunk has
 // it (no clamped address), and the block pointer advances by one add.
-template <int GA = 0>
+template <int GA = 0, int NT = 0, int LM = 0>
 __device__ __forceinline__ void hash_chunk_pl(const uint8_t* __restrict__ p, uint32_t clen, uint64_t j, bool root,
                                               uint32_t (&cv)[8]) {
   set_iv(cv);
@@ -168,16 +168,29 @@ __device__ __forceinline__ void hash_chunk_pl(const uint8_t* __restrict__ p, uin
 #pragma unroll 1
   for (uint32_t b = 0; b <= lb; b += 2, q += 2 * BLOCK_LEN) {
     const bool two = b + 1 <= lb;
-    load_full_block(q, m0);
-    if (two) load_full_block(q + BLOCK_LEN, m1);
+    if constexpr (NT) {
+      load_full_block_nt(q, m0);
+      if (two) load_full_block_nt(q + BLOCK_LEN, m1);
+    } else {
+      load_full_block(q, m0);
+      if (two) load_full_block(q + BLOCK_LEN, m1);
+    }
     {
       const bool last = b == lb;
-      if (last && lblen < BLOCK_LEN) mask_tail(m0, lblen);
+      if (last && lblen < BLOCK_LEN) {
+        uint32_t L = lblen;
+        if constexpr (LM) asm volatile("" : "+v"(L));  // keeps the mask inside the branch
+        mask_tail(m0, L);
+      }
       compress<GA>(cv, m0, j, last ? lblen : BLOCK_LEN, (b == 0 ? CHUNK_START : 0u) | (last ? endf : 0u));
     }
     if (two) {
       const bool last = b + 1 == lb;
-      if (last && lblen < BLOCK_LEN) mask_tail(m1, lblen);
+      if (last && lblen < BLOCK_LEN) {
+        uint32_t L = lblen;
+        if constexpr (LM) asm volatile("" : "+v"(L));
+        mask_tail(m1, L);
+      }
       compress<GA>(cv, m1, j, last ? lblen : BLOCK_LEN, last ? endf : 0u);
     }
   }
@@ -201,6 +214,10 @@ __device__ __forceinline__ void leaf_hash(const uint8_t* __restrict__ p, uint32_
     hash_chunk_ps<GA>(p, clen, j, root, cv);
   } else if constexpr (L == 9) {
     hash_chunk_pl<GA>(p, clen, j, root, cv);
+  } else if constexpr (L == 19) {  // 9 with non-temporal message loads (ablation)
+    hash_chunk_pl<GA, 1>(p, clen, j, root, cv);
+  } else if constexpr (L == 29) {  // 9 with the tail mask computed in its branch (ablation)
+    hash_chunk_pl<GA, 0, 1>(p, clen, j, root, cv);
   } else if constexpr (L == 4) {
     hash_chunk_pp<GA>(p, clen, j, root, cv);
   } else {
@@ -1216,6 +1233,9 @@ static const LeafVariant kLeafVariants[] = {
     ABL1(512, k_leaf_tree<512, 9, 1, 1, 2, 2>),   // 50: 49 keeping only the first slot's chunk (no spills)
     PROD1(512, k_leaf_tree<512, 109, 1, 1, 2, 2>),  // 51 (default): 50 with the asm G blocks (B3_G_ASM)
     PROD1(512, k_leaf_tree<512, 209, 1, 1, 2, 2>),  // 52: 51 with copy-free first column steps (compress<2>)
+    ABL1(512, k_leaf_tree<512, 119, 1, 1, 2, 2>),   // 53: 51 with non-temporal message loads (1.7x slower)
+    ABL1(512, k_leaf_tree<512, 129, 1, 1, 2, 2>),   // 54: 51 with the tail mask computed in its branch
+    ABL1(512, k_leaf_tree<512, 229, 1, 1, 2, 2>),   // 55: 52 with the same
 };
 #undef PROD
 #undef PROD1

@@ -169,7 +169,7 @@ def _exchange(send, send_counts, group, recv_counts=None):
 
 
 def identifier_dedup_distributed(stages, keys, has_key, status, ids, chunk_size=100,
-                                 existing_keys=None, existing_ids=None, group=None):
+                                 existing_keys=None, existing_ids=None, group=None, counts_on_device=False):
     """This rank's share of the identifier group-by.
 
     keys/has_key/status/ids: this rank's orphan file_paths (ids = their global
@@ -182,6 +182,12 @@ def identifier_dedup_distributed(stages, keys, has_key, status, ids, chunk_size=
     to the Object created by file j, -(e+1) = existing Object e, INT64_MIN =
     dropped); created/linked are the node-wide totals identifier_job_step
     would return summed over the job (mod.rs:349).
+
+    counts_on_device: in a world of one, return (link, counts) with counts an
+    int64[2] device tensor (created, linked) instead of two ints, so that the
+    call enqueues its work without waiting for it (a pipelined job reads the
+    counts when it writes its report). With an exchange the totals are read
+    on the host anyway (they carry the bucket overflow flag).
     """
     world = dist.get_world_size(group)
     # a world of one exchanges with itself: its records are already where
@@ -191,6 +197,8 @@ def identifier_dedup_distributed(stages, keys, has_key, status, ids, chunk_size=
     if world == 1 and hasattr(stages, "local"):
         stages.last_protocol = "local"
         link, cnt = stages.local(keys, has_key, status, ids, chunk_size, existing_keys, existing_ids)
+        if counts_on_device:
+            return link, cnt
         c = cnt.tolist()
         return link, int(c[0]), int(c[1])
     caps = getattr(stages, "bucket_caps", None)

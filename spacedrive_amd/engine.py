@@ -84,8 +84,8 @@ class Engine:
     progress report, job/worker.rs:458-480). cancel: optional
     ``ctypes.c_int32`` the caller may set nonzero from any thread to stop a
     path call (job/mod.rs:862-960); the call then raises ``Cancelled`` whose
-    ``partial`` holds the completed items. direct_io: file_checksum of files
-    over 1 MiB reads with O_DIRECT (cold storage).
+    ``partial`` holds the completed items. direct_io: the path calls
+    (generate_cas_ids, file_checksums) read with O_DIRECT (cold storage).
     """
 
     def __init__(self, device: int = 0, io_threads: int = 0, staging_bytes: int = 0, progress=None, cancel=None,
