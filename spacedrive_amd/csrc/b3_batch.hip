@@ -752,39 +752,67 @@ __global__ void __launch_bounds__(256) k_shape_hist(const uint64_t* __restrict__
   if (h[threadIdx.x]) atomicAdd(&counts[threadIdx.x], h[threadIdx.x]);
 }
 
+// Scatter in two steps so that the global writes are coalesced: the
+// workgroup's 4096 messages are first ordered by shape in LDS (2-byte local
+// indices), then written run by run — consecutive threads to consecutive
+// addresses of a bin's range. The second read of offs/lens (in LDS order) hits
+// the L2 lines the first read brought in.
 __global__ void __launch_bounds__(256) k_shape_scatter(const uint64_t* __restrict__ offs,
                                                        const uint64_t* __restrict__ lens, uint32_t n,
                                                        const uint32_t* __restrict__ counts,
                                                        uint32_t* __restrict__ cursor, uint32_t* __restrict__ perm,
                                                        uint64_t* __restrict__ soffs, uint64_t* __restrict__ slens) {
-  __shared__ uint32_t start[kShapeBins], h[kShapeBins], rank[kShapeBins];
+  __shared__ uint32_t gstart[kShapeBins], lstart[kShapeBins], h[kShapeBins];
+  __shared__ uint16_t order[kScatterPerWG];
+  __shared__ uint8_t keyof[kScatterPerWG];
   const uint32_t t = threadIdx.x;
   // exclusive scan of the global bin counts (256 entries, one per thread)
-  start[t] = counts[t];
+  gstart[t] = counts[t];
   h[t] = 0;
-  rank[t] = 0;
   __syncthreads();
   for (uint32_t d = 1; d < kShapeBins; d <<= 1) {
-    const uint32_t v = t >= d ? start[t - d] : 0u;
+    const uint32_t v = t >= d ? gstart[t - d] : 0u;
     __syncthreads();
-    start[t] += v;
+    gstart[t] += v;
     __syncthreads();
   }
-  const uint32_t excl = start[t] - counts[t];
+  const uint32_t excl = gstart[t] - counts[t];
   __syncthreads();
-  start[t] = excl;
-  const uint32_t lo = blockIdx.x * kScatterPerWG, hi = min(n, lo + kScatterPerWG);
-  for (uint32_t i = lo + t; i < hi; i += 256) atomicAdd(&h[shape_key(lens[i])], 1u);
+  gstart[t] = excl;
+  const uint32_t lo = blockIdx.x * kScatterPerWG, hi = min(n, lo + kScatterPerWG), m = hi - lo;
+  for (uint32_t k = t; k < m; k += 256) {
+    const uint32_t key = shape_key(lens[lo + k]);
+    keyof[k] = (uint8_t)key;
+    atomicAdd(&h[key], 1u);
+  }
   __syncthreads();
-  if (h[t]) start[t] += atomicAdd(&cursor[t], h[t]);  // this workgroup's range in bin t
+  // this workgroup's range in bin t, and the bin's start in the local order
+  const uint32_t cnt = h[t];
+  if (cnt) gstart[t] += atomicAdd(&cursor[t], cnt);
+  lstart[t] = cnt;
   __syncthreads();
-  for (uint32_t i = lo + t; i < hi; i += 256) {
-    const uint64_t L = lens[i];
-    const uint32_t k = shape_key(L);
-    const uint32_t pos = start[k] + atomicAdd(&rank[k], 1u);
+  for (uint32_t d = 1; d < kShapeBins; d <<= 1) {
+    const uint32_t v = t >= d ? lstart[t - d] : 0u;
+    __syncthreads();
+    lstart[t] += v;
+    __syncthreads();
+  }
+  lstart[t] -= cnt;  // exclusive
+  h[t] = 0;          // becomes the per-bin fill cursor
+  __syncthreads();
+  for (uint32_t k = t; k < m; k += 256) {
+    const uint32_t key = keyof[k];
+    order[lstart[key] + atomicAdd(&h[key], 1u)] = (uint16_t)k;
+  }
+  __syncthreads();
+  for (uint32_t p = t; p < m; p += 256) {
+    const uint32_t k = order[p];
+    const uint32_t key = keyof[k];
+    const uint32_t pos = gstart[key] + (p - lstart[key]);
+    const uint32_t i = lo + k;
     perm[pos] = i;
     soffs[pos] = offs[i];
-    slens[pos] = L;
+    slens[pos] = lens[i];
   }
 }
 
