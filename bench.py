@@ -683,11 +683,12 @@ def main():
             "frac_of_isa_peak": valu_rate / VALU_PEAK_ISA if valu_rate else None,
             "roof_compressions_per_s_measured": VALU_ROOF_MEASURED,
             "frac_of_measured_roof": valu_rate / VALU_ROOF_MEASURED if valu_rate else None,
-            "note": "BLAKE3 is integer ARX (no MFMA): the kernel is VALU-bound, not HBM-bound. spec peak = "
-                    "680 ops/compression as if every op issued at the full VALU lane rate; isa peak = the "
-                    "same 680 instructions at their measured issue cost on gfx950 (VOP3 v_alignbit/v_add3 "
-                    "4 cycles per wave64, VOP2 2 cycles) at the spec 2.4 GHz; measured roof = register-only "
-                    "compression loop (tools/ubench_compress.hip)",
+            "note": "BLAKE3 is integer ARX (no MFMA): the kernel is VALU-bound (and power-held: it runs at "
+                    "~1.9 GHz), not HBM-bound. spec peak = 680 ops/compression as if every op issued at the "
+                    "full VALU lane rate at 2.4 GHz; isa peak = round 1's issue model of the same 680 "
+                    "instructions (VOP3 4 cycles, VOP2 2 cycles per wave64) at 2.4 GHz, an upper bound; "
+                    "measured roof = the best register-only compression loop (asm G blocks, "
+                    "tools/ubench_compress.hip, 67 G/s)",
         },
     }
     if traffic:
