@@ -105,6 +105,7 @@ struct sdcas_ctx {
   std::string err;
   std::mutex mu;
   uint32_t io_threads = 8;
+  static constexpr uint32_t kMaxIoThreads = 256;
   std::unique_ptr<sdcas_io::WorkerPool> pool;  // io_threads readers (the calling thread is one)
   uint64_t staging_bytes = 256ull << 20;
   bool direct_io = false;  // SDCAS_OPT_DIRECT_IO: big-file checksum reads bypass the page cache
@@ -531,14 +532,13 @@ int sdcas_init(const sdcas_options* opts, sdcas_ctx** out) {
   int dev = -1;
   if (opts) {
     dev = opts->device;
-    if (opts->io_threads) c->io_threads = opts->io_threads;
+    if (opts->io_threads) c->io_threads = std::min<uint32_t>(opts->io_threads, sdcas_ctx::kMaxIoThreads);
     if (opts->staging_bytes) c->staging_bytes = std::max<uint64_t>(opts->staging_bytes, 1ull << 20);
     c->direct_io = (opts->flags & SDCAS_OPT_DIRECT_IO) != 0;
     c->progress = opts->progress;
     c->progress_user = opts->progress_user;
     c->cancel = opts->cancel;
   }
-  c->pool.reset(new sdcas_io::WorkerPool(c->io_threads));
   if (dev < 0) (void)hipGetDevice(&dev);
   if (dev >= count) {
     delete c;
@@ -716,6 +716,9 @@ struct PathCall {
   int rc = SDCAS_OK;
   explicit PathCall(sdcas_ctx* cc) : c(cc), g(cc->mu) {
     (void)hipSetDevice(c->device);
+    // the readers start with the context's first path call (a context used
+    // only for device-resident batches never creates them)
+    if (!c->pool) c->pool.reset(new sdcas_io::WorkerPool(c->io_threads));
     hipError_t e = c->fence_in(c->stream);
     if (e) rc = c->hip_fail(e, "stream wait");
   }
