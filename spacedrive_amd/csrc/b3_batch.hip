@@ -225,7 +225,7 @@ __device__ __forceinline__ void leaf_hash(const uint8_t* __restrict__ p, uint32_
     if constexpr (PF == 6) hash_chunk_pf2(p, clen, j, root, cv);
     else if constexpr (PF == 7) hash_chunk_pair(p, clen, j, root, cv);
     else if constexpr (PF == 5) hash_chunk_pf<true>(p, clen, j, root, cv);
-    else if constexpr (PF >= 2) hash_chunk_diag(p, clen, j, root, cv, PF);
+    else if constexpr (L == 2 || L == 3) hash_chunk_diag<GA>(p, clen, j, root, cv, L);
     else if constexpr (PF == 1) hash_chunk_pf(p, clen, j, root, cv);
     else hash_chunk(p, clen, j, root, cv);
 #else
@@ -1280,6 +1280,7 @@ static const LeafVariant kLeafVariants[] = {
     ABL1(512, k_leaf_tree<512, 119, 1, 1, 2, 2>),   // 53: 51 with non-temporal message loads (1.7x slower)
     ABL1(512, k_leaf_tree<512, 129, 1, 1, 2, 2>),   // 54: 51 with the tail mask computed in its branch
     ABL1(512, k_leaf_tree<512, 229, 1, 1, 2, 2>),   // 55: 52 with the same
+    ABL1(512, k_leaf_tree<512, 102, 1, 1, 2, 2>),   // 56 DIAGNOSTIC (wrong digests): 51's compression, no memory reads
 };
 #undef PROD
 #undef PROD1
