@@ -263,12 +263,17 @@ def test_rccl_world1(eng, oracle):
     store = dist.HashStore()
     dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=torch.device("cuda", 0))
     try:
-        link, c, l = identifier_dedup_distributed(DeviceStages(eng), k, h, s, ids, 100, ek, eids)
+        stages = DeviceStages(eng)
+        link, c, l = identifier_dedup_distributed(stages, k, h, s, ids, 100, ek, eids)
+        # the same with the counts left on the device (no host wait in the call)
+        link2, cnt = identifier_dedup_distributed(stages, k, h, s, ids, 100, ek, eids, counts_on_device=True)
     finally:
         dist.destroy_process_group()
     want, wc, wl = oracle.identifier_dedup(keys, has, status, 100, existing)
     assert np.array_equal(link.cpu().numpy(), want)
     assert (c, l) == (wc, wl)
+    assert cnt.is_cuda and cnt.tolist() == [wc, wl]
+    assert np.array_equal(link2.cpu().numpy(), want)
 
 
 @pytest.mark.gpu
