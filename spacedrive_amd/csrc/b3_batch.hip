@@ -156,7 +156,7 @@ __device__ __forceinline__ void hash_chunk_ps(const uint8_t* __restrict__ p, uin
 // flags are constants selected by one compare, the tail mask runs only on
 // the last block, the second half of a line is loaded only if the chunk has
 // it (no clamped address), and the block pointer advances by one add.
-template <int GA = 0, int NT = 0, int LM = 0>
+template <int GA = 0, int NT = 0, int LM = 0, uint32_t BS = BLOCK_LEN>
 __device__ __forceinline__ void hash_chunk_pl(const uint8_t* __restrict__ p, uint32_t clen, uint64_t j, bool root,
                                               uint32_t (&cv)[8]) {
   set_iv(cv);
@@ -166,14 +166,14 @@ __device__ __forceinline__ void hash_chunk_pl(const uint8_t* __restrict__ p, uin
   uint32_t m0[16], m1[16];
   const uint8_t* q = p;
 #pragma unroll 1
-  for (uint32_t b = 0; b <= lb; b += 2, q += 2 * BLOCK_LEN) {
+  for (uint32_t b = 0; b <= lb; b += 2, q += 2 * BS) {
     const bool two = b + 1 <= lb;
     if constexpr (NT) {
       load_full_block_nt(q, m0);
-      if (two) load_full_block_nt(q + BLOCK_LEN, m1);
+      if (two) load_full_block_nt(q + BS, m1);
     } else {
       load_full_block(q, m0);
-      if (two) load_full_block(q + BLOCK_LEN, m1);
+      if (two) load_full_block(q + BS, m1);
     }
     {
       const bool last = b == lb;
@@ -212,12 +212,25 @@ __device__ __forceinline__ void leaf_hash(const uint8_t* __restrict__ p, uint32_
   constexpr int L = PF % 100, GA = kGA<PF>;
   if constexpr (L == 8) {
     hash_chunk_ps<GA>(p, clen, j, root, cv);
-  } else if constexpr (L == 9) {
+  } else if constexpr (L == 9 || L == 49) {
     hash_chunk_pl<GA>(p, clen, j, root, cv);
   } else if constexpr (L == 19) {  // 9 with non-temporal message loads (ablation)
     hash_chunk_pl<GA, 1>(p, clen, j, root, cv);
   } else if constexpr (L == 29) {  // 9 with the tail mask computed in its branch (ablation)
     hash_chunk_pl<GA, 0, 1>(p, clen, j, root, cv);
+  } else if constexpr (L == 39) {
+    // DIAGNOSTIC (wrong digests): the same loop reading a wave-transposed
+    // image of the wave's 64 KiB — lane l reads block b at wave base + b * 4 KiB
+    // + l * 64, so each load instruction of the wave covers 4 KiB of
+    // contiguous bytes instead of 64 lines 1 KiB apart (DRAM row locality);
+    // the same bytes and compressions as 51 (needs 64 KiB of readable bytes
+    // past the wave's first chunk: tools/ab_leaf.py pads the blob)
+    const uint64_t pa = (uint64_t)p;
+    // (readfirstlane returns int: through uint32_t, or the low word sign-extends)
+    const uint64_t w0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(pa >> 32)) << 32) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)pa);
+    hash_chunk_pl<GA, 0, 0, 64 * BLOCK_LEN>(reinterpret_cast<const uint8_t*>(w0 + 64ull * __lane_id()), clen, j,
+                                            root, cv);
   } else if constexpr (L == 4) {
     hash_chunk_pp<GA>(p, clen, j, root, cv);
   } else {
@@ -232,6 +245,15 @@ __device__ __forceinline__ void leaf_hash(const uint8_t* __restrict__ p, uint32_
     static_assert(L == 8 || L == 9 || L == 4, "ablation block loops need -DSDCAS_ABLATIONS");
 #endif
   }
+}
+
+// DIAGNOSTIC loop 49 (wrong digests): loop 9 with every chunk's address
+// folded into the blob's first 2 MiB, which stay L2-resident — the same
+// loads, compressions and tree as 51 without HBM traffic
+template <int PF>
+__device__ __forceinline__ const uint8_t* leaf_ptr(const uint8_t* blob, const uint8_t* p) {
+  if constexpr (PF % 100 == 49) return blob + ((uint64_t)(p - blob) & ((2ull << 20) - 1));
+  return p;
 }
 
 __device__ __forceinline__ void store_digest(uint32_t m, const uint32_t (&d)[8], uint8_t* out32, uint64_t* out_keys) {
@@ -460,7 +482,7 @@ __global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __
       for (uint32_t r = 0; r < (CA == 1 ? R : 1); ++r) {
         if (!c_ok[r]) continue;
         uint32_t cv[8];
-        leaf_hash<PF>(c_p[r], c_clen[r], c_j[r], c_root[r], cv);
+        leaf_hash<PF>(leaf_ptr<PF>(blob, c_p[r]), c_clen[r], c_j[r], c_root[r], cv);
         if (c_root[r]) {
           store_digest(perm ? perm[c_m[r]] : c_m[r], cv, out32, out_keys);
         } else {
@@ -484,7 +506,7 @@ __global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __
       const uint32_t clen = len == 0 ? 0u : (uint32_t)min<uint64_t>(CHUNK_LEN, len - j * CHUNK_LEN);
       const bool root = (C == 1);
       uint32_t cv[8];
-      leaf_hash<PF>(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
+      leaf_hash<PF>(leaf_ptr<PF>(blob, blob + offs[m] + j * CHUNK_LEN), clen, j, root, cv);
       if (root) {
         store_digest(perm ? perm[m] : m, cv, out32, out_keys);
       } else {
@@ -1281,6 +1303,8 @@ static const LeafVariant kLeafVariants[] = {
     ABL1(512, k_leaf_tree<512, 129, 1, 1, 2, 2>),   // 54: 51 with the tail mask computed in its branch
     ABL1(512, k_leaf_tree<512, 229, 1, 1, 2, 2>),   // 55: 52 with the same
     ABL1(512, k_leaf_tree<512, 102, 1, 1, 2, 2>),   // 56 DIAGNOSTIC (wrong digests): 51's compression, no memory reads
+    ABL1(512, k_leaf_tree<512, 139, 1, 1, 2, 2>),   // 57 DIAGNOSTIC (wrong digests): 51 reading a wave-transposed image
+    ABL1(512, k_leaf_tree<512, 149, 1, 1, 2, 2>),   // 58 DIAGNOSTIC (wrong digests): 51 reading an L2-resident 2 MiB
 };
 #undef PROD
 #undef PROD1

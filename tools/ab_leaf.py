@@ -41,7 +41,7 @@ def main():
     padded = (lens + A - np.uint64(1)) // A * A
     offs = np.zeros(n, np.uint64)
     offs[1:] = np.cumsum(padded[:-1])
-    total = int(offs[-1] + padded[-1]) + 64
+    total = int(offs[-1] + padded[-1]) + 64 + (1 << 17)  # + 128 KiB: diagnostic 57 reads 64 KiB past a wave base
     chunks = int(np.maximum(np.uint64(1), (lens + np.uint64(1023)) // np.uint64(1024)).sum())
     eng = Engine()
     t = lambda x: torch.from_numpy(np.ascontiguousarray(x).view(np.int64)).to(dev)
