@@ -34,7 +34,8 @@ identifier job's CPU shape over real files, 100-file steps in series with
 cas.rs's reads, on a 200 k-file subset), e2e (c2, rank 0, N=1: the host-facing
 C ABI from a pinned host buffer and from files, timed outside the on-device
 loop; never `value`), parity.dedup (c3/c5 at N=1: every link and both counts
-against the chunked oracle).
+against the chunked oracle); at N > 1, parity = a sample of about 2000 files
+per rank against the oracle, summed over the ranks.
 """
 import argparse
 import ctypes
@@ -117,6 +118,14 @@ def max_over_ranks(torch, dist, dev, vals):
     t = torch.tensor(vals, dtype=torch.float64, device=dev if on_dev else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return [float(x) for x in t.tolist()]
+
+
+def sum_over_ranks(torch, dist, dev, vals):
+    """element-wise sum of a few integers over all ranks"""
+    on_dev = dist.get_backend() == "nccl"
+    t = torch.tensor(vals, dtype=torch.int64, device=dev if on_dev else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [int(x) for x in t.tolist()]
 
 
 def compressions(lens):
@@ -517,6 +526,14 @@ def run_c4(args, torch, dist, dev, rank, world, distributed, out_f):
                                           f"C4 files {pick[0]}..{pick[-1]} ({len(pick)} files)")
         out["cpu_baseline"] = base
         out["parity"]["cpu_baseline_sample"] = parity
+    elif distributed:
+        # every rank checks a sample of its own files against the oracle (the
+        # full checks above need the whole corpus on one host: N = 1 only)
+        gk = d_out.cpu().numpy().view(np.uint64)
+        p = sample_parity(gk, sizes, keys, 2000, seed=1 + rank)
+        checked, bad = sum_over_ranks(torch, dist, dev, [p["checked_files"], p["mismatches"]])
+        out["parity"] = {"checked_files": checked, "mismatches": bad, "ranks": world,
+                         "sample": "about 2000 files per rank (incl. sampled-branch files)", "oracle": p["oracle"]}
     if rank == 0:
         emit(out_f, out)
     eng.close()

@@ -109,10 +109,6 @@ __global__ void k_dd_starts(const uint64_t* __restrict__ rec, const uint32_t* __
   starts[r] = r == world ? U : lo;
 }
 
-
-
-
-
 __global__ void k_dd_apply(const uint64_t* __restrict__ ids, const uint32_t* __restrict__ slot, uint32_t n,
                            const int64_t* __restrict__ result, uint64_t cs, int64_t* __restrict__ link,
                            unsigned long long* __restrict__ counts) {
@@ -174,7 +170,6 @@ hipError_t ensure_n(DistWs& w, uint32_t n) {
     return e;
   return ensure_temp(w, n);
 }
-
 
 }  // namespace
 
