@@ -128,6 +128,14 @@ def sum_over_ranks(torch, dist, dev, vals):
     return [int(x) for x in t.tolist()]
 
 
+def digest_keys(dig):
+    """first 8 bytes of each 32-byte digest, big-endian (the oracle's key)"""
+    gk = np.zeros(dig.shape[0], np.uint64)
+    for b in range(8):
+        gk = (gk << np.uint64(8)) | dig[:, b].astype(np.uint64)
+    return gk
+
+
 def compressions(lens):
     n = lens.astype(np.int64)
     C = np.maximum(1, (n + 1023) // 1024)
@@ -518,22 +526,24 @@ def run_c4(args, torch, dist, dev, rank, world, distributed, out_f):
                 break
             pick.append(f)
             acc += int(sizes[f])
-        dig = out32.cpu().numpy()[[local[f] for f in pick]]
-        gk = np.zeros(len(pick), np.uint64)
-        for b in range(8):  # digest bytes 0..7 big-endian = the oracle's key
-            gk = (gk << np.uint64(8)) | dig[:, b].astype(np.uint64)
+        gk = digest_keys(out32.cpu().numpy()[[local[f] for f in pick]])
         base, parity = cpu_baseline_files(gk, sizes[pick], ckeys[pick], 1, args.cpu_threads,
                                           f"C4 files {pick[0]}..{pick[-1]} ({len(pick)} files)")
         out["cpu_baseline"] = base
         out["parity"]["cpu_baseline_sample"] = parity
     elif distributed:
-        # every rank checks a sample of its own files against the oracle (the
-        # full checks above need the whole corpus on one host: N = 1 only)
-        gk = d_out.cpu().numpy().view(np.uint64)
-        p = sample_parity(gk, sizes, keys, 2000, seed=1 + rank)
-        checked, bad = sum_over_ranks(torch, dist, dev, [p["checked_files"], p["mismatches"]])
-        out["parity"] = {"checked_files": checked, "mismatches": bad, "ranks": world,
-                         "sample": "about 2000 files per rank (incl. sampled-branch files)", "oracle": p["oracle"]}
+        # every rank checks the smallest file it holds a digest of (with the
+        # piece split: every file, through the all-reduce) against the oracle
+        cand = list(range(sizes.size)) if split == "pieces" else list(mine)
+        checked = bad = 0
+        if cand:
+            f = min(cand, key=lambda x: int(sizes[x]))
+            gk = digest_keys(out32.cpu().numpy()[[local[f]]])
+            _, p = cpu_baseline_files(gk, sizes[[f]], ckeys[[f]], 1, 4, f"C4 file {f}")
+            checked, bad = 1, (p["mismatches"] if p else 1)
+        checked, bad = sum_over_ranks(torch, dist, dev, [checked, bad])
+        out["parity"].update({"checked_files": checked, "mismatches": bad, "ranks": world,
+                              "sample": "each rank: its smallest file, whole-file checksum vs the oracle"})
     if rank == 0:
         emit(out_f, out)
     eng.close()
@@ -764,6 +774,14 @@ def main():
             out["e2e"] = e2e_c2(args, eng, torch, dev, d_blob, offs, lens, sizes, gk)
             if "cpu_baseline" in out and out["e2e"].get("reference_faithful"):
                 out["cpu_baseline"]["reference_faithful"] = out["e2e"].pop("reference_faithful")
+    elif distributed:
+        # every rank checks a sample of its own files against the oracle (the
+        # full checks above need the whole corpus on one host: N = 1 only)
+        gk = d_out.cpu().numpy().view(np.uint64)
+        p = sample_parity(gk, sizes, keys, 2000, seed=1 + rank)
+        checked, bad = sum_over_ranks(torch, dist, dev, [p["checked_files"], p["mismatches"]])
+        out["parity"] = {"checked_files": checked, "mismatches": bad, "ranks": world,
+                         "sample": "about 2000 files per rank (incl. sampled-branch files)", "oracle": p["oracle"]}
     if rank == 0:
         emit(out_f, out)
     eng.close()

@@ -236,3 +236,28 @@ def test_split_checksum_two_processes(oracle):
     for got in outs:
         for i, (k, n) in enumerate(zip(_split_keys(), SPLIT_SIZES)):
             assert bytes(got[i]).hex() == oracle.synth_checksum(k, n), n
+
+
+@pytest.mark.parametrize("workload", ["c2", "c5", "c4"])
+def test_bench_two_ranks(workload):
+    """bench.py as the driver launches it at N > 1 (torch.distributed.run, one
+    process per rank), on the one GPU with gloo standing in for RCCL: the line
+    reports both ranks, every rank's oracle sample matches, and the c5 dedup
+    exchange completes"""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, SDCAS_BENCH_BACKEND="gloo", OMP_NUM_THREADS="4")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+           "--workload", workload, "--files", "20000", "--steps", "2", "--warmup", "1", "--c4-total-gib", "4"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if '{"metric"' in l][-1]
+    d = json.loads(line[line.index('{"metric"'):])  # torchrun may prefix a rank tag
+    assert d["n_gpus"] == 2 and d["value"] > 0
+    assert d["parity"]["ranks"] == 2 and d["parity"]["checked_files"] >= (2 if workload == "c4" else 2000)
+    assert d["parity"]["mismatches"] == 0
+    if workload == "c5":
+        assert d["dedup"]["records_per_gpu"] == 20000
