@@ -419,3 +419,32 @@ def test_concurrent_contexts_and_shared_context(oracle):
             e.close()
     assert not errs, errs
     assert got == want
+
+
+def test_mid_size_batches_cut_into_slots(oracle, tmp_path):
+    """a call of a few slots' worth runs as several alternating slots (the
+    reads of one overlap the GPU's work on the other): 500 files (~25 MB)
+    through the default 256 MiB staging, every cas_id and checksum exact, a
+    1000-byte message batch through the pinned-buffer path likewise"""
+    from spacedrive_amd import Engine
+    rng = np.random.default_rng(17)
+    paths, sizes = [], []
+    for i in range(500):
+        n = int(rng.integers(1, 102400 + 1))
+        p = tmp_path / f"m{i}"
+        p.write_bytes(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+        paths.append(str(p))
+        sizes.append(n)
+    with Engine() as e:
+        keys, st = e.generate_cas_ids(paths, sizes)
+        assert (st == 0).all()
+        for i in range(len(paths)):
+            assert f"{int(keys[i]):016x}" == oracle.generate_cas_id(paths[i], sizes[i]), i
+        d32, st = e.file_checksums(paths[:300])
+        assert (st == 0).all()
+        for i in range(300):
+            assert bytes(d32[i]).hex() == oracle.file_checksum(paths[i]), i
+        msgs = [rng.integers(0, 256, int(rng.integers(0, 90000)), dtype=np.uint8).tobytes() for _ in range(600)]
+        out = e.hash_messages(*e.pack(msgs))
+        for m, d in zip(msgs, out):
+            assert bytes(d).hex() == oracle.hash(m)
