@@ -86,6 +86,7 @@ struct Slot {
   DevBuf<uint64_t> d_meta;  // offs | lens (or piece descriptors)
   DevBuf<uint8_t> d_res;
   hipEvent_t ev = nullptr;
+  hipEvent_t h2d = nullptr;  // the slot's uploads done (on the copy stream)
   bool busy = false, res32 = false;
   size_t n = 0;
   uint64_t used = 0, chunks = 0;
@@ -102,6 +103,7 @@ struct Slot {
 struct sdcas_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t copy_stream = nullptr;  // staging slots' host-to-device copies
   std::string err;
   std::mutex mu;
   uint32_t io_threads = 8;
@@ -287,6 +289,7 @@ int slot_prepare(sdcas_ctx* c, Slot& s, uint64_t bytes, size_t n) {
   if ((e = s.d_blob.ensure(s.h_cap)) || (e = s.d_meta.ensure(2 * s.cap_n)) || (e = s.d_res.ensure(32 * s.cap_n)))
     return c->hip_fail(e, "device staging");
   if (!s.ev && (e = hipEventCreateWithFlags(&s.ev, hipEventDisableTiming))) return c->hip_fail(e, "event");
+  if (!s.h2d && (e = hipEventCreateWithFlags(&s.h2d, hipEventDisableTiming))) return c->hip_fail(e, "event");
   return SDCAS_OK;
 }
 
@@ -300,7 +303,8 @@ void slot_release(Slot& s) {
   s.d_meta.release();
   s.d_res.release();
   if (s.ev) (void)hipEventDestroy(s.ev);
-  s.ev = nullptr;
+  if (s.h2d) (void)hipEventDestroy(s.h2d);
+  s.ev = s.h2d = nullptr;
 }
 
 // Both slots sized for `cap` staging bytes, and the kernel workspace for the
@@ -319,6 +323,19 @@ int slots_prepare(sdcas_ctx* c, uint64_t cap, size_t cap_n) {
   return SDCAS_OK;
 }
 
+// A slot's host-to-device copies run on the context's copy stream, so that
+// they overlap the other slot's kernels on the compute stream (PCIe and the
+// CUs work at once: the path calls are bound by the copy); the compute stream
+// waits for them before this slot's kernels. Refilling a slot waits for its
+// previous batch on the host first (slot_complete), so a copy never lands
+// under kernels still reading the slot.
+template <class Copies>
+hipError_t slot_upload(sdcas_ctx* c, Slot& s, Copies copies) {
+  hipError_t e;
+  if ((e = copies(c->copy_stream)) || (e = hipEventRecord(s.h2d, c->copy_stream))) return e;
+  return hipStreamWaitEvent(c->stream, s.h2d, 0);
+}
+
 // Enqueue the slot's batch: s.n messages at s.offs()/s.lens() in s.h (s.used
 // bytes, s.chunks chunks); results land in s.res() (digests if res32, else
 // cas keys) once s.ev has fired.
@@ -335,9 +352,13 @@ int slot_submit(sdcas_ctx* c, Slot& s, bool res32) {
     if ((rc = reserve_ws(c, std::max<size_t>(s.n, c->ws.cap_msgs), std::max<uint64_t>(s.chunks, c->ws.cap_chunks))))
       return rc;
   }
-  if ((e = hipMemcpyAsync(s.d_blob.p, s.src ? s.src : s.h, s.used, hipMemcpyHostToDevice, st)) ||
-      (e = hipMemcpyAsync(s.d_meta.p, s.hm, 8 * s.n, hipMemcpyHostToDevice, st)) ||
-      (e = hipMemcpyAsync(s.d_meta.p + s.cap_n, s.hm + s.cap_n, 8 * s.n, hipMemcpyHostToDevice, st)))
+  if ((e = slot_upload(c, s, [&](hipStream_t cs) {
+         hipError_t r;
+         if ((r = hipMemcpyAsync(s.d_blob.p, s.src ? s.src : s.h, s.used, hipMemcpyHostToDevice, cs)) ||
+             (r = hipMemcpyAsync(s.d_meta.p, s.hm, 8 * s.n, hipMemcpyHostToDevice, cs)))
+           return r;
+         return hipMemcpyAsync(s.d_meta.p + s.cap_n, s.hm + s.cap_n, 8 * s.n, hipMemcpyHostToDevice, cs);
+       })))
     return c->hip_fail(e, "H2D");
   if ((rc = launch_batch(c, s.d_blob.p, s.d_meta.p, s.d_meta.p + s.cap_n, (uint32_t)s.n, res32 ? s.d_res.p : nullptr,
                          res32 ? nullptr : reinterpret_cast<uint64_t*>(s.d_res.p), st)))
@@ -453,8 +474,10 @@ int run_big(sdcas_ctx* c, const std::vector<BigItem>& items, uint8_t* out32_host
     }
     PieceDesc* dp = reinterpret_cast<PieceDesc*>(s.d_meta.p);
     hipError_t ee;
-    if ((ee = hipMemcpyAsync(s.d_blob.p, s.h, used, hipMemcpyHostToDevice, st)) ||
-        (ee = hipMemcpyAsync(dp, hp, sizeof(PieceDesc) * jobs.size(), hipMemcpyHostToDevice, st)))
+    if ((ee = slot_upload(c, s, [&](hipStream_t cs) {
+           hipError_t r = hipMemcpyAsync(s.d_blob.p, s.h, used, hipMemcpyHostToDevice, cs);
+           return r ? r : hipMemcpyAsync(dp, hp, sizeof(PieceDesc) * jobs.size(), hipMemcpyHostToDevice, cs);
+         })))
       return c->hip_fail(ee, "H2D pieces");
     if ((ee = piece_hash(s.d_blob.p, dp, (uint32_t)jobs.size(), c->d_file_nodes.p, c->piece_ctr.p, c->piece_variant,
                          st)))
@@ -545,7 +568,9 @@ int sdcas_init(const sdcas_options* opts, sdcas_ctx** out) {
     return SDCAS_E_NO_DEVICE;
   }
   c->device = dev;
-  if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess) {
+    if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return SDCAS_E_NO_DEVICE;
   }
@@ -557,6 +582,7 @@ void sdcas_destroy(sdcas_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
   if (c->scratch_ev) (void)hipEventSynchronize(c->scratch_ev);
   for (auto* b : {&c->ws_S, &c->ws_total, &c->ws_soffs, &c->ws_slens, &c->dd_keys, &c->dd_ekeys, &c->dd_ids})
     b->release();
@@ -577,6 +603,7 @@ void sdcas_destroy(sdcas_ctx* c) {
   for (auto& p : c->ev_all) (void)hipEventDestroy(p.first), (void)hipEventDestroy(p.second);
   if (c->scratch_ev) (void)hipEventDestroy(c->scratch_ev);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   delete c;
 }
 
