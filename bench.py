@@ -500,6 +500,8 @@ def run_c4(args, torch, dist, dev, rank, world, distributed, out_f):
             "achieved": my_bytes * args.steps / (hash_s) / 1e9 if hash_s > 0 else None, "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "traffic": None, "algorithmic_bytes_per_launch": my_bytes,
             "valu": {"compressions_per_s_node": comp / hash_s,
+                     "peak_compressions_per_s_spec": VALU_PEAK_OPS / OPS_PER_COMPRESSION,
+                     "frac_of_spec_per_gpu": comp / hash_s / world / (VALU_PEAK_OPS / OPS_PER_COMPRESSION),
                      "peak_compressions_per_s_isa": VALU_PEAK_ISA,
                      "frac_of_isa_peak_per_gpu": comp / hash_s / world / VALU_PEAK_ISA,
                      "roof_compressions_per_s_measured": VALU_ROOF_MEASURED,
@@ -745,7 +747,8 @@ def main():
             dd["last"] = last
         _, created, linked = last
         out["dedup"] = {"ms_per_step": ms, "ms_median": med, "objects_created": created, "files_linked": linked,
-                        "records_per_gpu": n, "timing": "HIP events around the dedup stages, inside the step"}
+                        "records_per_gpu": n, "protocol": getattr(stages, "last_protocol", None),
+                        "timing": "HIP events around the dedup stages, inside the step"}
     if rank == 0 and world == 1:
         gk = d_out.cpu().numpy().view(np.uint64)
         if args.workload == "c2" and not args.no_cpu_baseline:
@@ -782,6 +785,24 @@ def main():
         checked, bad = sum_over_ranks(torch, dist, dev, [p["checked_files"], p["mismatches"]])
         out["parity"] = {"checked_files": checked, "mismatches": bad, "ranks": world,
                          "sample": "about 2000 files per rank (incl. sampled-branch files)", "oracle": p["oracle"]}
+        if dd is not None:
+            # the exchange's result over the whole job: every rank's keys and
+            # links (global ordinals rank * n + i) to rank 0, checked against
+            # the chunked oracle over the concatenated corpus
+            on_dev = dist.get_backend() == "nccl"
+            loc = lambda t: t if on_dev else t.cpu()
+            parts = [loc(torch.empty(2 * n, dtype=torch.int64, device=dev)) for _ in range(world)]
+            dist.all_gather(parts, loc(torch.cat([d_out, dd["last"][0]])))
+            if rank == 0:
+                from tests._oracle import load_oracle
+                allk = np.concatenate([x.cpu().numpy()[:n] for x in parts]).view(np.uint64)
+                alll = np.concatenate([x.cpu().numpy()[n:] for x in parts])
+                has = np.concatenate([(files_of(args.workload, r, n)[0] != 0) for r in range(world)]).astype(np.uint8)
+                want, wc, wl = load_oracle().identifier_dedup(allk, has, None, 100)
+                out["parity"]["dedup"] = {"files": int(alll.size), "link_mismatches": int((alll != want).sum()),
+                                          "counts_match": (wc, wl) == (dd["last"][1], dd["last"][2]),
+                                          "oracle": "chunked restatement of file_identifier/mod.rs:149-254 over "
+                                                    "all ranks' files (oracle/cas_ref.c)"}
     if rank == 0:
         emit(out_f, out)
     eng.close()

@@ -243,7 +243,7 @@ def test_bench_two_ranks(workload):
     """bench.py as the driver launches it at N > 1 (torch.distributed.run, one
     process per rank), on the one GPU with gloo standing in for RCCL: the line
     reports both ranks, every rank's oracle sample matches, and the c5 dedup
-    exchange completes"""
+    exchange gives the chunked oracle's links over both ranks' files"""
     import json
     import subprocess
     import sys
@@ -261,3 +261,5 @@ def test_bench_two_ranks(workload):
     assert d["parity"]["mismatches"] == 0
     if workload == "c5":
         assert d["dedup"]["records_per_gpu"] == 20000
+        pd = d["parity"]["dedup"]  # both ranks' links against the oracle over the whole corpus
+        assert pd["files"] == 40000 and pd["link_mismatches"] == 0 and pd["counts_match"]

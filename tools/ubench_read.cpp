@@ -104,6 +104,9 @@ int main(int argc, char** argv) {
     sizes[i] = (uint64_t)sb.st_size;
     total += sizes[i];
   }
+  // UB_NOATIME=1: open with O_NOATIME (no access-time update on read; the
+  // caller must own the files)
+  const int extra_flags = getenv("UB_NOATIME") ? O_NOATIME : 0;
   // (a) open + pread + close
   for (int r = 0; r < reps; ++r) {
     std::atomic<uint64_t> got{0};
@@ -114,7 +117,7 @@ int main(int argc, char** argv) {
         std::vector<char> buf(1 << 20);
         uint64_t g = 0;
         for (int i = t; i < n; i += T) {
-          int fd = open(paths[i].c_str(), O_RDONLY | O_CLOEXEC);
+          int fd = open(paths[i].c_str(), O_RDONLY | O_CLOEXEC | extra_flags);
           if (fd < 0) continue;
           ssize_t k = pread(fd, buf.data(), sizes[i] + 1, 0);
           if (k > 0) g += (uint64_t)k;
