@@ -1297,8 +1297,8 @@ static const LeafVariant kLeafVariants[] = {
     ABL(512, k_leaf_tree<512, 9, 1, 1, 1, 1>),    // 48: 47 with the leaf's chunk kept in registers from phase 1
     ABL1(512, k_leaf_tree<512, 9, 1, 1, 2, 1>),   // 49: 46 with the same
     ABL1(512, k_leaf_tree<512, 9, 1, 1, 2, 2>),   // 50: 49 keeping only the first slot's chunk (no spills)
-    PROD1(512, k_leaf_tree<512, 109, 1, 1, 2, 2>),  // 51 (default): 50 with the asm G blocks (B3_G_ASM)
-    PROD1(512, k_leaf_tree<512, 209, 1, 1, 2, 2>),  // 52: 51 with copy-free first column steps (compress<2>)
+    PROD1(512, k_leaf_tree<512, 109, 1, 1, 2, 2>),  // 51: 50 with the asm G blocks (B3_G_ASM)
+    PROD1(512, k_leaf_tree<512, 209, 1, 1, 2, 2>),  // 52 (default): 51 with copy-free first column steps (compress<2>)
     ABL1(512, k_leaf_tree<512, 119, 1, 1, 2, 2>),   // 53: 51 with non-temporal message loads (1.7x slower)
     ABL1(512, k_leaf_tree<512, 129, 1, 1, 2, 2>),   // 54: 51 with the tail mask computed in its branch
     ABL1(512, k_leaf_tree<512, 229, 1, 1, 2, 2>),   // 55: 52 with the same
@@ -1313,7 +1313,7 @@ static const LeafVariant kLeafVariants[] = {
 #undef ABLQ
 #undef RET
 constexpr int kNumLeafVariants = sizeof(kLeafVariants) / sizeof(kLeafVariants[0]);
-constexpr int kDefaultLeafVariant = 51;
+constexpr int kDefaultLeafVariant = 52;
 
 int leaf_variant_count() { return kNumLeafVariants; }
 bool leaf_variant_available(int v) { return v >= 0 && v < kNumLeafVariants && kLeafVariants[v].fn != nullptr; }
@@ -1408,10 +1408,12 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
   return hipGetLastError();
 }
 
-// Piece kernel variants. Product: 14 (default) = one workgroup per 1 MiB
-// piece, the leaf kernel's line-pair block loop, 6 waves/SIMD, every G step a
-// B3_G_ASM block (b3_device.h); 15 = 14 with the copy-free first column steps
-// (compress<2>; same time within noise, profiles/r02_ab_asm_g.txt). Ablation
+// Piece kernel variants. Product: 14 = one workgroup per 1 MiB piece, the
+// leaf kernel's line-pair block loop, 6 waves/SIMD, every G step a B3_G_ASM
+// block (b3_device.h); 15 (default) = 14 with the copy-free first column
+// steps (compress<2>: 6 fewer VALU instructions per compression; never slower
+// in three same-process A/Bs, profiles/r02_ab_asm_g.txt,
+// r02_ab_piece_14_15.txt). Ablation
 // library only: 4 = ping-pong block loop (round 1's default), 6 = 14 with the
 // compiler-scheduled G (round 2's default before B3_G_ASM: 10 % slower), 11
 // = persistent grid on a global piece counter (k_piece_dyn), 12 = 11 with the
@@ -1419,7 +1421,7 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
 // = 11 at 8 waves/SIMD (11-13 lost to the hardware dispatcher), and the older
 // plain / prefetch loops, rotated chunk orders, a round-robin persistent grid
 // and the DIAGNOSTIC 7 without memory reads.
-constexpr int kDefaultPieceVariant = 14;
+constexpr int kDefaultPieceVariant = 15;
 
 bool piece_variant_available(int v) {
   if (v == 14 || v == 15) return true;

@@ -70,8 +70,8 @@ def _kernel_stubs(path):
 
 
 def test_product_library_holds_only_product_kernels():
-    """libsdcas.so carries only the product kernels — leaf 51 (default) and
-    52, piece 14 (default) and 15, all bit-exact and GPU-tested — and no
+    """libsdcas.so carries only the product kernels — leaf 52 (default) and
+    51, piece 15 (default) and 14, all bit-exact and GPU-tested — and no
     ablation or
     DIAGNOSTIC variant (those produce wrong digests and live only in
     libsdcas_ablate.so)"""

@@ -33,5 +33,7 @@ echo "rocprof ok"
 bash tools/pmc_traffic.sh $OUT/pmc_c2 > $OUT/pmc_c2.log 2>&1 || exit 9
 bash tools/pmc_traffic.sh $OUT/pmc_c4 -- python $R/bench.py --workload c4 --steps 1 --warmup 0 --no-cpu-baseline \
   > $OUT/pmc_c4.log 2>&1 || exit 10
-VARIANT=51 bash tools/pmc_sq_workloads.sh $OUT/sqw > $OUT/sqw.log 2>&1 || exit 11
+VARIANT=52 bash tools/pmc_sq_workloads.sh $OUT/sqw > $OUT/sqw.log 2>&1 || exit 11
+timeout -k 10 300 python -u tools/e2e_big.py --gib 8 > $OUT/e2e_big.json 2> $OUT/e2e_big.err || exit 12
+timeout -k 10 300 python -u tools/batch_probe.py > $OUT/batch_probe.jsonl 2> $OUT/batch_probe.err || exit 13
 echo done
