@@ -635,8 +635,14 @@ def main():
     comp = int(compressions(lens).sum())
 
     eng = Engine(device=dev.index)
-    stream = torch.cuda.current_stream(dev)
+    # one real stream for the whole run: torch's default stream is the legacy
+    # NULL stream (handle 0), which the library reads as "the context's own
+    # stream" — the hash would then run unordered with the events recorded
+    # here, and the dedup's HIP-event span would swallow the hash
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
+    assert sp != 0
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).to(dev)
     d_blob = torch.empty(total_bytes, dtype=torch.uint8, device=dev)
     d_keys, d_sizes, d_offs, d_lens = t(keys), t(sizes), t(offs), t(lens)
