@@ -316,15 +316,20 @@ hipError_t dd_combine_buckets(DistWs& w, const uint64_t* keys, const uint8_t* ha
 // no sort. The all-ones key (a legal cas key) owns the extra entry at `cap`.
 constexpr uint64_t kEmptyKey = ~0ull;
 
-// Home slot = the key's top bits (cas keys are BLAKE3 output, uniform): the
-// table is ordered like the keys, so the key-sorted runs the owner receives
-// (one per source rank) insert into neighbouring lines instead of scattering
-// one line per record. A slot is read before it is CAS'd, and an entry's
-// minimum before it is atomicMin'd (both only ever decrease from all-ones).
+// Home slot = the key bits just below the 12 that chose the owner rank
+// (dd_owner; cas keys are BLAKE3 output, uniform): within one owner's share
+// the table is ordered like the keys, so the key-sorted runs the owner
+// receives (one per source rank) insert into neighbouring lines instead of
+// scattering one line per record. (The owner bits themselves would crowd an
+// owner's keys into 1/world of the table: at 8 ranks the probe runs grew
+// until a resolve took 640 ms instead of under 1 ms.) A slot is read before
+// it is CAS'd, and an entry's minimum before it is atomicMin'd (both only
+// ever decrease from all-ones).
+constexpr uint32_t kOwnerBits = 12;
 __device__ __forceinline__ uint32_t ht_find(unsigned long long* __restrict__ tkey, uint64_t key, uint32_t mask,
                                             uint32_t shift) {
   if (key == kEmptyKey) return mask + 1;
-  uint32_t h = (uint32_t)(key >> shift) & mask;
+  uint32_t h = (uint32_t)((key << kOwnerBits) >> shift) & mask;
   for (;;) {
     const unsigned long long cur = __hip_atomic_load(&tkey[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (cur == key) return h;

@@ -39,6 +39,9 @@ call whose buckets overflow, takes the exact protocol.
 from __future__ import annotations
 
 import ctypes
+import os
+import sys
+import time
 
 import numpy as np
 import torch
@@ -272,10 +275,33 @@ def _dedup_exact(stages, world, keys, has_key, status, ids, chunk_size, existing
     return link, int(c[0]), int(c[1])
 
 
+class _Trace:
+    """SDCAS_DEDUP_TRACE=1: wall time of each bucket-protocol stage on rank 0's
+    stderr, the device drained at every mark (a diagnostic: it adds host
+    synchronisations the protocol itself does not have)"""
+    on = bool(os.environ.get("SDCAS_DEDUP_TRACE"))
+
+    def __init__(self):
+        self.t, self.parts = time.perf_counter(), []
+
+    def mark(self, what):
+        if self.on:
+            torch.cuda.synchronize()
+            now = time.perf_counter()
+            self.parts.append(f"{what} {1e3 * (now - self.t):.2f}")
+            self.t = now
+
+    def done(self, group):
+        if self.on and dist.get_rank(group) == 0:
+            print("dedup buckets ms: " + ", ".join(self.parts), file=sys.stderr, flush=True)
+
+
 def _dedup_buckets(stages, world, caps, keys, has_key, status, ids, chunk_size, existing_keys, existing_ids,
                    group):
     """the exchange in fixed-capacity buckets: one host synchronisation (the
     totals); None when a bucket overflowed (the caller reruns the exact path)"""
+    tr = _Trace()
+    tr.mark("enter")
     fcap, ecap = caps
     has_ex = existing_keys is not None
     if has_ex and ecap == 0:
@@ -293,10 +319,13 @@ def _dedup_buckets(stages, world, caps, keys, has_key, status, ids, chunk_size, 
         sc = torch.stack([fcnt, ecnt], 1).contiguous()
     else:
         sc = fcnt.view(world, 1).contiguous()
+    tr.mark("combine")
     rc = torch.empty_like(sc)
     dist.all_to_all_single(rc, sc, group=group)  # equal splits: no host sizes
+    tr.mark("a2a counts")
     frecv = torch.empty_like(send)
     dist.all_to_all_single(frecv, send.contiguous(), group=group)
+    tr.mark(f"a2a buckets ({send.numel() * 8 >> 20} MiB)")
     if has_ex:
         erecv = torch.empty_like(esend)
         dist.all_to_all_single(erecv, esend.contiguous(), group=group)
@@ -304,15 +333,20 @@ def _dedup_buckets(stages, world, caps, keys, has_key, status, ids, chunk_size, 
     else:
         erecv, ercnt = None, None
     answer = stages.resolve_buckets(frecv, fcap, rc[:, 0].contiguous(), erecv, ecap if has_ex else 0, ercnt, world)
+    tr.mark("resolve")
     back = torch.empty_like(answer)
     dist.all_to_all_single(back, answer.contiguous(), group=group)
+    tr.mark("a2a answers")
     link, cnt = stages.apply(ids, slot, back, chunk_size)
+    tr.mark("apply")
     over = ovf.to(torch.int64) + (eovf.to(torch.int64) if has_ex else 0)
     tot = torch.cat([cnt.to(torch.int64), over])
     fills = torch.stack([fcnt.max(), ecnt.max() if has_ex else torch.full((), -1, dtype=torch.int64, device=dev)])
     dist.all_reduce(tot, group=group)
     dist.all_reduce(fills, op=dist.ReduceOp.MAX, group=group)
     tf = torch.cat([tot, fills]).tolist()  # the one host synchronisation
+    tr.mark("totals")
+    tr.done(group)
     t, f = tf[:3], tf[3:]
     _next_caps(stages, int(f[0]), int(f[1]))
     if t[2]:
