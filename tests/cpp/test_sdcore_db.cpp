@@ -225,6 +225,42 @@ static double now() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// forwards everything, timing each kind of call (where a step's DB time goes)
+struct Timed : Library {
+  Library& d;
+  double t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  explicit Timed(Library& x) : d(x) {}
+  template <class F>
+  auto tm(int k, F f) -> decltype(f()) {
+    const double t0 = now();
+    struct G {
+      double* acc;
+      double t0;
+      ~G() { *acc += now() - t0; }
+    } g{&t[k], t0};
+    return f();
+  }
+  size_t count_orphan_file_paths(int32_t l, const std::string& s) override {
+    return tm(0, [&] { return d.count_orphan_file_paths(l, s); });
+  }
+  std::vector<FilePathRow> get_orphan_file_paths(int32_t l, int32_t c, const std::string& s, size_t n) override {
+    return tm(1, [&] { return d.get_orphan_file_paths(l, c, s, n); });
+  }
+  void set_cas_id(int32_t i, const std::optional<std::string>& c) override { tm(2, [&] { d.set_cas_id(i, c); }); }
+  std::vector<std::pair<int32_t, std::vector<std::string>>> existing_objects(
+      const std::vector<std::string>& c) override {
+    return tm(3, [&] { return d.existing_objects(c); });
+  }
+  int32_t create_object(ObjectKind k, int64_t t_) override { return tm(4, [&] { return d.create_object(k, t_); }); }
+  void connect(int32_t f, int32_t o) override { tm(5, [&] { d.connect(f, o); }); }
+  std::vector<FilePathRow> file_paths_without_checksum(int32_t l, const std::string& s) override {
+    return d.file_paths_without_checksum(l, s);
+  }
+  void set_integrity_checksum(int32_t i, const std::string& c) override { d.set_integrity_checksum(i, c); }
+  void begin_batch() override { tm(6, [&] { d.begin_batch(); }); }
+  void end_batch() override { tm(7, [&] { d.end_batch(); }); }
+};
+
 static int bench(size_t n) {
   std::string out = "{\"what\": \"DB side of the identifier step (SqliteLibrary, WAL, synchronous=NORMAL), "
                     "group-by by the CPU oracle, metadata synthetic\", \"file_paths\": " + std::to_string(n);
@@ -254,15 +290,18 @@ static int bench(size_t n) {
       }
       sql->add_file_paths(rows);
       Autocommit ac(*sql);
-      Library& db = m.autocommit ? static_cast<Library&>(ac) : *sql;
+      Timed timed(m.autocommit ? static_cast<Library&>(ac) : *sql);
       const double t0 = now();
-      auto meta = run_job(db, 1, m.batch, rows_n / 3);
+      auto meta = run_job(timed, 1, m.batch, rows_n / 3);
       const double dt = now() - t0;
-      char b[256];
+      char b[512];
       std::snprintf(b, sizeof b,
                     ", \"%s\": {\"rows\": %zu, \"seconds\": %.3f, \"rows_per_s\": %.0f, \"created\": %zu, "
-                    "\"linked\": %zu}",
-                    m.name, rows_n, dt, rows_n / dt, meta.total_objects_created, meta.total_objects_linked);
+                    "\"linked\": %zu, \"seconds_by_call\": {\"count_orphans\": %.3f, \"get_orphans\": %.3f, "
+                    "\"set_cas_id\": %.3f, \"existing_objects\": %.3f, \"create_object\": %.3f, "
+                    "\"connect\": %.3f, \"begin\": %.3f, \"commit\": %.3f}}",
+                    m.name, rows_n, dt, rows_n / dt, meta.total_objects_created, meta.total_objects_linked,
+                    timed.t[0], timed.t[1], timed.t[2], timed.t[3], timed.t[4], timed.t[5], timed.t[6], timed.t[7]);
       out += b;
     }
     for (const char* suf : {"", "-wal", "-shm"}) std::remove((std::string(path) + suf).c_str());
