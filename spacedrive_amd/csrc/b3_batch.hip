@@ -1305,6 +1305,7 @@ static const LeafVariant kLeafVariants[] = {
     ABL1(512, k_leaf_tree<512, 102, 1, 1, 2, 2>),   // 56 DIAGNOSTIC (wrong digests): 51's compression, no memory reads
     ABL1(512, k_leaf_tree<512, 139, 1, 1, 2, 2>),   // 57 DIAGNOSTIC (wrong digests): 51 reading a wave-transposed image
     ABL1(512, k_leaf_tree<512, 149, 1, 1, 2, 2>),   // 58 DIAGNOSTIC (wrong digests): 51 reading an L2-resident 2 MiB
+    ABL1(512, k_leaf_tree<512, 209, 0, 1, 2, 2>),   // 59 DIAGNOSTIC (wrong digests): 52 without the in-tile tree
 };
 #undef PROD
 #undef PROD1
