@@ -546,6 +546,25 @@ def run_c4(args, torch, dist, dev, rank, world, distributed, out_f):
         checked, bad = sum_over_ranks(torch, dist, dev, [checked, bad])
         out["parity"].update({"checked_files": checked, "mismatches": bad, "ranks": world,
                               "sample": "each rank: its smallest file, whole-file checksum vs the oracle"})
+    if args.c4_full_parity:
+        # every file this rank holds a digest of, against the oracle's
+        # checksum of the same synthetic content (scalar restatement, one
+        # file per thread; ctypes releases the GIL)
+        from concurrent.futures import ThreadPoolExecutor
+        from tests._oracle import load_oracle
+        o = load_oracle()
+        # with the piece split every rank holds every digest: rank r checks files r, r + N, ...
+        cand = [f for f in range(sizes.size) if f % world == rank] if split == "pieces" else list(mine)
+        dig = out32.cpu().numpy()
+        with ThreadPoolExecutor(max(1, args.cpu_threads)) as ex:
+            want = list(ex.map(lambda f: o.synth_checksum(int(ckeys[f]), int(sizes[f])), cand))
+        bad = sum(bytes(dig[local[f]]).hex() != w for f, w in zip(cand, want))
+        nbytes = int(sum(int(sizes[f]) for f in cand))
+        checked, bad, nbytes = (sum_over_ranks(torch, dist, dev, [len(cand), bad, nbytes]) if distributed
+                                else (len(cand), bad, nbytes))
+        out["parity"]["all_files"] = {"checked_files": checked, "mismatches": bad, "bytes": nbytes,
+                                      "oracle": "scalar BLAKE3 restatement of each file's synthetic content "
+                                                "(oracle/cas_ref.c oracle_synth_checksum)"}
     if rank == 0:
         emit(out_f, out)
     eng.close()
@@ -585,6 +604,8 @@ def main():
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-faithful", action="store_true", help="e2e without the page-cache files legs")
     ap.add_argument("--piece-variant", type=int, default=-1, help="c4: piece kernel variant (-1 default)")
+    ap.add_argument("--c4-full-parity", action="store_true",
+                    help="c4: check every file's checksum against the oracle (16 CPU threads, about a minute)")
     ap.add_argument("--c4-split", default="auto", choices=["auto", "pieces", "files"],
                     help="c4 over N GPUs: split the files' pieces (auto at N > 1) or assign whole files")
     args = ap.parse_args()
