@@ -524,9 +524,13 @@ __global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __
     for (uint32_t k = 1; TR && k <= 10; ++k) {
       const uint32_t T = ntask[k];
       if (T == 0) continue;
+      // TR 2 (diagnostic, still bit-exact): every lane of a wave that holds
+      // tasks computes one — lanes past the level's last task repeat it and
+      // do not store — to price masked lanes against active ones
+      const uint32_t TT = TR == 2 ? (T + 63u) & ~63u : T;
 #pragma unroll 1
-      for (uint32_t t = tid; t < T; t += WG) {
-        const uint32_t e = task[task_base(k) + t];
+      for (uint32_t t = tid; t < TT; t += WG) {
+        const uint32_t e = task[task_base(k) + (TR == 2 ? min(t, T - 1) : t)];
         const uint32_t l = e & 1023u, r = (e >> 10) & 1023u;
         const bool root = e >> 31;
         uint32_t a[8], b[8], o[8];
@@ -536,6 +540,7 @@ __global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __
           b[q] = cvs[r][q];
         }
         parent<kGA<PF>>(a, b, root, o);
+        if (TR == 2 && t >= T) continue;
         if (root) {
           const uint32_t mm = m0 + ((e >> 20) & 2047u);
           store_digest(perm ? perm[mm] : mm, o, out32, out_keys);
@@ -1306,6 +1311,7 @@ static const LeafVariant kLeafVariants[] = {
     ABL1(512, k_leaf_tree<512, 139, 1, 1, 2, 2>),   // 57 DIAGNOSTIC (wrong digests): 51 reading a wave-transposed image
     ABL1(512, k_leaf_tree<512, 149, 1, 1, 2, 2>),   // 58 DIAGNOSTIC (wrong digests): 51 reading an L2-resident 2 MiB
     ABL1(512, k_leaf_tree<512, 209, 0, 1, 2, 2>),   // 59 DIAGNOSTIC (wrong digests): 52 without the in-tile tree
+    ABL1(512, k_leaf_tree<512, 209, 2, 1, 2, 2>),   // 60: 52 with every lane of a tree wave computing (prices masked lanes)
 };
 #undef PROD
 #undef PROD1
