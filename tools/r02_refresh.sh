@@ -18,7 +18,7 @@ timeout -k 10 400 python -u bench.py > $OUT/bench_c2.json 2> $OUT/bench_c2.err |
 for w in c3 c5; do
   timeout -k 10 300 python -u bench.py --workload $w --steps 10 --warmup 3 > $OUT/bench_$w.json 2> $OUT/bench_$w.err || exit 4
 done
-timeout -k 10 400 python -u bench.py --workload c4 --steps 3 --warmup 1 > $OUT/bench_c4.json 2> $OUT/bench_c4.err || exit 5
+timeout -k 10 600 python -u bench.py --workload c4 --steps 3 --warmup 1 --c4-full-parity > $OUT/bench_c4.json 2> $OUT/bench_c4.err || exit 5
 echo "bench ok"
 SDCAS_BENCH_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
   --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 \
