@@ -41,9 +41,13 @@ bool piece_variant_available(int v);
 // all pointers device pointers. Writes 32-byte digests to out32 and/or cas
 // keys (digest bytes 0..7 big-endian) to out_keys (either may be null).
 // Total chunks must not exceed ws.cap_chunks (checked by the caller).
+// max_chunks: the batch's chunk count if the caller knows it (the staging
+// slots do), which sizes the leaf and finish grids to the batch; 0 sizes them
+// to the workspace (device-resident batches, whose lengths the host never
+// sees).
 hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint64_t* offs, const uint64_t* lens,
-                      uint32_t n, uint8_t* out32, uint64_t* out_keys, hipStream_t st, hipEvent_t ev0 = nullptr,
-                      hipEvent_t ev1 = nullptr);
+                      uint32_t n, uint8_t* out32, uint64_t* out_keys, hipStream_t st, uint64_t max_chunks = 0,
+                      hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 
 // ---- big files (C > kTile chunks), hashed as 1 MiB pieces -------------------
 struct PieceDesc {

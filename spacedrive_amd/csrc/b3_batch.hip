@@ -761,6 +761,7 @@ __global__ void __launch_bounds__(kFinishWG) k_finish_t(const uint64_t* __restri
 // specified, which changes nothing but the slot a message lands in.
 constexpr uint32_t kShapeBins = 256;
 constexpr uint32_t kScatterPerWG = 4096;
+constexpr uint32_t kSortMinMsgs = 128;  // smaller batches keep the caller's order
 constexpr uint32_t kShapeManyChunks = 15 << 4;  // first shape key of messages of 15+ chunks
 
 __device__ __forceinline__ uint32_t shape_key(uint64_t L) {
@@ -1351,13 +1352,16 @@ int batch_grid(int device, int variant) {
 }
 
 hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint64_t* offs, const uint64_t* lens,
-                      uint32_t n, uint8_t* out32, uint64_t* out_keys, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1) {
+                      uint32_t n, uint8_t* out32, uint64_t* out_keys, hipStream_t st, uint64_t max_chunks,
+                      hipEvent_t ev0, hipEvent_t ev1) {
   if (n == 0) return hipSuccess;
   if (n > ws.cap_msgs) return hipErrorInvalidValue;
   const uint32_t tb = 256;
   hipError_t e;
   const uint32_t* perm = nullptr;
-  if (ws.sort && n > 1 && ws.perm) {
+  // A batch of a few messages fills a tile or two whatever their order: its
+  // three sort launches would only add latency (the reference's 100-file step).
+  if (ws.sort && n >= kSortMinMsgs && ws.perm) {
     uint32_t* counts = ws.sort_keys;  // [256] bin sizes, [256] per-bin cursors
     if ((e = hipMemsetAsync(counts, 0, 2 * kShapeBins * sizeof(uint32_t), st))) return e;
     const uint32_t hb = std::min<uint32_t>((n + 255) / 256, 1024u);
@@ -1388,11 +1392,15 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
     hipLaunchKernelGGL(k_tile_first, dim3((n + tb - 1) / tb), dim3(tb), 0, st, lens, ws.S, n, ws.cap_slots,
                        ws.tile_first, ws.total);
   }
+  // slots the batch may fill: a grid sized to the workspace instead costs a
+  // small batch ~45 us of empty workgroups (8449 of them at 256 MiB staging)
+  const uint64_t slots =
+      max_chunks ? std::min<uint64_t>(ws.cap_slots, max_chunks + (quad ? 3ull * n + 8 : 0)) : ws.cap_slots;
   if (ev0) (void)hipEventRecord(ev0, st);
   {
     int dev = 0;
     (void)hipGetDevice(&dev);
-    const int grid = kLeafVariants[v].one_tile ? (int)std::min<uint64_t>(ws.cap_slots / kTile + 1, 0x7FFFFFFF)
+    const int grid = kLeafVariants[v].one_tile ? (int)std::min<uint64_t>(slots / kTile + 1, 0x7FFFFFFF)
                                                : batch_grid(dev, v);
     void* args[] = {(void*)&blob,     (void*)&offs,          (void*)&lens,       (void*)&n,
                     (void*)&ws.S,     (void*)&ws.tile_first, (void*)&ws.total,   (void*)&ws.cap_slots,
@@ -1403,12 +1411,12 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
   if (ev1) (void)hipEventRecord(ev1, st);
   if (quad) {
 #ifdef SDCAS_ABLATIONS
-    const uint64_t tiles = ws.cap_slots / kQTile + 1;
+    const uint64_t tiles = slots / kQTile + 1;
     hipLaunchKernelGGL(k_finish_t<kQTile>, dim3((uint32_t)((tiles + kFinishWG - 1) / kFinishWG)), dim3(kFinishWG), 0,
                        st, lens, n, ws.S, ws.tile_first, ws.total, ws.cap_slots, ws.nodes, perm, out32, out_keys);
 #endif
   } else {
-    const uint64_t tiles = ws.cap_slots / kTile + 1;
+    const uint64_t tiles = slots / kTile + 1;
     hipLaunchKernelGGL(k_finish_t<kTile>, dim3((uint32_t)((tiles + kFinishWG - 1) / kFinishWG)), dim3(kFinishWG), 0,
                        st, lens, n, ws.S, ws.tile_first, ws.total, ws.cap_slots, ws.nodes, perm, out32, out_keys);
   }

@@ -214,7 +214,9 @@ int reserve_ws(sdcas_ctx* c, size_t max_msgs, uint64_t max_chunks) {
   if ((e = c->ws_S.ensure(max_msgs + 1))) return c->hip_fail(e, "workspace S");
   // room for the quad layout's padding too: < 4 dead slots per message (of
   // as many messages as the workspace takes)
-  const uint64_t tiles = (max_chunks + 3 * (uint64_t)(c->ws_S.cap - 1) + 8) / kTile + 2;
+  // (rounded up, +3: cap_chunks below comes out >= max_chunks, so that
+  // slots_prepare's check holds on the next call instead of re-reserving)
+  const uint64_t tiles = (max_chunks + 3 * (uint64_t)(c->ws_S.cap - 1) + 8 + kTile - 1) / kTile + 3;
   if ((e = c->ws_total.ensure(4))) return c->hip_fail(e, "workspace total");
   if ((e = c->ws_tile_first.ensure(tiles))) return c->hip_fail(e, "workspace tile_first");
   if ((e = c->ws_nodes.ensure(8 * (tiles * kTile)))) return c->hip_fail(e, "workspace nodes");
@@ -245,17 +247,17 @@ int reserve_ws(sdcas_ctx* c, size_t max_msgs, uint64_t max_chunks) {
 // Enqueue the hash of n device messages (the one launch sequence every API
 // ends in), with optional HIP-event profiling of the leaf kernel.
 int launch_batch(sdcas_ctx* c, const uint8_t* blob, const uint64_t* offs, const uint64_t* lens, uint32_t n,
-                 uint8_t* out32, uint64_t* keys, hipStream_t st) {
+                 uint8_t* out32, uint64_t* keys, hipStream_t st, uint64_t max_chunks = 0) {
   hipError_t e;
   if (c->profile) {
     hipEvent_t a = c->event(), b = c->event(), la = c->event(), lb = c->event();
     (void)hipEventRecord(a, st);
-    e = batch_hash(c->ws, blob, offs, lens, n, out32, keys, st, la, lb);
+    e = batch_hash(c->ws, blob, offs, lens, n, out32, keys, st, max_chunks, la, lb);
     (void)hipEventRecord(b, st);
     c->ev_all.push_back({a, b});
     c->ev_leaf.push_back({la, lb});
   } else {
-    e = batch_hash(c->ws, blob, offs, lens, n, out32, keys, st);
+    e = batch_hash(c->ws, blob, offs, lens, n, out32, keys, st, max_chunks);
   }
   if (e) return c->hip_fail(e, "batch_hash");
   return SDCAS_OK;
@@ -323,14 +325,19 @@ int slots_prepare(sdcas_ctx* c, uint64_t cap, size_t cap_n) {
   return SDCAS_OK;
 }
 
-// A slot's host-to-device copies run on the context's copy stream, so that
-// they overlap the other slot's kernels on the compute stream (PCIe and the
-// CUs work at once: the path calls are bound by the copy); the compute stream
-// waits for them before this slot's kernels. Refilling a slot waits for its
-// previous batch on the host first (slot_complete), so a copy never lands
-// under kernels still reading the slot.
+// While the other slot's batch is in flight, a slot's host-to-device copies
+// run on the context's copy stream, so that they overlap that batch's kernels
+// on the compute stream (PCIe and the CUs work at once: the path calls are
+// bound by the copy); the compute stream waits for them before this slot's
+// kernels. With nothing to overlap (a call's first or only slot) they go on
+// the compute stream itself: the event and the cross-stream wait would only
+// add latency. Refilling a slot waits for its previous batch on the host
+// first (slot_complete), so a copy never lands under kernels still reading
+// the slot.
 template <class Copies>
 hipError_t slot_upload(sdcas_ctx* c, Slot& s, Copies copies) {
+  const Slot& other = &s == &c->slots[0] ? c->slots[1] : c->slots[0];
+  if (!other.busy) return copies(c->stream);
   hipError_t e;
   if ((e = copies(c->copy_stream)) || (e = hipEventRecord(s.h2d, c->copy_stream))) return e;
   return hipStreamWaitEvent(c->stream, s.h2d, 0);
@@ -352,16 +359,22 @@ int slot_submit(sdcas_ctx* c, Slot& s, bool res32) {
     if ((rc = reserve_ws(c, std::max<size_t>(s.n, c->ws.cap_msgs), std::max<uint64_t>(s.chunks, c->ws.cap_chunks))))
       return rc;
   }
+  // offsets and lengths in one copy: the lengths are moved up behind the
+  // offsets when they fit there (each small copy is a blit kernel of its own)
+  const bool packed = 2 * s.n <= s.cap_n;
+  if (packed) memcpy(s.hm + s.n, s.lens(), 8 * s.n);
+  const uint64_t* d_lens = s.d_meta.p + (packed ? s.n : s.cap_n);
   if ((e = slot_upload(c, s, [&](hipStream_t cs) {
          hipError_t r;
          if ((r = hipMemcpyAsync(s.d_blob.p, s.src ? s.src : s.h, s.used, hipMemcpyHostToDevice, cs)) ||
-             (r = hipMemcpyAsync(s.d_meta.p, s.hm, 8 * s.n, hipMemcpyHostToDevice, cs)))
+             (r = hipMemcpyAsync(s.d_meta.p, s.hm, 8 * (packed ? 2 * s.n : s.n), hipMemcpyHostToDevice, cs)))
            return r;
-         return hipMemcpyAsync(s.d_meta.p + s.cap_n, s.hm + s.cap_n, 8 * s.n, hipMemcpyHostToDevice, cs);
+         return packed ? hipSuccess
+                       : hipMemcpyAsync(s.d_meta.p + s.cap_n, s.hm + s.cap_n, 8 * s.n, hipMemcpyHostToDevice, cs);
        })))
     return c->hip_fail(e, "H2D");
-  if ((rc = launch_batch(c, s.d_blob.p, s.d_meta.p, s.d_meta.p + s.cap_n, (uint32_t)s.n, res32 ? s.d_res.p : nullptr,
-                         res32 ? nullptr : reinterpret_cast<uint64_t*>(s.d_res.p), st)))
+  if ((rc = launch_batch(c, s.d_blob.p, s.d_meta.p, d_lens, (uint32_t)s.n, res32 ? s.d_res.p : nullptr,
+                         res32 ? nullptr : reinterpret_cast<uint64_t*>(s.d_res.p), st, s.chunks)))
     return rc;
   if ((e = hipMemcpyAsync(s.res(), s.d_res.p, (res32 ? 32 : 8) * s.n, hipMemcpyDeviceToHost, st)) ||
       (e = hipEventRecord(s.ev, st)))
@@ -905,7 +918,7 @@ struct IoTrace {
   }
   ~IoTrace() {
     if (on)
-      fprintf(stderr, "sdcas_cas_ids trace ms: drain %.1f plan %.1f read %.1f book %.1f submit %.1f\n", t[0], t[1],
+      fprintf(stderr, "sdcas_cas_ids trace ms: drain %.3f plan %.3f read %.3f book %.3f submit %.3f\n", t[0], t[1],
               t[2], t[3], t[4]);
   }
 };

@@ -1,0 +1,121 @@
+// ubench_latency.cpp — per-call wall time of sdcas_cas_ids at the C ABI (no
+// Python in the timed region), for one library or two side by side
+// (measurement tool; tools/latency_probe.py writes the files and runs it).
+//
+//   ubench_latency MANIFEST BATCHES CALLS LIB_A [LIB_B]
+//
+// MANIFEST: one "size path" line per file (files in the page cache). For each
+// batch size B, CALLS calls over consecutive slices of the manifest (a call
+// reads files its library has not just read, as the identifier's steps do);
+// with two libraries each slice is hashed by both, the order alternating per
+// call, and the keys must agree. Prints one JSON line per (library, B).
+#include <dlfcn.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../include/sdcas.h"
+
+namespace {
+
+struct Lib {
+  std::string path;
+  void* h = nullptr;
+  int (*init)(const sdcas_options*, sdcas_ctx**) = nullptr;
+  void (*destroy)(sdcas_ctx*) = nullptr;
+  int (*cas_ids)(sdcas_ctx*, const char* const*, const uint64_t*, size_t, uint64_t*, int32_t*) = nullptr;
+  sdcas_ctx* ctx = nullptr;
+  bool open(const std::string& p) {
+    path = p;
+    h = dlopen(p.c_str(), RTLD_NOW | RTLD_LOCAL);
+    if (!h) return fprintf(stderr, "dlopen %s: %s\n", p.c_str(), dlerror()), false;
+    init = (decltype(init))dlsym(h, "sdcas_init");
+    destroy = (decltype(destroy))dlsym(h, "sdcas_destroy");
+    cas_ids = (decltype(cas_ids))dlsym(h, "sdcas_cas_ids");
+    if (!init || !destroy || !cas_ids) return fprintf(stderr, "%s: missing symbols\n", p.c_str()), false;
+    sdcas_options o;
+    memset(&o, 0, sizeof o);
+    return init(&o, &ctx) == SDCAS_OK;
+  }
+};
+
+double median(std::vector<double> v) {
+  std::sort(v.begin(), v.end());
+  return v.empty() ? 0 : v[v.size() / 2];
+}
+double pct(std::vector<double> v, double q) {
+  std::sort(v.begin(), v.end());
+  return v.empty() ? 0 : v[std::min(v.size() - 1, (size_t)(q * v.size()))];
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc < 5) {
+    fprintf(stderr, "usage: %s MANIFEST BATCHES CALLS LIB_A [LIB_B]\n", argv[0]);
+    return 2;
+  }
+  std::vector<std::string> paths;
+  std::vector<uint64_t> sizes;
+  {
+    std::ifstream f(argv[1]);
+    uint64_t s;
+    std::string p;
+    while (f >> s >> p) sizes.push_back(s), paths.push_back(p);
+  }
+  std::vector<const char*> cp(paths.size());
+  for (size_t i = 0; i < paths.size(); ++i) cp[i] = paths[i].c_str();
+  std::vector<size_t> batches;
+  {
+    std::stringstream ss(argv[2]);
+    std::string t;
+    while (std::getline(ss, t, ',')) batches.push_back(std::stoul(t));
+  }
+  const size_t calls_max = std::stoul(argv[3]);
+  std::vector<Lib> libs(argc - 4);
+  for (size_t l = 0; l < libs.size(); ++l)
+    if (!libs[l].open(argv[4 + l])) return 1;
+  const size_t N = paths.size();
+  std::vector<uint64_t> keys(N), k2(N);
+  std::vector<int32_t> st(N);
+  // warm-up: contexts, reader pools, staging, page cache
+  for (auto& L : libs)
+    if (L.cas_ids(L.ctx, cp.data(), sizes.data(), N, keys.data(), st.data())) return 1;
+  int bad = 0;
+  for (size_t B : batches) {
+    if (B > N) continue;
+    const size_t calls = std::min(calls_max, N / B);
+    std::vector<std::vector<double>> lat(libs.size());
+    for (size_t c = 0; c < calls; ++c) {
+      const size_t lo = c * B;
+      for (size_t r = 0; r < libs.size(); ++r) {
+        const size_t l = (r + c) % libs.size();
+        auto& out = l ? k2 : keys;
+        const auto t0 = std::chrono::steady_clock::now();
+        const int rc = libs[l].cas_ids(libs[l].ctx, cp.data() + lo, sizes.data() + lo, B, out.data() + lo, st.data() + lo);
+        lat[l].push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+        if (rc) return fprintf(stderr, "call failed: %d\n", rc), 1;
+        for (size_t i = lo; i < lo + B; ++i) bad += st[i] != 0;
+      }
+      if (libs.size() > 1)
+        for (size_t i = lo; i < lo + B; ++i) bad += keys[i] != k2[i];
+    }
+    for (size_t l = 0; l < libs.size(); ++l) {
+      const double med = median(lat[l]);
+      printf("{\"lib\": \"%s\", \"batch\": %zu, \"calls\": %zu, \"median_ms\": %.4f, \"p10_ms\": %.4f, "
+             "\"p90_ms\": %.4f, \"files_per_s\": %.0f}\n",
+             libs[l].path.c_str(), B, calls, med, pct(lat[l], 0.1), pct(lat[l], 0.9), B / (med * 1e-3));
+    }
+    fflush(stdout);
+  }
+  for (auto& L : libs) L.destroy(L.ctx);
+  printf("{\"mismatches_or_errors\": %d}\n", bad);
+  return bad != 0;
+}
