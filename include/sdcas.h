@@ -105,7 +105,7 @@ typedef void (*sdcas_progress_fn)(void *user, uint64_t done, uint64_t total);
 
 typedef struct sdcas_options {
   int32_t device;          /* HIP device ordinal (-1: current device) */
-  uint32_t io_threads;     /* reader threads of the path calls (0: 8; at most 256), started by the first one */
+  uint32_t io_threads;     /* reader threads of the path calls (0: 16, or the CPU count if lower; at most 256), started by the first one */
   uint64_t staging_bytes;  /* pinned host staging per batch (0: 256 MiB) */
   uint32_t flags;          /* SDCAS_OPT_* */
   uint32_t reserved;

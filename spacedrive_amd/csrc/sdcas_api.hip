@@ -106,7 +106,10 @@ struct sdcas_ctx {
   hipStream_t copy_stream = nullptr;  // staging slots' host-to-device copies
   std::string err;
   std::mutex mu;
-  uint32_t io_threads = 8;
+  // reader threads: 16 unless the machine has fewer CPUs (C-ABI probe, C2
+  // files from the page cache, profiles/r02_latency_threads.json: 16 against
+  // 8 cut 100 / 1000 / 10000-file calls by 8 / 17 / 18 %; 32 no better)
+  uint32_t io_threads = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
   static constexpr uint32_t kMaxIoThreads = 256;
   std::unique_ptr<sdcas_io::WorkerPool> pool;  // io_threads readers (the calling thread is one)
   uint64_t staging_bytes = 256ull << 20;

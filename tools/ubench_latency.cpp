@@ -1,14 +1,16 @@
 // ubench_latency.cpp — per-call wall time of sdcas_cas_ids at the C ABI (no
-// Python in the timed region), for one library or two side by side
+// Python in the timed region), for one library or several side by side
 // (measurement tool; tools/latency_probe.py writes the files and runs it).
 //
-//   ubench_latency MANIFEST BATCHES CALLS LIB_A [LIB_B]
+//   ubench_latency MANIFEST BATCHES CALLS LIB[@IO_THREADS]...
 //
 // MANIFEST: one "size path" line per file (files in the page cache). For each
 // batch size B, CALLS calls over consecutive slices of the manifest (a call
 // reads files its library has not just read, as the identifier's steps do);
-// with two libraries each slice is hashed by both, the order alternating per
+// with several libraries each slice is hashed by all, the order rotating per
 // call, and the keys must agree. Prints one JSON line per (library, B).
+// "@N" sets the context's reader threads (sdcas_options.io_threads; default
+// 0 = the library's 8); the same library may be named twice with different N.
 #include <dlfcn.h>
 
 #include <algorithm>
@@ -27,13 +29,17 @@ namespace {
 
 struct Lib {
   std::string path;
+  uint32_t io_threads = 0;
   void* h = nullptr;
   int (*init)(const sdcas_options*, sdcas_ctx**) = nullptr;
   void (*destroy)(sdcas_ctx*) = nullptr;
   int (*cas_ids)(sdcas_ctx*, const char* const*, const uint64_t*, size_t, uint64_t*, int32_t*) = nullptr;
   sdcas_ctx* ctx = nullptr;
-  bool open(const std::string& p) {
-    path = p;
+  bool open(const std::string& spec) {
+    path = spec;
+    const size_t at = spec.rfind('@');
+    const std::string p = at == std::string::npos ? spec : spec.substr(0, at);
+    if (at != std::string::npos) io_threads = (uint32_t)std::stoul(spec.substr(at + 1));
     h = dlopen(p.c_str(), RTLD_NOW | RTLD_LOCAL);
     if (!h) return fprintf(stderr, "dlopen %s: %s\n", p.c_str(), dlerror()), false;
     init = (decltype(init))dlsym(h, "sdcas_init");
@@ -42,6 +48,7 @@ struct Lib {
     if (!init || !destroy || !cas_ids) return fprintf(stderr, "%s: missing symbols\n", p.c_str()), false;
     sdcas_options o;
     memset(&o, 0, sizeof o);
+    o.io_threads = io_threads;
     return init(&o, &ctx) == SDCAS_OK;
   }
 };
@@ -59,7 +66,7 @@ double pct(std::vector<double> v, double q) {
 
 int main(int argc, char** argv) {
   if (argc < 5) {
-    fprintf(stderr, "usage: %s MANIFEST BATCHES CALLS LIB_A [LIB_B]\n", argv[0]);
+    fprintf(stderr, "usage: %s MANIFEST BATCHES CALLS LIB[@IO_THREADS]...\n", argv[0]);
     return 2;
   }
   std::vector<std::string> paths;
@@ -83,11 +90,11 @@ int main(int argc, char** argv) {
   for (size_t l = 0; l < libs.size(); ++l)
     if (!libs[l].open(argv[4 + l])) return 1;
   const size_t N = paths.size();
-  std::vector<uint64_t> keys(N), k2(N);
+  std::vector<std::vector<uint64_t>> keys(libs.size(), std::vector<uint64_t>(N));
   std::vector<int32_t> st(N);
   // warm-up: contexts, reader pools, staging, page cache
-  for (auto& L : libs)
-    if (L.cas_ids(L.ctx, cp.data(), sizes.data(), N, keys.data(), st.data())) return 1;
+  for (size_t l = 0; l < libs.size(); ++l)
+    if (libs[l].cas_ids(libs[l].ctx, cp.data(), sizes.data(), N, keys[l].data(), st.data())) return 1;
   int bad = 0;
   for (size_t B : batches) {
     if (B > N) continue;
@@ -97,15 +104,15 @@ int main(int argc, char** argv) {
       const size_t lo = c * B;
       for (size_t r = 0; r < libs.size(); ++r) {
         const size_t l = (r + c) % libs.size();
-        auto& out = l ? k2 : keys;
         const auto t0 = std::chrono::steady_clock::now();
-        const int rc = libs[l].cas_ids(libs[l].ctx, cp.data() + lo, sizes.data() + lo, B, out.data() + lo, st.data() + lo);
+        const int rc =
+            libs[l].cas_ids(libs[l].ctx, cp.data() + lo, sizes.data() + lo, B, keys[l].data() + lo, st.data() + lo);
         lat[l].push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
         if (rc) return fprintf(stderr, "call failed: %d\n", rc), 1;
         for (size_t i = lo; i < lo + B; ++i) bad += st[i] != 0;
       }
-      if (libs.size() > 1)
-        for (size_t i = lo; i < lo + B; ++i) bad += keys[i] != k2[i];
+      for (size_t l = 1; l < libs.size(); ++l)
+        for (size_t i = lo; i < lo + B; ++i) bad += keys[l][i] != keys[0][i];
     }
     for (size_t l = 0; l < libs.size(); ++l) {
       const double med = median(lat[l]);
