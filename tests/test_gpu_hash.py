@@ -448,3 +448,26 @@ def test_mid_size_batches_cut_into_slots(oracle, tmp_path):
         out = e.hash_messages(*e.pack(msgs))
         for m, d in zip(msgs, out):
             assert bytes(d).hex() == oracle.hash(m)
+
+
+def test_small_calls_and_metadata_layouts(oracle):
+    """the small-call launch path: single messages and batches under the
+    shape-sort threshold (128) on the default 256 MiB staging (leaf and finish
+    grids sized to the slot), one after another on one context; then 20 000
+    messages of 0-100 bytes through 1 MiB staging, whose slots fill with more
+    messages than the packed offsets + lengths copy holds (the two-copy
+    layout) and end with a partial slot that packs"""
+    from spacedrive_amd import Engine
+    rng = np.random.default_rng(23)
+    with Engine() as e:
+        for n in (1, 1, 2, 3, 64, 127, 128, 129):
+            msgs = [rng.integers(0, 256, int(L), dtype=np.uint8).tobytes()
+                    for L in rng.integers(0, 300_000 if n < 64 else 40_000, n)]
+            out = e.hash_messages(*e.pack(msgs))
+            for m, d in zip(msgs, out):
+                assert bytes(d).hex() == oracle.hash(m), (n, len(m))
+    msgs = [rng.integers(0, 256, int(L), dtype=np.uint8).tobytes() for L in rng.integers(0, 101, 20_000)]
+    with Engine(staging_bytes=1 << 20) as e:
+        out = e.hash_messages(*e.pack(msgs))
+    bad = [i for i, (m, d) in enumerate(zip(msgs, out)) if bytes(d).hex() != oracle.hash(m)]
+    assert not bad, bad[:10]
