@@ -8,8 +8,10 @@ OUT=${1:-gpurun_out/latency}
 R=$(pwd)
 mkdir -p $OUT
 export TMPDIR=/tmp
+shopt -s nullglob
+LIBS=(spacedrive_amd/libsdcas.so tools/ab_libs/*.so)
 timeout -k 10 300 python -u tools/latency_probe.py --files 20000 --batches 1,10,100,1000,10000 --calls 200 \
-  spacedrive_amd/libsdcas.so tools/ab_libs/*.so > $OUT/probe.jsonl 2> $OUT/probe.err || exit 1
+  "${LIBS[@]}" > $OUT/probe.jsonl 2> $OUT/probe.err || exit 1
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --hip-runtime-trace --output-format csv \
    -d $R/$OUT/trace -o t -- python -u $R/tools/latency_probe.py --files 3000 --batches 1,100 --calls 20 \
    > $R/$OUT/trace.log 2>&1) || exit 2
