@@ -762,6 +762,8 @@ __global__ void __launch_bounds__(kFinishWG) k_finish_t(const uint64_t* __restri
 constexpr uint32_t kShapeBins = 256;
 constexpr uint32_t kScatterPerWG = 4096;
 constexpr uint32_t kSortMinMsgs = 128;  // smaller batches keep the caller's order
+constexpr uint32_t kHistPerThread = 8;
+constexpr uint32_t kScatterR = kScatterPerWG / 256;  // messages per scatter thread
 constexpr uint32_t kShapeManyChunks = 15 << 4;  // first shape key of messages of 15+ chunks
 
 __device__ __forceinline__ uint32_t shape_key(uint64_t L) {
@@ -776,7 +778,20 @@ __global__ void __launch_bounds__(256) k_shape_hist(const uint64_t* __restrict__
   __shared__ uint32_t h[kShapeBins];
   h[threadIdx.x] = 0;
   __syncthreads();
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) atomicAdd(&h[shape_key(lens[i])], 1u);
+  // kHistPerThread loads in flight before their LDS atomics (one load per
+  // iteration had each thread wait out the HBM latency once per message)
+  for (uint64_t base = (uint64_t)blockIdx.x * 256 * kHistPerThread; base < n;
+       base += (uint64_t)gridDim.x * 256 * kHistPerThread) {
+    uint64_t L[kHistPerThread];
+#pragma unroll
+    for (uint32_t r = 0; r < kHistPerThread; ++r) {
+      const uint64_t i = base + r * 256 + threadIdx.x;
+      L[r] = i < n ? lens[i] : 0;
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < kHistPerThread; ++r)
+      if (base + r * 256 + threadIdx.x < n) atomicAdd(&h[shape_key(L[r])], 1u);
+  }
   __syncthreads();
   if (h[threadIdx.x]) atomicAdd(&counts[threadIdx.x], h[threadIdx.x]);
 }
@@ -785,7 +800,10 @@ __global__ void __launch_bounds__(256) k_shape_hist(const uint64_t* __restrict__
 // workgroup's 4096 messages are first ordered by shape in LDS (2-byte local
 // indices), then written run by run — consecutive threads to consecutive
 // addresses of a bin's range. The second read of offs/lens (in LDS order) hits
-// the L2 lines the first read brought in.
+// the L2 lines the first read brought in. Each thread's kScatterR global
+// loads of a pass are issued together, ahead of their use: the workgroups
+// all fit the chip at once, so the kernel takes one workgroup's latency, and
+// a load per loop iteration made that kScatterR HBM round trips per pass.
 __global__ void __launch_bounds__(256) k_shape_scatter(const uint64_t* __restrict__ offs,
                                                        const uint64_t* __restrict__ lens, uint32_t n,
                                                        const uint32_t* __restrict__ counts,
@@ -817,17 +835,38 @@ __global__ void __launch_bounds__(256) k_shape_scatter(const uint64_t* __restric
   // keep the caller's order, as a coalesced copy. Every workgroup decides the
   // same from the same counts.
   if ((uint64_t)(n - few_chunks) * 10 > (uint64_t)n * 6) {
-    for (uint32_t k = t; k < m; k += 256) {
+    uint64_t o[kScatterR], l[kScatterR];
+#pragma unroll
+    for (uint32_t r = 0; r < kScatterR; ++r) {
+      const uint32_t k = t + r * 256;
+      o[r] = k < m ? offs[lo + k] : 0;
+      l[r] = k < m ? lens[lo + k] : 0;
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < kScatterR; ++r) {
+      const uint32_t k = t + r * 256;
+      if (k >= m) continue;
       perm[lo + k] = lo + k;
-      soffs[lo + k] = offs[lo + k];
-      slens[lo + k] = lens[lo + k];
+      soffs[lo + k] = o[r];
+      slens[lo + k] = l[r];
     }
     return;
   }
-  for (uint32_t k = t; k < m; k += 256) {
-    const uint32_t key = shape_key(lens[lo + k]);
-    keyof[k] = (uint8_t)key;
-    atomicAdd(&h[key], 1u);
+  {
+    uint64_t l[kScatterR];
+#pragma unroll
+    for (uint32_t r = 0; r < kScatterR; ++r) {
+      const uint32_t k = t + r * 256;
+      l[r] = k < m ? lens[lo + k] : 0;
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < kScatterR; ++r) {
+      const uint32_t k = t + r * 256;
+      if (k >= m) continue;
+      const uint32_t key = shape_key(l[r]);
+      keyof[k] = (uint8_t)key;
+      atomicAdd(&h[key], 1u);
+    }
   }
   __syncthreads();
   // this workgroup's range in bin t, and the bin's start in the local order
@@ -849,14 +888,24 @@ __global__ void __launch_bounds__(256) k_shape_scatter(const uint64_t* __restric
     order[lstart[key] + atomicAdd(&h[key], 1u)] = (uint16_t)k;
   }
   __syncthreads();
-  for (uint32_t p = t; p < m; p += 256) {
-    const uint32_t k = order[p];
-    const uint32_t key = keyof[k];
+  uint32_t kk[kScatterR];
+  uint64_t o[kScatterR], l[kScatterR];
+#pragma unroll
+  for (uint32_t r = 0; r < kScatterR; ++r) {
+    const uint32_t p = t + r * 256;
+    kk[r] = p < m ? order[p] : 0u;
+    o[r] = p < m ? offs[lo + kk[r]] : 0;
+    l[r] = p < m ? lens[lo + kk[r]] : 0;
+  }
+#pragma unroll
+  for (uint32_t r = 0; r < kScatterR; ++r) {
+    const uint32_t p = t + r * 256;
+    if (p >= m) continue;
+    const uint32_t key = keyof[kk[r]];
     const uint32_t pos = gstart[key] + (p - lstart[key]);
-    const uint32_t i = lo + k;
-    perm[pos] = i;
-    soffs[pos] = offs[i];
-    slens[pos] = lens[i];
+    perm[pos] = lo + kk[r];
+    soffs[pos] = o[r];
+    slens[pos] = l[r];
   }
 }
 
@@ -1364,7 +1413,7 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
   if (ws.sort && n >= kSortMinMsgs && ws.perm) {
     uint32_t* counts = ws.sort_keys;  // [256] bin sizes, [256] per-bin cursors
     if ((e = hipMemsetAsync(counts, 0, 2 * kShapeBins * sizeof(uint32_t), st))) return e;
-    const uint32_t hb = std::min<uint32_t>((n + 255) / 256, 1024u);
+    const uint32_t hb = std::min<uint32_t>((n + 256 * kHistPerThread - 1) / (256 * kHistPerThread), 1024u);
     hipLaunchKernelGGL(k_shape_hist, dim3(hb), dim3(256), 0, st, lens, n, counts);
     hipLaunchKernelGGL(k_shape_scatter, dim3((n + kScatterPerWG - 1) / kScatterPerWG), dim3(256), 0, st, offs, lens,
                        n, counts, counts + kShapeBins, ws.perm, ws.soffs, ws.slens);
