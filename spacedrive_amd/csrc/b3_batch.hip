@@ -730,7 +730,11 @@ __global__ void __launch_bounds__(kFinishWG) k_finish_t(const uint64_t* __restri
                                                        const uint32_t* __restrict__ nodes,
                                                        const uint32_t* __restrict__ perm, uint8_t* __restrict__ out32,
                                                        uint64_t* __restrict__ out_keys) {
-  __shared__ uint32_t lstack[kFinishWG][kFinishDepth][8];
+  // one lane's stack per row, rows an odd number of words apart: lane l's
+  // word w sits in bank (l * kFinishRow + w) mod 64, so a wave's stack
+  // accesses are conflict-free (a 192-word row put all 64 lanes in one bank)
+  constexpr uint32_t kFinishRow = kFinishDepth * 8 + 1;
+  __shared__ uint32_t lstack[kFinishWG][kFinishRow];
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t total = *total_p;
   if (total > cap_slots || t == 0 || t * TILE >= total) return;
@@ -742,7 +746,7 @@ __global__ void __launch_bounds__(kFinishWG) k_finish_t(const uint64_t* __restri
   uint32_t cv[8];
   // stack depth <= popcount(j) + 1 <= log2(C) + 1
   if (C < (1ull << (kFinishDepth - 2)))
-    merge_nodes_flat<TILE>(nodes, s0, C, [&](int d) { return &lstack[threadIdx.x][d][0]; }, cv);
+    merge_nodes_flat<TILE>(nodes, s0, C, [&](int d) { return &lstack[threadIdx.x][8 * d]; }, cv);
   else
     merge_nodes_deep<TILE>(nodes, s0, C, cv);
   store_digest(perm ? perm[m] : m, cv, out32, out_keys);
