@@ -8,6 +8,11 @@ namespace sdcas {
 
 constexpr uint32_t kTile = 1024;  // chunk slots per workgroup tile (1 MiB of message bytes)
 constexpr uint32_t kWG = 512;     // threads per workgroup: 2 slots per lane
+// The shape sort's 256 bin counters and 256 bin cursors, each alone in a
+// 128-byte line: every workgroup adds to most of them, and packed into 8 lines
+// those atomics queued at 8 L2 channels.
+constexpr uint32_t kBinStride = 32;
+constexpr uint32_t kSortKeyWords = 2 * 256 * kBinStride;
 
 // Device workspace owned by the library context (caller never sees it).
 struct BatchWorkspace {
@@ -28,7 +33,7 @@ struct BatchWorkspace {
   uint32_t* perm = nullptr;        // [cap_msgs]
   uint64_t* soffs = nullptr;       // [cap_msgs]
   uint64_t* slens = nullptr;       // [cap_msgs]
-  uint32_t* sort_keys = nullptr;   // [512] shape-bin counts and cursors
+  uint32_t* sort_keys = nullptr;   // [kSortKeyWords] shape-bin counts and cursors, one 128-byte line each
 };
 
 size_t batch_scan_temp_bytes(uint32_t max_msgs);

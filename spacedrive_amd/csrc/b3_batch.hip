@@ -764,6 +764,7 @@ __global__ void __launch_bounds__(kFinishWG) k_finish_t(const uint64_t* __restri
 // reserves each workgroup's range per bin): order inside a bin is not
 // specified, which changes nothing but the slot a message lands in.
 constexpr uint32_t kShapeBins = 256;
+static_assert(kSortKeyWords == 2 * kShapeBins * kBinStride, "ws.sort_keys holds counts and cursors");
 constexpr uint32_t kScatterPerWG = 4096;
 constexpr uint32_t kSortMinMsgs = 128;  // smaller batches keep the caller's order
 constexpr uint32_t kHistPerThread = 8;
@@ -797,7 +798,7 @@ __global__ void __launch_bounds__(256) k_shape_hist(const uint64_t* __restrict__
       if (base + r * 256 + threadIdx.x < n) atomicAdd(&h[shape_key(L[r])], 1u);
   }
   __syncthreads();
-  if (h[threadIdx.x]) atomicAdd(&counts[threadIdx.x], h[threadIdx.x]);
+  if (h[threadIdx.x]) atomicAdd(&counts[threadIdx.x * kBinStride], h[threadIdx.x]);
 }
 
 // Scatter in two steps so that the global writes are coalesced: the
@@ -819,7 +820,8 @@ __global__ void __launch_bounds__(256) k_shape_scatter(const uint64_t* __restric
   __shared__ uint32_t few_chunks;
   const uint32_t t = threadIdx.x;
   // exclusive scan of the global bin counts (256 entries, one per thread)
-  gstart[t] = counts[t];
+  const uint32_t bin_count = counts[t * kBinStride];
+  gstart[t] = bin_count;
   h[t] = 0;
   __syncthreads();
   for (uint32_t d = 1; d < kShapeBins; d <<= 1) {
@@ -829,7 +831,7 @@ __global__ void __launch_bounds__(256) k_shape_scatter(const uint64_t* __restric
     __syncthreads();
   }
   if (t == kShapeManyChunks - 1) few_chunks = gstart[t];  // messages of < 15 chunks
-  const uint32_t excl = gstart[t] - counts[t];
+  const uint32_t excl = gstart[t] - bin_count;
   __syncthreads();
   gstart[t] = excl;
   const uint32_t lo = blockIdx.x * kScatterPerWG, hi = min(n, lo + kScatterPerWG), m = hi - lo;
@@ -875,7 +877,7 @@ __global__ void __launch_bounds__(256) k_shape_scatter(const uint64_t* __restric
   __syncthreads();
   // this workgroup's range in bin t, and the bin's start in the local order
   const uint32_t cnt = h[t];
-  if (cnt) gstart[t] += atomicAdd(&cursor[t], cnt);
+  if (cnt) gstart[t] += atomicAdd(&cursor[t * kBinStride], cnt);
   lstart[t] = cnt;
   __syncthreads();
   for (uint32_t d = 1; d < kShapeBins; d <<= 1) {
@@ -1415,12 +1417,12 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
   // A batch of a few messages fills a tile or two whatever their order: its
   // three sort launches would only add latency (the reference's 100-file step).
   if (ws.sort && n >= kSortMinMsgs && ws.perm) {
-    uint32_t* counts = ws.sort_keys;  // [256] bin sizes, [256] per-bin cursors
-    if ((e = hipMemsetAsync(counts, 0, 2 * kShapeBins * sizeof(uint32_t), st))) return e;
+    uint32_t* counts = ws.sort_keys;  // 256 bin sizes, then 256 per-bin cursors (kBinStride apart)
+    if ((e = hipMemsetAsync(counts, 0, kSortKeyWords * sizeof(uint32_t), st))) return e;
     const uint32_t hb = std::min<uint32_t>((n + 256 * kHistPerThread - 1) / (256 * kHistPerThread), 1024u);
     hipLaunchKernelGGL(k_shape_hist, dim3(hb), dim3(256), 0, st, lens, n, counts);
     hipLaunchKernelGGL(k_shape_scatter, dim3((n + kScatterPerWG - 1) / kScatterPerWG), dim3(256), 0, st, offs, lens,
-                       n, counts, counts + kShapeBins, ws.perm, ws.soffs, ws.slens);
+                       n, counts, counts + kShapeBins * kBinStride, ws.perm, ws.soffs, ws.slens);
     offs = ws.soffs;
     lens = ws.slens;
     perm = ws.perm;
