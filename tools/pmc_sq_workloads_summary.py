@@ -7,7 +7,8 @@ run printed).
 Also writes profiles/r02_pmc_<w>.json for C3 and C5 (the HBM traffic per
 launch in tools/pmc_summarize.py's format, which bench.py reads); C2's comes
 from tools/pmc_traffic.sh's dedicated passes.
-usage: pmc_sq_workloads_summary.py SRC DST"""
+usage: pmc_sq_workloads_summary.py SRC DST [VARIANT]   (VARIANT: the leaf variant the
+passes ran, tools/pmc_sq_workloads.sh's $VARIANT, default 52)"""
 import collections
 import csv
 import glob
@@ -30,8 +31,9 @@ XCDS = 8
 
 def main():
     src, dst = sys.argv[1], sys.argv[2]
+    variant = int(sys.argv[3]) if len(sys.argv) > 3 else 52
     out = {"source": "rocprofv3 --pmc passes (tools/pmc_sq_workloads.sh) over tools/ab_leaf.py --product "
-                     "--variants <VARIANT> (51 unless noted), one counter group per run; FETCH_SIZE x2 per MI355X_MICROARCH.md",
+                     f"--variants {variant}, one counter group per run; FETCH_SIZE x2 per MI355X_MICROARCH.md",
            "workloads": {}}
     for w, n in WORKLOADS:
         sizes, _, _ = bench.files_of(w, 0, n)
@@ -73,7 +75,8 @@ def main():
             "counters_median": m,
         }
     json.dump(out, open(dst, "w"), indent=1)
-    kernel = "k_leaf_tree<512, 109, 1, 1, 2, 2>"
+    # the kernel name bench.load_traffic matches against its default kernel
+    kernel = {51: "k_leaf_tree<512, 109, 1, 1, 2, 2>", 52: "k_leaf_tree<512, 209, 1, 1, 2, 2>"}[variant]
     for w in ("c3", "c5"):
         d = out["workloads"].get(w)
         if not d:
