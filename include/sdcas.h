@@ -104,16 +104,26 @@ typedef void (*sdcas_progress_fn)(void *user, uint64_t done, uint64_t total);
                                    Same bytes, same statuses. */
 
 typedef struct sdcas_options {
+  uint32_t struct_size;    /* sizeof(sdcas_options) as the caller compiled it (SDCAS_OPTIONS_INIT sets it):
+                              sdcas_init refuses any other size with SDCAS_E_INVALID, so a caller built
+                              against another revision of this struct fails loudly instead of passing
+                              garbage for the fields it lacks */
   int32_t device;          /* HIP device ordinal (-1: current device) */
   uint32_t io_threads;     /* reader threads of the path calls (0: 16, or the CPU count if lower; at most 256), started by the first one */
-  uint64_t staging_bytes;  /* pinned host staging per batch (0: 256 MiB) */
   uint32_t flags;          /* SDCAS_OPT_* */
-  uint32_t reserved;
-  sdcas_progress_fn progress;      /* may be NULL */
+  uint64_t staging_bytes;  /* pinned host staging per batch (0: 256 MiB) */
+  sdcas_progress_fn progress;      /* may be NULL; runs on the calling thread and must not call back into
+                                      the same context (its lock is held) */
   void *progress_user;             /* passed to progress */
   const volatile int32_t *cancel;  /* may be NULL; caller-owned, read atomically: nonzero cancels */
 } sdcas_options;
+#define SDCAS_OPTIONS_INIT {(uint32_t)sizeof(sdcas_options), -1, 0, 0, 0, NULL, NULL, NULL}
 
+/* "sdcas-mi355x <major>.<minor>.<patch> (gfx950)"; the C ABI of this header is
+ * SDCAS_ABI_VERSION (changes: 2 added sdcas_options.progress/cancel; 3 the
+ * struct_size field, sdcas_dedup_window and the dedup step plan) */
+#define SDCAS_ABI_VERSION 3
+int sdcas_abi_version(void);
 const char *sdcas_version(void);
 
 /* Create / destroy a context bound to one GPU. opts may be NULL. */
@@ -209,17 +219,55 @@ int sdcas_dev_stream_import(sdcas_ctx *ctx, const uint8_t *d_src, size_t bytes, 
 
 /* ---- dedup / link (file_identifier/mod.rs:149-254) --------------------- */
 
-/* Canonical group-by of the identifier step over n orphan file_paths in id
- * order, processed in chunks of chunk_size (0 -> 100). has_key[i] == 0 marks
- * a cas_id of None (empty file, mod.rs:78-86); status[i] != 0 drops the file
- * (may be NULL). existing_keys are the cas keys of Objects already in the
- * library, in DB order (may be NULL when n_existing == 0).
- * out_link[i] = i        file i creates a new Object
+/* out_link codes besides the ordinals (below) */
+#define SDCAS_LINK_DROPPED INT64_MIN             /* I/O error: the file is dropped (mod.rs:125-141) */
+#define SDCAS_LINK_DEFERRED (INT64_MIN + 1)      /* no step the job runs reaches the file: it stays an
+                                                    orphan for the next batch / job */
+
+/* The file identifier job's step loop around one batch of its orphans
+ * (file_identifier_job.rs:86-236). A step reads the next chunk_size orphans
+ * with id >= cursor and the cursor becomes its LAST row (:296-319,
+ * mod.rs:401-405), so a last row that stays an orphan — an I/O error, or a
+ * cas_id of None, which gets an Object but keeps cas_id NULL — is read again
+ * by the next step, and the job runs a fixed task_count = ceil(orphans /
+ * chunk_size) steps (:146). */
+typedef struct sdcas_job_window {
+  uint64_t max_steps; /* in: steps the job may still run; 0 = ceil(n / chunk_size), the task_count of a
+                         job whose orphans are exactly these n rows */
+  uint32_t more;      /* in: nonzero when more orphans follow row n-1: a step that would reach past it is
+                         not run (its rows are DEFERRED) */
+  uint32_t reserved;
+  uint64_t steps;     /* out: steps run over the batch */
+  uint64_t rows;      /* out: 1 + the last row the steps read (0: none); the job's next cursor is the id
+                         of row rows-1, which the next batch reads again if it is still an orphan */
+  uint64_t rereads;   /* out: rows read by two consecutive steps */
+} sdcas_job_window;
+
+/* Canonical group-by of the identifier steps over n orphan file_paths in id
+ * order, chunk_size rows per step (0 -> 100). has_key[i] == 0 marks a cas_id
+ * of None (empty file, mod.rs:78-86); status[i] != 0 drops the file (may be
+ * NULL). existing_keys are the cas keys of Objects already in the library,
+ * in DB order (may be NULL when n_existing == 0).
+ * out_link[i] = i        file i creates a new Object (its last, if two steps read it)
  *             = j < i    file i links to the Object created by file j
  *             = -(e+1)   file i links to existing Object e
- *             = INT64_MIN dropped
+ *             = SDCAS_LINK_DROPPED / SDCAS_LINK_DEFERRED
  * *out_created / *out_linked receive the counts identifier_job_step returns
- * (mod.rs:349). */
+ * (mod.rs:349), summed over the steps. window may be NULL: the whole job over
+ * these n rows. */
+int sdcas_dedup_window(sdcas_ctx *ctx, const uint64_t *keys, const uint8_t *has_key, const int32_t *status,
+                       size_t n, size_t chunk_size, const uint64_t *existing_keys, size_t n_existing,
+                       sdcas_job_window *window, int64_t *out_link, int64_t *out_created, int64_t *out_linked);
+/* The same steps' bookkeeping on the host, no device: window->steps / rows /
+ * rereads for these rows, out_step[i] = the step that first reads row i
+ * (UINT64_MAX if none does) and out_reads[i] = how many steps read it (each
+ * read of a row without cas_id creates an Object); both may be NULL. The job
+ * calls it before writing the cas_ids of the rows its steps read
+ * (mod.rs:157-178 precede the existing Object lookup of :181-188);
+ * sdcas_dedup_window returns the same window. */
+int sdcas_job_plan(const uint8_t *has_key, const int32_t *status, size_t n, size_t chunk_size,
+                   sdcas_job_window *window, uint64_t *out_step, uint32_t *out_reads);
+/* sdcas_dedup_window with window = NULL */
 int sdcas_dedup(sdcas_ctx *ctx, const uint64_t *keys, const uint8_t *has_key, const int32_t *status,
                 size_t n, size_t chunk_size, const uint64_t *existing_keys, size_t n_existing,
                 int64_t *out_link, int64_t *out_created, int64_t *out_linked);
@@ -230,6 +278,8 @@ int sdcas_dedup(sdcas_ctx *ctx, const uint64_t *keys, const uint8_t *has_key, co
  * orphan file_paths (and existing Objects) are sharded over ranks. The host
  * runs, on every rank, with its own communicator (RCCL all-to-all over xGMI;
  * spacedrive_amd/dist_dedup.py is the reference driver):
+ *   0. stays(files)      -> this rank's stays ordinals; all-gather them and
+ *      plan                 build the job's step plan (the same on every rank)
  *   1. combine(files)    -> records grouped by owner rank + per-file slot
  *      combine(existing) -> records grouped by owner rank (ids = DB order)
  *   2. all-to-all both record sets (counts from out_starts)
@@ -242,6 +292,15 @@ int sdcas_dedup(sdcas_ctx *ctx, const uint64_t *keys, const uint8_t *has_key, co
  * out_starts. The owner of a key is its top 12 bits (the 3-hex thumbnail
  * shard prefix) split into `world` equal ranges.
  *
+ * stays: the ordinals of this rank's files that stay orphans after their
+ *   step (d_status != 0 or d_has_key == 0; both may be NULL) -> d_stays[cap],
+ *   ascending, padded with UINT64_MAX; *d_count (device int64) = all of them,
+ *   also when more than cap (then gather them again with a larger cap).
+ * plan: d_stays = every rank's stays lists (n_stays entries in any order,
+ *   UINT64_MAX entries ignored); the job's orphans are ordinals [0, n_total);
+ *   max_steps / more as in sdcas_job_window -> d_plan (device u64,
+ *   SDCAS_PLAN_WORDS(n_stays)): word 2 the steps run, 3 rows and 8 rereads
+ *   (as in sdcas_job_window); the rest is the plan's own (dist_dedup.h).
  * combine: d_ids[n] ascending; d_has_key / d_status may be NULL (all
  *   present / all ok). Writes d_rec[2*u], d_rec[2*u+1] = (cas key, min id)
  *   per key (a key whose top 32 bits another key shares may take more
@@ -254,22 +313,29 @@ int sdcas_dedup(sdcas_ctx *ctx, const uint64_t *keys, const uint8_t *has_key, co
  * resolve: d_result[p] for received file record p = -(db+1) if existing
  *   Object db carries the key (the first in DB order), else the lowest orphan
  *   ordinal carrying it on any rank.
- * apply: d_result indexed by this rank's records (in send order); d_counts
- *   (2 x u64, zeroed by the caller) += (created, linked). */
+ * apply: d_result indexed by this rank's records (in send order); d_plan from
+ *   plan (NULL: no file of the job stays an orphan and its steps read every
+ *   row); d_counts (2 x u64, zeroed by the caller) += (created, linked). */
+#define SDCAS_PLAN_HEADER_WORDS 12
+#define SDCAS_PLAN_WORDS(n_stays) (SDCAS_PLAN_HEADER_WORDS + (n_stays))
+int sdcas_dev_dedup_stays(sdcas_ctx *ctx, const uint8_t *d_has_key, const int32_t *d_status, const uint64_t *d_ids,
+                          size_t n, size_t cap, uint64_t *d_stays, int64_t *d_count, void *stream);
+int sdcas_dev_dedup_plan(sdcas_ctx *ctx, const uint64_t *d_stays, size_t n_stays, uint64_t n_total,
+                         size_t chunk_size, uint64_t max_steps, uint32_t more, uint64_t *d_plan, void *stream);
 int sdcas_dev_dedup_combine(sdcas_ctx *ctx, const uint64_t *d_keys, const uint8_t *d_has_key,
                             const int32_t *d_status, const uint64_t *d_ids, size_t n, uint32_t world,
                             uint64_t *d_rec, uint32_t *d_slot, uint64_t *out_starts, void *stream);
 int sdcas_dev_dedup_resolve(sdcas_ctx *ctx, const uint64_t *d_frec, size_t nf, const uint64_t *d_erec,
                             size_t ne, int64_t *d_result, void *stream);
 int sdcas_dev_dedup_apply(sdcas_ctx *ctx, const uint64_t *d_ids, const uint32_t *d_slot, size_t n,
-                          const int64_t *d_result, size_t chunk_size, int64_t *d_link, uint64_t *d_counts,
-                          void *stream);
+                          const int64_t *d_result, size_t chunk_size, const uint64_t *d_plan, int64_t *d_link,
+                          uint64_t *d_counts, void *stream);
 /* The same two stages without any host synchronisation, for RCCL's
  * all-to-all with equal splits (spacedrive_amd/dist_dedup.py): the combine
  * writes owner r's records to bucket r of d_send (world x cap records of 16 B,
  * record p of bucket r at d_send[2 * (r * cap + p)]), d_counts[r] (device
  * int64) = its valid records, d_slot[i] = the bucket position r * cap + p of
- * file i's record, and sets *d_overflow (device u32) to 1 when some owner has
+ * file i, and sets *d_overflow (device u32) to 1 when some owner has
  * more than cap records (the buckets are then unusable: rerun the exact
  * stages). resolve_buckets answers the received buckets (world x fcap file
  * records, world x ecap existing records, the first d_fcounts[r] /
@@ -282,14 +348,18 @@ int sdcas_dev_dedup_combine_buckets(sdcas_ctx *ctx, const uint64_t *d_keys, cons
 int sdcas_dev_dedup_resolve_buckets(sdcas_ctx *ctx, const uint64_t *d_frec, size_t fcap, const int64_t *d_fcounts,
                                     const uint64_t *d_erec, size_t ecap, const int64_t *d_ecounts, uint32_t world,
                                     int64_t *d_result, void *stream);
-/* A world of one: the three stages without the combine (nothing is
- * exchanged, so files and existing Objects go straight into resolve's table):
- * the same d_link / d_counts as combine -> resolve -> apply. d_ekeys/d_eids
- * [ne]: existing Objects' cas keys and DB indices (may be NULL when ne == 0). */
+/* A world of one: the stages without the combine (nothing is exchanged, so
+ * files and existing Objects go straight into resolve's table, and the plan
+ * comes from this call's own stays rows): the same d_link / d_counts as
+ * stays -> plan -> combine -> resolve -> apply. d_ekeys/d_eids [ne]: existing
+ * Objects' cas keys and DB indices (may be NULL when ne == 0). d_ids lie in
+ * [0, n_total) (n_total 0: n); max_steps / more as in sdcas_job_window.
+ * d_plan_header (may be NULL) receives the plan's SDCAS_PLAN_HEADER_WORDS. */
 int sdcas_dev_dedup_local(sdcas_ctx *ctx, const uint64_t *d_keys, const uint8_t *d_has_key,
                           const int32_t *d_status, const uint64_t *d_ids, size_t n, const uint64_t *d_ekeys,
-                          const uint64_t *d_eids, size_t ne, size_t chunk_size, int64_t *d_link,
-                          uint64_t *d_counts, void *stream);
+                          const uint64_t *d_eids, size_t ne, size_t chunk_size, uint64_t n_total,
+                          uint64_t max_steps, uint32_t more, int64_t *d_link, uint64_t *d_counts,
+                          uint64_t *d_plan_header, void *stream);
 
 /* ---- helpers ------------------------------------------------------------ */
 

@@ -98,13 +98,16 @@ class Engine {
   // hash.rs:11-25 over a batch: path -> 64 lowercase hex
   std::vector<Result<std::string>> file_checksums(const std::vector<std::string>& paths);
 
-  // the canonical group-by of mod.rs:149-254 (sdcas_dedup encoding of out_link)
+  // the canonical group-by of mod.rs:149-254 over the job's steps
+  // (sdcas_dedup_window; sdcas_dedup encoding of out_link). window may be
+  // null: the whole job over these rows.
   struct Dedup {
     std::vector<int64_t> link;
     int64_t created = 0, linked = 0;
   };
   Dedup dedup(const std::vector<uint64_t>& keys, const std::vector<uint8_t>& has_key,
-              const std::vector<int32_t>& status, size_t chunk_size, const std::vector<uint64_t>& existing_keys);
+              const std::vector<int32_t>& status, size_t chunk_size, const std::vector<uint64_t>& existing_keys,
+              sdcas_job_window* window = nullptr);
 
   sdcas_ctx* raw() { return ctx_; }
 
@@ -320,25 +323,43 @@ struct FileMetadata {
 std::vector<Result<FileMetadata>> file_metadata_batch(Engine& engine,
                                                       const std::vector<std::pair<std::string, ObjectKind>>& files);
 
-// The DB half of identifier_job_step (mod.rs:157-342): write each file's
-// cas_id, look up the existing Objects of the batch's cas_ids, group (the
-// GPU's sdcas_dedup in identifier_job_step; any function with its encoding
-// here), create Objects and link. md[i] is file_paths[i]'s FileMetadata.
+// The DB half of the job's steps over a batch of its orphans (mod.rs:157-342
+// per step): write the cas_id of every row the steps read, look up the
+// existing Objects of their cas_ids, group (the GPU's sdcas_dedup_window in
+// identifier_job_step; any function with its encoding here), create Objects
+// and link. md[i] is file_paths[i]'s FileMetadata. window (in: max_steps,
+// more; out: steps, rows, rereads) may be null: the whole job over these rows.
+// The steps' bookkeeping comes from sdcas_job_plan before any write. A batch
+// must not hold a row to re-identify — an Object but no cas_id (the indexer
+// nulls cas_id of a changed file) — past its first step: its cas_id, written
+// in its own step, makes its Object an existing one for the steps after
+// (mod.rs:157-188); the job cuts its batches there (run_file_identifier_job),
+// and this function throws std::invalid_argument if one is left.
 using GroupBy = std::function<Engine::Dedup(const std::vector<uint64_t>& keys, const std::vector<uint8_t>& has_key,
                                             const std::vector<int32_t>& status,
-                                            const std::vector<uint64_t>& existing_keys)>;
+                                            const std::vector<uint64_t>& existing_keys, sdcas_job_window& window)>;
 std::pair<size_t, size_t> identifier_step_db(Library& db, const std::vector<FilePathRow>& file_paths,
-                                             const std::vector<Result<FileMetadata>>& md, const GroupBy& group_by);
+                                             const std::vector<Result<FileMetadata>>& md, const GroupBy& group_by,
+                                             sdcas_job_window* window = nullptr,
+                                             size_t chunk_size = SDCAS_IDENTIFIER_CHUNK_SIZE);
 
-// identifier_job_step (mod.rs:98-350) over `file_paths` in id order. A batch
-// longer than `chunk_size` (the reference's CHUNK_SIZE = 100) gives the
-// result of the reference's consecutive steps over its 100-row chunks: the
-// group-by keeps chunk semantics (intra-chunk duplicates each create an
-// Object; later chunks link to the first Object). Returns (total_created,
-// total_linked) as mod.rs:349 does.
+// sdcas_job_plan over the rows' FileMetadata: per row the step that first
+// reads it (UINT64_MAX: none) and how many steps read it
+struct StepPlan {
+  std::vector<uint64_t> step;
+  std::vector<uint32_t> reads;
+};
+StepPlan plan_steps(const std::vector<Result<FileMetadata>>& md, size_t chunk_size, sdcas_job_window& window);
+
+// identifier_job_step (mod.rs:98-350) over `file_paths` in id order: one
+// step of the reference per chunk_size rows (CHUNK_SIZE = 100), the cursor
+// rule included (a step's last row that stays an orphan is read again by the
+// next step). window as in identifier_step_db. Returns (total_created,
+// total_linked) as mod.rs:349 does, summed over the steps.
 std::pair<size_t, size_t> identifier_job_step(Engine& engine, Library& db, const Location& location,
                                               const std::vector<FilePathRow>& file_paths,
-                                              size_t chunk_size = SDCAS_IDENTIFIER_CHUNK_SIZE);
+                                              size_t chunk_size = SDCAS_IDENTIFIER_CHUNK_SIZE,
+                                              sdcas_job_window* window = nullptr);
 
 // FileIdentifierJobRunMetadata (file_identifier_job.rs:54-71)
 struct FileIdentifierJobRunMetadata {
@@ -347,23 +368,34 @@ struct FileIdentifierJobRunMetadata {
   size_t total_objects_created = 0;
   size_t total_objects_linked = 0;
   size_t total_objects_ignored = 0;
-  size_t steps = 0;
+  size_t steps = 0;           // the reference's steps
+  size_t batches = 0;         // fetches of `batch` rows
+  size_t rereads = 0;         // rows two consecutive steps read
   bool early_finish = false;  // JobError::EarlyFinish (file_identifier_job.rs:184-191)
 };
 
-// FileIdentifierJobInit (file_identifier_job.rs:33-37); batch = rows per step
-// (the reference fetches CHUNK_SIZE = 100; a multiple of 100 batches several
-// reference steps into one GPU call with identical results)
+// FileIdentifierJobInit (file_identifier_job.rs:33-37); batch = orphans
+// fetched per GPU call (the reference fetches CHUNK_SIZE = 100 per step; a
+// larger batch runs several of its steps in one call with identical results)
 struct FileIdentifierJobInit {
   Location location;
   std::string sub_materialized_path;  // "" or "/sub/dir/"
   size_t batch = SDCAS_IDENTIFIER_CHUNK_SIZE;
 };
 
-// init (count orphans, cursor = first orphan id, ceil(count / batch) steps)
-// then execute_step per step (fetch `batch` orphans with id >= cursor, run
-// identifier_job_step, advance the cursor to the last row)
+// init (count orphans, cursor = first orphan id, task_count = ceil(count /
+// CHUNK_SIZE) steps, file_identifier_job.rs:125-176), then batches: fetch
+// `batch` orphans with id >= cursor, run as many of the job's steps over them
+// as fit (identifier_job_step with a window), advance the cursor to the last
+// row the steps read (mod.rs:401-405). meta.steps counts the reference's
+// steps, meta.batches the fetches.
 FileIdentifierJobRunMetadata run_file_identifier_job(Engine& engine, Library& db, const FileIdentifierJobInit& init);
+
+// the same loop with any group-by (tests: the CPU oracle), metadata from
+// `metadata` (tests: synthetic) instead of the files
+using MetadataFn = std::function<std::vector<Result<FileMetadata>>(const std::vector<FilePathRow>& rows)>;
+FileIdentifierJobRunMetadata run_file_identifier_job_with(Library& db, const FileIdentifierJobInit& init,
+                                                          const MetadataFn& metadata, const GroupBy& group_by);
 
 // ---- object validator -----------------------------------------------------------
 

@@ -4,8 +4,9 @@
  * CPU restatement of sd-core's content identification:
  *   oracle_generate_cas_id   <- core/src/object/cas.rs:23-62
  *   oracle_file_checksum     <- core/src/object/validation/hash.rs:9-25
- *   oracle_identifier_dedup  <- core/src/object/file_identifier/mod.rs:98-350
- *                               (+ chunking, mod.rs:34 and file_identifier_job.rs:296-319)
+ *   oracle_identifier_job    <- core/src/object/file_identifier/mod.rs:98-350 inside the
+ *                               job's step loop (file_identifier_job.rs:86-236,296-319,
+ *                               mod.rs:380-407)
  * The I/O pattern is kept (one whole read, or header / 4 samples / footer with
  * seeks; 1 MiB reads for the checksum) so this file also serves as the
  * reference-faithful CPU baseline.
@@ -231,20 +232,55 @@ static void kmap_insert_first(kmap *m, uint64_t k, int64_t v) {
   m->vals[i] = v;
 }
 
-int64_t oracle_identifier_dedup(size_t n, const uint64_t *keys, const uint8_t *has_key,
-                                const int32_t *status, size_t chunk_size, size_t n_existing,
-                                const uint64_t *existing_keys, int64_t *out_link, int64_t *linked) {
+/* The file identifier job's step loop around identifier_job_step, restated
+ * literally over a simulated file_path table whose rows 0..n-1 (id order) are
+ * the job's orphans:
+ *   init        task_count = ceil(orphans / CHUNK_SIZE) (file_identifier_job.rs:126-146),
+ *               cursor = the first orphan's id (:152-173)
+ *   each step   get_orphan_file_paths: orphans with id >= cursor, ORDER BY id,
+ *               LIMIT CHUNK_SIZE (:296-319, filter :251-278: object_id IS NULL
+ *               OR cas_id IS NULL); no rows -> EarlyFinish (:203-209);
+ *               identifier_job_step over them (mod.rs:98-350); cursor = the
+ *               chunk's LAST row (mod.rs:401-405)
+ * A row that stays an orphan after its step — an I/O error (the file is
+ * dropped, mod.rs:125-141) or a cas_id of None (it gets an Object but keeps
+ * cas_id NULL, mod.rs:78-86,246-254) — is read again by the next step when it
+ * was its chunk's last row (id >= cursor), and every later chunk boundary
+ * shifts by one.
+ * win (may be NULL = {0, 0}) cuts the loop to a batch of a longer job:
+ * max_steps = the steps the job may still run (0: ceil(n / chunk_size)); more
+ * != 0 when further orphans follow row n-1, so a step that would reach past
+ * it is left to the next batch. Out: steps run, rows = last row of the last
+ * step + 1 (the next cursor is row rows-1; 0 if no step ran), rereads =
+ * steps that began with the previous step's last row. */
+int64_t oracle_identifier_job(size_t n, const uint64_t *keys, const uint8_t *has_key, const int32_t *status,
+                              size_t chunk_size, size_t n_existing, const uint64_t *existing_keys,
+                              oracle_job_window *win, int64_t *out_link, int64_t *linked) {
   kmap objects; /* cas key -> first Object carrying it (library state) */
   kmap_init(&objects, n + n_existing);
   for (size_t e = 0; e < n_existing; e++) kmap_insert_first(&objects, existing_keys[e], -(int64_t)e - 1);
-  int64_t created = 0, nlinked = 0;
   if (chunk_size == 0) chunk_size = 100;
-  for (size_t c0 = 0; c0 < n; c0 += chunk_size) {
-    size_t c1 = c0 + chunk_size < n ? c0 + chunk_size : n;
+  uint8_t *orphan = (uint8_t *)malloc(n ? n : 1);
+  size_t *rows = (size_t *)malloc(sizeof(size_t) * chunk_size);
+  memset(orphan, 1, n);
+  for (size_t i = 0; i < n; i++) out_link[i] = ORACLE_LINK_DEFERRED;
+  const uint64_t task_count = (win && win->max_steps) ? win->max_steps : (n + chunk_size - 1) / chunk_size;
+  const int more = win ? win->more : 0;
+  int64_t created = 0, nlinked = 0;
+  uint64_t steps = 0, rereads = 0, rows_done = 0;
+  size_t cursor = 0, prev_last = (size_t)-1;
+  for (uint64_t step = 0; step < task_count; step++) {
+    size_t m = 0;
+    for (size_t id = cursor; id < n && m < chunk_size; id++)
+      if (orphan[id]) rows[m++] = id;
+    if (m == 0) break;                    /* EarlyFinish */
+    if (more && m < chunk_size) break;    /* the step's other rows are in the next batch */
+    if (rows[0] == prev_last) rereads++;
     /* mod.rs:181-238: files whose cas_id already belongs to an Object link to
      * the first such Object; the lookup sees the library as it was before
-     * this chunk */
-    for (size_t i = c0; i < c1; i++) {
+     * this step */
+    for (size_t r = 0; r < m; r++) {
+      const size_t i = rows[r];
       if (status && status[i] != 0) {
         out_link[i] = INT64_MIN; /* mod.rs:125-141: logged and dropped */
         continue;
@@ -260,11 +296,34 @@ int64_t oracle_identifier_dedup(size_t n, const uint64_t *keys, const uint8_t *h
         created++;
       }
     }
-    /* objects created by this chunk become visible to later chunks (mod.rs:314-342) */
-    for (size_t i = c0; i < c1; i++)
-      if (out_link[i] == (int64_t)i && has_key[i]) kmap_insert_first(&objects, keys[i], (int64_t)i);
+    /* objects created by this step become visible to later steps (mod.rs:314-342);
+     * a file with a cas_id and an Object is no longer an orphan */
+    for (size_t r = 0; r < m; r++) {
+      const size_t i = rows[r];
+      if (status && status[i] != 0) continue;
+      if (!has_key[i]) continue;
+      if (out_link[i] == (int64_t)i) kmap_insert_first(&objects, keys[i], (int64_t)i);
+      orphan[i] = 0;
+    }
+    cursor = prev_last = rows[m - 1];
+    rows_done = (uint64_t)cursor + 1;
+    steps++;
   }
+  free(rows);
+  free(orphan);
   kmap_free(&objects);
+  if (win) {
+    win->steps = steps;
+    win->rows = rows_done;
+    win->rereads = rereads;
+  }
   if (linked) *linked = nlinked;
   return created;
+}
+
+int64_t oracle_identifier_dedup(size_t n, const uint64_t *keys, const uint8_t *has_key,
+                                const int32_t *status, size_t chunk_size, size_t n_existing,
+                                const uint64_t *existing_keys, int64_t *out_link, int64_t *linked) {
+  return oracle_identifier_job(n, keys, has_key, status, chunk_size, n_existing, existing_keys, NULL, out_link,
+                               linked);
 }

@@ -63,17 +63,37 @@ void oracle_synth_checksum(uint64_t content_key, uint64_t size, uint8_t out[32])
 /* build the cas message of a synthetic file into out (capacity >= msg len) */
 size_t oracle_synth_cas_message(uint64_t content_key, uint64_t size, uint8_t *out);
 
-/* Dedup/link restatement of file_identifier/mod.rs:98-350 in its canonical,
- * deterministic form. Files are the orphan
- * file_paths in id order, processed in chunks of `chunk_size` (CHUNK_SIZE=100,
- * mod.rs:34). status[i] != 0 drops the file (mod.rs:125-141); has_key[i] == 0
- * is an empty file (cas_id None, mod.rs:78-86). existing_keys[e] are the cas
- * keys of Objects already in the library, in DB order.
- * out_link[i]: i            -> file i creates a new Object
+/* Dedup/link restatement of file_identifier/mod.rs:98-350 inside the file
+ * identifier job's step loop (file_identifier_job.rs:86-236,296-319,
+ * mod.rs:380-407), in its canonical, deterministic form (SURVEY.md §8a rows
+ * a6/a7). Files are the job's orphan file_paths in id order; each step reads
+ * the next `chunk_size` orphans (CHUNK_SIZE=100, mod.rs:34) with id >= the
+ * cursor, which is the previous step's LAST row — so a last row that stays an
+ * orphan (status != 0, or no cas_id) is read again by the next step.
+ * status[i] != 0 drops the file (mod.rs:125-141); has_key[i] == 0 is a cas_id
+ * of None (mod.rs:78-86). existing_keys[e] are the cas keys of Objects
+ * already in the library, in DB order.
+ * out_link[i]: i            -> file i creates a new Object (the last one, if
+ *                              it was read twice)
  *              j (<i)       -> file i links to the Object created by file j
  *              -(e+1)       -> file i links to existing Object e
  *              INT64_MIN    -> dropped (status != 0)
- * Returns created count; *linked receives the linked count (mod.rs:349). */
+ *              INT64_MIN+1  -> not reached by the steps (ORACLE_LINK_DEFERRED)
+ * Returns the created count; *linked receives the linked count (mod.rs:349
+ * summed over the steps). */
+#define ORACLE_LINK_DEFERRED (INT64_MIN + 1)
+typedef struct oracle_job_window {
+  uint64_t max_steps; /* in: steps the job may still run (0: ceil(n / chunk_size)) */
+  int32_t more;       /* in: nonzero when more orphans follow row n-1 */
+  int32_t reserved;
+  uint64_t steps;     /* out: steps run */
+  uint64_t rows;      /* out: last row of the last step + 1 (0: none) */
+  uint64_t rereads;   /* out: steps that began with the previous step's last row */
+} oracle_job_window;
+int64_t oracle_identifier_job(size_t n, const uint64_t *keys, const uint8_t *has_key, const int32_t *status,
+                              size_t chunk_size, size_t n_existing, const uint64_t *existing_keys,
+                              oracle_job_window *win, int64_t *out_link, int64_t *linked);
+/* the whole job over the n rows (win = NULL) */
 int64_t oracle_identifier_dedup(size_t n, const uint64_t *keys, const uint8_t *has_key,
                                 const int32_t *status, size_t chunk_size, size_t n_existing,
                                 const uint64_t *existing_keys, int64_t *out_link, int64_t *linked);

@@ -26,15 +26,20 @@ SDCAS_STATUS_UNEXPECTED_EOF = 100001
 SDCAS_STATUS_CANCELLED = 125
 SDCAS_MAX_BATCH = 0x7FFFFFFF
 SDCAS_OPT_DIRECT_IO = 1
+SDCAS_ABI_VERSION = 3
+SDCAS_LINK_DROPPED = -(1 << 63)
+SDCAS_LINK_DEFERRED = SDCAS_LINK_DROPPED + 1
+SDCAS_PLAN_HEADER_WORDS = 12
 
 # every entry point include/sdcas.h and include/sdcas_bench.h declare
 ABI_SYMBOLS = [
-    "sdcas_version", "sdcas_init", "sdcas_destroy", "sdcas_last_error", "sdcas_cas_ids",
+    "sdcas_version", "sdcas_abi_version", "sdcas_init", "sdcas_destroy", "sdcas_last_error", "sdcas_cas_ids",
     "sdcas_checksums", "sdcas_hash_messages", "sdcas_cas_ids_from_messages", "sdcas_dev_reserve",
-    "sdcas_dev_hash_messages", "sdcas_dev_sync", "sdcas_dedup", "sdcas_key_to_hex",
+    "sdcas_dev_hash_messages", "sdcas_dev_sync", "sdcas_dedup", "sdcas_dedup_window", "sdcas_job_plan",
+    "sdcas_key_to_hex",
     "sdcas_digest_to_hex", "sdcas_cas_message_len", "sdcas_dev_dedup_combine", "sdcas_dev_dedup_resolve",
     "sdcas_dev_dedup_apply", "sdcas_dev_dedup_local", "sdcas_dev_dedup_combine_buckets",
-    "sdcas_dev_dedup_resolve_buckets", "sdcas_dev_stream_begin", "sdcas_dev_stream_update",
+    "sdcas_dev_dedup_resolve_buckets", "sdcas_dev_dedup_stays", "sdcas_dev_dedup_plan", "sdcas_dev_stream_begin", "sdcas_dev_stream_update",
     "sdcas_dev_stream_finish", "sdcas_dev_stream_node_bytes", "sdcas_dev_stream_export", "sdcas_dev_stream_import",
     "sdcas_set_progress",
     # bench / test plumbing
@@ -64,10 +69,20 @@ PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_
 
 
 class Options(ctypes.Structure):
-    _fields_ = [("device", ctypes.c_int32), ("io_threads", ctypes.c_uint32),
-                ("staging_bytes", ctypes.c_uint64), ("flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+    """sdcas_options; struct_size is set to this layout's size"""
+    _fields_ = [("struct_size", ctypes.c_uint32), ("device", ctypes.c_int32), ("io_threads", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32), ("staging_bytes", ctypes.c_uint64),
                 ("progress", PROGRESS_FN),
                 ("progress_user", ctypes.c_void_p), ("cancel", ctypes.POINTER(ctypes.c_int32))]
+
+    def __init__(self, *a, **k):
+        super().__init__(ctypes.sizeof(Options), *a, **k)
+
+
+class JobWindow(ctypes.Structure):
+    """sdcas_job_window"""
+    _fields_ = [("max_steps", ctypes.c_uint64), ("more", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("steps", ctypes.c_uint64), ("rows", ctypes.c_uint64), ("rereads", ctypes.c_uint64)]
 
 
 _lib = None
@@ -106,6 +121,9 @@ def load():
                           "(or __graft_entry__.build()) — there is no CPU fallback")
     L = ctypes.CDLL(_lib_path)
     L.sdcas_version.restype = ctypes.c_char_p
+    L.sdcas_abi_version.restype = ctypes.c_int
+    if L.sdcas_abi_version() != SDCAS_ABI_VERSION:
+        raise ImportError(f"{_lib_path} has C ABI {L.sdcas_abi_version()}, this binding {SDCAS_ABI_VERSION}: rebuild")
     L.sdcas_init.argtypes = [ctypes.POINTER(Options), ctypes.POINTER(_vp)]
     L.sdcas_destroy.argtypes = [_vp]
     L.sdcas_last_error.argtypes = [_vp]
@@ -118,6 +136,9 @@ def load():
     L.sdcas_dev_hash_messages.argtypes = [_vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp]
     L.sdcas_dev_sync.argtypes = [_vp, _vp]
     L.sdcas_dedup.argtypes = [_vp, _vp, _vp, _vp, _sz, _sz, _vp, _sz, _vp, _vp, _vp]
+    L.sdcas_job_plan.argtypes = [_vp, _vp, _sz, _sz, ctypes.POINTER(JobWindow), _vp, _vp]
+    L.sdcas_dedup_window.argtypes = [_vp, _vp, _vp, _vp, _sz, _sz, _vp, _sz, ctypes.POINTER(JobWindow), _vp, _vp,
+                                     _vp]
     L.sdcas_key_to_hex.argtypes = [_u64, ctypes.c_char_p]
     L.sdcas_digest_to_hex.argtypes = [_vp, ctypes.c_char_p]
     L.sdcas_cas_message_len.argtypes = [_u64]
@@ -137,8 +158,11 @@ def load():
     L.sdcas_dev_dedup_resolve_buckets.argtypes = [_vp, _vp, _sz, _vp, _vp, _sz, _vp, ctypes.c_uint32, _vp, _vp]
     L.sdcas_dev_dedup_combine.argtypes = [_vp, _vp, _vp, _vp, _vp, _sz, ctypes.c_uint32, _vp, _vp, _vp, _vp]
     L.sdcas_dev_dedup_resolve.argtypes = [_vp, _vp, _sz, _vp, _sz, _vp, _vp]
-    L.sdcas_dev_dedup_apply.argtypes = [_vp, _vp, _vp, _sz, _vp, _sz, _vp, _vp, _vp]
-    L.sdcas_dev_dedup_local.argtypes = [_vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _sz, _sz, _vp, _vp, _vp]
+    L.sdcas_dev_dedup_apply.argtypes = [_vp, _vp, _vp, _sz, _vp, _sz, _vp, _vp, _vp, _vp]
+    L.sdcas_dev_dedup_local.argtypes = [_vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _sz, _sz, _u64, _u64,
+                                        ctypes.c_uint32, _vp, _vp, _vp, _vp]
+    L.sdcas_dev_dedup_stays.argtypes = [_vp, _vp, _vp, _vp, _sz, _sz, _vp, _vp, _vp]
+    L.sdcas_dev_dedup_plan.argtypes = [_vp, _vp, _sz, _u64, _sz, _u64, ctypes.c_uint32, _vp, _vp]
     L.sdcas_dev_stream_begin.argtypes = [_vp, _vp, _sz]
     L.sdcas_dev_stream_update.argtypes = [_vp, _sz, _vp, _vp, _vp, _vp, _vp]
     L.sdcas_dev_stream_finish.argtypes = [_vp, _vp, _vp]

@@ -49,8 +49,50 @@ struct DistWs {
   Buf<uint64_t> tkey, tmin;  // resolve's hash table: keys, (files' min, existing min) per entry
   Buf<uint32_t> tpos;        // table entry of each received file record
   Buf<uint8_t> valid, temp;
+  Buf<uint32_t> stay_idx, nstay;  // the batch's stay-orphan rows (dd_local's plan)
+  Buf<uint64_t> plan, stay_sorted;
   void release();
 };
+
+// ---- the job's steps over the batch (file_identifier_job.rs:180-236) ----------
+//
+// The reference reads its orphans CHUNK_SIZE at a time with id >= cursor, the
+// cursor being the previous step's LAST row (file_identifier_job.rs:296-319,
+// mod.rs:401-405). A row that stays an orphan after its step (an I/O error,
+// mod.rs:125-141, or a cas_id of None, mod.rs:78-86 — "stays" rows) is read
+// again by the next step when it was the last row, so every later step starts
+// one row earlier. In the sequence of rows the steps read — a re-read row
+// twice — step k covers positions [k*cs, (k+1)*cs): file ordinal o sits at
+// position o + (re-reads of ordinals below o). The plan holds what that
+// needs: the re-read ordinals, found by one wave walking the sorted stays
+// ordinals, and the position limit of the steps the job may run.
+constexpr uint32_t kPlanHeader = 12;  // u64 words before the re-read ordinals (SDCAS_PLAN_HEADER_WORDS)
+enum : uint32_t {
+  kPlanLimit = 0,    // first position not run (steps * cs)
+  kPlanRereads = 1,  // re-read ordinals that follow the header (ascending)
+  kPlanSteps = 2,    // steps run
+  kPlanRows = 3,     // last ordinal the steps read + 1 (0: none)
+  kPlanNTotal = 4,
+  kPlanChunk = 5,
+  kPlanLoop = 6,       // a row every remaining step reads again (all-ones: none); rows after it are not reached
+  kPlanLoopReads = 7,  // how many steps read it
+  kPlanRereadsRun = 8, // rows two steps the job runs read (sdcas_job_window.rereads)
+};
+struct StepWindow {
+  uint64_t n_total = 0;    // the job's orphans are ordinals [0, n_total)
+  uint64_t max_steps = 0;  // steps the job may run (0: ceil(n_total / cs), file_identifier_job.rs:146)
+  uint32_t more = 0;       // more orphans follow ordinal n_total - 1: a step reaching past it is not run
+};
+
+// ordinals of this rank's stays rows -> out[0..cap) ascending, padded with
+// all-ones; count (device int64) = every stays row, even past cap (the
+// caller then gathers exactly)
+hipError_t dd_stays(DistWs& w, const uint8_t* has_key, const int32_t* status, const uint64_t* ids, uint32_t n,
+                    uint32_t cap, uint64_t* out, int64_t* count, hipStream_t st);
+// the plan from every rank's stays ordinals (n_stays entries in any order,
+// all-ones entries ignored) -> plan[kPlanHeader + n_stays] (device)
+hipError_t dd_plan(DistWs& w, const uint64_t* stays, uint32_t n_stays, uint64_t cs, const StepWindow& win,
+                   uint64_t* plan, hipStream_t st);
 
 // Stage 1. keys/has_key/status/ids: [n] (has_key, status may be null = all
 // present / all ok); ids ascending (the rank's files in orphan order, or the
@@ -92,14 +134,22 @@ hipError_t dd_resolve(DistWs& w, const uint64_t* frec, uint32_t nf, const uint64
 // rep id otherwise — a file in the chunk of the key's first file creates its
 // own Object (mod.rs:246-254), later chunks link to that file's Object.
 // counts[0..1] += (created, linked) (device, zeroed by the caller).
+// With a plan (may be null: no stays rows and the steps read every row),
+// chunks are the steps' positions, a file past the plan's limit is
+// SDCAS_LINK_DEFERRED, and a re-read file without cas_id creates a second
+// Object when its second read is inside the limit.
 hipError_t dd_apply(const uint64_t* ids, const uint32_t* slot, uint32_t n, const int64_t* result,
-                    uint64_t chunk_size, int64_t* link, unsigned long long* counts, hipStream_t st);
+                    uint64_t chunk_size, const uint64_t* plan, int64_t* link, unsigned long long* counts,
+                    hipStream_t st);
 
 // Stages 1-3 fused for a world of one (no exchange, so no combine): files
 // and existing Objects (ekeys/eids[ne], eids = DB order) go straight into the
-// resolve table. Same link / counts as combine -> resolve -> apply.
+// resolve table. Same link / counts as combine -> resolve -> apply. The plan
+// is built from this batch's own stays rows (a world of one holds them all)
+// into w.plan, whose header the caller may read after the call.
 hipError_t dd_local(DistWs& w, const uint64_t* keys, const uint8_t* has_key, const int32_t* status,
                     const uint64_t* ids, uint32_t n, const uint64_t* ekeys, const uint64_t* eids, uint32_t ne,
-                    uint64_t chunk_size, int64_t* link, unsigned long long* counts, hipStream_t st);
+                    uint64_t chunk_size, const StepWindow& win, int64_t* link, unsigned long long* counts,
+                    hipStream_t st);
 
 }  // namespace sdcas

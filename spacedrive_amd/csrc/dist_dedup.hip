@@ -26,6 +26,7 @@ namespace sdcas {
 namespace {
 
 constexpr uint32_t TB = 256;
+constexpr int64_t kLinkDeferred = INT64_MIN + 1;  // SDCAS_LINK_DEFERRED
 inline uint32_t blocks(uint32_t n) { return (n + TB - 1) / TB; }
 
 __global__ void k_dd_prepare(const uint8_t* __restrict__ has_key, const int32_t* __restrict__ status, uint32_t n,
@@ -109,32 +110,73 @@ __global__ void k_dd_starts(const uint64_t* __restrict__ rec, const uint32_t* __
   starts[r] = r == world ? U : lo;
 }
 
-__global__ void k_dd_apply(const uint64_t* __restrict__ ids, const uint32_t* __restrict__ slot, uint32_t n,
-                           const int64_t* __restrict__ result, uint64_t cs, int64_t* __restrict__ link,
-                           unsigned long long* __restrict__ counts) {
-  __shared__ unsigned long long sc[2];
-  if (threadIdx.x < 2) sc[threadIdx.x] = 0;
-  __syncthreads();
-  // grid-stride over a bounded grid: one global atomic pair per workgroup
-  // (thousands of workgroups adding to one address serialise in L2)
-  unsigned long long c = 0, l = 0;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const uint32_t s = slot[i];
-    const int64_t me = (int64_t)ids[i];
-    int64_t v;
-    if (s == kSlotDropped) {
-      v = INT64_MIN;
-    } else if (s == kSlotNoKey) {
-      v = me;  // mod.rs:246-254: a file without cas_id gets its own Object
-    } else {
-      const int64_t r = result[s];
-      if (r < 0) v = r;
-      else v = ((uint64_t)me / cs == (uint64_t)r / cs) ? me : r;  // created in the key's first chunk
-    }
-    link[i] = v;
-    if (v == me) c += 1;
-    else if (v != INT64_MIN) l += 1;
+// ---- the steps' positions (see dist_dedup.h, "the job's steps") -------------------
+
+struct PlanView {
+  const uint64_t* rr;  // re-read ordinals, ascending (null: none)
+  uint64_t nrr, limit;
+  uint64_t loop, loop_reads;  // a row read by every step left (~0: none)
+};
+
+__device__ __forceinline__ PlanView plan_view(const uint64_t* plan) {
+  if (!plan) return PlanView{nullptr, 0, ~0ull, ~0ull, 0};
+  return PlanView{plan + kPlanHeader, plan[kPlanRereads], plan[kPlanLimit], plan[kPlanLoop], plan[kPlanLoopReads]};
+}
+
+// re-read ordinals below x
+__device__ __forceinline__ uint64_t rr_below(const PlanView& pv, uint64_t x) {
+  uint64_t lo = 0, hi = pv.nrr;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (pv.rr[mid] < x) lo = mid + 1;
+    else hi = mid;
   }
+  return lo;
+}
+
+enum : int { kFileKeyed = 0, kFileNoKey = 1, kFileDropped = 2 };
+
+// identifier_job_step's outcome for one file over the job's steps
+// (mod.rs:125-141, 202-254): r = the key's answer for a keyed file (-(db+1)
+// existing Object, else the key's lowest ordinal)
+__device__ __forceinline__ int64_t step_link(int kind, int64_t me, int64_t r, uint64_t cs, const PlanView& pv,
+                                             unsigned long long& c, unsigned long long& l) {
+  if ((uint64_t)me >= pv.loop) {  // the repeated row, and the rows no step reaches after it
+    if ((uint64_t)me > pv.loop) return kLinkDeferred;
+    if (kind == kFileDropped) return INT64_MIN;
+    c += pv.loop_reads;  // a stays row: no cas_id, an Object per read
+    return me;
+  }
+  uint64_t pos = (uint64_t)me;
+  bool twice = false;
+  if (pv.rr) {
+    const uint64_t b = rr_below(pv, (uint64_t)me);
+    pos += b;
+    twice = b < pv.nrr && pv.rr[b] == (uint64_t)me;
+  }
+  if (pos >= pv.limit) return kLinkDeferred;  // no step the job runs reaches it
+  if (kind == kFileDropped) return INT64_MIN;
+  if (kind == kFileNoKey) {  // mod.rs:246-254: its own Object, per step that reads it
+    c += 1 + (twice && pos + 1 < pv.limit ? 1 : 0);
+    return me;
+  }
+  if (r < 0) {
+    l += 1;
+    return r;
+  }
+  // created in the key's first step: a file of that step creates its own
+  // Object (mod.rs:246-254), files of later steps link to the first one
+  const uint64_t rpos = pv.rr ? (uint64_t)r + rr_below(pv, (uint64_t)r) : (uint64_t)r;
+  if (pos / cs == rpos / cs) {
+    c += 1;
+    return me;
+  }
+  l += 1;
+  return r;
+}
+
+__device__ __forceinline__ void add_counts(unsigned long long c, unsigned long long l, unsigned long long* sc,
+                                           unsigned long long* counts) {
   for (int off = 32; off > 0; off >>= 1) {
     c += __shfl_down(c, off);
     l += __shfl_down(l, off);
@@ -147,6 +189,141 @@ __global__ void k_dd_apply(const uint64_t* __restrict__ ids, const uint32_t* __r
   if (threadIdx.x == 0 && counts) {
     atomicAdd(&counts[0], sc[0]);
     atomicAdd(&counts[1], sc[1]);
+  }
+}
+
+__global__ void k_dd_apply(const uint64_t* __restrict__ ids, const uint32_t* __restrict__ slot, uint32_t n,
+                           const int64_t* __restrict__ result, uint64_t cs, const uint64_t* __restrict__ plan,
+                           int64_t* __restrict__ link, unsigned long long* __restrict__ counts) {
+  __shared__ unsigned long long sc[2];
+  if (threadIdx.x < 2) sc[threadIdx.x] = 0;
+  __syncthreads();
+  const PlanView pv = plan_view(plan);
+  // grid-stride over a bounded grid: one global atomic pair per workgroup
+  // (thousands of workgroups adding to one address serialise in L2)
+  unsigned long long c = 0, l = 0;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t s = slot[i];
+    const int kind = s == kSlotDropped ? kFileDropped : s == kSlotNoKey ? kFileNoKey : kFileKeyed;
+    link[i] = step_link(kind, (int64_t)ids[i], kind == kFileKeyed ? result[s] : 0, cs, pv, c, l);
+  }
+  add_counts(c, l, sc, counts);
+}
+
+// stays rows: their step leaves them orphans (file_identifier_job.rs:258-264)
+struct StayPred {
+  const uint8_t* has_key;
+  const int32_t* status;
+  __host__ __device__ __forceinline__ bool operator()(const uint32_t& i) const {
+    return (status && status[i] != 0) || (has_key && !has_key[i]);
+  }
+};
+
+__global__ void k_stays_gather(const uint32_t* __restrict__ idx, const uint32_t* __restrict__ m_p,
+                               const uint64_t* __restrict__ ids, uint32_t cap, uint64_t* __restrict__ out,
+                               int64_t* __restrict__ count) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t m = *m_p;
+  if (j == 0 && count) *count = (int64_t)m;
+  if (j < cap) out[j] = j < m ? ids[idx[j]] : ~0ull;
+}
+
+// One wave walks the stays ordinals in order. Ordinal p ends a step — and is
+// read again by the next — when its position p + r is the step's last,
+// (p + r) % cs == cs - 1, r being the re-reads before it; the job's last
+// orphan is never read again by a step inside the batch. 64 candidates at a
+// time: the first lane whose test holds is a re-read; the lanes after it
+// test again with r + 1. Two cases repeat a row for every step left (the
+// reference re-reads it while its cursor stays put): chunks of one row
+// (each step's only row is its last), and steps the job may still run after
+// its last row when that row stays an orphan (only with max_steps above
+// what the rows need).
+__global__ __launch_bounds__(64) void k_plan_walk(const uint64_t* __restrict__ stays, const uint32_t* __restrict__ idx,
+                                                  const uint64_t* __restrict__ ids, uint32_t cap,
+                                                  const uint32_t* __restrict__ m_p, uint64_t n_total, uint64_t cs,
+                                                  uint64_t max_steps, uint32_t more, uint64_t* __restrict__ plan) {
+  const int lane = (int)threadIdx.x;
+  const uint32_t m = m_p ? min(*m_p, cap) : cap;
+  uint64_t* rr = plan + kPlanHeader;
+  uint64_t r = 0;
+  uint64_t first = ~0ull, last_stay = ~0ull;  // smallest / largest valid stays ordinal
+  for (uint32_t base = 0; base < m; base += 64) {
+    const uint32_t j = base + (uint32_t)lane;
+    uint64_t p = ~0ull;
+    if (j < m) p = idx ? ids[idx[j]] : stays[j];
+    const bool in = p < n_total;
+    const unsigned long long inm = __ballot(in);
+    if (inm) {
+      const int lo = __ffsll((long long)inm) - 1, hi = 63 - __clzll((long long)inm);
+      const uint64_t plo = __shfl(p, lo), phi = __shfl(p, hi);
+      if (first == ~0ull) first = plo;
+      last_stay = phi;
+    }
+    const bool cand = cs > 1 && in && p + 1 < n_total;
+    int last = -1;
+    for (;;) {
+      const bool hit = cand && lane > last && (p + r) % cs == cs - 1;
+      const unsigned long long mask = __ballot(hit);
+      if (!mask) break;
+      const int f = __ffsll((long long)mask) - 1;
+      if (lane == f) rr[r] = p;
+      ++r;
+      last = f;
+    }
+    if (__ballot(j < m && !in)) break;  // sorted: padding from here on
+  }
+  if (lane == 0) {
+    const uint64_t T = max_steps ? max_steps : (n_total + cs - 1) / cs;
+    uint64_t loop = ~0ull, reads = 0, steps, limit, rows = 0;
+    if (cs == 1 && first != ~0ull && first < T) {
+      // one-row steps: the first stays row is read by every step from its own on
+      loop = first;
+      reads = T - first;
+      steps = T;
+      limit = first;  // positions below the loop row are ordinary steps
+      rows = first + 1;
+    } else {
+      const uint64_t E = n_total + r;  // positions the rows take
+      const uint64_t avail = more ? E / cs : (E + cs - 1) / cs;
+      steps = avail < T ? avail : T;
+      limit = steps * cs;
+      if (steps) {
+        // the ordinal at the last position run: P minus the second reads at or before it
+        const uint64_t P = (limit < E ? limit : E) - 1;
+        uint64_t lo = 0, hi = r;  // second reads sit at rr[k] + k + 1
+        while (lo < hi) {
+          const uint64_t mid = (lo + hi) >> 1;
+          if (rr[mid] + mid + 1 <= P) lo = mid + 1;
+          else hi = mid;
+        }
+        rows = P - lo + 1;
+      }
+      if (!more && T > avail && n_total && last_stay == n_total - 1) {
+        loop = n_total - 1;  // steps left after the last row: each reads it again
+        reads = 1 + (T - avail);
+        steps = T;
+      }
+    }
+    plan[kPlanLimit] = limit;
+    plan[kPlanRereads] = r;
+    plan[kPlanSteps] = steps;
+    plan[kPlanRows] = rows;
+    plan[kPlanNTotal] = n_total;
+    plan[kPlanChunk] = cs;
+    plan[kPlanLoop] = loop;
+    plan[kPlanLoopReads] = reads;
+    uint64_t run = 0;  // re-reads whose second read is a step the job runs
+    {
+      uint64_t lo = 0, hi = r;
+      while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (rr[mid] + mid + 1 < limit) lo = mid + 1;
+        else hi = mid;
+      }
+      run = lo;
+    }
+    plan[kPlanRereadsRun] = run + (loop != ~0ull ? reads - 1 : 0);
+    plan[9] = plan[10] = plan[11] = 0;
   }
 }
 
@@ -178,6 +355,7 @@ void DistWs::release() {
   idx_a.release(); idx_b.release(); scan.release(); nvalid.release(); starts.release(); hi_a.release();
   hi_b.release(); tkey.release(); tmin.release(); tpos.release();
   valid.release(); temp.release();
+  stay_idx.release(); nstay.release(); plan.release(); stay_sorted.release();
 }
 
 // the combine up to its device outputs: rec, slot, w.starts[0..world] (n > 0)
@@ -494,51 +672,95 @@ __global__ void k_solo_insert(const uint64_t* __restrict__ keys, const uint8_t* 
 // k_dd_apply with the answer read from the file's own table entry
 __global__ void k_solo_apply(const uint64_t* __restrict__ ids, const uint32_t* __restrict__ pos, uint32_t n,
                              const uint64_t* __restrict__ tab, const uint64_t* __restrict__ emin, uint64_t cs,
-                             int64_t* __restrict__ link, unsigned long long* __restrict__ counts) {
+                             const uint64_t* __restrict__ plan, int64_t* __restrict__ link,
+                             unsigned long long* __restrict__ counts) {
   __shared__ unsigned long long sc[2];
   if (threadIdx.x < 2) sc[threadIdx.x] = 0;
   __syncthreads();
+  const PlanView pv = plan_view(plan);
   unsigned long long c = 0, l = 0;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint32_t h = pos[i];
-    const int64_t me = (int64_t)ids[i];
-    int64_t v;
-    if (h == kSlotDropped) {
-      v = INT64_MIN;
-    } else if (h == kSlotNoKey) {
-      v = me;  // mod.rs:246-254: a file without cas_id gets its own Object
-    } else {
+    const int kind = h == kSlotDropped ? kFileDropped : h == kSlotNoKey ? kFileNoKey : kFileKeyed;
+    int64_t r = 0;
+    if (kind == kFileKeyed) {
+      // mod.rs:202-238: the first existing Object; else the key's first file
       const uint64_t e = emin ? emin[h] : ~0ull;
-      // mod.rs:202-238: the first existing Object; else the key's first file,
-      // whose chunk creates one Object per file (mod.rs:246-254)
-      const int64_t r = e != ~0ull ? -(int64_t)e - 1 : (int64_t)tab[2 * (uint64_t)h + 1];
-      if (r < 0) v = r;
-      else v = ((uint64_t)me / cs == (uint64_t)r / cs) ? me : r;
+      r = e != ~0ull ? -(int64_t)e - 1 : (int64_t)tab[2 * (uint64_t)h + 1];
     }
-    link[i] = v;
-    if (v == me) c += 1;
-    else if (v != INT64_MIN) l += 1;
+    link[i] = step_link(kind, (int64_t)ids[i], r, cs, pv, c, l);
   }
-  for (int off = 32; off > 0; off >>= 1) {
-    c += __shfl_down(c, off);
-    l += __shfl_down(l, off);
+  add_counts(c, l, sc, counts);
+}
+
+hipError_t dd_stays(DistWs& w, const uint8_t* has_key, const int32_t* status, const uint64_t* ids, uint32_t n,
+                    uint32_t cap, uint64_t* out, int64_t* count, hipStream_t st) {
+  hipError_t e;
+  if ((e = w.nstay.ensure(1))) return e;
+  if (n == 0 || (!has_key && !status)) {
+    if ((e = hipMemsetAsync(w.nstay.p, 0, sizeof(uint32_t), st))) return e;
+  } else {
+    if ((e = w.stay_idx.ensure(n))) return e;
+    size_t need = 0;
+    (void)hipcub::DeviceSelect::If(nullptr, need, hipcub::CountingInputIterator<uint32_t>(0), w.stay_idx.p,
+                                   w.nstay.p, (int)n, StayPred{has_key, status}, st);
+    if ((e = w.temp.ensure(need + 256))) return e;
+    size_t tmp = w.temp.cap;
+    if ((e = hipcub::DeviceSelect::If(w.temp.p, tmp, hipcub::CountingInputIterator<uint32_t>(0), w.stay_idx.p,
+                                      w.nstay.p, (int)n, StayPred{has_key, status}, st)))
+      return e;
   }
-  if ((threadIdx.x & 63) == 0) {
-    atomicAdd(&sc[0], c);
-    atomicAdd(&sc[1], l);
+  const uint32_t g = cap ? cap : 1;
+  hipLaunchKernelGGL(k_stays_gather, dim3(blocks(g)), dim3(TB), 0, st, w.stay_idx.p, w.nstay.p, ids, cap, out, count);
+  return hipGetLastError();
+}
+
+hipError_t dd_plan(DistWs& w, const uint64_t* stays, uint32_t n_stays, uint64_t cs, const StepWindow& win,
+                   uint64_t* plan, hipStream_t st) {
+  hipError_t e;
+  const uint64_t* sorted = stays;
+  if (n_stays > 1) {
+    // the ranks' lists concatenated: one radix sort (all-ones padding last)
+    if ((e = w.stay_sorted.ensure(n_stays))) return e;
+    size_t need = 0;
+    (void)hipcub::DeviceRadixSort::SortKeys(nullptr, need, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                            (int)n_stays, 0, 64, st);
+    if ((e = w.temp.ensure(need + 256))) return e;
+    size_t tmp = w.temp.cap;
+    if ((e = hipcub::DeviceRadixSort::SortKeys(w.temp.p, tmp, stays, w.stay_sorted.p, (int)n_stays, 0, 64, st)))
+      return e;
+    sorted = w.stay_sorted.p;
   }
-  __syncthreads();
-  if (threadIdx.x == 0 && counts) {
-    atomicAdd(&counts[0], sc[0]);
-    atomicAdd(&counts[1], sc[1]);
-  }
+  hipLaunchKernelGGL(k_plan_walk, dim3(1), dim3(64), 0, st, sorted, (const uint32_t*)nullptr,
+                     (const uint64_t*)nullptr, n_stays, (const uint32_t*)nullptr, win.n_total, cs, win.max_steps,
+                     win.more, plan);
+  return hipGetLastError();
 }
 
 hipError_t dd_local(DistWs& w, const uint64_t* keys, const uint8_t* has_key, const int32_t* status,
                     const uint64_t* ids, uint32_t n, const uint64_t* ekeys, const uint64_t* eids, uint32_t ne,
-                    uint64_t chunk_size, int64_t* link, unsigned long long* counts, hipStream_t st) {
+                    uint64_t chunk_size, const StepWindow& win, int64_t* link, unsigned long long* counts,
+                    hipStream_t st) {
   hipError_t e;
-  if (n == 0) return hipSuccess;
+  if (chunk_size == 0) chunk_size = 100;
+  // the steps' plan from this batch's stays rows (all of the job's: a world of one)
+  if ((e = w.nstay.ensure(1)) || (e = w.plan.ensure(kPlanHeader + (uint64_t)n + 1))) return e;
+  if (n && (has_key || status)) {
+    if ((e = w.stay_idx.ensure(n))) return e;
+    size_t need = 0;
+    (void)hipcub::DeviceSelect::If(nullptr, need, hipcub::CountingInputIterator<uint32_t>(0), w.stay_idx.p,
+                                   w.nstay.p, (int)n, StayPred{has_key, status}, st);
+    if ((e = w.temp.ensure(need + 256))) return e;
+    size_t tmp = w.temp.cap;
+    if ((e = hipcub::DeviceSelect::If(w.temp.p, tmp, hipcub::CountingInputIterator<uint32_t>(0), w.stay_idx.p,
+                                      w.nstay.p, (int)n, StayPred{has_key, status}, st)))
+      return e;
+  } else if ((e = hipMemsetAsync(w.nstay.p, 0, sizeof(uint32_t), st))) {
+    return e;
+  }
+  hipLaunchKernelGGL(k_plan_walk, dim3(1), dim3(64), 0, st, (const uint64_t*)nullptr, w.stay_idx.p, ids, n,
+                     w.nstay.p, win.n_total ? win.n_total : (uint64_t)n, chunk_size, win.max_steps, win.more, w.plan.p);
+  if (n == 0) return hipGetLastError();
   uint64_t cap = 1024;
   while (cap < 2 * ((uint64_t)n + ne)) cap <<= 1;
   if (cap > (1ull << 31)) return hipErrorInvalidValue;
@@ -557,15 +779,15 @@ hipError_t dd_local(DistWs& w, const uint64_t* keys, const uint8_t* has_key, con
   hipLaunchKernelGGL(k_solo_insert, dim3(blocks(n)), dim3(TB), 0, st, keys, has_key, status, ids, n, tab,
                      (unsigned long long*)nullptr, mask, shift, w.tpos.p);
   hipLaunchKernelGGL(k_solo_apply, dim3(blocks(n) < 1024 ? blocks(n) : 1024), dim3(TB), 0, st, ids, w.tpos.p, n,
-                     w.tmin.p, ne ? w.tkey.p : nullptr, chunk_size ? chunk_size : 100, link, counts);
+                     w.tmin.p, ne ? w.tkey.p : nullptr, chunk_size, w.plan.p, link, counts);
   return hipGetLastError();
 }
 
 hipError_t dd_apply(const uint64_t* ids, const uint32_t* slot, uint32_t n, const int64_t* result, uint64_t chunk_size,
-                    int64_t* link, unsigned long long* counts, hipStream_t st) {
+                    const uint64_t* plan, int64_t* link, unsigned long long* counts, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_dd_apply, dim3(blocks(n) < 1024 ? blocks(n) : 1024), dim3(TB), 0, st, ids, slot, n, result, chunk_size ? chunk_size : 100,
-                     link, counts);
+  hipLaunchKernelGGL(k_dd_apply, dim3(blocks(n) < 1024 ? blocks(n) : 1024), dim3(TB), 0, st, ids, slot, n, result,
+                     chunk_size ? chunk_size : 100, plan, link, counts);
   return hipGetLastError();
 }
 

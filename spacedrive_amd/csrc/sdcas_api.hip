@@ -179,8 +179,11 @@ struct sdcas_ctx {
     return fail(e == hipErrorOutOfMemory ? SDCAS_E_OOM : SDCAS_E_HIP, "%s: %s", what, hipGetErrorString(e));
   }
   // before enqueuing on st: wait for the previous call's use of the scratch
+  // (also on the same stream handle: a handle value may have been reused by a
+  // new stream after the caller destroyed the old one; a same-stream wait is
+  // nearly free)
   hipError_t fence_in(hipStream_t st) {
-    if (!scratch_pending || st == scratch_st) return hipSuccess;
+    if (!scratch_pending) return hipSuccess;
     return hipStreamWaitEvent(st, scratch_ev, 0);
   }
   // after enqueuing on st
@@ -560,11 +563,14 @@ int run_big(sdcas_ctx* c, const std::vector<BigItem>& items, uint8_t* out32_host
 
 extern "C" {
 
-const char* sdcas_version(void) { return "sdcas-mi355x 0.1.0 (gfx950)"; }
+const char* sdcas_version(void) { return "sdcas-mi355x 0.3.0 (gfx950)"; }
+
+int sdcas_abi_version(void) { return SDCAS_ABI_VERSION; }
 
 int sdcas_init(const sdcas_options* opts, sdcas_ctx** out) {
   if (!out) return SDCAS_E_INVALID;
   *out = nullptr;
+  if (opts && opts->struct_size != sizeof(sdcas_options)) return SDCAS_E_INVALID;  // another revision of the struct
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return SDCAS_E_NO_DEVICE;
   auto* c = new sdcas_ctx();
@@ -635,6 +641,72 @@ int sdcas_set_progress(sdcas_ctx* c, sdcas_progress_fn progress, void* user, con
 }
 
 uint64_t sdcas_cas_message_len(uint64_t size) { return size <= kMin ? size + 8 : SDCAS_SAMPLED_MESSAGE_LEN; }
+
+// The host's copy of k_plan_walk (dist_dedup.hip; the rule is described
+// there): the job needs to know which rows its steps read before it writes
+// their cas_ids (mod.rs:157-178 precede the lookup of :181-188), and that
+// depends only on the rows' status and has_key.
+int sdcas_job_plan(const uint8_t* has_key, const int32_t* status, size_t n, size_t chunk_size,
+                   sdcas_job_window* win, uint64_t* out_step, uint32_t* out_reads) {
+  if (!win || (n && !has_key)) return SDCAS_E_INVALID;
+  const uint64_t cs = chunk_size ? chunk_size : SDCAS_IDENTIFIER_CHUNK_SIZE;
+  auto stays = [&](size_t i) { return (status && status[i] != 0) || !has_key[i]; };
+  std::vector<uint64_t> rr;  // re-read rows
+  size_t first = SIZE_MAX;
+  for (size_t p = 0; p < n; ++p) {
+    if (!stays(p)) continue;
+    if (first == SIZE_MAX) first = p;
+    if (cs > 1 && p + 1 < n && (p + rr.size()) % cs == cs - 1) rr.push_back(p);
+  }
+  const uint64_t T = win->max_steps ? win->max_steps : (n + cs - 1) / cs;
+  uint64_t loop = UINT64_MAX, reads = 0, steps, limit, rows = 0;
+  if (cs == 1 && first != SIZE_MAX && first < T) {
+    loop = first;
+    reads = T - first;
+    steps = T;
+    limit = first;
+    rows = first + 1;
+  } else {
+    const uint64_t E = n + rr.size();
+    const uint64_t avail = win->more ? E / cs : (E + cs - 1) / cs;
+    steps = std::min(avail, T);
+    limit = steps * cs;
+    if (steps) {
+      const uint64_t P = std::min(limit, E) - 1;
+      uint64_t k = 0;
+      while (k < rr.size() && rr[k] + k + 1 <= P) ++k;
+      rows = P - k + 1;
+    }
+    if (!win->more && T > avail && n && stays(n - 1)) {
+      loop = n - 1;
+      reads = 1 + (T - avail);
+      steps = T;
+    }
+  }
+  uint64_t run = 0;
+  while (run < rr.size() && rr[run] + run + 1 < limit) ++run;
+  win->steps = steps;
+  win->rows = rows;
+  win->rereads = run + (loop != UINT64_MAX ? reads - 1 : 0);
+  if (out_step || out_reads) {
+    size_t k = 0;
+    for (size_t i = 0; i < n; ++i) {
+      while (k < rr.size() && rr[k] < i) ++k;
+      const uint64_t pos = i + k;
+      uint64_t s = UINT64_MAX;
+      uint32_t r = 0;
+      if (loop != UINT64_MAX && i >= loop) {
+        if (i == loop) s = pos / cs, r = (uint32_t)std::min<uint64_t>(reads, UINT32_MAX);
+      } else if (pos < limit) {
+        s = pos / cs;
+        r = 1 + (k < rr.size() && rr[k] == i && pos + 1 < limit ? 1 : 0);
+      }
+      if (out_step) out_step[i] = s;
+      if (out_reads) out_reads[i] = r;
+    }
+  }
+  return SDCAS_OK;
+}
 
 void sdcas_key_to_hex(uint64_t key, char out[17]) {
   static const char* H = "0123456789abcdef";
@@ -1154,9 +1226,9 @@ static hipError_t iota(DevBuf<uint64_t>& b, size_t n, hipStream_t st) {
 // the resolve table holds 2 * (files + existing) entries, at most 2^31
 static bool dedup_fits(size_t n, size_t ne) { return (uint64_t)n + ne <= (1ull << 30); }
 
-int sdcas_dedup(sdcas_ctx* c, const uint64_t* keys, const uint8_t* has_key, const int32_t* status, size_t n,
-                size_t chunk_size, const uint64_t* existing_keys, size_t n_existing, int64_t* out_link,
-                int64_t* out_created, int64_t* out_linked) {
+int sdcas_dedup_window(sdcas_ctx* c, const uint64_t* keys, const uint8_t* has_key, const int32_t* status, size_t n,
+                       size_t chunk_size, const uint64_t* existing_keys, size_t n_existing, sdcas_job_window* win,
+                       int64_t* out_link, int64_t* out_created, int64_t* out_linked) {
   if (!c || (n && (!keys || !has_key || !out_link)) || (n_existing && !existing_keys)) return SDCAS_E_INVALID;
   if (!dedup_fits(n, n_existing))
     return c->fail(SDCAS_E_CAPACITY, "dedup of %zu files + %zu Objects exceeds 2^30", n, n_existing);
@@ -1178,17 +1250,36 @@ int sdcas_dedup(sdcas_ctx* c, const uint64_t* keys, const uint8_t* has_key, cons
   // files are ordinals 0..n-1 in orphan order, existing Objects 0..ne-1 in DB
   // order: one iota serves both (ids of the first min(n, ne) coincide)
   if ((e = iota(c->dd_ids, std::max(n, n_existing), st))) return c->hip_fail(e, "dedup ids");
+  StepWindow sw;
+  sw.n_total = n;
+  sw.max_steps = win ? win->max_steps : 0;
+  sw.more = win ? win->more : 0;
   if ((e = dd_local(c->dist, c->dd_keys.p, c->dd_has.p, status ? c->dd_status.p : nullptr, c->dd_ids.p, (uint32_t)n,
-                    c->dd_ekeys.p, c->dd_ids.p, (uint32_t)n_existing, chunk_size, c->dd_link.p, c->dd_counts.p, st)))
+                    c->dd_ekeys.p, c->dd_ids.p, (uint32_t)n_existing, chunk_size, sw, c->dd_link.p, c->dd_counts.p,
+                    st)))
     return c->hip_fail(e, "dedup");
   unsigned long long cnt[2] = {0, 0};
-  if (n && ((e = hipMemcpyAsync(out_link, c->dd_link.p, 8 * n, hipMemcpyDeviceToHost, st)) ||
-            (e = hipMemcpyAsync(cnt, c->dd_counts.p, sizeof cnt, hipMemcpyDeviceToHost, st))))
+  uint64_t hdr[kPlanHeader] = {};
+  if ((n && (e = hipMemcpyAsync(out_link, c->dd_link.p, 8 * n, hipMemcpyDeviceToHost, st))) ||
+      (e = hipMemcpyAsync(cnt, c->dd_counts.p, sizeof cnt, hipMemcpyDeviceToHost, st)) ||
+      (e = hipMemcpyAsync(hdr, c->dist.plan.p, sizeof hdr, hipMemcpyDeviceToHost, st)))
     return c->hip_fail(e, "dedup D2H");
   if ((e = hipStreamSynchronize(st))) return c->hip_fail(e, "dedup sync");
   if (out_created) *out_created = (int64_t)cnt[0];
   if (out_linked) *out_linked = (int64_t)cnt[1];
+  if (win) {
+    win->steps = hdr[kPlanSteps];
+    win->rows = hdr[kPlanRows];
+    win->rereads = hdr[kPlanRereadsRun];
+  }
   return SDCAS_OK;
+}
+
+int sdcas_dedup(sdcas_ctx* c, const uint64_t* keys, const uint8_t* has_key, const int32_t* status, size_t n,
+                size_t chunk_size, const uint64_t* existing_keys, size_t n_existing, int64_t* out_link,
+                int64_t* out_created, int64_t* out_linked) {
+  return sdcas_dedup_window(c, keys, has_key, status, n, chunk_size, existing_keys, n_existing, nullptr, out_link,
+                            out_created, out_linked);
 }
 
 int sdcas_dev_dedup(sdcas_ctx* c, const uint64_t* d_keys, const uint8_t* d_has_key, const int32_t* d_status,
@@ -1202,7 +1293,7 @@ int sdcas_dev_dedup(sdcas_ctx* c, const uint64_t* d_keys, const uint8_t* d_has_k
   if (d_counts && (e = hipMemsetAsync(d_counts, 0, 2 * sizeof(uint64_t), call.st))) return c->hip_fail(e, "counts");
   if ((e = iota(c->dd_ids, n, call.st))) return c->hip_fail(e, "dev_dedup ids");
   e = dd_local(c->dist, d_keys, d_has_key, d_status, c->dd_ids.p, (uint32_t)n, nullptr, nullptr, 0, chunk_size,
-               d_out_link, (unsigned long long*)d_counts, call.st);
+               StepWindow{}, d_out_link, (unsigned long long*)d_counts, call.st);
   return e ? c->hip_fail(e, "dev_dedup") : SDCAS_OK;
 }
 
@@ -1308,26 +1399,59 @@ int sdcas_dev_dedup_resolve_buckets(sdcas_ctx* c, const uint64_t* d_frec, size_t
 
 int sdcas_dev_dedup_local(sdcas_ctx* c, const uint64_t* d_keys, const uint8_t* d_has_key, const int32_t* d_status,
                           const uint64_t* d_ids, size_t n, const uint64_t* d_ekeys, const uint64_t* d_eids, size_t ne,
-                          size_t chunk_size, int64_t* d_link, uint64_t* d_counts, void* stream) {
+                          size_t chunk_size, uint64_t n_total, uint64_t max_steps, uint32_t more, int64_t* d_link,
+                          uint64_t* d_counts, uint64_t* d_plan_header, void* stream) {
   if (!c || (n && (!d_keys || !d_ids || !d_link)) || (ne && (!d_ekeys || !d_eids))) return SDCAS_E_INVALID;
   if (!dedup_fits(n, ne)) return c->fail(SDCAS_E_CAPACITY, "dedup_local: %zu + %zu records exceed 2^30", n, ne);
   DevCall call(c, stream);
   if (call.rc) return call.rc;
+  StepWindow sw;
+  sw.n_total = n_total;
+  sw.max_steps = max_steps;
+  sw.more = more;
   hipError_t e = dd_local(c->dist, d_keys, d_has_key, d_status, d_ids, (uint32_t)n, d_ekeys, d_eids, (uint32_t)ne,
-                          chunk_size ? chunk_size : SDCAS_IDENTIFIER_CHUNK_SIZE, d_link,
+                          chunk_size ? chunk_size : SDCAS_IDENTIFIER_CHUNK_SIZE, sw, d_link,
                           (unsigned long long*)d_counts, call.st);
+  if (!e && d_plan_header)
+    e = hipMemcpyAsync(d_plan_header, c->dist.plan.p, 8 * kPlanHeader, hipMemcpyDeviceToDevice, call.st);
   return e ? c->hip_fail(e, "dedup_local") : SDCAS_OK;
 }
 
+int sdcas_dev_dedup_stays(sdcas_ctx* c, const uint8_t* d_has_key, const int32_t* d_status, const uint64_t* d_ids,
+                          size_t n, size_t cap, uint64_t* d_stays, int64_t* d_count, void* stream) {
+  if (!c || (n && (d_has_key || d_status) && !d_ids) || (cap && !d_stays)) return SDCAS_E_INVALID;
+  if (n > SDCAS_MAX_BATCH || cap > SDCAS_MAX_BATCH)
+    return c->fail(SDCAS_E_CAPACITY, "dedup_stays: %zu files / %zu entries exceed 2^31 - 1", n, cap);
+  DevCall call(c, stream);
+  if (call.rc) return call.rc;
+  hipError_t e = dd_stays(c->dist, d_has_key, d_status, d_ids, (uint32_t)n, (uint32_t)cap, d_stays, d_count, call.st);
+  return e ? c->hip_fail(e, "dedup_stays") : SDCAS_OK;
+}
+
+int sdcas_dev_dedup_plan(sdcas_ctx* c, const uint64_t* d_stays, size_t n_stays, uint64_t n_total, size_t chunk_size,
+                         uint64_t max_steps, uint32_t more, uint64_t* d_plan, void* stream) {
+  if (!c || !d_plan || (n_stays && !d_stays)) return SDCAS_E_INVALID;
+  if (n_stays > SDCAS_MAX_BATCH) return c->fail(SDCAS_E_CAPACITY, "dedup_plan: %zu entries exceed 2^31 - 1", n_stays);
+  DevCall call(c, stream);
+  if (call.rc) return call.rc;
+  StepWindow sw;
+  sw.n_total = n_total;
+  sw.max_steps = max_steps;
+  sw.more = more;
+  hipError_t e = dd_plan(c->dist, d_stays, (uint32_t)n_stays, chunk_size ? chunk_size : SDCAS_IDENTIFIER_CHUNK_SIZE,
+                         sw, d_plan, call.st);
+  return e ? c->hip_fail(e, "dedup_plan") : SDCAS_OK;
+}
+
 int sdcas_dev_dedup_apply(sdcas_ctx* c, const uint64_t* d_ids, const uint32_t* d_slot, size_t n,
-                          const int64_t* d_result, size_t chunk_size, int64_t* d_link, uint64_t* d_counts,
-                          void* stream) {
+                          const int64_t* d_result, size_t chunk_size, const uint64_t* d_plan, int64_t* d_link,
+                          uint64_t* d_counts, void* stream) {
   if (!c || (n && (!d_ids || !d_slot || !d_link))) return SDCAS_E_INVALID;
   if (n > SDCAS_MAX_BATCH) return c->fail(SDCAS_E_CAPACITY, "dedup_apply: %zu files exceed 2^31 - 1", n);
   DevCall call(c, stream);
   if (call.rc) return call.rc;
   hipError_t e = dd_apply(d_ids, d_slot, (uint32_t)n, d_result, chunk_size ? chunk_size : SDCAS_IDENTIFIER_CHUNK_SIZE,
-                          d_link, (unsigned long long*)d_counts, call.st);
+                          d_plan, d_link, (unsigned long long*)d_counts, call.st);
   return e ? c->hip_fail(e, "dedup_apply") : SDCAS_OK;
 }
 

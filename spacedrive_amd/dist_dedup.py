@@ -101,9 +101,11 @@ class DeviceStages:
         self.eng._check(rc, "sdcas_dev_dedup_resolve")
         return result[:nf]
 
-    def local(self, keys, has_key, status, ids, chunk_size, existing_keys=None, existing_ids=None):
-        """combine + resolve + apply for a world of one (nothing to exchange,
-        so no combine): -> (link int64[n], counts int64[2]) on the device"""
+    def local(self, keys, has_key, status, ids, chunk_size, existing_keys=None, existing_ids=None, n_total=0,
+              max_steps=0, more=False, header=None):
+        """stays + plan + combine + resolve + apply for a world of one (nothing
+        to exchange, so no combine): -> (link int64[n], counts int64[2]) on
+        the device; `header` (int64[8] device tensor) receives the plan's header"""
         n = int(ids.numel())
         link = torch.empty(max(n, 1), dtype=torch.int64, device=ids.device)
         counts = torch.zeros(2, dtype=torch.int64, device=ids.device)
@@ -111,10 +113,36 @@ class DeviceStages:
         p = lambda t: t.data_ptr() if t is not None and t.numel() else None
         rc = self.eng.L.sdcas_dev_dedup_local(self.eng.ctx, p(keys), p(has_key), p(status), p(ids), n,
                                               p(existing_keys) if ne else None, p(existing_ids) if ne else None,
-                                              ne, int(chunk_size), p(link), counts.data_ptr(), self._enter())
-        self._leave(keys, has_key, status, ids, existing_keys, existing_ids, link, counts)
+                                              ne, int(chunk_size), int(n_total), int(max_steps), int(bool(more)),
+                                              p(link), counts.data_ptr(), p(header), self._enter())
+        self._leave(keys, has_key, status, ids, existing_keys, existing_ids, link, counts, header)
         self.eng._check(rc, "sdcas_dev_dedup_local")
         return link[:n], counts
+
+    def stays(self, has_key, status, ids, cap):
+        """-> (this rank's stays ordinals int64[cap] padded with -1 (all ones),
+        their count int64[1]), on the device"""
+        n = int(ids.numel())
+        out = torch.empty(max(cap, 1), dtype=torch.int64, device=ids.device)
+        count = torch.empty(1, dtype=torch.int64, device=ids.device)
+        p = lambda t: t.data_ptr() if t is not None and t.numel() else None
+        rc = self.eng.L.sdcas_dev_dedup_stays(self.eng.ctx, p(has_key), p(status), p(ids), n, int(cap), p(out),
+                                              count.data_ptr(), self._enter())
+        self._leave(has_key, status, ids, out, count)
+        self.eng._check(rc, "sdcas_dev_dedup_stays")
+        return out[:cap], count
+
+    def plan(self, stays, n_total, chunk_size, max_steps=0, more=False):
+        """every rank's stays ordinals (any order, -1 = padding) -> the job's
+        step plan int64[SDCAS_PLAN_HEADER_WORDS + len] on the device"""
+        m = int(stays.numel())
+        plan = torch.empty(N.SDCAS_PLAN_HEADER_WORDS + m, dtype=torch.int64, device=stays.device)
+        rc = self.eng.L.sdcas_dev_dedup_plan(self.eng.ctx, stays.data_ptr() if m else None, m, int(n_total),
+                                             int(chunk_size), int(max_steps), int(bool(more)), plan.data_ptr(),
+                                             self._enter())
+        self._leave(stays, plan)
+        self.eng._check(rc, "sdcas_dev_dedup_plan")
+        return plan
 
     def combine_buckets(self, keys, has_key, status, ids, world, cap, need_slot=True):
         """-> (send int64[world * cap, 2], slot int32[n] or None, counts int64[world],
@@ -143,15 +171,15 @@ class DeviceStages:
         self.eng._check(rc, "sdcas_dev_dedup_resolve_buckets")
         return result[: world * fcap]
 
-    def apply(self, ids, slot, result, chunk_size):
+    def apply(self, ids, slot, result, chunk_size, plan=None):
         """-> (link int64[n], counts int64[2] = (created, linked)) on the device"""
         n = int(ids.numel())
         link = torch.empty(max(n, 1), dtype=torch.int64, device=ids.device)
         counts = torch.zeros(2, dtype=torch.int64, device=ids.device)
-        p = lambda t: t.data_ptr() if t.numel() else None
+        p = lambda t: t.data_ptr() if t is not None and t.numel() else None
         rc = self.eng.L.sdcas_dev_dedup_apply(self.eng.ctx, p(ids), p(slot), n, p(result), int(chunk_size),
-                                              p(link), counts.data_ptr(), self._enter())
-        self._leave(ids, slot, result, link, counts)
+                                              p(plan), p(link), counts.data_ptr(), self._enter())
+        self._leave(ids, slot, result, plan, link, counts)
         self.eng._check(rc, "sdcas_dev_dedup_apply")
         return link[:n], counts
 
@@ -171,8 +199,33 @@ def _exchange(send, send_counts, group, recv_counts=None):
     return recv, recv_counts
 
 
+_META_GROUPS = {}
+
+
+def _meta_group(group):
+    """a gloo group over the same ranks for host-known integers (file and
+    Object counts): exchanging them never waits for the device"""
+    if dist.get_backend(group) == "gloo":
+        return group
+    key = id(group)
+    if key not in _META_GROUPS:
+        ranks = dist.get_process_group_ranks(group) if group is not None else None
+        _META_GROUPS[key] = dist.new_group(ranks=ranks, backend="gloo")
+    return _META_GROUPS[key]
+
+
+def _meta(n, ne, group):
+    """every rank's (files, existing Objects) -> int64[world, 2] on the host"""
+    world = dist.get_world_size(group)
+    mine = torch.tensor([n, ne], dtype=torch.int64)
+    parts = [torch.empty(2, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(parts, mine, group=_meta_group(group))
+    return torch.stack(parts).numpy()
+
+
 def identifier_dedup_distributed(stages, keys, has_key, status, ids, chunk_size=100,
-                                 existing_keys=None, existing_ids=None, group=None, counts_on_device=False):
+                                 existing_keys=None, existing_ids=None, group=None, counts_on_device=False,
+                                 n_total=0, max_steps=0, more=False):
     """This rank's share of the identifier group-by.
 
     keys/has_key/status/ids: this rank's orphan file_paths (ids = their global
@@ -183,8 +236,13 @@ def identifier_dedup_distributed(stages, keys, has_key, status, ids, chunk_size=
     this (it is collective). Returns (link int64[n], created, linked): link
     uses sdcas_dedup's encoding with global ordinals (i = creates, j = links
     to the Object created by file j, -(e+1) = existing Object e, INT64_MIN =
-    dropped); created/linked are the node-wide totals identifier_job_step
-    would return summed over the job (mod.rs:349).
+    dropped, INT64_MIN + 1 = deferred); created/linked are the node-wide
+    totals identifier_job_step returns summed over the job's steps (mod.rs:349).
+
+    The steps (file_identifier_job.rs:180-236; sdcas_job_window): the job's
+    orphans are ordinals [0, n_total) (0: the sum of every rank's files),
+    the job may run max_steps more steps (0: ceil(n_total / chunk_size)),
+    more = further orphans follow ordinal n_total - 1.
 
     counts_on_device: in a world of one, return (link, counts) with counts an
     int64[2] device tensor (created, linked) instead of two ints, so that the
@@ -199,37 +257,87 @@ def identifier_dedup_distributed(stages, keys, has_key, status, ids, chunk_size=
     # that offer the fused single-rank path take it
     if world == 1 and hasattr(stages, "local"):
         stages.last_protocol = "local"
-        link, cnt = stages.local(keys, has_key, status, ids, chunk_size, existing_keys, existing_ids)
+        link, cnt = stages.local(keys, has_key, status, ids, chunk_size, existing_keys, existing_ids,
+                                 n_total or int(ids.numel()), max_steps, more)
         if counts_on_device:
             return link, cnt
         c = cnt.tolist()
         return link, int(c[0]), int(c[1])
-    caps = getattr(stages, "bucket_caps", None)
-    if world > 1 and caps is not None and hasattr(stages, "combine_buckets"):
+    n, ne = int(ids.numel()), int(existing_keys.numel()) if existing_keys is not None else 0
+    meta = _meta(n, ne, group) if world > 1 else np.array([[n, ne]], np.int64)
+    win = dict(n_total=int(n_total) or int(meta[:, 0].sum()), max_steps=int(max_steps), more=bool(more),
+               max_n=int(meta[:, 0].max()), max_ne=int(meta[:, 1].max()))
+    if existing_keys is not None and int(meta[:, 1].sum()) == 0:
+        existing_keys = existing_ids = None  # nobody holds an existing Object: nothing to exchange for them
+    if world > 1 and hasattr(stages, "combine_buckets"):
         stages.last_protocol = "buckets"
-        out = _dedup_buckets(stages, world, caps, keys, has_key, status, ids, chunk_size, existing_keys,
-                             existing_ids, group)
+        out = _dedup_buckets(stages, world, keys, has_key, status, ids, chunk_size, existing_keys,
+                             existing_ids, group, win)
         if out is not None:
             return out
         stages.last_protocol = "buckets-overflow"
     else:
         stages.last_protocol = "exact"
-    return _dedup_exact(stages, world, keys, has_key, status, ids, chunk_size, existing_keys, existing_ids, group)
+    return _dedup_exact(stages, world, keys, has_key, status, ids, chunk_size, existing_keys, existing_ids, group,
+                        win)
 
 
-def _next_caps(stages, fill_f, fill_e):
-    """bucket capacities for the next call from the node's largest buckets of
-    this one (identical on every rank: the fills are all-reduced maxima)"""
-    def cap(fill, old):
-        want = int(fill * 1.125) + 256
-        # keep the old capacity unless it overflowed or is more than twice too big
-        return old if old and fill <= old and old <= 2 * want else want
-    old = getattr(stages, "bucket_caps", None) or (0, 0)
-    stages.bucket_caps = (cap(fill_f, old[0]), cap(fill_e, old[1]) if fill_e >= 0 else 0)
+def _cap(fill, n_prev, n_now):
+    """a bucket capacity for n_now items from a fill seen at n_prev items"""
+    return int(fill * max(1.0, n_now / max(n_prev, 1)) * 1.125) + 256
 
 
-def _dedup_exact(stages, world, keys, has_key, status, ids, chunk_size, existing_keys, existing_ids, group):
+def _caps(stages, world, win, has_ex):
+    """(file, existing, stays) bucket capacities, identical on every rank
+    (they follow from all-gathered counts and all-reduced fills): the last
+    call's largest buckets scaled to this call's largest share, or — on a
+    stages object's first call — an even split of the largest share (owners
+    are key ranges of uniform BLAKE3 output) with 12.5 % + 256 headroom"""
+    forced = stages.__dict__.pop("force_caps", None)  # tests: one call's capacities chosen by the caller
+    if forced is not None:
+        return forced[0], forced[1] if has_ex else 0, forced[2] if len(forced) > 2 else 256
+    seen = getattr(stages, "bucket_seen", None)
+    if seen is None:
+        f = _cap(win["max_n"] / world, 1, 1)
+        e = _cap(win["max_ne"] / world, 1, 1) if has_ex else 0
+        s = 256
+    else:
+        f = _cap(seen["fill_f"], seen["max_n"], win["max_n"])
+        e = _cap(max(seen["fill_e"], 0), seen["max_ne"], win["max_ne"]) if has_ex else 0
+        s = _cap(seen["fill_s"], seen["max_n"], win["max_n"])
+    return f, e, s
+
+
+def _learn(stages, win, fill_f, fill_e, fill_s):
+    """what this call's buckets held (all-reduced maxima), for the next call"""
+    stages.bucket_seen = dict(fill_f=int(fill_f), fill_e=int(fill_e), fill_s=int(fill_s), max_n=win["max_n"],
+                              max_ne=win["max_ne"])
+    f, e, _ = _caps(stages, 1, win, True)
+    stages.bucket_caps = (f, e)  # (reported by the bench; the next call rescales)
+
+
+def _plan(stages, has_key, status, ids, chunk_size, win, group, world, cap, exact=False):
+    """the job's step plan from every rank's stays rows: an equal-split
+    all-gather of cap ordinals per rank. -> (plan or None, this rank's stays
+    count (device int64[1]))"""
+    if has_key is None and status is None and not win["more"] and not win["max_steps"]:
+        return None, None  # no stays rows and every row within the job's steps: fixed chunks
+    st, cnt = stages.stays(has_key, status, ids, cap)
+    if exact:
+        cs = [torch.empty_like(cnt) for _ in range(world)]
+        dist.all_gather(cs, cnt, group=group)
+        cap2 = max(1, max(int(c.item()) for c in cs))
+        if cap2 > cap:
+            st, cnt = stages.stays(has_key, status, ids, cap2)
+            cap = cap2
+    parts = [torch.empty_like(st) for _ in range(world)]
+    dist.all_gather(parts, st.contiguous(), group=group)
+    return stages.plan(torch.cat(parts), win["n_total"], chunk_size, win["max_steps"], win["more"]), cnt
+
+
+def _dedup_exact(stages, world, keys, has_key, status, ids, chunk_size, existing_keys, existing_ids, group, win):
     solo = world == 1
+    plan, scnt = _plan(stages, has_key, status, ids, chunk_size, win, group, world, 256, exact=True)
     rec, slot, starts = stages.combine(keys, has_key, status, ids, world)
     counts = [starts[r + 1] - starts[r] for r in range(world)]
     ecounts = [0] * world
@@ -260,18 +368,19 @@ def _dedup_exact(stages, world, keys, has_key, status, ids, chunk_size, existing
     # the answers retrace the file records' route: this rank receives back
     # exactly what it sent
     back = answer if solo else _exchange(answer, fcounts, group, recv_counts=counts)[0]
-    link, cnt = stages.apply(ids, slot, back, chunk_size)
+    link, cnt = stages.apply(ids, slot, back, chunk_size, plan)
     if solo:
         c = cnt.tolist()
         return link, int(c[0]), int(c[1])
     # totals, and the node's largest buckets for the next call's capacities
-    fills = torch.tensor([max(counts), max(ecounts) if existing_keys is not None else -1],
-                         dtype=torch.int64, device=cnt.device)
+    fills = torch.stack([torch.tensor(max(counts), dtype=torch.int64),
+                         torch.tensor(max(ecounts) if existing_keys is not None else -1, dtype=torch.int64),
+                         (scnt.cpu()[0] if scnt is not None else torch.tensor(0, dtype=torch.int64))]).to(cnt.device)
     dist.all_reduce(cnt, group=group)
     dist.all_reduce(fills, op=dist.ReduceOp.MAX, group=group)
     c, f = cnt.tolist(), fills.tolist()
     if hasattr(stages, "combine_buckets"):
-        _next_caps(stages, int(f[0]), int(f[1]))
+        _learn(stages, win, f[0], f[1], f[2])
     return link, int(c[0]), int(c[1])
 
 
@@ -296,16 +405,16 @@ class _Trace:
             print("dedup buckets ms: " + ", ".join(self.parts), file=sys.stderr, flush=True)
 
 
-def _dedup_buckets(stages, world, caps, keys, has_key, status, ids, chunk_size, existing_keys, existing_ids,
-                   group):
-    """the exchange in fixed-capacity buckets: one host synchronisation (the
-    totals); None when a bucket overflowed (the caller reruns the exact path)"""
+def _dedup_buckets(stages, world, keys, has_key, status, ids, chunk_size, existing_keys, existing_ids, group, win):
+    """the exchange in fixed-capacity buckets: one host synchronisation of the
+    device (the totals; the counts agreed before it are host integers); None
+    when a bucket overflowed (the caller reruns the exact path)"""
     tr = _Trace()
     tr.mark("enter")
-    fcap, ecap = caps
     has_ex = existing_keys is not None
-    if has_ex and ecap == 0:
-        return None  # the previous call had no existing Objects: no capacity agreed
+    fcap, ecap, scap = _caps(stages, world, win, has_ex)
+    stages.bucket_caps = (fcap, ecap)
+    plan, scnt = _plan(stages, has_key, status, ids, chunk_size, win, group, world, scap)
     send, slot, fcnt, ovf = stages.combine_buckets(keys, has_key, status, ids, world, fcap)
     dev = fcnt.device
     if has_ex:
@@ -319,7 +428,7 @@ def _dedup_buckets(stages, world, caps, keys, has_key, status, ids, chunk_size, 
         sc = torch.stack([fcnt, ecnt], 1).contiguous()
     else:
         sc = fcnt.view(world, 1).contiguous()
-    tr.mark("combine")
+    tr.mark("stays+plan+combine")
     rc = torch.empty_like(sc)
     dist.all_to_all_single(rc, sc, group=group)  # equal splits: no host sizes
     tr.mark("a2a counts")
@@ -337,18 +446,23 @@ def _dedup_buckets(stages, world, caps, keys, has_key, status, ids, chunk_size, 
     back = torch.empty_like(answer)
     dist.all_to_all_single(back, answer.contiguous(), group=group)
     tr.mark("a2a answers")
-    link, cnt = stages.apply(ids, slot, back, chunk_size)
+    link, cnt = stages.apply(ids, slot, back, chunk_size, plan)
     tr.mark("apply")
-    over = ovf.to(torch.int64) + (eovf.to(torch.int64) if has_ex else 0)
-    tot = torch.cat([cnt.to(torch.int64), over])
-    fills = torch.stack([fcnt.max(), ecnt.max() if has_ex else torch.full((), -1, dtype=torch.int64, device=dev)])
+    zero = torch.zeros((), dtype=torch.int64, device=dev)
+    sfill = scnt.to(dev)[0] if scnt is not None else zero
+    over = ovf.to(torch.int64) + (eovf.to(torch.int64) if has_ex else 0) + (sfill > scap).to(torch.int64)
+    tot = torch.cat([cnt.to(torch.int64), over.view(1)])
+    fills = torch.stack([fcnt.max(), ecnt.max() if has_ex else torch.full((), -1, dtype=torch.int64, device=dev),
+                         sfill])
     dist.all_reduce(tot, group=group)
     dist.all_reduce(fills, op=dist.ReduceOp.MAX, group=group)
     tf = torch.cat([tot, fills]).tolist()  # the one host synchronisation
     tr.mark("totals")
     tr.done(group)
     t, f = tf[:3], tf[3:]
-    _next_caps(stages, int(f[0]), int(f[1]))
+    # an overflowing call learns its true fills from the exact rerun (the
+    # bucket counts here are clamped to the capacity)
+    _learn(stages, win, f[0], f[1], f[2])
     if t[2]:
         return None
     return link, int(t[0]), int(t[1])

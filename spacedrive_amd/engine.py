@@ -93,7 +93,7 @@ class Engine:
         self.L = N.load()
         self._cb = self._progress_fn(progress)
         self._cancel = cancel
-        opts = N.Options(device, io_threads, staging_bytes, N.SDCAS_OPT_DIRECT_IO if direct_io else 0, 0, self._cb,
+        opts = N.Options(device, io_threads, N.SDCAS_OPT_DIRECT_IO if direct_io else 0, staging_bytes, self._cb,
                          None, ctypes.pointer(cancel) if cancel is not None else None)
         ctx = ctypes.c_void_p()
         rc = self.L.sdcas_init(ctypes.byref(opts), ctypes.byref(ctx))
@@ -209,6 +209,15 @@ class Engine:
 
     # -- dedup ------------------------------------------------------------------------
     def identifier_dedup(self, keys, has_key, status=None, chunk_size=100, existing_keys=()):
+        """the file identifier job's group-by over these orphans (sdcas_dedup)
+        -> (link int64[n], created, linked)"""
+        link, created, linked, _ = self.identifier_dedup_window(keys, has_key, status, chunk_size, existing_keys)
+        return link, created, linked
+
+    def identifier_dedup_window(self, keys, has_key, status=None, chunk_size=100, existing_keys=(), max_steps=0,
+                                more=False):
+        """sdcas_dedup_window: the job's steps over one batch of its orphans
+        -> (link, created, linked, {"steps", "rows", "rereads"})"""
         keys = _arr(keys, np.uint64)
         n = keys.size
         has_key = _arr(has_key, np.uint8)
@@ -216,10 +225,11 @@ class Engine:
         ex = _arr(existing_keys, np.uint64)
         out = np.zeros(n, np.int64)
         created, linked = ctypes.c_int64(0), ctypes.c_int64(0)
-        self._check(self.L.sdcas_dedup(self.ctx, _ptr(keys), _ptr(has_key), _ptr(st), n, chunk_size,
-                                       _ptr(ex), ex.size, _ptr(out), ctypes.byref(created),
-                                       ctypes.byref(linked)), "sdcas_dedup")
-        return out, created.value, linked.value
+        win = N.JobWindow(int(max_steps), int(bool(more)), 0, 0, 0, 0)
+        self._check(self.L.sdcas_dedup_window(self.ctx, _ptr(keys), _ptr(has_key), _ptr(st), n, chunk_size,
+                                              _ptr(ex), ex.size, ctypes.byref(win), _ptr(out), ctypes.byref(created),
+                                              ctypes.byref(linked)), "sdcas_dedup_window")
+        return out, created.value, linked.value, {"steps": win.steps, "rows": win.rows, "rereads": win.rereads}
 
     # -- device-resident (pointers are ints: device addresses, e.g. tensor.data_ptr())
     def dev_reserve(self, max_msgs, max_chunks):

@@ -25,7 +25,14 @@ void Engine::fail(int rc, const char* what) const {
 }
 
 std::unique_ptr<Engine> Engine::open(const Options& o) {
-  sdcas_options opts{o.device, o.io_threads, o.staging_bytes, o.flags, 0, o.progress, o.progress_user, o.cancel};
+  sdcas_options opts = SDCAS_OPTIONS_INIT;
+  opts.device = o.device;
+  opts.io_threads = o.io_threads;
+  opts.flags = o.flags;
+  opts.staging_bytes = o.staging_bytes;
+  opts.progress = o.progress;
+  opts.progress_user = o.progress_user;
+  opts.cancel = o.cancel;
   sdcas_ctx* c = nullptr;
   const int rc = sdcas_init(&opts, &c);
   if (rc != SDCAS_OK) {
@@ -98,17 +105,20 @@ std::vector<Result<std::string>> Engine::file_checksums(const std::vector<std::s
 
 Engine::Dedup Engine::dedup(const std::vector<uint64_t>& keys, const std::vector<uint8_t>& has_key,
                             const std::vector<int32_t>& status, size_t chunk_size,
-                            const std::vector<uint64_t>& existing_keys) {
+                            const std::vector<uint64_t>& existing_keys, sdcas_job_window* window) {
   const size_t n = keys.size();
   if (has_key.size() != n || (!status.empty() && status.size() != n))
     throw std::invalid_argument("dedup: keys / has_key / status lengths differ");
   Dedup r;
   r.link.assign(n, 0);
-  if (!n) return r;
-  const int rc = sdcas_dedup(ctx_, keys.data(), has_key.data(), status.empty() ? nullptr : status.data(), n,
-                             chunk_size, existing_keys.empty() ? nullptr : existing_keys.data(),
-                             existing_keys.size(), r.link.data(), &r.created, &r.linked);
-  if (rc != SDCAS_OK) fail(rc, "sdcas_dedup");
+  if (!n) {
+    if (window) window->steps = window->rows = window->rereads = 0;
+    return r;
+  }
+  const int rc = sdcas_dedup_window(ctx_, keys.data(), has_key.data(), status.empty() ? nullptr : status.data(), n,
+                                    chunk_size, existing_keys.empty() ? nullptr : existing_keys.data(),
+                                    existing_keys.size(), window, r.link.data(), &r.created, &r.linked);
+  if (rc != SDCAS_OK) fail(rc, "sdcas_dedup_window");
   return r;
 }
 
@@ -331,10 +341,53 @@ std::vector<Result<FileMetadata>> file_metadata_batch(Engine& engine,
   return out;
 }
 
+static void flags_of(const std::vector<Result<FileMetadata>>& md, std::vector<uint8_t>& has_key,
+                     std::vector<int32_t>& status) {
+  const size_t n = md.size();
+  has_key.assign(n, 0);
+  status.assign(n, 0);
+  for (size_t i = 0; i < n; ++i) {
+    if (!md[i].ok()) status[i] = md[i].error().code;
+    else has_key[i] = md[i].value().cas_id ? 1 : 0;
+  }
+}
+
+StepPlan plan_steps(const std::vector<Result<FileMetadata>>& md, size_t chunk_size, sdcas_job_window& window) {
+  std::vector<uint8_t> has_key;
+  std::vector<int32_t> status;
+  flags_of(md, has_key, status);
+  StepPlan p;
+  p.step.resize(md.size());
+  p.reads.resize(md.size());
+  const int rc =
+      sdcas_job_plan(has_key.data(), status.data(), md.size(), chunk_size, &window, p.step.data(), p.reads.data());
+  if (rc != SDCAS_OK) throw LibraryError(rc, "sdcas_job_plan");
+  return p;
+}
+
+// a row to re-identify: an Object but no cas_id (the indexer nulled it when
+// the file changed); writing its new cas_id makes its Object "existing" for
+// that cas_id from its own step on (mod.rs:157-188)
+static bool reidentified(const FilePathRow& r, const Result<FileMetadata>& md) {
+  return r.object_id && !r.cas_id && md.ok() && md.value().cas_id;
+}
+
 std::pair<size_t, size_t> identifier_step_db(Library& db, const std::vector<FilePathRow>& file_paths,
-                                             const std::vector<Result<FileMetadata>>& md, const GroupBy& group_by) {
+                                             const std::vector<Result<FileMetadata>>& md, const GroupBy& group_by,
+                                             sdcas_job_window* window, size_t chunk_size) {
   const size_t n = file_paths.size();
   if (md.size() != n) throw std::invalid_argument("identifier_step_db: one metadata per file_path");
+  sdcas_job_window win{};
+  if (window) {
+    win.max_steps = window->max_steps;
+    win.more = window->more;
+  }
+  // which rows the steps read: only theirs are written (mod.rs:157-178)
+  const StepPlan plan = plan_steps(md, chunk_size, win);
+  const auto& step = plan.step;
+  for (size_t i = 0; i < n; ++i)
+    if (step[i] != UINT64_MAX && step[i] > 0 && reidentified(file_paths[i], md[i]))
+      throw std::invalid_argument("identifier_step_db: a row to re-identify past the batch's first step");
   std::vector<uint64_t> keys(n, 0);
   std::vector<uint8_t> has_key(n, 0);
   std::vector<int32_t> status(n, 0);
@@ -350,8 +403,9 @@ std::pair<size_t, size_t> identifier_step_db(Library& db, const std::vector<File
     if (cas) {
       keys[i] = hex_to_key(*cas);
       has_key[i] = 1;
-      if (seen.insert(*cas).second) unique.push_back(*cas);
     }
+    if (step[i] == UINT64_MAX) continue;  // no step reads it: it stays as it is
+    if (cas && seen.insert(*cas).second) unique.push_back(*cas);
     db.set_cas_id(file_paths[i].id, cas);  // mod.rs:157-178
   }
   db.end_batch();
@@ -366,67 +420,116 @@ std::pair<size_t, size_t> identifier_step_db(Library& db, const std::vector<File
       ekeys.push_back(hex_to_key(c));
       eobj.push_back(oid);
     }
-  auto d = group_by(keys, has_key, status, ekeys);
+  sdcas_job_window gw{};
+  gw.max_steps = win.max_steps;
+  gw.more = win.more;
+  auto d = group_by(keys, has_key, status, ekeys, gw);
   if (d.link.size() != n) throw std::logic_error("identifier_step_db: group-by returned a wrong link count");
-  // links and new Objects (mod.rs:202-342): new Objects take the kind and
-  // date_created of their file (mod.rs:266-291)
+  if (gw.steps != win.steps || gw.rows != win.rows)
+    throw std::logic_error("identifier_step_db: the group-by ran other steps than the plan");
+  // new Objects (mod.rs:246-342) in the order the steps create them: step by
+  // step, rows in id order within a step; a row without cas_id that several
+  // steps read gets an Object from each, the last one its link. They take
+  // the kind and date_created of their file (mod.rs:266-291).
+  std::vector<std::pair<uint64_t, size_t>> creates;
+  for (size_t i = 0; i < n; ++i)
+    if (d.link[i] == (int64_t)i)
+      for (uint32_t r = 0; r < plan.reads[i]; ++r) creates.emplace_back(plan.step[i] + r, i);
+  std::stable_sort(creates.begin(), creates.end(),
+                   [](const std::pair<uint64_t, size_t>& a, const std::pair<uint64_t, size_t>& b) {
+                     return a.first < b.first;
+                   });
   std::vector<int32_t> created_object(n, 0);
   db.begin_batch();
+  for (const auto& [s, i] : creates) {
+    created_object[i] = db.create_object(md[i].value().kind, file_paths[i].date_created);
+    db.connect(file_paths[i].id, created_object[i]);
+  }
+  // links to the first Object carrying the cas_id (mod.rs:202-238)
   for (size_t i = 0; i < n; ++i) {
     const int64_t l = d.link[i];
-    if (l == INT64_MIN) continue;
-    if (l == (int64_t)i) {
-      created_object[i] = db.create_object(md[i].value().kind, file_paths[i].date_created);
-      db.connect(file_paths[i].id, created_object[i]);
-    } else if (l >= 0) {
-      db.connect(file_paths[i].id, created_object[(size_t)l]);
-    } else {
-      db.connect(file_paths[i].id, eobj[(size_t)(-(l + 1))]);
-    }
+    if (l == SDCAS_LINK_DROPPED || l == SDCAS_LINK_DEFERRED || l == (int64_t)i) continue;
+    db.connect(file_paths[i].id, l >= 0 ? created_object[(size_t)l] : eobj[(size_t)(-(l + 1))]);
   }
   db.end_batch();
+  if (window) *window = win;
   return {(size_t)d.created, (size_t)d.linked};
 }
-
 std::pair<size_t, size_t> identifier_job_step(Engine& engine, Library& db, const Location& location,
-                                              const std::vector<FilePathRow>& file_paths, size_t chunk_size) {
+                                              const std::vector<FilePathRow>& file_paths, size_t chunk_size,
+                                              sdcas_job_window* window) {
   const size_t n = file_paths.size();
   std::vector<std::pair<std::string, ObjectKind>> files(n);
   for (size_t i = 0; i < n; ++i) files[i] = {full_path(location, file_paths[i]), file_paths[i].kind};
   // FileMetadata::new for every row (mod.rs:105-147): failing files are
   // logged and left out of the rest of the step (mod.rs:125-141)
   auto md = file_metadata_batch(engine, files);
-  return identifier_step_db(db, file_paths, md,
-                            [&](const std::vector<uint64_t>& k, const std::vector<uint8_t>& h,
-                                const std::vector<int32_t>& st, const std::vector<uint64_t>& e) {
-                              return engine.dedup(k, h, st, chunk_size, e);
-                            });
+  return identifier_step_db(
+      db, file_paths, md,
+      [&](const std::vector<uint64_t>& k, const std::vector<uint8_t>& h, const std::vector<int32_t>& st,
+          const std::vector<uint64_t>& e, sdcas_job_window& w) { return engine.dedup(k, h, st, chunk_size, e, &w); },
+      window, chunk_size);
 }
 
-FileIdentifierJobRunMetadata run_file_identifier_job(Engine& engine, Library& db, const FileIdentifierJobInit& init) {
+FileIdentifierJobRunMetadata run_file_identifier_job_with(Library& db, const FileIdentifierJobInit& init,
+                                                          const MetadataFn& metadata, const GroupBy& group_by) {
   FileIdentifierJobRunMetadata meta;
-  const size_t batch = std::max<size_t>(1, init.batch);
+  const size_t cs = SDCAS_IDENTIFIER_CHUNK_SIZE;
+  const size_t batch = std::max(cs, init.batch);  // a batch holds at least one whole step
   const int32_t loc = init.location.id;
   // init (file_identifier_job.rs:125-176)
   meta.total_orphan_paths = db.count_orphan_file_paths(loc, init.sub_materialized_path);
   if (meta.total_orphan_paths == 0) return meta;
   auto first = db.get_orphan_file_paths(loc, 0, init.sub_materialized_path, 1);
   meta.cursor = first.empty() ? 0 : first[0].id;
-  const size_t task_count = (meta.total_orphan_paths + batch - 1) / batch;
-  // execute_step (file_identifier_job.rs:178-223)
-  for (size_t step = 0; step < task_count; ++step) {
+  uint64_t steps_left = (meta.total_orphan_paths + cs - 1) / cs;  // task_count (:146)
+  while (steps_left) {
+    // execute_step's query (file_identifier_job.rs:296-319), `batch` rows at a time
     auto rows = db.get_orphan_file_paths(loc, meta.cursor, init.sub_materialized_path, batch);
-    if (rows.empty()) {
+    if (rows.empty()) {  // EarlyFinish (:203-209)
       meta.early_finish = true;
       break;
     }
-    auto [created, linked] = identifier_job_step(engine, db, init.location, rows);
+    const auto md = metadata(rows);
+    if (meta.batches && rows[0].id == meta.cursor) ++meta.rereads;  // the cursor row is still an orphan
+    sdcas_job_window w{};
+    w.max_steps = steps_left;
+    w.more = rows.size() == batch;
+    // a row to re-identify must sit in the batch's first step (identifier_step_db)
+    {
+      sdcas_job_window probe = w;
+      const StepPlan plan = plan_steps(md, cs, probe);
+      uint64_t cut = UINT64_MAX;
+      for (size_t i = 0; i < rows.size(); ++i)
+        if (plan.step[i] != UINT64_MAX && plan.step[i] > 0 && reidentified(rows[i], md[i]))
+          cut = std::min(cut, plan.step[i]);
+      if (cut != UINT64_MAX) w.max_steps = cut;
+    }
+    auto [created, linked] = identifier_step_db(db, rows, md, group_by, &w, cs);
+    if (w.steps == 0) break;  // cannot happen: a batch of `batch` >= cs rows holds a whole step
     meta.total_objects_created += created;
     meta.total_objects_linked += linked;
-    meta.cursor = rows.back().id;  // process_identifier_file_paths (mod.rs:394-403)
-    ++meta.steps;
+    meta.steps += w.steps;
+    meta.rereads += w.rereads;
+    ++meta.batches;
+    steps_left -= std::min<uint64_t>(steps_left, w.steps);
+    meta.cursor = rows[w.rows - 1].id;  // process_identifier_file_paths (mod.rs:401-405)
   }
   return meta;
+}
+
+FileIdentifierJobRunMetadata run_file_identifier_job(Engine& engine, Library& db, const FileIdentifierJobInit& init) {
+  return run_file_identifier_job_with(
+      db, init,
+      [&](const std::vector<FilePathRow>& rows) {
+        std::vector<std::pair<std::string, ObjectKind>> files(rows.size());
+        for (size_t i = 0; i < rows.size(); ++i) files[i] = {full_path(init.location, rows[i]), rows[i].kind};
+        return file_metadata_batch(engine, files);
+      },
+      [&](const std::vector<uint64_t>& k, const std::vector<uint8_t>& h, const std::vector<int32_t>& st,
+          const std::vector<uint64_t>& e, sdcas_job_window& w) {
+        return engine.dedup(k, h, st, SDCAS_IDENTIFIER_CHUNK_SIZE, e, &w);
+      });
 }
 
 // ---- object validator -----------------------------------------------------------------

@@ -13,6 +13,8 @@ import torch
 from spacedrive_amd.dist_dedup import owner_of
 
 NOKEY = np.uint32(0xFFFFFFFF)
+ALL_ONES = np.uint64(2**64 - 1)
+H = 12  # SDCAS_PLAN_HEADER_WORDS
 DROPPED = np.uint32(0xFFFFFFFE)
 
 
@@ -45,6 +47,7 @@ def dedup_virtual(stages_for, shards, chunk_size, existing_shards=None):
     linked)."""
     R = len(shards)
     st = [stages_for(r) for r in range(R)]
+    plan = virtual_plan(st, shards, chunk_size)
     recs, slots, counts = [], [], []
     for r, (k, h, s, ids) in enumerate(shards):
         rec, slot, starts = st[r].combine(k, h, s, ids, R)
@@ -67,12 +70,23 @@ def dedup_virtual(stages_for, shards, chunk_size, existing_shards=None):
     back, _ = virtual_exchange(answers, fc)
     links, created, linked = [], 0, 0
     for r, (k, h, s, ids) in enumerate(shards):
-        link, cnt = st[r].apply(ids, slots[r], back[r], chunk_size)
+        link, cnt = st[r].apply(ids, slots[r], back[r], chunk_size, plan)
         links.append(link)
         c = cnt.cpu().tolist()
         created += int(c[0])
         linked += int(c[1])
     return links, created, linked
+
+
+def virtual_plan(st, shards, chunk_size, n_total=None):
+    """stays of every virtual rank, gathered, then one plan (every rank would
+    build the same)"""
+    n_total = n_total if n_total is not None else sum(int(x[3].numel()) for x in shards)
+    parts = []
+    for r, (k, h, s, ids) in enumerate(shards):
+        out, cnt = st[r].stays(h, s, ids, max(int(ids.numel()), 1))
+        parts.append(out)
+    return st[0].plan(torch.cat(parts), n_total, chunk_size)
 
 
 class NumpyStages:
@@ -161,22 +175,98 @@ class NumpyStages:
         out[fsel] = ans
         return torch.from_numpy(out)
 
-    def apply(self, ids, slot, result, chunk_size):
+    def stays(self, has_key, status, ids, cap):
+        """ordinals of the rows that stay orphans after their step (the
+        device's dd_stays): int64[cap] padded with -1, count int64[1]"""
+        ids_np = _u64(ids)
+        n = ids_np.size
+        ok = np.ones(n, bool) if status is None else status.numpy() == 0
+        has = np.ones(n, bool) if has_key is None else has_key.numpy() != 0
+        s = ids_np[~(ok & has)]
+        out = np.full(cap, ALL_ONES, np.uint64)
+        out[:min(cap, s.size)] = s[:cap]
+        return _t64(out), torch.tensor([s.size], dtype=torch.int64)
+
+    def plan(self, stays, n_total, chunk_size, max_steps=0, more=False):
+        """the job's step plan (dist_dedup.h "the job's steps"), walking the
+        stays ordinals one at a time"""
+        cs = int(chunk_size)
+        s = np.sort(_u64(stays))
+        s = [int(x) for x in s[s < np.uint64(n_total)]]
+        rr = []
+        if cs > 1:
+            for p in s:
+                if p + 1 < n_total and (p + len(rr)) % cs == cs - 1:
+                    rr.append(p)
+        T = int(max_steps) or -(-n_total // cs)
+        loop, reads, rows = -1, 0, 0
+        if cs == 1 and s and s[0] < T:
+            loop, reads, steps, limit, rows = s[0], T - s[0], T, s[0], s[0] + 1
+        else:
+            E = n_total + len(rr)
+            avail = E // cs if more else -(-E // cs)
+            steps = min(avail, T)
+            limit = steps * cs
+            if steps:
+                P = min(limit, E) - 1
+                rows = P - sum(1 for k, q in enumerate(rr) if q + k + 1 <= P) + 1
+            if not more and T > avail and n_total and s and s[-1] == n_total - 1:
+                loop, reads, steps = n_total - 1, 1 + T - avail, T
+        run = sum(1 for k, q in enumerate(rr) if q + k + 1 < limit) + (reads - 1 if loop >= 0 else 0)
+        head = [limit, len(rr), steps, rows, n_total, cs, loop, reads, run, 0, 0, 0]
+        assert len(head) == H
+        return torch.tensor(head + rr, dtype=torch.int64)
+
+    def apply(self, ids, slot, result, chunk_size, plan=None):
         ids_np = _u64(ids).astype(np.int64)
         s = slot.numpy().view(np.uint32)
         r = result.numpy()
+        cs = int(chunk_size)
+        if plan is None:
+            limit, rr, loop, reads = 2**63, [], 2**63, 0
+        else:
+            pl = plan.numpy()
+            limit, nrr = int(pl[0]), int(pl[1])
+            rr = [int(x) for x in pl[H:H + nrr]]
+            loop = int(pl[6]) if int(pl[6]) >= 0 else 2**63
+            reads = int(pl[7])
+        below = lambda x: int(np.searchsorted(np.array(rr, np.int64), x, side="left")) if rr else 0
         link = np.empty(ids_np.size, np.int64)
+        created = linked = 0
+        MIN = np.iinfo(np.int64).min
         for i in range(ids_np.size):
             me = int(ids_np[i])
-            if s[i] == DROPPED:
-                link[i] = np.iinfo(np.int64).min
-            elif s[i] == NOKEY:
+            kind = "drop" if s[i] == DROPPED else "nokey" if s[i] == NOKEY else "key"
+            if me >= loop:
+                if me > loop:
+                    link[i] = MIN + 1
+                elif kind == "drop":
+                    link[i] = MIN
+                else:
+                    link[i] = me
+                    created += reads
+                continue
+            b = below(me)
+            pos = me + b
+            twice = b < len(rr) and rr[b] == me
+            if pos >= limit:
+                link[i] = MIN + 1
+            elif kind == "drop":
+                link[i] = MIN
+            elif kind == "nokey":
                 link[i] = me
+                created += 1 + (1 if twice and pos + 1 < limit else 0)
             else:
                 v = int(r[s[i]])
-                link[i] = v if v < 0 else (me if me // chunk_size == v // chunk_size else v)
-        created = int((link == ids_np).sum())
-        linked = int(((link != ids_np) & (link != np.iinfo(np.int64).min)).sum())
+                if v < 0:
+                    link[i] = v
+                    linked += 1
+                elif pos // cs == (v + below(v)) // cs:
+                    link[i] = me
+                    created += 1
+                else:
+                    link[i] = v
+                    linked += 1
         return torch.from_numpy(link), torch.tensor([created, linked], dtype=torch.int64)
 
 
@@ -248,9 +338,10 @@ def dedup_virtual_buckets(stages_for, shards, chunk_size, existing_shards, caps)
         ec = torch.tensor([int(ecnts[s][d]) for s in range(R)], dtype=torch.int64, device=dev)
         answers.append(st[d].resolve_buckets(frecv[d], fcap, fc, erecv[d] if ecap else None, ecap, ec, R))
     back = xchg(answers, fcap)
+    plan = virtual_plan(st, shards, chunk_size)
     links, created, linked = [], 0, 0
     for r, (k, h, s, ids) in enumerate(shards):
-        link, cnt = st[r].apply(ids, slots[r], back[r], chunk_size)
+        link, cnt = st[r].apply(ids, slots[r], back[r], chunk_size, plan)
         links.append(link)
         c = cnt.cpu().tolist()
         created += int(c[0])

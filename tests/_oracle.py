@@ -18,6 +18,16 @@ LIB = os.path.join(ROOT, "oracle", "build", "liboracle.so")
 _u64p = ctypes.POINTER(ctypes.c_uint64)
 
 
+LINK_DROPPED = np.iinfo(np.int64).min
+LINK_DEFERRED = LINK_DROPPED + 1
+
+
+class JobWindow(ctypes.Structure):
+    """oracle_job_window (oracle/oracle.h), the layout of sdcas_job_window"""
+    _fields_ = [("max_steps", ctypes.c_uint64), ("more", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("steps", ctypes.c_uint64), ("rows", ctypes.c_uint64), ("rereads", ctypes.c_uint64)]
+
+
 class Oracle:
     def __init__(self, lib):
         self.lib = lib
@@ -38,6 +48,10 @@ class Oracle:
                                               ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
                                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_identifier_dedup.restype = ctypes.c_int64
+        L.oracle_identifier_job.argtypes = [ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p,
+                                            ctypes.POINTER(JobWindow), ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_identifier_job.restype = ctypes.c_int64
         L.oracle_subtree_cv.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int,
                                         ctypes.c_void_p]
         L.oracle_periodic_checksum.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int,
@@ -133,6 +147,13 @@ class Oracle:
         return keys, st, secs.value, hasher
 
     def identifier_dedup(self, keys, has_key, status=None, chunk_size=100, existing_keys=()):
+        """the file identifier job over these orphans -> (link, created, linked)"""
+        link, created, linked, _ = self.identifier_job(keys, has_key, status, chunk_size, existing_keys)
+        return link, created, linked
+
+    def identifier_job(self, keys, has_key, status=None, chunk_size=100, existing_keys=(), max_steps=0,
+                       more=False):
+        """oracle_identifier_job -> (link, created, linked, window dict)"""
         keys = np.ascontiguousarray(keys, dtype=np.uint64)
         n = keys.size
         has_key = np.ascontiguousarray(has_key, dtype=np.uint8)
@@ -140,11 +161,12 @@ class Oracle:
         ex = np.ascontiguousarray(existing_keys, dtype=np.uint64)
         out = np.zeros(n, np.int64)
         linked = ctypes.c_int64(0)
-        created = self.lib.oracle_identifier_dedup(
+        win = JobWindow(max_steps, int(bool(more)), 0, 0, 0, 0)
+        created = self.lib.oracle_identifier_job(
             n, keys.ctypes.data, has_key.ctypes.data, None if st is None else st.ctypes.data,
-            chunk_size, ex.size, ex.ctypes.data if ex.size else None, out.ctypes.data,
+            chunk_size, ex.size, ex.ctypes.data if ex.size else None, ctypes.byref(win), out.ctypes.data,
             ctypes.byref(linked))
-        return out, int(created), int(linked.value)
+        return out, int(created), int(linked.value), {"steps": win.steps, "rows": win.rows, "rereads": win.rereads}
 
 
 def build_oracle():

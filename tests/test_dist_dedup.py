@@ -38,23 +38,25 @@ def _gloo_corpus(seed, n, existing_mode):
     return keys, has, status, existing
 
 
-def _gloo_worker(rank, world, port, outdir, seed, n, chunk_size, existing_mode="full", caps=None):
+def _gloo_worker(rank, world, port, outdir, seed, n, chunk_size, existing_mode="full", caps=None, grow=1):
     import torch.distributed as dist
 
     from spacedrive_amd.dist_dedup import identifier_dedup_distributed
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
-        keys, has, status, existing = _gloo_corpus(seed, n, existing_mode)
-        shards, ex = shard(keys, has, status, existing, world)
-        k, h, s, ids = shards[rank]
-        ek, eids = ex[rank] if existing_mode != "none" else (None, None)
         st = NumpyStages()
         if caps is not None:
-            st.bucket_caps = caps
-        # the same stages object twice: the first call agrees bucket capacities
-        # (exact protocol, or the given caps), the second uses them
+            st.force_caps = caps  # the first call's capacities
+        # the same stages object twice: the first call seeds its bucket
+        # capacities from the all-gathered file counts (or takes the given
+        # caps), the second rescales the first's fills to its own load
+        # (`grow` times the first's files)
         out = {}
         for call in range(2):
+            keys, has, status, existing = _gloo_corpus(seed + call, n * (grow if call else 1), existing_mode)
+            shards, ex = shard(keys, has, status, existing, world)
+            k, h, s, ids = shards[rank]
+            ek, eids = ex[rank] if existing_mode != "none" else (None, None)
             link, created, linked = identifier_dedup_distributed(st, k, h, s, ids, chunk_size, ek, eids)
             out[f"link{call}"] = link.numpy()
             out[f"count{call}"] = np.array([created, linked])
@@ -64,41 +66,45 @@ def _gloo_worker(rank, world, port, outdir, seed, n, chunk_size, existing_mode="
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,chunk_size,existing_mode", [
-    (1, 100, "full"), (2, 100, "full"), (4, 7, "full"), (3, 1, "full"), (1, 100, "none"), (2, 100, "none"),
-    (3, 100, "sparse")])
-def test_gloo_protocol_vs_oracle(oracle, world, chunk_size, existing_mode):
-    """exact protocol on the first call, fixed-capacity buckets on the second"""
+@pytest.mark.parametrize("world,chunk_size,existing_mode,grow", [
+    (1, 100, "full", 1), (2, 100, "full", 1), (4, 7, "full", 1), (3, 1, "full", 1), (1, 100, "none", 1),
+    (2, 100, "none", 1), (3, 100, "sparse", 1), (2, 100, "full", 3), (3, 100, "none", 3)])
+def test_gloo_protocol_vs_oracle(oracle, world, chunk_size, existing_mode, grow):
+    """fixed-capacity buckets from the first call on (one device sync per
+    call), also when the second call carries 3x the first's files"""
     import torch.multiprocessing as mp
     seed, n = 1000 + world, 3000
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_gloo_worker, args=(world, _free_port(), d, seed, n, chunk_size, existing_mode),
+        mp.start_processes(_gloo_worker, args=(world, _free_port(), d, seed, n, chunk_size, existing_mode, None,
+                                               grow),
                            nprocs=world, join=True, start_method="spawn")
         parts = [np.load(os.path.join(d, f"r{r}.npz")) for r in range(world)]
-    keys, has, status, existing = _gloo_corpus(seed, n, existing_mode)
-    want, wc, wl = oracle.identifier_dedup(keys, has, status, chunk_size, existing)
     for call in range(2):
+        keys, has, status, existing = _gloo_corpus(seed + call, n * (grow if call else 1), existing_mode)
+        want, wc, wl = oracle.identifier_dedup(keys, has, status, chunk_size, existing)
         got = np.concatenate([p[f"link{call}"] for p in parts])
         assert np.array_equal(got, want)
         for p in parts:  # node-wide totals on every rank
             assert tuple(int(x) for x in p[f"count{call}"]) == (wc, wl)
     if world > 1:
-        assert [str(p["proto0"]) for p in parts] == ["exact"] * world
+        assert [str(p["proto0"]) for p in parts] == ["buckets"] * world
         assert [str(p["proto1"]) for p in parts] == ["buckets"] * world
 
 
-def test_gloo_bucket_overflow_falls_back(oracle):
-    """buckets too small for the records: the overflow flag travels with the
-    totals, every rank reruns the exact protocol, links still exact"""
+@pytest.mark.parametrize("caps", [(8, 8), (100_000, 100_000, 3)])
+def test_gloo_bucket_overflow_falls_back(oracle, caps):
+    """buckets too small for the records (or the stays gather too small for
+    the rows that stay orphans): the overflow flag travels with the totals,
+    every rank reruns the exact protocol, links still exact"""
     import torch.multiprocessing as mp
     world, seed, n = 3, 77, 3000
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_gloo_worker, args=(world, _free_port(), d, seed, n, 100, "full", (8, 8)),
+        mp.start_processes(_gloo_worker, args=(world, _free_port(), d, seed, n, 100, "full", caps),
                            nprocs=world, join=True, start_method="spawn")
         parts = [np.load(os.path.join(d, f"r{r}.npz")) for r in range(world)]
-    keys, has, status, existing = _gloo_corpus(seed, n, "full")
-    want, wc, wl = oracle.identifier_dedup(keys, has, status, 100, existing)
     for call in range(2):
+        keys, has, status, existing = _gloo_corpus(seed + call, n, "full")
+        want, wc, wl = oracle.identifier_dedup(keys, has, status, 100, existing)
         assert np.array_equal(np.concatenate([p[f"link{call}"] for p in parts]), want)
         for p in parts:
             assert tuple(int(x) for x in p[f"count{call}"]) == (wc, wl)
@@ -114,6 +120,45 @@ def test_virtual_protocol_numpy_vs_oracle(oracle, R):
     want, wc, wl = oracle.identifier_dedup(keys, has, status, 100, existing)
     assert np.array_equal(np.concatenate([x.numpy() for x in links]), want)
     assert (c, l) == (wc, wl)
+
+
+def _numpy_window(keys, has, status, existing, cs, max_steps=0, more=False):
+    """one rank's numpy stages with the job window -> (link, created, linked, plan header)"""
+    st = NumpyStages()
+    (k, h, s, ids), = shard(keys, has, status, existing, 1)[0]
+    ek = torch.from_numpy(np.ascontiguousarray(existing).view(np.int64))
+    eids = torch.arange(existing.size, dtype=torch.int64)
+    rec, slot, _ = st.combine(k, h, s, ids, 1)
+    erec, _, _ = st.combine(ek, None, None, eids, 1)
+    ans = st.resolve(rec, erec)
+    stays, _ = st.stays(h, s, ids, max(keys.size, 1))
+    plan = st.plan(stays, keys.size, cs, max_steps, more)
+    link, cnt = st.apply(ids, slot, ans, cs, plan)
+    return link.numpy(), int(cnt[0]), int(cnt[1]), plan.numpy()[:12]
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_step_plan_matches_literal_step_loop(oracle, seed):
+    """the plan's closed form (re-reads from the stays ordinals, positions,
+    limit, repeated rows) against the oracle's literal cursor loop, on small
+    dense cases: every chunk size from 1, stays rows at chunk ends, budgets
+    above and below what the rows need, windows with more rows to come"""
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(1, 60))
+    cs = int(rng.choice([1, 2, 3, 4, 7, 10, 100]))
+    pool = rng.integers(0, 2**64, max(2, n // 3), dtype=np.uint64)
+    keys = pool[rng.integers(0, pool.size, n)]
+    has = (rng.random(n) > rng.random() * 0.5).astype(np.uint8)
+    status = np.where(rng.random(n) < rng.random() * 0.4, 5, 0).astype(np.int32)
+    existing = pool[rng.integers(0, pool.size, int(rng.integers(0, 4)))]
+    for max_steps, more in ((0, False), (int(rng.integers(1, 2 * n + 2)), False),
+                            (int(rng.integers(1, 2 * n + 2)), True), (0, True)):
+        want, wc, wl, ww = oracle.identifier_job(keys, has, status, cs, existing, max_steps, more)
+        got, gc, gl, head = _numpy_window(keys, has, status, existing, cs, max_steps, more)
+        case = (n, cs, max_steps, more)
+        assert np.array_equal(got, want), case
+        assert (gc, gl) == (wc, wl), case
+        assert (int(head[2]), int(head[3]), int(head[8])) == (ww["steps"], ww["rows"], ww["rereads"]), case
 
 
 def collision_corpus(seed=11, n=8000):
@@ -321,6 +366,63 @@ def test_device_local_vs_oracle(eng, oracle, corpus, chunk_size):
     want, wc, wl = oracle.identifier_dedup(np.array([5, 5, 6], np.uint64), np.array([0, 1, 1], np.uint8),
                                            np.array([0, 3, 3], np.int32), 100, np.zeros(0, np.uint64))
     assert np.array_equal(link.cpu().numpy(), want) and tuple(cnt.tolist()) == (wc, wl)
+
+
+def _plan_cases(count, seed0=0):
+    """small dense cases of the step plan: every chunk size from 1, stays rows
+    at step ends, budgets above and below what the rows need, windows"""
+    for seed in range(seed0, seed0 + count):
+        rng = np.random.default_rng(seed)
+        n = int(rng.integers(1, 60))
+        cs = int(rng.choice([1, 2, 3, 4, 7, 10, 100]))
+        pool = rng.integers(0, 2**64, max(2, n // 3), dtype=np.uint64)
+        keys = pool[rng.integers(0, pool.size, n)]
+        has = (rng.random(n) > rng.random() * 0.5).astype(np.uint8)
+        status = np.where(rng.random(n) < rng.random() * 0.4, 5, 0).astype(np.int32)
+        existing = pool[rng.integers(0, pool.size, int(rng.integers(0, 4)))]
+        for max_steps, more in ((0, False), (int(rng.integers(1, 2 * n + 2)), False),
+                                (int(rng.integers(1, 2 * n + 2)), True), (0, True)):
+            yield keys, has, status, existing, cs, max_steps, more
+
+
+@pytest.mark.gpu
+def test_device_step_plan_matches_literal_step_loop(eng, oracle):
+    """the device's plan (k_plan_walk) through sdcas_dedup_window and through
+    sdcas_dev_dedup_local, against the oracle's literal cursor loop"""
+    from spacedrive_amd.dist_dedup import DeviceStages
+    st = DeviceStages(eng)
+    header = torch.zeros(12, dtype=torch.int64, device="cuda")
+    for keys, has, status, existing, cs, max_steps, more in _plan_cases(300):
+        want, wc, wl, ww = oracle.identifier_job(keys, has, status, cs, existing, max_steps, more)
+        case = (keys.size, cs, max_steps, more)
+        got, gc, gl, gw = eng.identifier_dedup_window(keys, has, status, cs, existing, max_steps, more)
+        assert np.array_equal(got, want) and (gc, gl) == (wc, wl), case
+        assert gw == ww, case
+        (k, h, s, ids), = shard(keys, has, status, existing, 1, device="cuda")[0]
+        ek = torch.from_numpy(existing.view(np.int64)).cuda()
+        eids = torch.arange(existing.size, dtype=torch.int64, device="cuda")
+        link, cnt = st.local(k, h, s, ids, cs, ek, eids, keys.size, max_steps, more, header=header)
+        assert np.array_equal(link.cpu().numpy(), want) and tuple(cnt.tolist()) == (wc, wl), case
+        hd = header.cpu().numpy()
+        assert (int(hd[2]), int(hd[3]), int(hd[8])) == (ww["steps"], ww["rows"], ww["rereads"]), case
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R,chunk_size", [(1, 100), (3, 100), (8, 7), (2, 1)])
+def test_device_stages_dense_stays_vs_oracle(eng, oracle, R, chunk_size):
+    """a corpus where many rows stay orphans (20 % errors, 20 % without a
+    cas_id), so most steps re-read their predecessor's last row: the device
+    stays + plan + combine + resolve + apply over R virtual ranks"""
+    from spacedrive_amd.dist_dedup import DeviceStages
+    keys, has, status, existing = make_corpus(300 + R, 30000, pool=3000, p_none=0.2, p_err=0.2)
+    want, wc, wl, ww = oracle.identifier_job(keys, has, status, chunk_size, existing)
+    assert ww["rereads"] > 10 or chunk_size == 1
+    shards, ex = shard(keys, has, status, existing, R, device="cuda")
+    st = DeviceStages(eng)
+    links, c, l = dedup_virtual(lambda r: st, shards, chunk_size, ex)
+    got = np.concatenate([x.cpu().numpy() for x in links])
+    assert np.array_equal(got, want)
+    assert (c, l) == (wc, wl)
 
 
 # ---- the piece split of big-file checksums (spacedrive_amd/dist_checksum.py) ----

@@ -123,6 +123,111 @@ def test_dedup_existing_and_errors(oracle):
     assert created == 2 and linked == 1
 
 
+MIN = np.iinfo(np.int64).min
+DEFERRED = MIN + 1
+
+
+def test_dedup_last_row_none_is_read_again(oracle):
+    """file_identifier_job.rs:296-319 + mod.rs:401-405: the next step starts AT
+    the previous step's last row (id >= cursor); a row with cas_id None keeps
+    cas_id NULL, stays an orphan (file_identifier_job.rs:258-264) and, being
+    the last row, is read again and gets a second Object (mod.rs:246-254)"""
+    keys = np.array([10, 11, 0, 10, 12, 11, 13], np.uint64)
+    has = np.array([1, 1, 0, 1, 1, 1, 1], np.uint8)
+    out, created, linked, win = oracle.identifier_job(keys, has, chunk_size=3)
+    # step 1: rows 0,1,2 (2 is None: new Object); step 2: rows 2,3,4 (2 again:
+    # another Object; 3 links to 0; 4 new); step 3: rows 5,6 (5 links to 1)
+    assert out.tolist() == [0, 1, 2, 0, 4, 1, 6]
+    assert (created, linked) == (6, 2)
+    assert win == {"steps": 3, "rows": 7, "rereads": 1}
+
+
+def test_dedup_error_at_chunk_end_shifts_boundaries(oracle):
+    """an errored last row shifts every later chunk: rows 4 and 5 (same
+    cas_id) land in different steps, so 5 links to 4's Object instead of
+    creating its own; the fixed 3-row chunks would give 6 Objects"""
+    keys = np.array([1, 2, 0, 3, 4, 4, 6], np.uint64)
+    has = np.ones(7, np.uint8)
+    status = np.array([0, 0, 5, 0, 0, 0, 0], np.int32)
+    out, created, linked, win = oracle.identifier_job(keys, has, status, chunk_size=3)
+    assert out.tolist() == [0, 1, MIN, 3, 4, 4, 6]
+    assert (created, linked) == (5, 1)
+    assert win == {"steps": 3, "rows": 7, "rereads": 1}
+
+
+def test_dedup_task_count_leaves_tail_for_next_job(oracle):
+    """task_count = ceil(orphans / 100) is fixed at init (file_identifier_job.rs:146):
+    a re-read costs a row of the budget, so the last row is not reached"""
+    keys = np.array([1, 2, 0, 3, 4, 5], np.uint64)
+    status = np.array([0, 0, 5, 0, 0, 0], np.int32)
+    out, created, linked, win = oracle.identifier_job(keys, np.ones(6, np.uint8), status, chunk_size=3)
+    assert out.tolist() == [0, 1, MIN, 3, 4, DEFERRED]
+    assert (created, linked) == (4, 0)
+    assert win == {"steps": 2, "rows": 5, "rereads": 1}
+
+
+def test_dedup_window_of_a_longer_job(oracle):
+    """a batch of the job (more orphans follow): a step that would reach past
+    the batch is left to the next batch, whose cursor is row rows-1"""
+    keys = np.array([1, 2, 0, 3, 4], np.uint64)
+    has = np.array([1, 1, 0, 1, 1], np.uint8)
+    out, created, linked, win = oracle.identifier_job(keys, has, chunk_size=3, max_steps=10, more=True)
+    assert out.tolist() == [0, 1, 2, 3, 4] and (created, linked) == (6, 0)
+    assert win == {"steps": 2, "rows": 5, "rereads": 1}
+    out, created, linked, win = oracle.identifier_job(np.array([1, 2, 3, 4], np.uint64), np.ones(4, np.uint8),
+                                                      chunk_size=3, max_steps=10, more=True)
+    assert out.tolist() == [0, 1, 2, DEFERRED] and win == {"steps": 1, "rows": 3, "rereads": 0}
+    # the budget caps a window too
+    out, _, _, win = oracle.identifier_job(np.arange(9, dtype=np.uint64), np.ones(9, np.uint8), chunk_size=3,
+                                           max_steps=2)
+    assert out.tolist() == list(range(6)) + [DEFERRED] * 3 and win["steps"] == 2 and win["rows"] == 6
+
+
+def test_dedup_batches_equal_the_100_row_job(oracle):
+    """a job run in windows of 1000 rows, each window's next cursor from the
+    oracle's `rows`, equals the job run 100 rows at a time over the same rows:
+    the windows reproduce the 100-row chunks exactly (the re-read row is the
+    next window's first row)"""
+    rng = np.random.default_rng(3)
+    n = 5000
+    pool = rng.integers(0, 2**64, 600, dtype=np.uint64)
+    keys = pool[rng.integers(0, 600, n)]
+    has = (rng.random(n) > 0.05).astype(np.uint8)
+    status = np.where(rng.random(n) < 0.05, 5, 0).astype(np.int32)
+    # force stay-orphans onto many chunk ends
+    has[99::100] = 0
+    status[198::100] = 7
+    whole, wc, wl, ww = oracle.identifier_job(keys, has, status, 100)
+    assert ww["rereads"] >= 5
+    for batch in (100, 300, 1000, 4096):
+        link = np.full(n, DEFERRED, np.int64)
+        start, steps_left, created, linked = 0, (n + 99) // 100, 0, 0
+        obj_key, obj_row = [], []  # the library's Objects with a cas_id, DB (creation) order
+        while steps_left and start < n:
+            hi = min(n, start + batch)
+            out, c, l, w = oracle.identifier_job(keys[start:hi], has[start:hi], status[start:hi], 100,
+                                                 np.array(obj_key, np.uint64), max_steps=steps_left, more=hi < n)
+            if w["steps"] == 0:
+                break
+            for i in range(int(w["rows"])):
+                v = int(out[i])
+                if v == DEFERRED:
+                    continue
+                link[start + i] = v + start if v >= 0 else (v if v == MIN else obj_row[-v - 1])
+            for i in range(int(w["rows"])):
+                if int(out[i]) == i and has[start + i] and status[start + i] == 0:
+                    obj_key.append(keys[start + i])
+                    obj_row.append(start + i)
+            created += c
+            linked += l
+            steps_left -= int(w["steps"])
+            start += int(w["rows"]) - 1  # the cursor row: read again if it is still an orphan
+            if start < n and status[start] == 0 and has[start]:
+                start += 1  # no longer an orphan: the next query skips it
+        assert (created, linked) == (wc, wl), batch
+        assert np.array_equal(link, whole), batch
+
+
 def test_mix64_python_matches_header():
     # sds_mix64(0) reference value computed from the header's definition
     assert int(mix64(np.uint64(0))) == 0xE220A8397B1DCDAF

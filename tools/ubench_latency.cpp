@@ -46,8 +46,8 @@ struct Lib {
     destroy = (decltype(destroy))dlsym(h, "sdcas_destroy");
     cas_ids = (decltype(cas_ids))dlsym(h, "sdcas_cas_ids");
     if (!init || !destroy || !cas_ids) return fprintf(stderr, "%s: missing symbols\n", p.c_str()), false;
-    sdcas_options o;
-    memset(&o, 0, sizeof o);
+    sdcas_options o = SDCAS_OPTIONS_INIT;
+    o.device = 0;
     o.io_threads = io_threads;
     return init(&o, &ctx) == SDCAS_OK;
   }
