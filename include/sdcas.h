@@ -50,9 +50,13 @@
  *     sdcas_cas_ids_from_messages) call the context's progress function after
  *     every staging slot / 1 MiB-piece window completes, with bytes of input
  *     whose results are final, and stop at the next such point once the
- *     cancel flag reads nonzero: items already complete keep their results
- *     and status, every other item gets SDCAS_STATUS_CANCELLED, and the call
- *     returns SDCAS_E_CANCELLED.
+ *     cancel flag reads nonzero, returning SDCAS_E_CANCELLED. sdcas_cas_ids
+ *     and sdcas_checksums report per item: items already complete keep their
+ *     results and status, every other item gets SDCAS_STATUS_CANCELLED. The
+ *     two message calls have no per-item status: after SDCAS_E_CANCELLED
+ *     their outputs are undefined. The progress function runs on the calling
+ *     thread with the context's lock held: it must not call into the same
+ *     context.
  *   - Limits: a batch holds at most SDCAS_MAX_BATCH (2^31 - 1) items.
  */
 #ifndef SDCAS_H
@@ -140,7 +144,12 @@ int sdcas_set_progress(sdcas_ctx *ctx, sdcas_progress_fn progress, void *user, c
 /* cas_id of n files: generate_cas_id(paths[i], sizes[i]) (cas.rs:23-62).
  * sizes[i] is fs::metadata().len() as the identifier passes it (mod.rs:78-79);
  * it feeds the size prefix and the sample spacing, while file bytes come from
- * the file as it is now. out_keys[i] is valid iff out_status[i] == 0. */
+ * the file as it is now. out_keys[i] is valid iff out_status[i] == 0.
+ * A small file (size <= 100 KiB) that has grown past its staging room when
+ * read is read again with room for its new length, up to 4 times; one that
+ * keeps growing through all of them gets out_status EAGAIN (the reference's
+ * fs::read would hash whatever it read at that moment — a race with the
+ * writer either way; the caller may retry the file later). */
 int sdcas_cas_ids(sdcas_ctx *ctx, const char *const *paths, const uint64_t *sizes, size_t n,
                   uint64_t *out_keys, int32_t *out_status);
 

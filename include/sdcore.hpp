@@ -218,6 +218,12 @@ class Library {
   virtual size_t count_orphan_file_paths(int32_t location_id, const std::string& sub_materialized_path) = 0;
   virtual std::vector<FilePathRow> get_orphan_file_paths(int32_t location_id, int32_t cursor,
                                                          const std::string& sub_materialized_path, size_t take) = 0;
+  // the shallow identifier's orphan_path_filters (shallow.rs:120-142): the
+  // same with materialized_path = dir (one directory level, "/" = the
+  // location's root) instead of the sub-path prefix
+  virtual size_t count_orphan_file_paths_in_dir(int32_t location_id, const std::string& dir) = 0;
+  virtual std::vector<FilePathRow> get_orphan_file_paths_in_dir(int32_t location_id, int32_t cursor,
+                                                                const std::string& dir, size_t take) = 0;
   // mod.rs:157-178: file_path.cas_id = ? per processed file
   virtual void set_cas_id(int32_t file_path_id, const std::optional<std::string>& cas_id) = 0;
   // mod.rs:181-188: Objects having a file_path whose cas_id is in `cas_ids`,
@@ -252,6 +258,9 @@ class MemoryLibrary : public Library {
   size_t count_orphan_file_paths(int32_t location_id, const std::string& sub) override;
   std::vector<FilePathRow> get_orphan_file_paths(int32_t location_id, int32_t cursor, const std::string& sub,
                                                  size_t take) override;
+  size_t count_orphan_file_paths_in_dir(int32_t location_id, const std::string& dir) override;
+  std::vector<FilePathRow> get_orphan_file_paths_in_dir(int32_t location_id, int32_t cursor, const std::string& dir,
+                                                        size_t take) override;
   void set_cas_id(int32_t file_path_id, const std::optional<std::string>& cas_id) override;
   std::vector<std::pair<int32_t, std::vector<std::string>>> existing_objects(
       const std::vector<std::string>& cas_ids) override;
@@ -290,6 +299,9 @@ class SqliteLibrary : public Library {
   size_t count_orphan_file_paths(int32_t location_id, const std::string& sub) override;
   std::vector<FilePathRow> get_orphan_file_paths(int32_t location_id, int32_t cursor, const std::string& sub,
                                                  size_t take) override;
+  size_t count_orphan_file_paths_in_dir(int32_t location_id, const std::string& dir) override;
+  std::vector<FilePathRow> get_orphan_file_paths_in_dir(int32_t location_id, int32_t cursor, const std::string& dir,
+                                                        size_t take) override;
   void set_cas_id(int32_t file_path_id, const std::optional<std::string>& cas_id) override;
   std::vector<std::pair<int32_t, std::vector<std::string>>> existing_objects(
       const std::vector<std::string>& cas_ids) override;
@@ -396,6 +408,26 @@ FileIdentifierJobRunMetadata run_file_identifier_job(Engine& engine, Library& db
 using MetadataFn = std::function<std::vector<Result<FileMetadata>>(const std::vector<FilePathRow>& rows)>;
 FileIdentifierJobRunMetadata run_file_identifier_job_with(Library& db, const FileIdentifierJobInit& init,
                                                           const MetadataFn& metadata, const GroupBy& group_by);
+
+// the shallow identifier (file_identifier/shallow.rs:24-118, run by
+// light_scan_location): the same steps over the orphans of ONE directory
+// level (materialized_path = dir; "" or "/" = the location's root), task_count
+// = ceil(orphans / CHUNK_SIZE) with no early finish — a step that finds no
+// rows leaves the cursor where it is (mod.rs:401-405). Its first cursor comes
+// from an unordered find_first (shallow.rs:74-84, `.order_by` commented out):
+// the canonical pick here is the lowest orphan id, which is what SQLite returns
+// for that query when it scans in rowid order. `batch` as in
+// FileIdentifierJobInit.
+struct ShallowIdentifierReport {
+  size_t orphans = 0, steps = 0, batches = 0, rereads = 0;
+  size_t created = 0, linked = 0;
+  int32_t cursor = 0;
+};
+ShallowIdentifierReport shallow_file_identifier(Engine& engine, Library& db, const Location& location,
+                                                const std::string& dir, size_t batch = SDCAS_IDENTIFIER_CHUNK_SIZE);
+ShallowIdentifierReport shallow_file_identifier_with(Library& db, const Location& location, const std::string& dir,
+                                                     size_t batch, const MetadataFn& metadata,
+                                                     const GroupBy& group_by);
 
 // ---- object validator -----------------------------------------------------------
 

@@ -212,48 +212,28 @@ __device__ __forceinline__ void leaf_hash(const uint8_t* __restrict__ p, uint32_
   constexpr int L = PF % 100, GA = kGA<PF>;
   if constexpr (L == 8) {
     hash_chunk_ps<GA>(p, clen, j, root, cv);
-  } else if constexpr (L == 9 || L == 49) {
+  } else if constexpr (L == 9) {
     hash_chunk_pl<GA>(p, clen, j, root, cv);
-  } else if constexpr (L == 19) {  // 9 with non-temporal message loads (ablation)
-    hash_chunk_pl<GA, 1>(p, clen, j, root, cv);
-  } else if constexpr (L == 29) {  // 9 with the tail mask computed in its branch (ablation)
-    hash_chunk_pl<GA, 0, 1>(p, clen, j, root, cv);
-  } else if constexpr (L == 39) {
-    // DIAGNOSTIC (wrong digests): the same loop reading a wave-transposed
-    // image of the wave's 64 KiB — lane l reads block b at wave base + b * 4 KiB
-    // + l * 64, so each load instruction of the wave covers 4 KiB of
-    // contiguous bytes instead of 64 lines 1 KiB apart (DRAM row locality);
-    // the same bytes and compressions as 51 (needs 64 KiB of readable bytes
-    // past the wave's first chunk: tools/ab_leaf.py pads the blob)
-    const uint64_t pa = (uint64_t)p;
-    // (readfirstlane returns int: through uint32_t, or the low word sign-extends)
-    const uint64_t w0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(pa >> 32)) << 32) |
-                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)pa);
-    hash_chunk_pl<GA, 0, 0, 64 * BLOCK_LEN>(reinterpret_cast<const uint8_t*>(w0 + 64ull * __lane_id()), clen, j,
-                                            root, cv);
   } else if constexpr (L == 4) {
     hash_chunk_pp<GA>(p, clen, j, root, cv);
   } else {
 #ifdef SDCAS_ABLATIONS
-    if constexpr (PF == 6) hash_chunk_pf2(p, clen, j, root, cv);
-    else if constexpr (PF == 7) hash_chunk_pair(p, clen, j, root, cv);
-    else if constexpr (PF == 5) hash_chunk_pf<true>(p, clen, j, root, cv);
-    else if constexpr (L == 2 || L == 3) hash_chunk_diag<GA>(p, clen, j, root, cv, L);
-    else if constexpr (PF == 1) hash_chunk_pf(p, clen, j, root, cv);
-    else hash_chunk(p, clen, j, root, cv);
+    leaf_hash_ablation<PF>(p, clen, j, root, cv);  // b3_ablate_loops.inc
 #else
     static_assert(L == 8 || L == 9 || L == 4, "ablation block loops need -DSDCAS_ABLATIONS");
 #endif
   }
 }
 
-// DIAGNOSTIC loop 49 (wrong digests): loop 9 with every chunk's address
-// folded into the blob's first 2 MiB, which stay L2-resident — the same
-// loads, compressions and tree as 51 without HBM traffic
+// the message address of a leaf chunk (an ablation loop may fold it)
 template <int PF>
 __device__ __forceinline__ const uint8_t* leaf_ptr(const uint8_t* blob, const uint8_t* p) {
-  if constexpr (PF % 100 == 49) return blob + ((uint64_t)(p - blob) & ((2ull << 20) - 1));
+#ifdef SDCAS_ABLATIONS
+  return leaf_ptr_ablation<PF>(blob, p);
+#else
+  (void)blob;
   return p;
+#endif
 }
 
 __device__ __forceinline__ void store_digest(uint32_t m, const uint32_t (&d)[8], uint8_t* out32, uint64_t* out_keys) {
@@ -1283,10 +1263,10 @@ size_t batch_scan_temp_bytes(uint32_t max_msgs) {
 
 // Leaf/tree kernel variants, numbered as in the A/B runs of rounds 1-2
 //  so that profiles/ and tools/ keep their meaning. libsdcas.so
-// holds only the bit-exact, GPU-tested product kernels (the default, 50, and
-// round 1's default, 43); every other entry is compiled only into the
-// ablation library (ABL), and the stagger / priority experiments (8, 9, 11,
-// 12, 37) are retired (RET).
+// holds only the bit-exact, GPU-tested product kernels (PROD: the default,
+// 52, and 51, the same without its copy-free first column steps); every other
+// entry is compiled only into the ablation library (ABL), and the stagger /
+// priority experiments (8, 9, 11, 12, 37) are retired (RET).
 struct LeafVariant {
   const void* fn;
   int wg;

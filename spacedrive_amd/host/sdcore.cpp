@@ -260,6 +260,26 @@ std::vector<FilePathRow> MemoryLibrary::get_orphan_file_paths(int32_t location_i
   return out;
 }
 
+static bool orphan_in_dir(const FilePathRow& r, int32_t location_id, const std::string& dir) {
+  return (!r.object_id || !r.cas_id) && !r.is_dir && r.location_id == location_id && r.size_in_bytes != 0 &&
+         r.materialized_path == dir;
+}
+
+size_t MemoryLibrary::count_orphan_file_paths_in_dir(int32_t location_id, const std::string& dir) {
+  return (size_t)std::count_if(file_paths.begin(), file_paths.end(),
+                               [&](const FilePathRow& r) { return orphan_in_dir(r, location_id, dir); });
+}
+
+std::vector<FilePathRow> MemoryLibrary::get_orphan_file_paths_in_dir(int32_t location_id, int32_t cursor,
+                                                                     const std::string& dir, size_t take) {
+  std::vector<FilePathRow> out;
+  for (const auto& r : file_paths) {
+    if (out.size() >= take) break;
+    if (r.id >= cursor && orphan_in_dir(r, location_id, dir)) out.push_back(r);
+  }
+  return out;
+}
+
 void MemoryLibrary::set_cas_id(int32_t id, const std::optional<std::string>& cas_id) {
   if (auto* r = find(id)) r->cas_id = cas_id;
 }
@@ -471,27 +491,33 @@ std::pair<size_t, size_t> identifier_job_step(Engine& engine, Library& db, const
       window, chunk_size);
 }
 
-FileIdentifierJobRunMetadata run_file_identifier_job_with(Library& db, const FileIdentifierJobInit& init,
-                                                          const MetadataFn& metadata, const GroupBy& group_by) {
-  FileIdentifierJobRunMetadata meta;
+namespace {
+// The steps of the identifier over its orphans, `batch` rows per fetch
+// (file_identifier_job.rs:180-236 and shallow.rs:92-112 share it): each batch
+// runs as many of the job's 100-row steps as it holds (identifier_step_db),
+// and the cursor moves to the last row they read (mod.rs:401-405).
+struct StepLoop {
+  size_t created = 0, linked = 0, steps = 0, batches = 0, rereads = 0;
+  int32_t cursor = 0;
+  bool ran_dry = false;  // a fetch found no rows
+};
+using Fetch = std::function<std::vector<FilePathRow>(int32_t cursor, size_t take)>;
+
+StepLoop run_steps(Library& db, uint64_t task_count, int32_t cursor, size_t batch_rows, const Fetch& fetch,
+                   const MetadataFn& metadata, const GroupBy& group_by) {
+  StepLoop L;
+  L.cursor = cursor;
   const size_t cs = SDCAS_IDENTIFIER_CHUNK_SIZE;
-  const size_t batch = std::max(cs, init.batch);  // a batch holds at least one whole step
-  const int32_t loc = init.location.id;
-  // init (file_identifier_job.rs:125-176)
-  meta.total_orphan_paths = db.count_orphan_file_paths(loc, init.sub_materialized_path);
-  if (meta.total_orphan_paths == 0) return meta;
-  auto first = db.get_orphan_file_paths(loc, 0, init.sub_materialized_path, 1);
-  meta.cursor = first.empty() ? 0 : first[0].id;
-  uint64_t steps_left = (meta.total_orphan_paths + cs - 1) / cs;  // task_count (:146)
+  const size_t batch = std::max(cs, batch_rows);  // a batch holds at least one whole step
+  uint64_t steps_left = task_count;
   while (steps_left) {
-    // execute_step's query (file_identifier_job.rs:296-319), `batch` rows at a time
-    auto rows = db.get_orphan_file_paths(loc, meta.cursor, init.sub_materialized_path, batch);
-    if (rows.empty()) {  // EarlyFinish (:203-209)
-      meta.early_finish = true;
+    auto rows = fetch(L.cursor, batch);  // id >= cursor ORDER BY id (file_identifier_job.rs:296-319)
+    if (rows.empty()) {
+      L.ran_dry = true;
       break;
     }
     const auto md = metadata(rows);
-    if (meta.batches && rows[0].id == meta.cursor) ++meta.rereads;  // the cursor row is still an orphan
+    if (L.batches && rows[0].id == L.cursor) ++L.rereads;  // the cursor row is still an orphan
     sdcas_job_window w{};
     w.max_steps = steps_left;
     w.more = rows.size() == batch;
@@ -507,29 +533,94 @@ FileIdentifierJobRunMetadata run_file_identifier_job_with(Library& db, const Fil
     }
     auto [created, linked] = identifier_step_db(db, rows, md, group_by, &w, cs);
     if (w.steps == 0) break;  // cannot happen: a batch of `batch` >= cs rows holds a whole step
-    meta.total_objects_created += created;
-    meta.total_objects_linked += linked;
-    meta.steps += w.steps;
-    meta.rereads += w.rereads;
-    ++meta.batches;
+    L.created += created;
+    L.linked += linked;
+    L.steps += w.steps;
+    L.rereads += w.rereads;
+    ++L.batches;
     steps_left -= std::min<uint64_t>(steps_left, w.steps);
-    meta.cursor = rows[w.rows - 1].id;  // process_identifier_file_paths (mod.rs:401-405)
+    L.cursor = rows[w.rows - 1].id;
   }
+  return L;
+}
+}  // namespace
+
+FileIdentifierJobRunMetadata run_file_identifier_job_with(Library& db, const FileIdentifierJobInit& init,
+                                                          const MetadataFn& metadata, const GroupBy& group_by) {
+  FileIdentifierJobRunMetadata meta;
+  const int32_t loc = init.location.id;
+  const std::string& sub = init.sub_materialized_path;
+  // init (file_identifier_job.rs:125-176)
+  meta.total_orphan_paths = db.count_orphan_file_paths(loc, sub);
+  if (meta.total_orphan_paths == 0) return meta;
+  auto first = db.get_orphan_file_paths(loc, 0, sub, 1);
+  meta.cursor = first.empty() ? 0 : first[0].id;
+  const uint64_t task_count = (meta.total_orphan_paths + SDCAS_IDENTIFIER_CHUNK_SIZE - 1) / SDCAS_IDENTIFIER_CHUNK_SIZE;
+  const StepLoop L = run_steps(
+      db, task_count, meta.cursor, init.batch,
+      [&](int32_t cursor, size_t take) { return db.get_orphan_file_paths(loc, cursor, sub, take); }, metadata,
+      group_by);
+  meta.total_objects_created = L.created;
+  meta.total_objects_linked = L.linked;
+  meta.steps = L.steps;
+  meta.batches = L.batches;
+  meta.rereads = L.rereads;
+  meta.cursor = L.cursor;
+  meta.early_finish = L.ran_dry;  // EarlyFinish (:203-209)
   return meta;
+}
+
+ShallowIdentifierReport shallow_file_identifier_with(Library& db, const Location& location, const std::string& dir,
+                                                     size_t batch, const MetadataFn& metadata,
+                                                     const GroupBy& group_by) {
+  ShallowIdentifierReport rep;
+  const std::string d = dir.empty() ? "/" : dir;  // materialized_path_for_children of the root
+  rep.orphans = db.count_orphan_file_paths_in_dir(location.id, d);  // shallow.rs:62-66
+  if (rep.orphans == 0) return rep;
+  // find_first without ordering (shallow.rs:74-84): the lowest orphan id
+  auto first = db.get_orphan_file_paths_in_dir(location.id, 0, d, 1);
+  if (first.empty()) return rep;  // "another Job finishing first" (shallow.rs:81-83)
+  const uint64_t task_count = (rep.orphans + SDCAS_IDENTIFIER_CHUNK_SIZE - 1) / SDCAS_IDENTIFIER_CHUNK_SIZE;
+  // every step runs (shallow.rs:92-112): one that finds no rows changes
+  // nothing, so the loop may stop at the first empty fetch
+  const StepLoop L = run_steps(
+      db, task_count, first[0].id, batch,
+      [&](int32_t cursor, size_t take) { return db.get_orphan_file_paths_in_dir(location.id, cursor, d, take); },
+      metadata, group_by);
+  rep.steps = L.steps;
+  rep.batches = L.batches;
+  rep.rereads = L.rereads;
+  rep.created = L.created;
+  rep.linked = L.linked;
+  rep.cursor = L.cursor;
+  return rep;
+}
+
+static std::vector<Result<FileMetadata>> metadata_of(Engine& engine, const Location& location,
+                                                     const std::vector<FilePathRow>& rows) {
+  std::vector<std::pair<std::string, ObjectKind>> files(rows.size());
+  for (size_t i = 0; i < rows.size(); ++i) files[i] = {full_path(location, rows[i]), rows[i].kind};
+  return file_metadata_batch(engine, files);
+}
+
+static GroupBy gpu_group_by(Engine& engine) {
+  return [&engine](const std::vector<uint64_t>& k, const std::vector<uint8_t>& h, const std::vector<int32_t>& st,
+                   const std::vector<uint64_t>& e, sdcas_job_window& w) {
+    return engine.dedup(k, h, st, SDCAS_IDENTIFIER_CHUNK_SIZE, e, &w);
+  };
+}
+
+ShallowIdentifierReport shallow_file_identifier(Engine& engine, Library& db, const Location& location,
+                                                const std::string& dir, size_t batch) {
+  return shallow_file_identifier_with(
+      db, location, dir, batch, [&](const std::vector<FilePathRow>& rows) { return metadata_of(engine, location, rows); },
+      gpu_group_by(engine));
 }
 
 FileIdentifierJobRunMetadata run_file_identifier_job(Engine& engine, Library& db, const FileIdentifierJobInit& init) {
   return run_file_identifier_job_with(
-      db, init,
-      [&](const std::vector<FilePathRow>& rows) {
-        std::vector<std::pair<std::string, ObjectKind>> files(rows.size());
-        for (size_t i = 0; i < rows.size(); ++i) files[i] = {full_path(init.location, rows[i]), rows[i].kind};
-        return file_metadata_batch(engine, files);
-      },
-      [&](const std::vector<uint64_t>& k, const std::vector<uint8_t>& h, const std::vector<int32_t>& st,
-          const std::vector<uint64_t>& e, sdcas_job_window& w) {
-        return engine.dedup(k, h, st, SDCAS_IDENTIFIER_CHUNK_SIZE, e, &w);
-      });
+      db, init, [&](const std::vector<FilePathRow>& rows) { return metadata_of(engine, init.location, rows); },
+      gpu_group_by(engine));
 }
 
 // ---- object validator -----------------------------------------------------------------

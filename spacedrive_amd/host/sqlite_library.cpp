@@ -42,6 +42,7 @@ PubId pub_id(uint32_t tag, int64_t id) {
 
 struct SqliteLibrary::Impl {
   sqlite3* db = nullptr;
+  Stmt count_orphans_dir, get_orphans_dir;
   Stmt count_orphans, get_orphans, set_cas, want_clear, want_add, existing, new_object, connect, no_checksum,
       set_checksum, add_path, get_path, all_objects;
   int64_t next_object = 1;
@@ -121,6 +122,10 @@ struct SqliteLibrary::Impl {
   "(object_id IS NULL OR cas_id IS NULL) AND is_dir = 0 AND location_id = ?1 AND "                      \
   "size_in_bytes_bytes != x'0000000000000000' AND substr(materialized_path, 1, length(?2)) = ?2"
 
+#define SD_ORPHAN_DIR                                                                                   \
+  "(object_id IS NULL OR cas_id IS NULL) AND is_dir = 0 AND location_id = ?1 AND "                      \
+  "size_in_bytes_bytes != x'0000000000000000' AND materialized_path = ?2"
+
 SqliteLibrary::SqliteLibrary(std::unique_ptr<Impl> d) : d_(std::move(d)) {}
 
 SqliteLibrary::~SqliteLibrary() {
@@ -165,6 +170,10 @@ std::unique_ptr<SqliteLibrary> SqliteLibrary::open(const std::string& path, bool
   // step rescan the whole location: quadratic over a job)
   x.prepare(x.get_orphans,
             "SELECT " SD_COLS " FROM file_path NOT INDEXED WHERE " SD_ORPHAN " AND id >= ?3 ORDER BY id LIMIT ?4");
+  // shallow.rs:120-142: one directory level (materialized_path = ?2)
+  x.prepare(x.count_orphans_dir, "SELECT COUNT(*) FROM file_path WHERE " SD_ORPHAN_DIR);
+  x.prepare(x.get_orphans_dir,
+            "SELECT " SD_COLS " FROM file_path WHERE " SD_ORPHAN_DIR " AND id >= ?3 ORDER BY id LIMIT ?4");
   x.prepare(x.set_cas, "UPDATE file_path SET cas_id = ?1 WHERE id = ?2");
   x.prepare(x.want_clear, "DELETE FROM want_cas");
   x.prepare(x.want_add, "INSERT OR IGNORE INTO want_cas (cas_id) VALUES (?1)");
@@ -281,6 +290,25 @@ size_t SqliteLibrary::count_orphan_file_paths(int32_t location_id, const std::st
   sqlite3_reset(x.count_orphans.s);
   sqlite3_clear_bindings(x.count_orphans.s);
   return n;
+}
+
+size_t SqliteLibrary::count_orphan_file_paths_in_dir(int32_t location_id, const std::string& dir) {
+  Impl& x = *d_;
+  x.bind_scope(x.count_orphans_dir, location_id, dir);
+  if (sqlite3_step(x.count_orphans_dir.s) != SQLITE_ROW) x.fail("count orphans in dir");
+  const size_t n = (size_t)sqlite3_column_int64(x.count_orphans_dir.s, 0);
+  sqlite3_reset(x.count_orphans_dir.s);
+  sqlite3_clear_bindings(x.count_orphans_dir.s);
+  return n;
+}
+
+std::vector<FilePathRow> SqliteLibrary::get_orphan_file_paths_in_dir(int32_t location_id, int32_t cursor,
+                                                                     const std::string& dir, size_t take) {
+  Impl& x = *d_;
+  x.bind_scope(x.get_orphans_dir, location_id, dir);
+  sqlite3_bind_int64(x.get_orphans_dir.s, 3, cursor);
+  sqlite3_bind_int64(x.get_orphans_dir.s, 4, (int64_t)take);
+  return x.rows(x.get_orphans_dir);
 }
 
 std::vector<FilePathRow> SqliteLibrary::get_orphan_file_paths(int32_t location_id, int32_t cursor,

@@ -366,6 +366,64 @@ static void test_location_scan(Engine& eng, const std::string& dir) {
               ids.size(), meta.total_objects_created, meta.total_objects_linked);
 }
 
+// light_scan_location's shallow identifier (shallow.rs:24-142) on the GPU:
+// only the orphans of one directory level, against the oracle's job over them
+static void test_shallow_scan(Engine& eng, const std::string& dir) {
+  const std::string root = dir + "/shallow";
+  mkdir(root.c_str(), 0755);
+  mkdir((root + "/docs").c_str(), 0755);
+  mkdir((root + "/docs/old").c_str(), 0755);
+  std::mt19937_64 g(5);
+  for (int i = 0; i < 900; ++i) {
+    const char* d = i % 3 == 0 ? "" : (i % 3 == 1 ? "/docs" : "/docs/old");
+    const uint64_t which = g() % 150;
+    const size_t size = which % 17 == 3 ? 0 : 1 + (which * 104729) % 200000;  // some empty files
+    write_file(root + d + "/g" + std::to_string(i) + ".dat", content(which + 7000, size));
+  }
+  auto rows = walk_location(Location{4, root});
+  for (auto& r : rows)
+    if (!r.is_dir && r.size_in_bytes == 0) r.size_in_bytes = 1;  // indexed before the file was emptied
+  auto sql = SqliteLibrary::open(":memory:");
+  sql->add_file_paths(rows);
+  auto rep = shallow_file_identifier(eng, *sql, Location{4, root}, "/docs/", 1000);
+  std::vector<uint64_t> keys;
+  std::vector<uint8_t> has;
+  std::vector<int32_t> ids;
+  for (const auto& r : rows) {
+    if (r.is_dir || r.materialized_path != "/docs/") continue;
+    const std::string p = full_path(Location{4, root}, r);
+    struct stat sb;
+    stat(p.c_str(), &sb);
+    int st = 0;
+    const std::string cas = sb.st_size ? oracle_cas(p, (uint64_t)sb.st_size, &st) : std::string();
+    keys.push_back(cas.empty() ? 0 : hex_to_key(cas));
+    has.push_back(!cas.empty());
+    ids.push_back(r.id);
+  }
+  std::vector<int64_t> link(keys.size());
+  int64_t linked = 0;
+  const int64_t created =
+      oracle_identifier_dedup(keys.size(), keys.data(), has.data(), nullptr, 100, 0, nullptr, link.data(), &linked);
+  CHECK(rep.orphans == ids.size() && (int64_t)rep.created == created && (int64_t)rep.linked == linked,
+        "shallow: %zu orphans created/linked %zu/%zu, oracle %zu %lld/%lld", rep.orphans, rep.created, rep.linked,
+        ids.size(), (long long)created, (long long)linked);
+  for (size_t k = 0; k < ids.size(); ++k) {
+    auto r = sql->file_path(ids[k]);
+    if (link[k] == SDCAS_LINK_DEFERRED) continue;
+    CHECK(r && r->object_id, "shallow row %d has no Object", ids[k]);
+    if (has[k]) CHECK(r->cas_id && hex_to_key(*r->cas_id) == keys[k], "shallow cas_id of row %d", ids[k]);
+    if (link[k] >= 0 && link[k] != (int64_t)k)
+      CHECK(r->object_id == sql->file_path(ids[(size_t)link[k]])->object_id, "shallow object of row %d", ids[k]);
+  }
+  for (const auto& r : rows)
+    if (r.materialized_path != "/docs/") {
+      auto s = sql->file_path(r.id);
+      CHECK(s && !s->cas_id && !s->object_id, "shallow touched row %d outside its level", r.id);
+    }
+  std::printf("shallow identifier /docs/: %zu orphans, created %zu linked %zu in %zu steps (%zu re-reads)\n",
+              rep.orphans, rep.created, rep.linked, rep.steps, rep.rereads);
+}
+
 int main(int argc, char** argv) {
   if (argc > 1 && std::strcmp(argv[1], "--no-gpu") == 0) {
     try {
@@ -384,6 +442,7 @@ int main(int argc, char** argv) {
   test_identifier_job(*eng, dir);
   test_validator(*eng, dir);
   test_location_scan(*eng, dir);
+  test_shallow_scan(*eng, dir);
   std::string cmd = "rm -rf " + dir;
   if (std::system(cmd.c_str()) != 0) std::fprintf(stderr, "cleanup failed\n");
   std::printf("%s (%d failures)\n", failures ? "FAILED" : "ALL OK", failures);

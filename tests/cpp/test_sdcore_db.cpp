@@ -126,6 +126,69 @@ static bool same_rows(const std::vector<FilePathRow>& a, const std::vector<FileP
   return true;
 }
 
+// the shallow identifier (shallow.rs:24-142) on memory and SQLite, batches of
+// 100 and 10000: one directory level only, its own task_count, the same
+// cursor steps; against the oracle's job over exactly that level's orphans
+static void test_shallow() {
+  MemoryLibrary base;
+  auto rows = make_rows(4000, 17);
+  for (auto& r : rows) r = base.add_file_path(r);
+  g_err_mod = 7;
+  g_none_mod = 5;
+  for (const char* dir : {"/sub/", "", "/sub/deeper/", "/nope/"}) {
+    // a fresh library per level, so the oracle sees no existing Objects
+    MemoryLibrary mem = base, mem_b = base;
+    auto sql = SqliteLibrary::open(":memory:");
+    std::vector<FilePathRow> copy = base.file_paths;
+    sql->add_file_paths(copy);
+    const std::string d = *dir ? dir : "/";
+    const auto orphans = mem.get_orphan_file_paths_in_dir(1, 0, d, 1u << 30);
+    for (const auto& r : orphans) CHECK(r.materialized_path == d, "shallow orphan outside %s", d.c_str());
+    CHECK(mem.count_orphan_file_paths_in_dir(1, d) == orphans.size() &&
+              sql->count_orphan_file_paths_in_dir(1, d) == orphans.size(),
+          "shallow count %s", d.c_str());
+    // the oracle over the level's orphans in id order (nothing exists before)
+    auto md = make_metadata(orphans, 300);
+    std::vector<uint64_t> keys(orphans.size(), 0);
+    std::vector<uint8_t> has(orphans.size(), 0);
+    std::vector<int32_t> st(orphans.size(), 0);
+    for (size_t i = 0; i < orphans.size(); ++i) {
+      if (!md[i].ok()) st[i] = md[i].error().code;
+      else if (md[i].value().cas_id) has[i] = 1, keys[i] = hex_to_key(*md[i].value().cas_id);
+    }
+    std::vector<int64_t> link(orphans.size());
+    int64_t linked = 0;
+    const int64_t created = oracle_identifier_dedup(orphans.size(), keys.data(), has.data(), st.data(), 100, 0,
+                                                    nullptr, link.data(), &linked);
+    auto meta = [&](const std::vector<FilePathRow>& r) { return make_metadata(r, 300); };
+    const Location loc{1, "/nowhere"};
+    auto a = shallow_file_identifier_with(mem, loc, dir, 100, meta, oracle_group_by(100));
+    auto b = shallow_file_identifier_with(*sql, loc, dir, 100, meta, oracle_group_by(100));
+    auto c = shallow_file_identifier_with(mem_b, loc, dir, 10000, meta, oracle_group_by(100));
+    CHECK(a.orphans == orphans.size() && (int64_t)a.created == created && (int64_t)a.linked == linked,
+          "shallow %s: created/linked %zu/%zu, oracle %lld/%lld", d.c_str(), a.created, a.linked, (long long)created,
+          (long long)linked);
+    for (const auto* o : {&b, &c})
+      CHECK(o->created == a.created && o->linked == a.linked && o->steps == a.steps && o->cursor == a.cursor &&
+                o->rereads == a.rereads,
+            "shallow %s: %zu/%zu/%zu steps vs %zu/%zu/%zu", d.c_str(), a.created, a.linked, a.steps, o->created,
+            o->linked, o->steps);
+    std::printf("shallow %s: %zu orphans, created %zu linked %zu in %zu steps, %zu re-reads (memory == sqlite, "
+                "batches 100 == 10000 == oracle)\n",
+                d.c_str(), a.orphans, a.created, a.linked, a.steps, a.rereads);
+    for (const auto& r : mem.file_paths) {
+      auto s = sql->file_path(r.id);
+      CHECK(s && same_row(r, *s), "shallow row %d memory vs sqlite", r.id);
+      const FilePathRow* b = mem_b.file_path(r.id);
+      CHECK(b && same_row(r, *b), "shallow row %d batch 100 vs 10000", r.id);
+      // rows of other levels are untouched
+      if (r.materialized_path != d) CHECK(same_row(r, *base.file_path(r.id)), "shallow touched row %d", r.id);
+    }
+  }
+  g_err_mod = 97;
+  g_none_mod = 31;
+}
+
 static void test_parity(bool cas_index) {
   MemoryLibrary mem;
   auto sql = SqliteLibrary::open(":memory:", cas_index);
@@ -226,6 +289,13 @@ struct Autocommit : Library {
   std::vector<FilePathRow> get_orphan_file_paths(int32_t l, int32_t c, const std::string& s, size_t t) override {
     return d.get_orphan_file_paths(l, c, s, t);
   }
+  size_t count_orphan_file_paths_in_dir(int32_t l, const std::string& s) override {
+    return d.count_orphan_file_paths_in_dir(l, s);
+  }
+  std::vector<FilePathRow> get_orphan_file_paths_in_dir(int32_t l, int32_t c, const std::string& s,
+                                                        size_t t) override {
+    return d.get_orphan_file_paths_in_dir(l, c, s, t);
+  }
   void set_cas_id(int32_t i, const std::optional<std::string>& c) override { d.set_cas_id(i, c); }
   std::vector<std::pair<int32_t, std::vector<std::string>>> existing_objects(
       const std::vector<std::string>& c) override {
@@ -263,6 +333,13 @@ struct Timed : Library {
   }
   std::vector<FilePathRow> get_orphan_file_paths(int32_t l, int32_t c, const std::string& s, size_t n) override {
     return tm(1, [&] { return d.get_orphan_file_paths(l, c, s, n); });
+  }
+  size_t count_orphan_file_paths_in_dir(int32_t l, const std::string& s) override {
+    return d.count_orphan_file_paths_in_dir(l, s);
+  }
+  std::vector<FilePathRow> get_orphan_file_paths_in_dir(int32_t l, int32_t c, const std::string& s,
+                                                        size_t n) override {
+    return tm(1, [&] { return d.get_orphan_file_paths_in_dir(l, c, s, n); });
   }
   void set_cas_id(int32_t i, const std::optional<std::string>& c) override { tm(2, [&] { d.set_cas_id(i, c); }); }
   std::vector<std::pair<int32_t, std::vector<std::string>>> existing_objects(
@@ -467,6 +544,7 @@ int main(int argc, char** argv) {
   if (argc > 2 && std::strcmp(argv[1], "--bench") == 0) return bench((size_t)std::atoll(argv[2]));
   test_parity(true);
   test_parity(false);
+  test_shallow();
   // many rows that stay orphans: re-reads at most step ends
   g_err_mod = 7;
   g_none_mod = 5;

@@ -240,6 +240,36 @@ def test_cas_ids_cancel_per_slot(oracle, tmp_path):
         assert (ex.value.partial[1] == N.SDCAS_STATUS_CANCELLED).all()
 
 
+def test_message_calls_cancel(oracle):
+    """sdcas_hash_messages over many staging slots, cancelled after about a
+    third: the call returns SDCAS_E_CANCELLED (its outputs carry no per-item
+    status, so Cancelled holds no partial results); with the flag cleared the
+    same context hashes the batch exactly"""
+    import ctypes
+    from spacedrive_amd import Engine
+    from spacedrive_amd import _native as N
+    rng = np.random.default_rng(12)
+    msgs = [rng.integers(0, 256, int(rng.integers(1, 100_000)), dtype=np.uint8).tobytes() for _ in range(600)]
+    blob, offs, lens = Engine.pack(msgs)
+    flag = ctypes.c_int32(0)
+
+    def progress(done, total):
+        if done >= total // 3:
+            flag.value = 1
+
+    with Engine(staging_bytes=1 * MiB, io_threads=4, progress=progress, cancel=flag) as e:
+        with pytest.raises(N.Cancelled) as ex:
+            e.hash_messages(blob, offs, lens)
+        assert ex.value.partial is None
+        with pytest.raises(N.Cancelled):
+            e.cas_ids_from_messages(blob, offs, lens)
+        flag.value = 0
+        e.set_progress(None, flag)
+        out = e.hash_messages(blob, offs, lens)
+        for i in range(0, len(msgs), 37):
+            assert bytes(out[i]).hex() == oracle.hash(msgs[i]), i
+
+
 @pytest.mark.parametrize("direct", [False, True])
 def test_checksums_parallel_pieces_and_direct_io(oracle, tmp_path, direct):
     """file_checksum of files over 1 MiB: a window's 1 MiB pieces are read by
