@@ -370,6 +370,39 @@ int sdcas_dev_dedup_local(sdcas_ctx *ctx, const uint64_t *d_keys, const uint8_t 
                           uint64_t max_steps, uint32_t more, int64_t *d_link, uint64_t *d_counts,
                           uint64_t *d_plan_header, void *stream);
 
+/* ---- one process, several GPUs (a node) ----------------------------------
+ *
+ * sd-core is one process (Node::new, apps/server/src/main.rs:40; jobs run
+ * in-process, job/manager.rs:32). A node is one context per entry of
+ * `devices` (a device may repeat: two contexts on one GPU), with the batch
+ * calls sharded over them and the dedup's exchange run in this process —
+ * RCCL (ncclCommInitAll, grouped ncclSend / ncclRecv) when every device is
+ * distinct, device-to-device copies otherwise (or with the environment
+ * variable SDCAS_NODE_EXCHANGE=copy). Results are those of the single-context
+ * calls. opts (may be NULL) applies to every context; its progress function
+ * receives the node's sums and may run on any of the node's threads (one at a
+ * time). Calls on one node serialise. */
+typedef struct sdcas_node sdcas_node;
+int sdcas_node_init(const int32_t *devices, size_t n_devices, const sdcas_options *opts, sdcas_node **out_node);
+void sdcas_node_destroy(sdcas_node *node);
+const char *sdcas_node_last_error(const sdcas_node *node);
+size_t sdcas_node_size(const sdcas_node *node);
+/* 1 when the dedup exchange runs over RCCL, 0 over device copies */
+int sdcas_node_uses_rccl(const sdcas_node *node);
+int sdcas_node_set_progress(sdcas_node *node, sdcas_progress_fn progress, void *user, const volatile int32_t *cancel);
+/* sdcas_cas_ids with the files cut into contiguous ranges of about equal
+ * cas-message bytes, one per context */
+int sdcas_node_cas_ids(sdcas_node *node, const char *const *paths, const uint64_t *sizes, size_t n,
+                       uint64_t *out_keys, int32_t *out_status);
+/* sdcas_checksums with the files assigned largest first to the least loaded context */
+int sdcas_node_checksums(sdcas_node *node, const char *const *paths, size_t n, uint8_t *out32, int32_t *out_status);
+/* sdcas_dedup_window over the node: contiguous ordinal ranges per context,
+ * stays all-gathered and planned on every context, records exchanged to the
+ * key's owner context (top 12 key bits), resolved there, answers returned */
+int sdcas_node_dedup_window(sdcas_node *node, const uint64_t *keys, const uint8_t *has_key, const int32_t *status,
+                            size_t n, size_t chunk_size, const uint64_t *existing_keys, size_t n_existing,
+                            sdcas_job_window *window, int64_t *out_link, int64_t *out_created, int64_t *out_linked);
+
 /* ---- helpers ------------------------------------------------------------ */
 
 void sdcas_key_to_hex(uint64_t key, char out[17]);

@@ -6,8 +6,8 @@ Object dedup of core/src/object/file_identifier/mod.rs:98-350, executed by the
 HIP kernels of libsdcas.so (spacedrive_amd/csrc) through the C ABI of
 include/sdcas.h.
 """
-from .engine import (Engine, default_engine, digest_to_hex, file_checksum, generate_cas_id, io_error,
+from .engine import (Engine, Node, default_engine, digest_to_hex, file_checksum, generate_cas_id, io_error,
                      key_to_hex)
 
-__all__ = ["Engine", "default_engine", "digest_to_hex", "file_checksum", "generate_cas_id", "io_error",
+__all__ = ["Engine", "Node", "default_engine", "digest_to_hex", "file_checksum", "generate_cas_id", "io_error",
            "key_to_hex"]

@@ -41,7 +41,9 @@ ABI_SYMBOLS = [
     "sdcas_dev_dedup_apply", "sdcas_dev_dedup_local", "sdcas_dev_dedup_combine_buckets",
     "sdcas_dev_dedup_resolve_buckets", "sdcas_dev_dedup_stays", "sdcas_dev_dedup_plan", "sdcas_dev_stream_begin", "sdcas_dev_stream_update",
     "sdcas_dev_stream_finish", "sdcas_dev_stream_node_bytes", "sdcas_dev_stream_export", "sdcas_dev_stream_import",
-    "sdcas_set_progress",
+    "sdcas_set_progress", "sdcas_node_init", "sdcas_node_destroy", "sdcas_node_last_error", "sdcas_node_size",
+    "sdcas_node_uses_rccl", "sdcas_node_set_progress", "sdcas_node_cas_ids", "sdcas_node_checksums",
+    "sdcas_node_dedup_window",
     # bench / test plumbing
     "sdcas_dev_synth_cas_messages", "sdcas_dev_synth_content", "sdcas_dev_dedup", "sdcas_dev_profile",
     "sdcas_dev_last_kernel_ms", "sdcas_dev_set_leaf_variant", "sdcas_dev_set_piece_variant", "sdcas_dev_set_sort",
@@ -170,5 +172,17 @@ def load():
     L.sdcas_dev_stream_node_bytes.restype = _sz
     L.sdcas_dev_stream_export.argtypes = [_vp, _vp, _sz, _vp]
     L.sdcas_dev_stream_import.argtypes = [_vp, _vp, _sz, _vp]
+    L.sdcas_node_init.argtypes = [_vp, _sz, ctypes.POINTER(Options), ctypes.POINTER(_vp)]
+    L.sdcas_node_destroy.argtypes = [_vp]
+    L.sdcas_node_last_error.argtypes = [_vp]
+    L.sdcas_node_last_error.restype = ctypes.c_char_p
+    L.sdcas_node_size.argtypes = [_vp]
+    L.sdcas_node_size.restype = _sz
+    L.sdcas_node_uses_rccl.argtypes = [_vp]
+    L.sdcas_node_set_progress.argtypes = [_vp, PROGRESS_FN, _vp, ctypes.POINTER(ctypes.c_int32)]
+    L.sdcas_node_cas_ids.argtypes = [_vp, _vp, _vp, _sz, _vp, _vp]
+    L.sdcas_node_checksums.argtypes = [_vp, _vp, _sz, _vp, _vp]
+    L.sdcas_node_dedup_window.argtypes = [_vp, _vp, _vp, _vp, _sz, _sz, _vp, _sz, ctypes.POINTER(JobWindow), _vp,
+                                          _vp, _vp]
     _lib = L
     return L

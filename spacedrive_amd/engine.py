@@ -320,3 +320,97 @@ def file_checksum(path) -> str:
 
 __all__ = ["Engine", "generate_cas_id", "file_checksum", "key_to_hex", "digest_to_hex", "io_error",
            "default_engine"]
+
+
+class Node:
+    """sdcas_node: one process driving several GPUs (one context per entry of
+    `devices`; a device may repeat). The batch calls shard over the contexts
+    and the dedup's exchange runs in this process (RCCL between distinct
+    devices, device copies otherwise)."""
+
+    def __init__(self, devices=(0,), io_threads: int = 0, staging_bytes: int = 0, direct_io=False, progress=None,
+                 cancel=None):
+        self.L = N.load()
+        self._cb = Engine._progress_fn(progress)
+        self._cancel = cancel
+        opts = N.Options(-1, io_threads, N.SDCAS_OPT_DIRECT_IO if direct_io else 0, staging_bytes, self._cb,
+                         None, ctypes.pointer(cancel) if cancel is not None else None)
+        devs = (ctypes.c_int32 * len(devices))(*devices)
+        node = ctypes.c_void_p()
+        rc = self.L.sdcas_node_init(devs, len(devices), ctypes.byref(opts), ctypes.byref(node))
+        if rc != N.SDCAS_OK:
+            raise N.SdcasError(rc, "sdcas_node_init failed")
+        self.node = node
+
+    @property
+    def size(self):
+        return int(self.L.sdcas_node_size(self.node))
+
+    @property
+    def uses_rccl(self):
+        return bool(self.L.sdcas_node_uses_rccl(self.node))
+
+    def close(self):
+        if getattr(self, "node", None):
+            self.L.sdcas_node_destroy(self.node)
+            self.node = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what, partial=None):
+        if rc != N.SDCAS_OK:
+            msg = self.L.sdcas_node_last_error(self.node).decode(errors="replace")
+            if rc == N.SDCAS_E_CANCELLED:
+                raise N.Cancelled(f"{what}: {msg}", partial)
+            raise N.SdcasError(rc, f"{what}: {msg}")
+
+    def generate_cas_ids(self, paths, sizes):
+        n = len(paths)
+        buf, parr = _cpaths(paths)
+        sizes = _arr(sizes, np.uint64)
+        keys = np.zeros(n, np.uint64)
+        st = np.zeros(n, np.int32)
+        self._check(self.L.sdcas_node_cas_ids(self.node, _ptr(parr), _ptr(sizes), n, _ptr(keys), _ptr(st)),
+                    "sdcas_node_cas_ids", (keys, st))
+        del buf
+        return keys, st
+
+    def file_checksums(self, paths):
+        n = len(paths)
+        buf, parr = _cpaths(paths)
+        out = np.zeros((n, 32), np.uint8)
+        st = np.zeros(n, np.int32)
+        self._check(self.L.sdcas_node_checksums(self.node, _ptr(parr), n, _ptr(out), _ptr(st)),
+                    "sdcas_node_checksums", (out, st))
+        del buf
+        return out, st
+
+    def identifier_dedup_window(self, keys, has_key, status=None, chunk_size=100, existing_keys=(), max_steps=0,
+                                more=False):
+        keys = _arr(keys, np.uint64)
+        n = keys.size
+        has_key = _arr(has_key, np.uint8)
+        st = None if status is None else _arr(status, np.int32)
+        ex = _arr(existing_keys, np.uint64)
+        out = np.zeros(n, np.int64)
+        created, linked = ctypes.c_int64(0), ctypes.c_int64(0)
+        win = N.JobWindow(int(max_steps), int(bool(more)), 0, 0, 0, 0)
+        self._check(self.L.sdcas_node_dedup_window(self.node, _ptr(keys), _ptr(has_key), _ptr(st), n, chunk_size,
+                                                   _ptr(ex), ex.size, ctypes.byref(win), _ptr(out),
+                                                   ctypes.byref(created), ctypes.byref(linked)),
+                    "sdcas_node_dedup_window")
+        return out, created.value, linked.value, {"steps": win.steps, "rows": win.rows, "rereads": win.rereads}
+
+    def identifier_dedup(self, keys, has_key, status=None, chunk_size=100, existing_keys=()):
+        link, c, l, _ = self.identifier_dedup_window(keys, has_key, status, chunk_size, existing_keys)
+        return link, c, l

@@ -1,0 +1,73 @@
+"""A node: one process driving several GPU contexts (sdcas_node_*,
+spacedrive_amd.Node) — sd-core is one process (apps/server/src/main.rs:40,
+job/manager.rs:32), so the multi-GPU paths must be reachable without a
+process per GPU. On this one-GPU box the node is [0, 0]: two contexts on one
+device, the exchange as device-to-device copies; between distinct devices
+the same calls exchange over RCCL (ncclCommInitAll), unmeasured here.
+Everything against the oracle."""
+import numpy as np
+import pytest
+
+from tests._dist_stages import make_corpus
+from tests._oracle import cas_windows, content, content_key, write_sparse_file
+
+pytestmark = pytest.mark.gpu
+MiB = 1 << 20
+
+
+@pytest.fixture(scope="module", params=[(0,), (0, 0), (0, 0, 0)], ids=["node1", "node2", "node3"])
+def node(request):
+    from spacedrive_amd import Node
+    n = Node(devices=request.param, staging_bytes=16 * MiB)
+    assert n.size == len(request.param) and not n.uses_rccl
+    yield n
+    n.close()
+
+
+def test_node_dedup_vs_oracle(node, oracle):
+    """stays + plan on every context, records to their owner context, resolve,
+    answers back: the links and counts of the job over these orphans"""
+    for seed, p_none, p_err, cs in ((3, 0.02, 0.01, 100), (4, 0.2, 0.2, 100), (5, 0.05, 0.05, 7)):
+        keys, has, status, existing = make_corpus(seed, 30000, pool=5000, p_none=p_none, p_err=p_err)
+        want, wc, wl, ww = oracle.identifier_job(keys, has, status, cs, existing)
+        got, gc, gl, gw = node.identifier_dedup_window(keys, has, status, cs, existing)
+        assert np.array_equal(got, want), seed
+        assert (gc, gl) == (wc, wl) and gw == ww, seed
+    # a window of a longer job, and no existing Objects at all
+    keys, has, status, existing = make_corpus(6, 12345, p_none=0.1, p_err=0.1)
+    want, wc, wl, ww = oracle.identifier_job(keys, has, status, 100, (), 70, True)
+    got, gc, gl, gw = node.identifier_dedup_window(keys, has, status, 100, (), 70, True)
+    assert np.array_equal(got, want) and (gc, gl) == (wc, wl) and gw == ww
+    # fewer files than contexts
+    got, gc, gl, gw = node.identifier_dedup_window(keys[:1], has[:1], status[:1], 100, existing[:3])
+    want, wc, wl, ww = oracle.identifier_job(keys[:1], has[:1], status[:1], 100, existing[:3])
+    assert np.array_equal(got, want) and (gc, gl) == (wc, wl)
+
+
+def test_node_cas_ids_and_checksums(node, oracle, tmp_path):
+    """files sharded over the contexts (contiguous ranges by cas-message bytes;
+    checksums largest file first): every key and digest exact, errors in place"""
+    rng = np.random.default_rng(9)
+    paths, sizes = [], []
+    for i in range(400):
+        size = int(rng.choice([0, 1, 1017, 60_000, 102_400, 102_401, 3 * MiB + 7]))
+        k = content_key(0x5D0003, 5000 + i)
+        p = tmp_path / f"f{i}"
+        write_sparse_file(str(p), "synth", k, size, cas_windows(size))
+        paths.append(str(p))
+        sizes.append(size)
+    paths.append(str(tmp_path / "missing"))
+    sizes.append(10)
+    keys, st = node.generate_cas_ids(paths, sizes)
+    assert st[-1] == 2 and not st[:-1].any()
+    for i in range(0, 400, 7):
+        assert f"{int(keys[i]):016x}" == oracle.generate_cas_id(paths[i], sizes[i]), i
+    big = []
+    for i, size in enumerate([2 * MiB + 3, 5000, 9 * MiB, 1, 0, MiB + 1]):
+        p = tmp_path / f"c{i}"
+        p.write_bytes(content("synth", 0, size, content_key(0x5D0004, i)).tobytes())
+        big.append(str(p))
+    out, st = node.file_checksums(big + [str(tmp_path / "missing")])
+    assert st[-1] == 2 and not st[:-1].any()
+    for i, p in enumerate(big):
+        assert bytes(out[i]).hex() == oracle.file_checksum(p), p
