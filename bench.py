@@ -331,6 +331,71 @@ def e2e_c2(args, eng, torch, dev, d_blob, offs, lens, sizes, gpu_keys):
     return out
 
 
+def e2e_c3(args, eng, torch, dev, d_blob, offs, lens, sizes, gpu_keys):
+    """End-to-end C3 from files (never `value`): the first `--e2e-files` C3
+    files written to disk as SPARSE files holding only the bytes cas.rs reads
+    — the whole file up to 100 KiB, else the 8 KiB header, the four 10 KiB
+    samples at 8192 + k * ((size - 16384) / 4) and the 8 KiB footer
+    (cas.rs:30-59) — at their full apparent sizes (up to 64 GiB), taken from
+    the same cas messages the on-device loop hashes. Timed:
+      files              sdcas_cas_ids (open + one read, or open + six reads at
+                         the sampled offsets, by the library's I/O threads)
+      reference_faithful the identifier job's CPU shape over the same files
+                         (100-file steps in series, cas.rs's reads on an I/O
+                         pool, BLAKE3 on ONE thread; oracle/cpu_bench.c)"""
+    import shutil
+    import tempfile
+    from tests._oracle import load_oracle
+    m = min(int(args.e2e_files), int(lens.size))
+    end = int(offs[m - 1] + lens[m - 1])
+    host = d_blob[:end].cpu().numpy()
+    want = gpu_keys[:m]
+    sampled = int((sizes[:m] > S.MIN_FILE).sum())
+    out = {"workload": f"C3 files [0,{m}) ({sampled} sampled-branch files as sparse files)", "files": m,
+           "message_bytes": int(lens[:m].sum()), "io_threads": args.cpu_threads}
+    root = tempfile.mkdtemp(prefix="sdcas_e2e_c3_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        paths = []
+        t0 = time.perf_counter()
+        for i in range(m):
+            p = os.path.join(root, f"{i:07d}")
+            o, size = int(offs[i]), int(sizes[i])
+            msg = host[o + 8:o + int(lens[i])]
+            with open(p, "wb") as f:
+                if size <= S.MIN_FILE:
+                    f.write(msg)
+                else:
+                    jump = (size - 16384) // 4
+                    f.truncate(size)
+                    f.write(msg[:8192])
+                    for k in range(4):
+                        f.seek(8192 + k * jump)
+                        f.write(msg[8192 + k * 10240:8192 + (k + 1) * 10240])
+                    f.seek(size - 8192)
+                    f.write(msg[8192 + 40960:])
+            paths.append(p)
+        out["files_written_s"] = time.perf_counter() - t0
+        best = None
+        for _ in range(2):
+            t0 = time.perf_counter()
+            got, st = eng.generate_cas_ids(paths, sizes[:m])
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        out["files"] = {"files_per_s": m / best, "seconds": best, "mismatches": int((got != want).sum()),
+                        "errors": int((st != 0).sum()), "storage": "page cache (files just written)"}
+        keys, st, secs, hasher = load_oracle().cpu_faithful(paths, sizes[:m], 100, args.cpu_threads)
+        out["reference_faithful"] = {
+            "value": m / secs, "unit": "files/s", "cores": 1, "io_threads": args.cpu_threads, "kind": "port",
+            "seconds": secs, "mismatches": int((keys != want).sum()), "errors": int((st != 0).sum()),
+            "sample": f"C3 files [0,{m}) as sparse files in the page cache: the identifier job's CPU shape — "
+                      f"100-file steps in series (job/mod.rs:559-673), per step metadata + cas.rs reads on "
+                      f"{args.cpu_threads} I/O threads and {hasher} on ONE thread (file_identifier/mod.rs:105-147)",
+            "gpu_same_files_speedup": (m / out["files"]["seconds"]) / (m / secs)}
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+    return out
+
+
 def c4_assign(sizes, world):
     """largest-first greedy assignment of files to ranks"""
     load = [0] * world
@@ -815,6 +880,8 @@ def main():
                                       "counts_match": (wc, wl) == (dd["last"][1], dd["last"][2]),
                                       "oracle": "chunked restatement of file_identifier/mod.rs:149-254 "
                                                 "(oracle/cas_ref.c)"}
+        if args.workload == "c3" and not args.no_e2e:
+            out["e2e"] = e2e_c3(args, eng, torch, dev, d_blob, offs, lens, sizes, gk)
         if args.workload == "c2" and not args.no_e2e:
             out["e2e"] = e2e_c2(args, eng, torch, dev, d_blob, offs, lens, sizes, gk)
             if "cpu_baseline" in out and out["e2e"].get("reference_faithful"):

@@ -88,7 +88,14 @@ def test_two_process_device_dedup(oracle, existing_mode):
         assert np.array_equal(np.concatenate([p[f"link{call}"] for p in parts]), want), call
         for p in parts:
             assert tuple(int(x) for x in p[f"count{call}"]) == (wc, wl)
-    assert [str(p["proto0"]) for p in parts] == ["exact"] * world
+    # the first call takes the buckets (capacities from the all-gathered file
+    # counts) unless a rank holds more rows that stay orphans than the first
+    # call's gather of them takes (256): it then reruns the exact protocol;
+    # the second call uses what the first learned
+    cuts = [keys.size * r // world for r in range(world + 1)]
+    stays = [int(((status[a:b] != 0) | (has[a:b] == 0)).sum()) for a, b in zip(cuts, cuts[1:])]
+    first = "buckets-overflow" if max(stays) > 256 else "buckets"
+    assert [str(p["proto0"]) for p in parts] == [first] * world
     assert [str(p["proto1"]) for p in parts] == ["buckets"] * world
 
 
