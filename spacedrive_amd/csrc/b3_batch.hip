@@ -326,8 +326,10 @@ __device__ __forceinline__ void leaf_order(uint32_t tid, const uint32_t (&bin)[k
   __syncthreads();
 }
 
-template <int WG, int PF, int TR = 1, int ORD = 0, int DYN = 0, int CA = 0>
-__global__ void __launch_bounds__(WG, ORD ? 6 : 1) k_leaf_tree(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ offs,
+// MINW: waves per SIMD the register allocation must allow (0: 6 with the
+// leaf order, else 1)
+template <int WG, int PF, int TR = 1, int ORD = 0, int DYN = 0, int CA = 0, int MINW = 0>
+__global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ offs,
                                                    const uint64_t* __restrict__ lens, uint32_t n,
                                                    const uint64_t* __restrict__ S,
                                                    const uint32_t* __restrict__ tile_first,
@@ -1348,6 +1350,9 @@ static const LeafVariant kLeafVariants[] = {
     ABL1(512, k_leaf_tree<512, 149, 1, 1, 2, 2>),   // 58 DIAGNOSTIC (wrong digests): 51 reading an L2-resident 2 MiB
     ABL1(512, k_leaf_tree<512, 209, 0, 1, 2, 2>),   // 59 DIAGNOSTIC (wrong digests): 52 without the in-tile tree
     ABL1(512, k_leaf_tree<512, 209, 2, 1, 2, 2>),   // 60: 52 with every lane of a tree wave computing (prices masked lanes)
+    ABL1(1024, k_leaf_tree<1024, 229, 1, 1, 2, 2, 8>),  // 61: 55 at 1024 threads, one slot per lane, 8 waves/SIMD
+    ABL1(1024, k_leaf_tree<1024, 209, 1, 1, 2, 2, 8>),  // 62: 52 at 1024 threads, one slot per lane, 8 waves/SIMD
+    ABL1(1024, k_leaf_tree<1024, 229, 1, 1, 2, 2, 6>),  // 63: 61 at 6 waves/SIMD (register budget of 52)
 };
 #undef PROD
 #undef PROD1

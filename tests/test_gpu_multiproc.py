@@ -127,8 +127,8 @@ def test_two_streams_share_one_context(oracle):
             for b, s in zip(bufs, (s1, s2)):
                 rc = eng.L.sdcas_dev_dedup_local(eng.ctx, b["k"].data_ptr(), b["h"].data_ptr(), b["s"].data_ptr(),
                                                  b["ids"].data_ptr(), b["k"].numel(), b["ek"].data_ptr(),
-                                                 b["eids"].data_ptr(), b["ek"].numel(), 100, b["link"].data_ptr(),
-                                                 b["cnt"].data_ptr(), s.cuda_stream)
+                                                 b["eids"].data_ptr(), b["ek"].numel(), 100, 0, 0, 0,
+                                                 b["link"].data_ptr(), b["cnt"].data_ptr(), None, s.cuda_stream)
                 eng._check(rc, "sdcas_dev_dedup_local")
             torch.cuda.synchronize()
             for (keys, has, status, existing), b in zip(corpora, bufs):
