@@ -230,6 +230,20 @@ class Library {
   // in DB order, each with the cas_ids of its file_paths
   virtual std::vector<std::pair<int32_t, std::vector<std::string>>> existing_objects(
       const std::vector<std::string>& cas_ids) = 0;
+  // what the identifier step takes from that lookup (mod.rs:181-188 with the
+  // find of :214-224): per cas_id, the first Object in DB order having a
+  // file_path with it, in no particular order; cas_ids without one are left
+  // out. The default derives it from existing_objects; a database can answer
+  // it with one index probe per cas_id.
+  virtual std::vector<std::pair<std::string, int32_t>> first_objects(const std::vector<std::string>& cas_ids);
+  // set_cas_id then connect of one row as one write: the row's state after
+  // mod.rs:157-178 and :352-377. The step uses it for rows without an Object,
+  // whose cas_id no lookup of the step can see before the link.
+  virtual void set_cas_id_and_connect(int32_t file_path_id, const std::optional<std::string>& cas_id,
+                                      int32_t object_id) {
+    set_cas_id(file_path_id, cas_id);
+    connect(file_path_id, object_id);
+  }
   // mod.rs:290-327: object::create_unchecked(kind, date_created) -> object id
   virtual int32_t create_object(ObjectKind kind, int64_t date_created) = 0;
   // connect_file_path_to_object (mod.rs:352-377)
@@ -305,6 +319,11 @@ class SqliteLibrary : public Library {
   void set_cas_id(int32_t file_path_id, const std::optional<std::string>& cas_id) override;
   std::vector<std::pair<int32_t, std::vector<std::string>>> existing_objects(
       const std::vector<std::string>& cas_ids) override;
+  // one probe of the cas_id index per cas_id (the reference's schema, without
+  // that index: the existing_objects query)
+  std::vector<std::pair<std::string, int32_t>> first_objects(const std::vector<std::string>& cas_ids) override;
+  void set_cas_id_and_connect(int32_t file_path_id, const std::optional<std::string>& cas_id,
+                              int32_t object_id) override;
   int32_t create_object(ObjectKind kind, int64_t date_created) override;
   void connect(int32_t file_path_id, int32_t object_id) override;
   std::vector<FilePathRow> file_paths_without_checksum(int32_t location_id, const std::string& sub) override;

@@ -298,6 +298,16 @@ std::vector<std::pair<int32_t, std::vector<std::string>>> MemoryLibrary::existin
   return {by_object.begin(), by_object.end()};
 }
 
+std::vector<std::pair<std::string, int32_t>> Library::first_objects(const std::vector<std::string>& cas_ids) {
+  const std::set<std::string> want(cas_ids.begin(), cas_ids.end());
+  std::set<std::string> got;
+  std::vector<std::pair<std::string, int32_t>> out;
+  for (const auto& [oid, cs] : existing_objects(cas_ids))  // objects in DB order
+    for (const auto& c : cs)
+      if (want.count(c) && got.insert(c).second) out.emplace_back(c, oid);
+  return out;
+}
+
 int32_t MemoryLibrary::create_object(ObjectKind kind, int64_t date_created) {
   ObjectRow o;
   o.id = next_object_id_++;
@@ -413,6 +423,10 @@ std::pair<size_t, size_t> identifier_step_db(Library& db, const std::vector<File
   std::vector<int32_t> status(n, 0);
   std::vector<std::string> unique;
   std::set<std::string> seen;
+  // cas_id writes (mod.rs:157-178): a row with an Object now, since the
+  // lookup below can find its Object by it; a row without one together with
+  // its link (set_cas_id_and_connect), the same end state in one write
+  std::vector<uint8_t> cas_pending(n, 0);
   db.begin_batch();
   for (size_t i = 0; i < n; ++i) {
     if (!md[i].ok()) {
@@ -426,20 +440,18 @@ std::pair<size_t, size_t> identifier_step_db(Library& db, const std::vector<File
     }
     if (step[i] == UINT64_MAX) continue;  // no step reads it: it stays as it is
     if (cas && seen.insert(*cas).second) unique.push_back(*cas);
-    db.set_cas_id(file_paths[i].id, cas);  // mod.rs:157-178
+    if (file_paths[i].object_id) db.set_cas_id(file_paths[i].id, cas);
+    else cas_pending[i] = 1;
   }
   db.end_batch();
-  // existing Objects carrying any of these cas_ids, DB order (mod.rs:181-188);
-  // one existing-key entry per (object, cas_id) so "the first object whose
-  // file_paths carry the cas_id" (mod.rs:214-224) is the first entry
-  auto existing = db.existing_objects(unique);
+  // the first existing Object carrying each cas_id, DB order (mod.rs:181-188
+  // and the find of :214-224): one existing-key entry per cas_id
   std::vector<uint64_t> ekeys;
   std::vector<int32_t> eobj;
-  for (const auto& [oid, cas_ids] : existing)
-    for (const auto& c : cas_ids) {
-      ekeys.push_back(hex_to_key(c));
-      eobj.push_back(oid);
-    }
+  for (const auto& [c, oid] : db.first_objects(unique)) {
+    ekeys.push_back(hex_to_key(c));
+    eobj.push_back(oid);
+  }
   sdcas_job_window gw{};
   gw.max_steps = win.max_steps;
   gw.more = win.more;
@@ -460,17 +472,27 @@ std::pair<size_t, size_t> identifier_step_db(Library& db, const std::vector<File
                      return a.first < b.first;
                    });
   std::vector<int32_t> created_object(n, 0);
+  auto link_row = [&](size_t i, int32_t oid) {
+    if (cas_pending[i]) {
+      db.set_cas_id_and_connect(file_paths[i].id, md[i].value().cas_id, oid);
+      cas_pending[i] = 0;
+    } else {
+      db.connect(file_paths[i].id, oid);
+    }
+  };
   db.begin_batch();
   for (const auto& [s, i] : creates) {
     created_object[i] = db.create_object(md[i].value().kind, file_paths[i].date_created);
-    db.connect(file_paths[i].id, created_object[i]);
+    link_row(i, created_object[i]);
   }
   // links to the first Object carrying the cas_id (mod.rs:202-238)
   for (size_t i = 0; i < n; ++i) {
     const int64_t l = d.link[i];
     if (l == SDCAS_LINK_DROPPED || l == SDCAS_LINK_DEFERRED || l == (int64_t)i) continue;
-    db.connect(file_paths[i].id, l >= 0 ? created_object[(size_t)l] : eobj[(size_t)(-(l + 1))]);
+    link_row(i, l >= 0 ? created_object[(size_t)l] : eobj[(size_t)(-(l + 1))]);
   }
+  for (size_t i = 0; i < n; ++i)  // read but not linked (none such today)
+    if (cas_pending[i]) db.set_cas_id(file_paths[i].id, md[i].value().cas_id);
   db.end_batch();
   if (window) *window = win;
   return {(size_t)d.created, (size_t)d.linked};

@@ -44,8 +44,9 @@ struct SqliteLibrary::Impl {
   sqlite3* db = nullptr;
   Stmt count_orphans_dir, get_orphans_dir;
   Stmt count_orphans, get_orphans, set_cas, want_clear, want_add, existing, new_object, connect, no_checksum,
-      set_checksum, add_path, get_path, all_objects;
+      set_checksum, add_path, get_path, all_objects, first_object, set_cas_connect;
   int64_t next_object = 1;
+  bool cas_index = false;
   int batch_depth = 0;
 
   [[noreturn]] void fail(const std::string& what) {
@@ -146,6 +147,10 @@ std::unique_ptr<SqliteLibrary> SqliteLibrary::open(const std::string& path, bool
   }
   d->exec("PRAGMA journal_mode = WAL");
   d->exec("PRAGMA synchronous = NORMAL");
+  // the step's random probes and index updates stay in memory: a 256 MiB
+  // page cache (SQLite's default is 2 MiB) and reads through mmap
+  d->exec("PRAGMA cache_size = -262144");
+  d->exec("PRAGMA mmap_size = 4294967296");
   d->exec(
       "CREATE TABLE IF NOT EXISTS object ("
       " id INTEGER PRIMARY KEY AUTOINCREMENT, pub_id BLOB NOT NULL UNIQUE, kind INTEGER, key_id INTEGER,"
@@ -195,6 +200,14 @@ std::unique_ptr<SqliteLibrary> SqliteLibrary::open(const std::string& path, bool
               " (SELECT cas_id FROM want_cas)) ORDER BY fp.object_id, fp.id");
   x.prepare(x.new_object, "INSERT INTO object (pub_id, kind, date_created) VALUES (?1, ?2, ?3)");
   x.prepare(x.connect, "UPDATE file_path SET object_id = ?1 WHERE id = ?2");
+  x.prepare(x.set_cas_connect, "UPDATE file_path SET cas_id = ?1, object_id = ?2 WHERE id = ?3");
+  // first_objects: the smallest object id among the file_paths with the
+  // cas_id (objects come back in id order from existing_objects' query)
+  x.cas_index = cas_id_index;
+  if (cas_id_index)
+    x.prepare(x.first_object,
+              "SELECT MIN(object_id) FROM file_path INDEXED BY file_path_cas_id_idx"
+              " WHERE cas_id = ?1 AND object_id IS NOT NULL");
   x.prepare(x.no_checksum,
             "SELECT " SD_COLS " FROM file_path WHERE location_id = ?1 AND is_dir = 0 AND integrity_checksum IS NULL"
             " AND substr(materialized_path, 1, length(?2)) = ?2 ORDER BY id");
@@ -359,6 +372,32 @@ int32_t SqliteLibrary::create_object(ObjectKind kind, int64_t date_created) {
   const int64_t id = sqlite3_last_insert_rowid(x.db);
   x.next_object = id + 1;
   return (int32_t)id;
+}
+
+std::vector<std::pair<std::string, int32_t>> SqliteLibrary::first_objects(const std::vector<std::string>& cas_ids) {
+  Impl& x = *d_;
+  if (!x.cas_index) return Library::first_objects(cas_ids);
+  std::vector<std::pair<std::string, int32_t>> out;
+  begin_batch();
+  for (const auto& c : cas_ids) {
+    x.text(x.first_object, 1, c);
+    if (sqlite3_step(x.first_object.s) != SQLITE_ROW) x.fail("first object");
+    if (sqlite3_column_type(x.first_object.s, 0) != SQLITE_NULL)
+      out.emplace_back(c, (int32_t)sqlite3_column_int64(x.first_object.s, 0));
+    sqlite3_reset(x.first_object.s);
+  }
+  sqlite3_clear_bindings(x.first_object.s);
+  end_batch();
+  return out;
+}
+
+void SqliteLibrary::set_cas_id_and_connect(int32_t file_path_id, const std::optional<std::string>& cas_id,
+                                           int32_t object_id) {
+  Impl& x = *d_;
+  x.opt_text(x.set_cas_connect, 1, cas_id);
+  sqlite3_bind_int64(x.set_cas_connect.s, 2, object_id);
+  sqlite3_bind_int64(x.set_cas_connect.s, 3, file_path_id);
+  x.done(x.set_cas_connect);
 }
 
 void SqliteLibrary::connect(int32_t file_path_id, int32_t object_id) {

@@ -9,9 +9,9 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
-#include <tuple>
-
+#include <algorithm>
 #include <chrono>
+#include <tuple>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -229,6 +229,57 @@ static void test_parity(bool cas_index) {
   for (int k = 0; k < 60; k += 3) want.push_back(key_to_hex(mix((uint64_t)k)));
   CHECK(mem.existing_objects(want) == sql->existing_objects(want), "existing objects");
   CHECK(sql->existing_objects({}).empty(), "existing objects of nothing");
+  {
+    auto a = mem.first_objects(want), b = sql->first_objects(want);  // one pair per cas_id, any order
+    std::sort(a.begin(), a.end());
+    std::sort(b.begin(), b.end());
+    CHECK(a == b && !a.empty(), "first objects");
+  }
+  CHECK(sql->first_objects({}).empty(), "first objects of nothing");
+  {
+    // one cas_id on two Objects (the smaller id is the first in DB order),
+    // an Object with two cas_ids, a row without an Object, a cas_id nowhere
+    for (bool index : {true, false}) {
+      auto s = SqliteLibrary::open(":memory:", index);
+      MemoryLibrary m;
+      std::vector<FilePathRow> rows(5);
+      const char* cas[5] = {"00000000000000aa", "00000000000000aa", "00000000000000aa", "00000000000000bb",
+                            "00000000000000cc"};
+      for (int i = 0; i < 5; ++i) {
+        rows[i].location_id = 1;
+        rows[i].materialized_path = "/";
+        rows[i].name = "f" + std::to_string(i);
+        rows[i].size_in_bytes = 1;
+        rows[i].cas_id = std::string(cas[i]);
+      }
+      s->add_file_paths(rows);
+      for (auto& r : rows) m.add_file_path(r);
+      for (int k = 0; k < 3; ++k) {
+        s->create_object(1, 0);
+        m.create_object(1, 0);
+      }
+      const int32_t link[5][2] = {{1, 2}, {2, 1}, {3, 0}, {4, 3}, {5, 3}};
+      for (const auto& l : link)
+        if (l[1]) {
+          s->connect(l[0], l[1]);
+          m.connect(l[0], l[1]);
+        }
+      const std::vector<std::string> q{"00000000000000aa", "00000000000000bb", "00000000000000cc", "00000000000000dd"};
+      const std::vector<std::pair<std::string, int32_t>> expect{
+          {"00000000000000aa", 1}, {"00000000000000bb", 3}, {"00000000000000cc", 3}};
+      auto fs = s->first_objects(q), fm = m.first_objects(q);
+      std::sort(fs.begin(), fs.end());
+      std::sort(fm.begin(), fm.end());
+      CHECK(fs == expect, "first objects (cas_id index %d)", (int)index);
+      CHECK(fm == expect, "first objects in memory");
+      // the combined write leaves the row as set_cas_id then connect would
+      s->set_cas_id_and_connect(3, std::string("00000000000000dd"), 2);
+      const auto r3 = s->file_path(3);
+      CHECK(r3 && r3->cas_id == std::string("00000000000000dd") && r3->object_id == 2, "set_cas_id_and_connect");
+      s->set_cas_id_and_connect(3, std::nullopt, 1);
+      CHECK(!s->file_path(3)->cas_id && s->file_path(3)->object_id == 1, "set_cas_id_and_connect null cas");
+    }
+  }
 
   // the identifier job on both: 100-row fetches (the reference's steps) on
   // one copy of each library, 1000- and 10000-row batches on others; every
@@ -301,6 +352,12 @@ struct Autocommit : Library {
       const std::vector<std::string>& c) override {
     return d.existing_objects(c);
   }
+  std::vector<std::pair<std::string, int32_t>> first_objects(const std::vector<std::string>& c) override {
+    return d.first_objects(c);
+  }
+  void set_cas_id_and_connect(int32_t i, const std::optional<std::string>& c, int32_t o) override {
+    d.set_cas_id_and_connect(i, c, o);
+  }
   int32_t create_object(ObjectKind k, int64_t t) override { return d.create_object(k, t); }
   void connect(int32_t f, int32_t o) override { d.connect(f, o); }
   std::vector<FilePathRow> file_paths_without_checksum(int32_t l, const std::string& s) override {
@@ -316,8 +373,12 @@ static double now() {
 // forwards everything, timing each kind of call (where a step's DB time goes)
 struct Timed : Library {
   Library& d;
-  double t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  explicit Timed(Library& x) : d(x) {}
+  double t[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  // reference_calls: the reference's calls only (the existing-Object query;
+  // set_cas_id and connect as two writes), not first_objects' probes or the
+  // combined write
+  bool reference_calls;
+  explicit Timed(Library& x, bool ref = false) : d(x), reference_calls(ref) {}
   template <class F>
   auto tm(int k, F f) -> decltype(f()) {
     const double t0 = now();
@@ -345,6 +406,14 @@ struct Timed : Library {
   std::vector<std::pair<int32_t, std::vector<std::string>>> existing_objects(
       const std::vector<std::string>& c) override {
     return tm(3, [&] { return d.existing_objects(c); });
+  }
+  std::vector<std::pair<std::string, int32_t>> first_objects(const std::vector<std::string>& c) override {
+    if (reference_calls) return Library::first_objects(c);  // times existing_objects
+    return tm(3, [&] { return d.first_objects(c); });
+  }
+  void set_cas_id_and_connect(int32_t i, const std::optional<std::string>& c, int32_t o) override {
+    if (reference_calls) return Library::set_cas_id_and_connect(i, c, o);  // times both writes
+    tm(8, [&] { d.set_cas_id_and_connect(i, c, o); });
   }
   int32_t create_object(ObjectKind k, int64_t t_) override { return tm(4, [&] { return d.create_object(k, t_); }); }
   void connect(int32_t f, int32_t o) override { tm(5, [&] { d.connect(f, o); }); }
@@ -385,7 +454,7 @@ static int bench(size_t n) {
       }
       sql->add_file_paths(rows);
       Autocommit ac(*sql);
-      Timed timed(m.autocommit ? static_cast<Library&>(ac) : *sql);
+      Timed timed(m.autocommit ? static_cast<Library&>(ac) : *sql, !m.cas_index);
       const double t0 = now();
       auto meta = run_job(timed, 1, m.batch, rows_n / 3);
       const double dt = now() - t0;
@@ -394,9 +463,10 @@ static int bench(size_t n) {
                     ", \"%s\": {\"rows\": %zu, \"seconds\": %.3f, \"rows_per_s\": %.0f, \"created\": %zu, "
                     "\"linked\": %zu, \"seconds_by_call\": {\"count_orphans\": %.3f, \"get_orphans\": %.3f, "
                     "\"set_cas_id\": %.3f, \"existing_objects\": %.3f, \"create_object\": %.3f, "
-                    "\"connect\": %.3f, \"begin\": %.3f, \"commit\": %.3f}}",
+                    "\"connect\": %.3f, \"set_cas_id_and_connect\": %.3f, \"begin\": %.3f, \"commit\": %.3f}}",
                     m.name, rows_n, dt, rows_n / dt, meta.total_objects_created, meta.total_objects_linked,
-                    timed.t[0], timed.t[1], timed.t[2], timed.t[3], timed.t[4], timed.t[5], timed.t[6], timed.t[7]);
+                    timed.t[0], timed.t[1], timed.t[2], timed.t[3], timed.t[4], timed.t[5], timed.t[8], timed.t[6],
+                    timed.t[7]);
       out += b;
     }
     for (const char* suf : {"", "-wal", "-shm"}) std::remove((std::string(path) + suf).c_str());

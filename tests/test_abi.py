@@ -77,7 +77,7 @@ def test_product_library_holds_only_product_kernels():
     libsdcas_ablate.so)"""
     stubs = _kernel_stubs(N.LIB_PATH)
     leaf = [s for s in stubs if s.startswith("k_leaf")]
-    assert leaf == ["k_leaf_tree<512, 109, 1, 1, 2, 2>", "k_leaf_tree<512, 209, 1, 1, 2, 2>"], leaf
+    assert leaf == ["k_leaf_tree<512, 109, 1, 1, 2, 2, 0>", "k_leaf_tree<512, 209, 1, 1, 2, 2, 0>"], leaf
     assert not [s for s in stubs if "slim" in s or "quad" in s]
     pieces = [s for s in stubs if s.startswith("k_piece")]
     assert sorted(pieces) == ["k_piece_tree<108, 6, 1, 0>", "k_piece_tree<208, 6, 1, 0>"], pieces
