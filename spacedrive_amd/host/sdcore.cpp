@@ -8,7 +8,9 @@
 #include <algorithm>
 #include <cerrno>
 #include <cstring>
+#include <future>
 #include <set>
+#include <thread>
 #include <unordered_map>
 
 namespace sdcore {
@@ -340,17 +342,37 @@ std::vector<Result<FileMetadata>> file_metadata_batch(Engine& engine,
   const size_t n = files.size();
   std::vector<std::optional<IoError>> err(n);
   std::vector<FileMetadata> md(n);
+  std::vector<uint8_t> is_dir(n, 0);
+  // fs::metadata and the kind per file (mod.rs:63-76), on up to 16 threads for
+  // a big batch (the reference's join_all runs them concurrently too)
+  auto stat_range = [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) {
+      struct stat sb;
+      if (::stat(files[i].first.c_str(), &sb) != 0) {  // fs::metadata (mod.rs:63-65)
+        err[i] = IoError{errno, files[i].first};
+        continue;
+      }
+      if (S_ISDIR(sb.st_mode)) {
+        is_dir[i] = 1;
+        continue;
+      }
+      md[i].kind = files[i].second >= 0 ? files[i].second : object_kind_of(files[i].first);  // mod.rs:72-76
+      md[i].len = (uint64_t)sb.st_size;
+    }
+  };
+  const size_t threads = std::min<size_t>(16, n / 512);
+  if (threads < 2) {
+    stat_range(0, n);
+  } else {
+    std::vector<std::thread> pool;
+    for (size_t t = 0; t < threads; ++t) pool.emplace_back(stat_range, n * t / threads, n * (t + 1) / threads);
+    for (auto& th : pool) th.join();
+  }
   std::vector<std::pair<std::string, uint64_t>> to_hash;
   std::vector<size_t> hashed_index;
   for (size_t i = 0; i < n; ++i) {
-    struct stat sb;
-    if (::stat(files[i].first.c_str(), &sb) != 0) {  // fs::metadata (mod.rs:63-65)
-      err[i] = IoError{errno, files[i].first};
-      continue;
-    }
-    if (S_ISDIR(sb.st_mode)) throw std::logic_error("We can't generate cas_id for directories");  // mod.rs:67-70
-    md[i].kind = files[i].second >= 0 ? files[i].second : object_kind_of(files[i].first);  // mod.rs:72-76
-    md[i].len = (uint64_t)sb.st_size;
+    if (is_dir[i]) throw std::logic_error("We can't generate cas_id for directories");  // mod.rs:67-70
+    if (err[i]) continue;
     if (md[i].len != 0) {  // mod.rs:78-86: empty files get no cas_id
       to_hash.emplace_back(files[i].first, md[i].len);
       hashed_index.push_back(i);
@@ -402,9 +424,23 @@ static bool reidentified(const FilePathRow& r, const Result<FileMetadata>& md) {
   return r.object_id && !r.cas_id && md.ok() && md.value().cas_id;
 }
 
+// after the group-by, before the Objects are written: the job's loop reads
+// its next batch there (run_steps)
+using OnGrouped = std::function<void(const sdcas_job_window& done)>;
+
+static std::pair<size_t, size_t> step_db(Library& db, const std::vector<FilePathRow>& file_paths,
+                                         const std::vector<Result<FileMetadata>>& md, const GroupBy& group_by,
+                                         sdcas_job_window* window, size_t chunk_size, const OnGrouped* on_grouped);
+
 std::pair<size_t, size_t> identifier_step_db(Library& db, const std::vector<FilePathRow>& file_paths,
                                              const std::vector<Result<FileMetadata>>& md, const GroupBy& group_by,
                                              sdcas_job_window* window, size_t chunk_size) {
+  return step_db(db, file_paths, md, group_by, window, chunk_size, nullptr);
+}
+
+static std::pair<size_t, size_t> step_db(Library& db, const std::vector<FilePathRow>& file_paths,
+                                         const std::vector<Result<FileMetadata>>& md, const GroupBy& group_by,
+                                         sdcas_job_window* window, size_t chunk_size, const OnGrouped* on_grouped) {
   const size_t n = file_paths.size();
   if (md.size() != n) throw std::invalid_argument("identifier_step_db: one metadata per file_path");
   sdcas_job_window win{};
@@ -459,6 +495,7 @@ std::pair<size_t, size_t> identifier_step_db(Library& db, const std::vector<File
   if (d.link.size() != n) throw std::logic_error("identifier_step_db: group-by returned a wrong link count");
   if (gw.steps != win.steps || gw.rows != win.rows)
     throw std::logic_error("identifier_step_db: the group-by ran other steps than the plan");
+  if (on_grouped) (*on_grouped)(win);
   // new Objects (mod.rs:246-342) in the order the steps create them: step by
   // step, rows in id order within a step; a row without cas_id that several
   // steps read gets an Object from each, the last one its link. They take
@@ -532,13 +569,15 @@ StepLoop run_steps(Library& db, uint64_t task_count, int32_t cursor, size_t batc
   const size_t cs = SDCAS_IDENTIFIER_CHUNK_SIZE;
   const size_t batch = std::max(cs, batch_rows);  // a batch holds at least one whole step
   uint64_t steps_left = task_count;
+  std::vector<FilePathRow> rows = fetch(L.cursor, batch);  // id >= cursor ORDER BY id (file_identifier_job.rs:296-319)
+  std::vector<Result<FileMetadata>> md;
+  bool have_md = false;
   while (steps_left) {
-    auto rows = fetch(L.cursor, batch);  // id >= cursor ORDER BY id (file_identifier_job.rs:296-319)
     if (rows.empty()) {
       L.ran_dry = true;
       break;
     }
-    const auto md = metadata(rows);
+    if (!have_md) md = metadata(rows);
     if (L.batches && rows[0].id == L.cursor) ++L.rereads;  // the cursor row is still an orphan
     sdcas_job_window w{};
     w.max_steps = steps_left;
@@ -553,7 +592,29 @@ StepLoop run_steps(Library& db, uint64_t task_count, int32_t cursor, size_t batc
           cut = std::min(cut, plan.step[i]);
       if (cut != UINT64_MAX) w.max_steps = cut;
     }
-    auto [created, linked] = identifier_step_db(db, rows, md, group_by, &w, cs);
+    // The next batch is read while this one's Objects are written: the next
+    // fetch (id >= the cursor) is the cursor row if it stays an orphan (an
+    // error or no cas_id: nothing makes it whole) and then orphans past the
+    // cursor, which this batch does not write. Those are fetched and their
+    // FileMetadata computed on another thread after the group-by; the cursor
+    // row is fetched again once the writes are done.
+    std::vector<FilePathRow> next;
+    std::future<std::vector<Result<FileMetadata>>> next_md;
+    bool stays = false;
+    int32_t next_cursor = 0;
+    const OnGrouped prefetch = [&](const sdcas_job_window& done) {
+      if (done.steps == 0 || done.steps >= steps_left) return;
+      const size_t last = done.rows - 1;
+      next_cursor = rows[last].id;
+      stays = !md[last].ok() || !md[last].value().cas_id;
+      next = fetch(next_cursor + 1, batch - (stays ? 1 : 0));
+      std::vector<FilePathRow> ahead;
+      if (stays) ahead.push_back(rows[last]);  // the same file; its row is re-read below
+      ahead.insert(ahead.end(), next.begin(), next.end());
+      if (ahead.empty()) return;
+      next_md = std::async(std::launch::async, [&metadata, ahead = std::move(ahead)] { return metadata(ahead); });
+    };
+    auto [created, linked] = step_db(db, rows, md, group_by, &w, cs, &prefetch);
     if (w.steps == 0) break;  // cannot happen: a batch of `batch` >= cs rows holds a whole step
     L.created += created;
     L.linked += linked;
@@ -562,6 +623,20 @@ StepLoop run_steps(Library& db, uint64_t task_count, int32_t cursor, size_t batc
     ++L.batches;
     steps_left -= std::min<uint64_t>(steps_left, w.steps);
     L.cursor = rows[w.rows - 1].id;
+    have_md = false;
+    if (next_md.valid()) {
+      auto ahead_md = next_md.get();
+      std::vector<FilePathRow> cur;
+      if (stays) cur = fetch(L.cursor, 1);
+      if (!stays || (cur.size() == 1 && cur[0].id == L.cursor)) {
+        rows = std::move(cur);
+        rows.insert(rows.end(), next.begin(), next.end());
+        md = std::move(ahead_md);
+        have_md = true;
+        continue;
+      }
+    }
+    if (steps_left) rows = fetch(L.cursor, batch);
   }
   return L;
 }

@@ -4,11 +4,12 @@ kernel's VALU / SALU / LDS / VMEM instructions per compression, VALU issue per
 SIMD per cycle, HBM read bytes over the algorithmic message bytes, and the
 clock the kernel ran at (GRBM_GUI_ACTIVE per XCD over the kernel time the same
 run printed).
-Also writes profiles/r02_pmc_<w>.json for C3 and C5 (the HBM traffic per
+Also writes profiles/<PREFIX>_pmc_<w>.json for C3 and C5 (the HBM traffic per
 launch in tools/pmc_summarize.py's format, which bench.py reads); C2's comes
 from tools/pmc_traffic.sh's dedicated passes.
-usage: pmc_sq_workloads_summary.py SRC DST [VARIANT]   (VARIANT: the leaf variant the
-passes ran, tools/pmc_sq_workloads.sh's $VARIANT, default 52)"""
+usage: pmc_sq_workloads_summary.py SRC DST [VARIANT [PREFIX]]   (VARIANT: the leaf
+variant the passes ran, tools/pmc_sq_workloads.sh's $VARIANT, default 52;
+PREFIX: the round prefix of the per-workload traffic files, default r03)"""
 import collections
 import csv
 import glob
@@ -32,6 +33,7 @@ XCDS = 8
 def main():
     src, dst = sys.argv[1], sys.argv[2]
     variant = int(sys.argv[3]) if len(sys.argv) > 3 else 52
+    prefix = sys.argv[4] if len(sys.argv) > 4 else "r03"
     out = {"source": "rocprofv3 --pmc passes (tools/pmc_sq_workloads.sh) over tools/ab_leaf.py --product "
                      f"--variants {variant}, one counter group per run; FETCH_SIZE x2 per MI355X_MICROARCH.md",
            "workloads": {}}
@@ -76,7 +78,7 @@ def main():
         }
     json.dump(out, open(dst, "w"), indent=1)
     # the kernel name bench.load_traffic matches against its default kernel
-    kernel = {51: "k_leaf_tree<512, 109, 1, 1, 2, 2>", 52: "k_leaf_tree<512, 209, 1, 1, 2, 2>"}[variant]
+    kernel = {51: "k_leaf_tree<512, 109, 1, 1, 2, 2, 0>", 52: "k_leaf_tree<512, 209, 1, 1, 2, 2, 0>"}[variant]
     for w in ("c3", "c5"):
         d = out["workloads"].get(w)
         if not d:
@@ -88,7 +90,7 @@ def main():
               "algorithmic_bytes_per_launch": d["message_bytes"],
               "traffic_over_algorithmic": (rd + m["WRITE_SIZE"] * 1024) / d["message_bytes"],
               "source": out["source"] + f"; {w.upper()} {d['files']} files"}
-        json.dump(tr, open(os.path.join(os.path.dirname(dst), f"r02_pmc_{w}.json"), "w"), indent=1)
+        json.dump(tr, open(os.path.join(os.path.dirname(dst), f"{prefix}_pmc_{w}.json"), "w"), indent=1)
     for w, d in out["workloads"].items():
         print(w, {k: round(v, 4) if isinstance(v, float) else v for k, v in d.items() if k != "counters_median"})
 
