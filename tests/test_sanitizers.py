@@ -8,7 +8,9 @@ is checked on the CPU:
   shrunk / missing / directory paths;
 * test_sdcore_db_asan: the C++ host mirror (libsdcore: the identifier and
   validator jobs over MemoryLibrary and SqliteLibrary, the indexer walk and
-  kind detection) built with ASan + UBSan, running the DB-side tests.
+  kind detection) built with ASan + UBSan, running the DB-side tests;
+* test_sdcore_db_tsan: the same under TSan (the job loop reads its next batch
+  on another thread while the current batch's Objects are written).
 
 A sanitizer report makes the binary fail (-fno-sanitize-recover, LSan at exit).
 """
@@ -29,7 +31,8 @@ def built():
     return os.path.join(CPP, "build")
 
 
-@pytest.mark.parametrize("binary", ["test_cas_io", "test_cas_io_asan", "test_cas_io_tsan", "test_sdcore_db_asan"])
+@pytest.mark.parametrize("binary", ["test_cas_io", "test_cas_io_asan", "test_cas_io_tsan", "test_sdcore_db_asan",
+                                    "test_sdcore_db_tsan"])
 def test_sanitized_host_code(built, binary):
     env = dict(os.environ, ASAN_OPTIONS="abort_on_error=0:detect_leaks=1", TSAN_OPTIONS="halt_on_error=1")
     r = subprocess.run([os.path.join(built, binary)], capture_output=True, text=True, timeout=600, env=env)
