@@ -151,6 +151,23 @@ __device__ __forceinline__ void hash_chunk_ps(const uint8_t* __restrict__ p, uin
   }
 }
 
+// A chunk known to be whole (1024 bytes, not the root): sixteen full blocks,
+// both halves of each 128-byte line requested together as in hash_chunk_ps;
+// the block index is wave-uniform, so the flags are scalar selects and no
+// lane computes a length or a tail mask.
+template <int GA = 0>
+__device__ __forceinline__ void hash_chunk_full(const uint8_t* __restrict__ p, uint64_t j, uint32_t (&cv)[8]) {
+  set_iv(cv);
+  uint32_t m0[16], m1[16];
+#pragma unroll 1
+  for (uint32_t b = 0; b < CHUNK_LEN / BLOCK_LEN; b += 2) {
+    load_full_block(p + b * BLOCK_LEN, m0);
+    load_full_block(p + (b + 1) * BLOCK_LEN, m1);
+    compress<GA>(cv, m0, j, BLOCK_LEN, b == 0 ? CHUNK_START : 0u);
+    compress<GA>(cv, m1, j, BLOCK_LEN, b + 2 == CHUNK_LEN / BLOCK_LEN ? CHUNK_END : 0u);
+  }
+}
+
 // The line-pair loop with its per-block bookkeeping cut to compares against
 // the chunk's last block index (computed once): a full block's length and
 // flags are constants selected by one compare, the tail mask runs only on
@@ -216,11 +233,14 @@ __device__ __forceinline__ void leaf_hash(const uint8_t* __restrict__ p, uint32_
     hash_chunk_pl<GA>(p, clen, j, root, cv);
   } else if constexpr (L == 4) {
     hash_chunk_pp<GA>(p, clen, j, root, cv);
+  } else if constexpr (L == 7) {
+    if (clen == CHUNK_LEN && !root) hash_chunk_full<GA>(p, j, cv);
+    else hash_chunk_ps<GA>(p, clen, j, root, cv);
   } else {
 #ifdef SDCAS_ABLATIONS
     leaf_hash_ablation<PF>(p, clen, j, root, cv);  // b3_ablate_loops.inc
 #else
-    static_assert(L == 8 || L == 9 || L == 4, "ablation block loops need -DSDCAS_ABLATIONS");
+    static_assert(L == 8 || L == 9 || L == 4 || L == 7, "ablation block loops need -DSDCAS_ABLATIONS");
 #endif
   }
 }
@@ -911,7 +931,7 @@ __global__ void __launch_bounds__(256) k_shape_scatter(const uint64_t* __restric
 // may arrive over many launches (streamed windows); k_bigfile_finish merges a
 // file's list once all of it is there.
 
-template <int PF, int MINW, int DIRECT = 0, int ROT = 0>
+template <int PF, int MINW, int DIRECT = 0, int ROT = 0, int TOP = 10>
 __global__ void __launch_bounds__(kWG, MINW) k_piece_tree(const uint8_t* __restrict__ blob,
                                                           const PieceDesc* __restrict__ pieces, uint32_t npieces,
                                                           uint32_t* __restrict__ file_nodes) {
@@ -938,7 +958,7 @@ __global__ void __launch_bounds__(kWG, MINW) k_piece_tree(const uint8_t* __restr
       for (int i = 0; i < 8; ++i) cvs[s][i] = cv[i];
     }
     __syncthreads();
-    for (uint32_t k = 1; (1u << k) <= kTile; ++k) {
+    for (uint32_t k = 1; (1u << k) <= kTile && k <= TOP; ++k) {  // TOP < 10: DIAGNOSTIC (wrong digests)
       const uint32_t w = 1u << k;
       uint32_t T;
       if (DIRECT) {
@@ -1463,25 +1483,28 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
   return hipGetLastError();
 }
 
-// Piece kernel variants. Product: 14 = one workgroup per 1 MiB piece, the
+// Piece kernel variants. Product: 15 = one workgroup per 1 MiB piece, the
 // leaf kernel's line-pair block loop, 6 waves/SIMD, every G step a B3_G_ASM
-// block (b3_device.h); 15 (default) = 14 with the copy-free first column
-// steps (compress<2>: 6 fewer VALU instructions per compression; never slower
-// in three same-process A/Bs, profiles/r02_ab_asm_g.txt,
-// r02_ab_piece_14_15.txt). Ablation
-// library only: 4 = ping-pong block loop (round 1's default), 6 = 14 with the
-// compiler-scheduled G (round 2's default before B3_G_ASM: 10 % slower), 11
-// = persistent grid on a global piece counter (k_piece_dyn), 12 = 11 with the
-// next piece's first line loaded before the current piece's tree levels, 13
-// = 11 at 8 waves/SIMD (11-13 lost to the hardware dispatcher), and the older
-// plain / prefetch loops, rotated chunk orders, a round-robin persistent grid
-// and the DIAGNOSTIC 7 without memory reads.
-constexpr int kDefaultPieceVariant = 15;
+// block with the copy-free first column steps (b3_device.h, compress<2>);
+// 17 (default since round 3) = 15 with whole chunks through hash_chunk_full
+// (no per-block length, flag or tail-mask work on a lane; the block index is
+// wave-uniform): 1.7 % faster in a same-process A/B
+// (profiles/r03_ab_piece_15_17.txt). Ablation library only: 14 = 15 without
+// the copy-free first column steps (round 2's product pair), 4 = ping-pong
+// block loop (round 1's default), 6 = 14 with the compiler-scheduled G (round
+// 2's default before B3_G_ASM: 10 % slower), 11 = persistent grid on a global
+// piece counter (k_piece_dyn), 12 = 11 with the next piece's first line loaded
+// before the current piece's tree levels, 13 = 11 at 8 waves/SIMD (11-13 lost
+// to the hardware dispatcher), the older plain / prefetch loops, rotated chunk
+// orders, a round-robin persistent grid, and the DIAGNOSTIC 7 (no memory
+// reads), 16 and 18 (15 and 17 without the in-piece tree levels 5-10: what
+// the one-wave levels cost).
+constexpr int kDefaultPieceVariant = 17;
 
 bool piece_variant_available(int v) {
-  if (v == 14 || v == 15) return true;
+  if (v == 15 || v == 17) return true;
 #ifdef SDCAS_ABLATIONS
-  if (v >= 0 && v <= 13) return true;
+  if (v >= 0 && v <= 18) return true;
 #endif
   return false;
 }
@@ -1522,6 +1545,15 @@ static hipError_t piece_hash_ablation(int v, const uint8_t* blob, const PieceDes
   if (v == 11) return launch_piece_dyn<6, 0>(blob, pieces, npieces, file_nodes, ctr, st);
   if (v == 12) return launch_piece_dyn<6, 1>(blob, pieces, npieces, file_nodes, ctr, st);
   if (v == 13) return launch_piece_dyn<8, 0>(blob, pieces, npieces, file_nodes, ctr, st);
+  if (v == 16)  // DIAGNOSTIC (wrong digests): 15 without the in-piece tree levels 5-10
+    hipLaunchKernelGGL((k_piece_tree<208, 6, 1, 0, 4>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces,
+                       file_nodes);
+  else if (v == 14)  // 15 without the copy-free first column steps
+    hipLaunchKernelGGL((k_piece_tree<108, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
+  else if (v == 18)  // DIAGNOSTIC (wrong digests): 17 without the in-piece tree levels 5-10
+    hipLaunchKernelGGL((k_piece_tree<207, 6, 1, 0, 4>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces,
+                       file_nodes);
+  if (v >= 14) return hipGetLastError();
   if (v == 0) hipLaunchKernelGGL((k_piece_tree<0, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   else if (v == 1)
     hipLaunchKernelGGL((k_piece_tree<1, 8>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
@@ -1559,11 +1591,11 @@ hipError_t piece_hash(const uint8_t* blob, const PieceDesc* pieces, uint32_t npi
     return hipGetLastError();
   }
 #ifdef SDCAS_ABLATIONS
-  if (v != 14) return piece_hash_ablation(v, blob, pieces, npieces, file_nodes, ctr, st);
+  if (v != 17) return piece_hash_ablation(v, blob, pieces, npieces, file_nodes, ctr, st);
 #else
   (void)ctr;
 #endif
-  hipLaunchKernelGGL((k_piece_tree<108, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
+  hipLaunchKernelGGL((k_piece_tree<207, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   return hipGetLastError();
 }
 

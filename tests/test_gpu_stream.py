@@ -134,12 +134,12 @@ def test_stream_over_4tib_golden(eng):
         assert bytes(out.cpu().numpy()[0]).hex() == c["checksum"], n
 
 
-@pytest.mark.parametrize("variant", [14, 15])
+@pytest.mark.parametrize("variant", [15, 17])
 def test_piece_variants_vs_oracle(oracle, variant):
-    """every product piece kernel (4: one workgroup per piece; 11-13: the
-    persistent grid on a piece counter, with / without the next piece's first
-    line preloaded, at 6 / 8 waves per SIMD) over multi-window files whose
-    windows hold many pieces and a ragged tail, against the oracle"""
+    """every product piece kernel (15: one workgroup per piece, the line-pair
+    block loop; 17: 15 with whole chunks through the full-chunk loop) over
+    multi-window files whose windows hold many pieces and a ragged tail,
+    against the oracle"""
     from spacedrive_amd import Engine
     rng = np.random.default_rng(40 + variant)
     sizes = [MiB + 1, 5 * MiB + 17, 16 * MiB, 9 * MiB + 4095, 2 * MiB - 1, 40 * MiB + 3]
