@@ -589,7 +589,7 @@ def run_c4(args, torch, dist, dev, rank, world, distributed, out_f):
     hb["frac"] = hb["achieved"] / HBM_PEAK_GBS if hb["achieved"] else None
     # PMC traffic of the kernel this run launched (the default piece kernel
     # unless --piece-variant chose another)
-    piece_kernels = {15: "k_piece_tree<208, 6, 1, 0, 10>", 17: "k_piece_tree<207, 6, 1, 0, 10>"}
+    piece_kernels = {15: "k_piece_tree<208, 6, 1, 0, 10>", 17: "k_piece_tree<259, 6, 1, 0, 10>"}
     pv = DEFAULT_PIECE_VARIANT if args.piece_variant < 0 else args.piece_variant
     tr = load_traffic("c4", piece_kernels[pv]) if pv in piece_kernels else None
     if tr and resident and tr.get("algorithmic_bytes_per_launch") == my_bytes:

@@ -218,9 +218,12 @@ __device__ __forceinline__ void hash_chunk_pl(const uint8_t* __restrict__ p, uin
 #endif
 
 // Block loop of a leaf chunk: PF 8 = hash_chunk_ps, 9 = hash_chunk_pl, 4 =
-// hash_chunk_pp; PF + 100 = the same loop with the asm G blocks (B3_G_ASM,
-// b3_device.h), PF + 200 = with the copy-free first column steps too
-// (compress<2>); any other PF names an ablation loop.
+// hash_chunk_pp, 59 = hash_chunk_full for a whole non-root chunk (per lane)
+// else hash_chunk_ps, 69 = hash_chunk_full when every active lane of the wave
+// holds a whole non-root chunk else hash_chunk_pl; PF + 100 = the same loop
+// with the asm G blocks (B3_G_ASM, b3_device.h), PF + 200 = with the
+// copy-free first column steps too (compress<2>); any other PF names an
+// ablation loop.
 template <int PF>
 constexpr int kGA = PF / 100;
 template <int PF>
@@ -233,14 +236,19 @@ __device__ __forceinline__ void leaf_hash(const uint8_t* __restrict__ p, uint32_
     hash_chunk_pl<GA>(p, clen, j, root, cv);
   } else if constexpr (L == 4) {
     hash_chunk_pp<GA>(p, clen, j, root, cv);
-  } else if constexpr (L == 7) {
+  } else if constexpr (L == 59) {
     if (clen == CHUNK_LEN && !root) hash_chunk_full<GA>(p, j, cv);
     else hash_chunk_ps<GA>(p, clen, j, root, cv);
+  } else if constexpr (L == 69) {
+    // a wave whose active lanes all hold whole non-root chunks takes the
+    // full-chunk loop; any other wave the last-block-index loop
+    if (__all(clen == CHUNK_LEN && !root)) hash_chunk_full<GA>(p, j, cv);
+    else hash_chunk_pl<GA>(p, clen, j, root, cv);
   } else {
 #ifdef SDCAS_ABLATIONS
     leaf_hash_ablation<PF>(p, clen, j, root, cv);  // b3_ablate_loops.inc
 #else
-    static_assert(L == 8 || L == 9 || L == 4 || L == 7, "ablation block loops need -DSDCAS_ABLATIONS");
+    static_assert(L == 8 || L == 9 || L == 4 || L == 59 || L == 69, "ablation block loops need -DSDCAS_ABLATIONS");
 #endif
   }
 }
@@ -294,7 +302,7 @@ __device__ __forceinline__ uint32_t leaf_bin(uint64_t len, uint64_t j) {
 // layout do not change: a leaf still writes its CV at its own slot.
 constexpr uint32_t kGroups = kTile / 64;
 
-template <int WG>
+template <int WG, uint32_t NB = 17>
 __device__ __forceinline__ void leaf_order(uint32_t tid, const uint32_t (&bin)[kTile / WG], uint16_t* __restrict__ order,
                                            uint16_t* __restrict__ gcnt) {
   const uint32_t lane = tid & 63;
@@ -304,23 +312,23 @@ __device__ __forceinline__ void leaf_order(uint32_t tid, const uint32_t (&bin)[k
     const uint32_t g = (tid + r * WG) >> 6;
     uint32_t mine = 0, cnt_l = 0;
 #pragma unroll 1
-    for (uint32_t b = 0; b < 17; ++b) {
+    for (uint32_t b = 0; b < NB; ++b) {
       const uint64_t m = __ballot(bin[r] == b);
       if (bin[r] == b) mine = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
       if (lane == b) cnt_l = (uint32_t)__popcll(m);
     }
     rk[r] = mine;
-    if (lane < 17) gcnt[lane * kGroups + g] = (uint16_t)cnt_l;
+    if (lane < NB) gcnt[lane * kGroups + g] = (uint16_t)cnt_l;
   }
   __syncthreads();
   if (tid < 64) {
-    // exclusive scan of the 17 x kGroups counts in bin-major order
-    constexpr uint32_t kPer = (17 * kGroups + 63) / 64;
+    // exclusive scan of the NB x kGroups counts in bin-major order
+    constexpr uint32_t kPer = (NB * kGroups + 63) / 64;
     uint32_t v[kPer], sum = 0;
 #pragma unroll
     for (uint32_t q = 0; q < kPer; ++q) {
       const uint32_t e = tid * kPer + q;
-      v[q] = e < 17 * kGroups ? gcnt[e] : 0u;
+      v[q] = e < NB * kGroups ? gcnt[e] : 0u;
       sum += v[q];
     }
     uint32_t inc = sum;
@@ -333,7 +341,7 @@ __device__ __forceinline__ void leaf_order(uint32_t tid, const uint32_t (&bin)[k
 #pragma unroll
     for (uint32_t q = 0; q < kPer; ++q) {
       const uint32_t e = tid * kPer + q;
-      if (e < 17 * kGroups) gcnt[e] = (uint16_t)acc;
+      if (e < NB * kGroups) gcnt[e] = (uint16_t)acc;
       acc += v[q];
     }
   }
@@ -466,18 +474,30 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
     // message) than a wave has lanes — fewer cannot fill a wave of their own —
     // and not in a run of single-chunk messages, which the shape sort already
     // grouped by block count. The test is uniform over the workgroup.
-    const bool ord = ORD && cnt > 64 && chunk_count(lens[m0 + cnt - 1]) > 1;
+    // ORD 2: every other tile is put in a two-bin order — whole non-root
+    // chunks first, then the rest, then past-the-end slots — so that the
+    // waves over whole chunks take the full-chunk loop (PF % 100 == 6)
+    const bool ord17 = ORD && cnt > 64 && chunk_count(lens[m0 + cnt - 1]) > 1;
+    const bool ord = ord17 || ORD == 2;
     if (ord) {
       uint32_t bin[kTile / WG];
 #pragma unroll
       for (uint32_t r = 0; r < kTile / WG; ++r) {
         const uint32_t s = tid + r * WG;
         const uint32_t mi = smsg[s];
-        bin[r] = mi == kNoMsg ? 16u : leaf_bin(lens[m0 + mi], tbase + s - sS[mi]);
+        if (ord17) {
+          bin[r] = mi == kNoMsg ? 16u : leaf_bin(lens[m0 + mi], tbase + s - sS[mi]);
+        } else if (mi == kNoMsg) {
+          bin[r] = 2u;
+        } else {
+          const uint64_t len = lens[m0 + mi], j = tbase + s - sS[mi];
+          bin[r] = (len - j * CHUNK_LEN >= CHUNK_LEN && len > CHUNK_LEN) ? 0u : 1u;
+        }
       }
       // the per (bin, 64-slot group) counts borrow cvs, which no one reads
       // between the previous tile's last barrier and this tile's leaves
-      leaf_order<WG>(tid, bin, order, reinterpret_cast<uint16_t*>(&cvs[0][0]));
+      if (ord17) leaf_order<WG>(tid, bin, order, reinterpret_cast<uint16_t*>(&cvs[0][0]));
+      else leaf_order<WG, 3>(tid, bin, order, reinterpret_cast<uint16_t*>(&cvs[0][0]));
     }
     if (CA && !ord) {
 #pragma unroll
@@ -1373,6 +1393,9 @@ static const LeafVariant kLeafVariants[] = {
     ABL1(1024, k_leaf_tree<1024, 229, 1, 1, 2, 2, 8>),  // 61: 55 at 1024 threads, one slot per lane, 8 waves/SIMD
     ABL1(1024, k_leaf_tree<1024, 209, 1, 1, 2, 2, 8>),  // 62: 52 at 1024 threads, one slot per lane, 8 waves/SIMD
     ABL1(1024, k_leaf_tree<1024, 229, 1, 1, 2, 2, 6>),  // 63: 61 at 6 waves/SIMD (register budget of 52)
+    ABL1(512, k_leaf_tree<512, 269, 1, 2, 2, 2>),   // 64: 52 with whole chunks first in every tile and waves of whole chunks through hash_chunk_full
+    ABL1(512, k_leaf_tree<512, 269, 1, 1, 2, 2>),   // 65: 64 without the two-bin order (the full-chunk loop where a wave happens to hold only whole chunks)
+    ABL1(512, k_leaf_tree<512, 209, 1, 2, 2, 2>),   // 66: 52 with the two-bin order only (its cost)
 };
 #undef PROD
 #undef PROD1
@@ -1551,7 +1574,7 @@ static hipError_t piece_hash_ablation(int v, const uint8_t* blob, const PieceDes
   else if (v == 14)  // 15 without the copy-free first column steps
     hipLaunchKernelGGL((k_piece_tree<108, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   else if (v == 18)  // DIAGNOSTIC (wrong digests): 17 without the in-piece tree levels 5-10
-    hipLaunchKernelGGL((k_piece_tree<207, 6, 1, 0, 4>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces,
+    hipLaunchKernelGGL((k_piece_tree<259, 6, 1, 0, 4>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces,
                        file_nodes);
   if (v >= 14) return hipGetLastError();
   if (v == 0) hipLaunchKernelGGL((k_piece_tree<0, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
@@ -1595,7 +1618,7 @@ hipError_t piece_hash(const uint8_t* blob, const PieceDesc* pieces, uint32_t npi
 #else
   (void)ctr;
 #endif
-  hipLaunchKernelGGL((k_piece_tree<207, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
+  hipLaunchKernelGGL((k_piece_tree<259, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   return hipGetLastError();
 }
 

@@ -80,7 +80,7 @@ def test_product_library_holds_only_product_kernels():
     assert leaf == ["k_leaf_tree<512, 109, 1, 1, 2, 2, 0>", "k_leaf_tree<512, 209, 1, 1, 2, 2, 0>"], leaf
     assert not [s for s in stubs if "slim" in s or "quad" in s]
     pieces = [s for s in stubs if s.startswith("k_piece")]
-    assert sorted(pieces) == ["k_piece_tree<207, 6, 1, 0, 10>", "k_piece_tree<208, 6, 1, 0, 10>"], pieces
+    assert sorted(pieces) == ["k_piece_tree<208, 6, 1, 0, 10>", "k_piece_tree<259, 6, 1, 0, 10>"], pieces
 
 
 def test_ablation_build_is_separate():
