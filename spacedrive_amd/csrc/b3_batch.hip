@@ -151,6 +151,36 @@ __device__ __forceinline__ void hash_chunk_ps(const uint8_t* __restrict__ p, uin
   }
 }
 
+// Tail masks by the length of a message's last block: row b keeps bytes
+// [0, b) of a 64-byte block (word w: all ones, none, or its low 8 * (b - 4w)
+// bits). Four 16-byte loads of an L1-resident 4 KiB table replace the ~100
+// VALU instructions of computing the sixteen masks.
+struct alignas(16) TailMasks {
+  uint32_t w[BLOCK_LEN + 1][16];
+};
+constexpr TailMasks make_tail_masks() {
+  TailMasks t{};
+  for (int b = 0; b <= (int)BLOCK_LEN; ++b)
+    for (int w = 0; w < 16; ++w) {
+      const int r = b - 4 * w;
+      t.w[b][w] = r >= 4 ? 0xFFFFFFFFu : (r <= 0 ? 0u : ((1u << (8 * r)) - 1u));
+    }
+  return t;
+}
+__device__ const TailMasks kTailMasks = make_tail_masks();
+
+__device__ __forceinline__ void mask_tail_table(uint32_t (&m)[16], uint32_t blen) {
+  const uint4* q = reinterpret_cast<const uint4*>(kTailMasks.w[blen]);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint4 v = q[k];
+    m[4 * k] &= v.x;
+    m[4 * k + 1] &= v.y;
+    m[4 * k + 2] &= v.z;
+    m[4 * k + 3] &= v.w;
+  }
+}
+
 // A chunk known to be whole (1024 bytes, not the root): sixteen full blocks,
 // both halves of each 128-byte line requested together as in hash_chunk_ps;
 // the block index is wave-uniform, so the flags are scalar selects and no
@@ -173,7 +203,7 @@ __device__ __forceinline__ void hash_chunk_full(const uint8_t* __restrict__ p, u
 // flags are constants selected by one compare, the tail mask runs only on
 // the last block, the second half of a line is loaded only if the chunk has
 // it (no clamped address), and the block pointer advances by one add.
-template <int GA = 0, int NT = 0, int LM = 0, uint32_t BS = BLOCK_LEN>
+template <int GA = 0, int NT = 0, int LM = 0, uint32_t BS = BLOCK_LEN, int MT = 0>
 __device__ __forceinline__ void hash_chunk_pl(const uint8_t* __restrict__ p, uint32_t clen, uint64_t j, bool root,
                                               uint32_t (&cv)[8]) {
   set_iv(cv);
@@ -197,7 +227,8 @@ __device__ __forceinline__ void hash_chunk_pl(const uint8_t* __restrict__ p, uin
       if (last && lblen < BLOCK_LEN) {
         uint32_t L = lblen;
         if constexpr (LM) asm volatile("" : "+v"(L));  // keeps the mask inside the branch
-        mask_tail(m0, L);
+        if constexpr (MT) mask_tail_table(m0, L);
+        else mask_tail(m0, L);
       }
       compress<GA>(cv, m0, j, last ? lblen : BLOCK_LEN, (b == 0 ? CHUNK_START : 0u) | (last ? endf : 0u));
     }
@@ -206,7 +237,8 @@ __device__ __forceinline__ void hash_chunk_pl(const uint8_t* __restrict__ p, uin
       if (last && lblen < BLOCK_LEN) {
         uint32_t L = lblen;
         if constexpr (LM) asm volatile("" : "+v"(L));
-        mask_tail(m1, L);
+        if constexpr (MT) mask_tail_table(m1, L);
+        else mask_tail(m1, L);
       }
       compress<GA>(cv, m1, j, last ? lblen : BLOCK_LEN, last ? endf : 0u);
     }
@@ -239,6 +271,11 @@ __device__ __forceinline__ void leaf_hash(const uint8_t* __restrict__ p, uint32_
   } else if constexpr (L == 59) {
     if (clen == CHUNK_LEN && !root) hash_chunk_full<GA>(p, j, cv);
     else hash_chunk_ps<GA>(p, clen, j, root, cv);
+  } else if constexpr (L == 79) {
+    hash_chunk_pl<GA, 0, 0, BLOCK_LEN, 1>(p, clen, j, root, cv);
+  } else if constexpr (L == 89) {
+    if (__all(clen == CHUNK_LEN && !root)) hash_chunk_full<GA>(p, j, cv);
+    else hash_chunk_pl<GA, 0, 0, BLOCK_LEN, 1>(p, clen, j, root, cv);
   } else if constexpr (L == 69) {
     // a wave whose active lanes all hold whole non-root chunks takes the
     // full-chunk loop; any other wave the last-block-index loop
@@ -248,7 +285,7 @@ __device__ __forceinline__ void leaf_hash(const uint8_t* __restrict__ p, uint32_
 #ifdef SDCAS_ABLATIONS
     leaf_hash_ablation<PF>(p, clen, j, root, cv);  // b3_ablate_loops.inc
 #else
-    static_assert(L == 8 || L == 9 || L == 4 || L == 59 || L == 69, "ablation block loops need -DSDCAS_ABLATIONS");
+    static_assert(L == 8 || L == 9 || L == 4 || L == 59 || L == 69 || L == 79 || L == 89, "ablation block loops need -DSDCAS_ABLATIONS");
 #endif
   }
 }
@@ -1380,8 +1417,8 @@ static const LeafVariant kLeafVariants[] = {
     ABL(512, k_leaf_tree<512, 9, 1, 1, 1, 1>),    // 48: 47 with the leaf's chunk kept in registers from phase 1
     ABL1(512, k_leaf_tree<512, 9, 1, 1, 2, 1>),   // 49: 46 with the same
     ABL1(512, k_leaf_tree<512, 9, 1, 1, 2, 2>),   // 50: 49 keeping only the first slot's chunk (no spills)
-    PROD1(512, k_leaf_tree<512, 109, 1, 1, 2, 2>),  // 51: 50 with the asm G blocks (B3_G_ASM)
-    PROD1(512, k_leaf_tree<512, 209, 1, 1, 2, 2>),  // 52 (default): 51 with copy-free first column steps (compress<2>)
+    ABL1(512, k_leaf_tree<512, 109, 1, 1, 2, 2>),   // 51: 50 with the asm G blocks (B3_G_ASM)
+    PROD1(512, k_leaf_tree<512, 209, 1, 1, 2, 2>),  // 52 (round 2's default): 51 with copy-free first column steps (compress<2>)
     ABL1(512, k_leaf_tree<512, 119, 1, 1, 2, 2>),   // 53: 51 with non-temporal message loads (1.7x slower)
     ABL1(512, k_leaf_tree<512, 129, 1, 1, 2, 2>),   // 54: 51 with the tail mask computed in its branch
     ABL1(512, k_leaf_tree<512, 229, 1, 1, 2, 2>),   // 55: 52 with the same
@@ -1396,6 +1433,8 @@ static const LeafVariant kLeafVariants[] = {
     ABL1(512, k_leaf_tree<512, 269, 1, 2, 2, 2>),   // 64: 52 with whole chunks first in every tile and waves of whole chunks through hash_chunk_full
     ABL1(512, k_leaf_tree<512, 269, 1, 1, 2, 2>),   // 65: 64 without the two-bin order (the full-chunk loop where a wave happens to hold only whole chunks)
     ABL1(512, k_leaf_tree<512, 209, 1, 2, 2, 2>),   // 66: 52 with the two-bin order only (its cost)
+    PROD1(512, k_leaf_tree<512, 279, 1, 1, 2, 2>),  // 67 (default since round 3): 52 with the tail masks from a table
+    ABL1(512, k_leaf_tree<512, 289, 1, 1, 2, 2>),   // 68: 65 with the tail masks from a table
 };
 #undef PROD
 #undef PROD1
@@ -1404,7 +1443,7 @@ static const LeafVariant kLeafVariants[] = {
 #undef ABLQ
 #undef RET
 constexpr int kNumLeafVariants = sizeof(kLeafVariants) / sizeof(kLeafVariants[0]);
-constexpr int kDefaultLeafVariant = 52;
+constexpr int kDefaultLeafVariant = 67;
 
 int leaf_variant_count() { return kNumLeafVariants; }
 bool leaf_variant_available(int v) { return v >= 0 && v < kNumLeafVariants && kLeafVariants[v].fn != nullptr; }

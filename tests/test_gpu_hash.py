@@ -181,7 +181,7 @@ def test_tile_straddles_vs_oracle(eng, oracle):
         assert bytes(d).hex() == oracle.hash(m), len(m)
 
 
-@pytest.mark.parametrize("variant", [51, 52])
+@pytest.mark.parametrize("variant", [52, 67])
 def test_tile_straddles_per_variant(oracle, variant):
     """the straddle corpus through each product leaf variant, in caller
     order (shape sort off) so messages straddle tiles at every level"""
@@ -205,14 +205,14 @@ def test_tile_straddles_per_variant(oracle, variant):
     assert not bad, [len(msgs[i]) for i in bad[:10]]
 
 
-@pytest.mark.parametrize("variant", [51, 52])
+@pytest.mark.parametrize("variant", [52, 67])
 def test_many_short_multichunk_messages(oracle, variant):
     """C5-shaped batches — mostly 2..5-chunk messages, so tiles hold far more
     partial last chunks than a wave has lanes and the leaf kernel's block-count
     order is taken — next to runs of single-chunk messages and a few long
-    ones; every digest against the oracle, for round 1's kernel (43:
-    persistent tiles, line-pair loads) and the default (50: one tile per
-    workgroup, the last-block-index loop, the first chunk kept from phase 1)"""
+    ones; every digest against the oracle, for both product kernels (52:
+    one tile per workgroup, the last-block-index loop, the first chunk kept
+    from phase 1; 67, the default: 52 with the tail masks from a table)"""
     from spacedrive_amd import Engine
     rng = np.random.default_rng(55 + variant)
     lens = np.concatenate([rng.integers(1025, 5 * 1024 + 1, 12000), rng.integers(0, 1025, 3000),
@@ -237,7 +237,7 @@ def test_diagnostic_variants_unreachable(eng, oracle):
     bit-exact"""
     import subprocess
     import sys
-    for v in (4, 5, 6, 7, 26, 27, 28, 39, 40, 41, 1, 25, 29, 36, 43, 46, 47, 48, 49, 50):
+    for v in (4, 5, 6, 7, 26, 27, 28, 39, 40, 41, 1, 25, 29, 36, 43, 46, 47, 48, 49, 50, 51, 64, 65, 66, 68):
         assert not eng.dev_set_leaf_variant(v), v
     for v in (4, 6, 7, 11, 14, 16, 18):
         assert not eng.dev_set_piece_variant(v), v

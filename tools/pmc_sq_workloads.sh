@@ -10,7 +10,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 for WN in ${2:-c2:1000000 c3:1250000 c5:6250000}; do
   W=${WN%%:*}; N=${WN##*:}
-  PROG="python $R/tools/ab_leaf.py --product --rounds 1 --reps 2 --variants ${VARIANT:-52} --workload $W --files $N"
+  PROG="python $R/tools/ab_leaf.py --product --rounds 1 --reps 2 --variants ${VARIANT:-67} --workload $W --files $N"
   (cd /tmp && timeout -s KILL 180 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
      SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD -d $R/$OUT/s_$W -o s_$W --output-format csv \
      -- $PROG > $R/$OUT/s_$W.log 2>&1) || exit 1

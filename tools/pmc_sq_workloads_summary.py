@@ -8,7 +8,7 @@ Also writes profiles/<PREFIX>_pmc_<w>.json for C3 and C5 (the HBM traffic per
 launch in tools/pmc_summarize.py's format, which bench.py reads); C2's comes
 from tools/pmc_traffic.sh's dedicated passes.
 usage: pmc_sq_workloads_summary.py SRC DST [VARIANT [PREFIX]]   (VARIANT: the leaf
-variant the passes ran, tools/pmc_sq_workloads.sh's $VARIANT, default 52;
+variant the passes ran, tools/pmc_sq_workloads.sh's $VARIANT, default 67;
 PREFIX: the round prefix of the per-workload traffic files, default r03)"""
 import collections
 import csv
@@ -32,7 +32,7 @@ XCDS = 8
 
 def main():
     src, dst = sys.argv[1], sys.argv[2]
-    variant = int(sys.argv[3]) if len(sys.argv) > 3 else 52
+    variant = int(sys.argv[3]) if len(sys.argv) > 3 else 67
     prefix = sys.argv[4] if len(sys.argv) > 4 else "r03"
     out = {"source": "rocprofv3 --pmc passes (tools/pmc_sq_workloads.sh) over tools/ab_leaf.py --product "
                      f"--variants {variant}, one counter group per run; FETCH_SIZE x2 per MI355X_MICROARCH.md",
@@ -78,7 +78,8 @@ def main():
         }
     json.dump(out, open(dst, "w"), indent=1)
     # the kernel name bench.load_traffic matches against its default kernel
-    kernel = {51: "k_leaf_tree<512, 109, 1, 1, 2, 2, 0>", 52: "k_leaf_tree<512, 209, 1, 1, 2, 2, 0>"}[variant]
+    kernel = {51: "k_leaf_tree<512, 109, 1, 1, 2, 2, 0>", 52: "k_leaf_tree<512, 209, 1, 1, 2, 2, 0>",
+              67: "k_leaf_tree<512, 279, 1, 1, 2, 2, 0>"}[variant]
     for w in ("c3", "c5"):
         d = out["workloads"].get(w)
         if not d:

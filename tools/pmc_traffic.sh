@@ -2,12 +2,12 @@
 # HBM traffic of one kernel from PMC counters, each counter group in a run of
 # its own (MI355X_MICROARCH.md, HBM / rocprofv3 section).
 # Usage: tools/pmc_traffic.sh <outdir> [-- program args...]
-# (default program: the C2 leaf kernel through tools/ab_leaf.py, the default variant 52)
+# (default program: the C2 leaf kernel through tools/ab_leaf.py, the default variant 67)
 set -u
 OUT=${1:-gpurun_out/pmc_traffic}
 shift || true
 R=$(pwd)
-if [ "${1:-}" = "--" ]; then shift; PROG="$*"; else PROG="python $R/tools/ab_leaf.py --product --rounds 1 --reps 2 --variants 52"; fi
+if [ "${1:-}" = "--" ]; then shift; PROG="$*"; else PROG="python $R/tools/ab_leaf.py --product --rounds 1 --reps 2 --variants 67"; fi
 mkdir -p $OUT
 export TMPDIR=/tmp
 pass() {

@@ -39,6 +39,6 @@ else
   bash tools/pmc_traffic.sh $OUT/pmc_c2 > $OUT/pmc_c2.log 2>&1 || exit 9
   bash tools/pmc_traffic.sh $OUT/pmc_c4 -- python $R/bench.py --workload c4 --steps 1 --warmup 0 --no-cpu-baseline \
     > $OUT/pmc_c4.log 2>&1 || exit 10
-  VARIANT=52 bash tools/pmc_sq_workloads.sh $OUT/sqw > $OUT/sqw.log 2>&1 || exit 11
+  VARIANT=67 bash tools/pmc_sq_workloads.sh $OUT/sqw > $OUT/sqw.log 2>&1 || exit 11
   echo done
 fi
