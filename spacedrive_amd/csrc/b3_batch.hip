@@ -580,7 +580,8 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
     const uint64_t nt = DYN == 2 ? ntiles : (DYN ? next_tile : tile + gridDim.x);
 
     // (3) the tree, level by level: every task of a level is independent
-    for (uint32_t k = 1; TR && k <= 10; ++k) {
+    // (TR 3: DIAGNOSTIC, wrong digests — levels 5-10 skipped, what they cost)
+    for (uint32_t k = 1; TR && k <= (TR == 3 ? 4u : 10u); ++k) {
       const uint32_t T = ntask[k];
       if (T == 0) continue;
       // TR 2 (diagnostic, still bit-exact): every lane of a wave that holds
@@ -1435,6 +1436,8 @@ static const LeafVariant kLeafVariants[] = {
     ABL1(512, k_leaf_tree<512, 209, 1, 2, 2, 2>),   // 66: 52 with the two-bin order only (its cost)
     PROD1(512, k_leaf_tree<512, 279, 1, 1, 2, 2>),  // 67 (default since round 3): 52 with the tail masks from a table
     ABL1(512, k_leaf_tree<512, 289, 1, 1, 2, 2>),   // 68: 65 with the tail masks from a table
+    ABL1(512, k_leaf_tree<512, 279, 3, 1, 2, 2>),   // 69 DIAGNOSTIC (wrong digests): 67 without the tree levels 5-10
+    ABL1(512, k_leaf_tree<512, 279, 0, 1, 2, 2>),   // 70 DIAGNOSTIC (wrong digests): 67 without the in-tile tree
 };
 #undef PROD
 #undef PROD1
