@@ -148,7 +148,7 @@ def compressions(lens):
 
 # the library's default kernels (spacedrive_amd/csrc/b3_batch.hip
 # kDefaultLeafVariant / kDefaultPieceVariant): the PMC traffic files are per kernel
-DEFAULT_LEAF_KERNEL = "k_leaf_tree<512, 279, 1, 1, 2, 2, 0>"
+DEFAULT_LEAF_KERNEL = "k_leaf_tree<512, 279, 1, 1, 2, 2, 0, 1024u>"
 DEFAULT_PIECE_VARIANT = 17
 
 

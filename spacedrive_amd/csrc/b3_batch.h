@@ -8,6 +8,13 @@ namespace sdcas {
 
 constexpr uint32_t kTile = 1024;  // chunk slots per workgroup tile (1 MiB of message bytes)
 constexpr uint32_t kWG = 512;     // threads per workgroup: 2 slots per lane
+// Batches of at most kSmallSlots chunk slots (the staging slots of a path call
+// that small, e.g. the reference's 100-file step) run the small-batch kernel:
+// tiles of kSmallTile slots, so that they spread over many CUs instead of
+// running a few 1 MiB tiles one CU each (leaf variant kSmallVariant).
+constexpr uint32_t kSmallTile = 128;
+constexpr uint64_t kSmallSlots = 1ull << 14;
+constexpr int kSmallVariant = 71;
 // The shape sort's 256 bin counters and 256 bin cursors, each alone in a
 // 128-byte line: every workgroup adds to most of them, and packed into 8 lines
 // those atomics queued at 8 L2 channels.
@@ -26,6 +33,9 @@ struct BatchWorkspace {
   uint64_t cap_chunks = 0;  // chunks a batch of up to cap_msgs messages may hold
   uint64_t cap_slots = 0;   // slots the workspace holds (chunks + the quad layout's padding)
   int variant = -1;  // leaf kernel variant (-1: default / SDCAS_LEAF_VARIANT; unavailable ones: default)
+  uint64_t small_slots = kSmallSlots;  // default variant: batches up to this many slots take the small kernel (0: never)
+  int small_variant = kSmallVariant;   // which small-tile variant (A/B runs)
+  uint64_t cap_small_tiles = 0;        // tile_first entries (the small kernel's tiles need kTile / kSmallTile times more)
   // length-sorted slot order (messages of equal length share waves, so the
   // lanes of a wave run the same number of blocks): perm[slot-order index] =
   // caller index; soffs/slens = offsets/lengths in slot order
@@ -40,6 +50,7 @@ size_t batch_scan_temp_bytes(uint32_t max_msgs);
 int leaf_variant();
 int leaf_variant_count();
 bool leaf_variant_available(int v);  // compiled into this build (the diagnostic ones never are in libsdcas.so)
+bool leaf_variant_forced();          // SDCAS_LEAF_VARIANT names an available variant
 bool piece_variant_available(int v);
 
 // Hash n messages (blob + offs[i], lens[i] bytes; offsets 16-byte aligned),

@@ -74,6 +74,13 @@ __host__ __device__ inline uint32_t node_level_t(uint64_t j, uint64_t C, uint32_
 __host__ __device__ inline uint32_t node_level(uint64_t j, uint64_t C, uint32_t s) { return node_level_t<kTile>(j, C, s); }
 
 // Is the level-k node at (j, s) consumed by a parent computed in the same tile?
+template <uint32_t TILE>
+__host__ __device__ inline bool parent_in_tile_t(uint64_t j, uint64_t C, uint32_t s, uint32_t k) {
+  uint64_t w = 1ull << k;
+  if (!((j >> k) & 1)) return false;
+  return j + w <= C && 2 * w < C && s >= w && (uint64_t)s + w <= TILE;
+}
+
 __host__ __device__ inline bool parent_in_tile(uint64_t j, uint64_t C, uint32_t s, uint32_t k) {
   uint64_t w = 1ull << k;
   if (!((j >> k) & 1)) return false;  // left children's parents start at s: not computed
@@ -84,6 +91,7 @@ struct ChunkCountOp {
   __host__ __device__ uint64_t operator()(uint64_t len) const { return chunk_count(len); }
 };
 
+template <uint32_t TILE = kTile>
 __global__ void k_tile_first(const uint64_t* __restrict__ lens, const uint64_t* __restrict__ S, uint32_t n,
                              uint64_t cap_chunks, uint32_t* __restrict__ tile_first, uint64_t* __restrict__ total) {
   uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
@@ -93,7 +101,7 @@ __global__ void k_tile_first(const uint64_t* __restrict__ lens, const uint64_t* 
     total[0] = s0 + C;
     total[2] = 0;  // k_leaf_tree<DYN>'s tile counter
   }
-  for (uint64_t t = (s0 + kTile - 1) / kTile; t * kTile < s0 + C && t * kTile < cap_chunks; ++t) tile_first[t] = m;
+  for (uint64_t t = (s0 + TILE - 1) / TILE; t * TILE < s0 + C && t * TILE < cap_chunks; ++t) tile_first[t] = m;
 }
 
 // Same, unrolled by two blocks with ping-pong message registers (no
@@ -313,8 +321,10 @@ __device__ __forceinline__ void store_digest(uint32_t m, const uint32_t (&d)[8],
 // per-level task regions of the in-tile tree: level k (1..10) holds at most
 // 2 * (kTile >> k) tasks (regular level-k nodes are disjoint 2^k blocks, spine
 // steps consume disjoint maximal 2^(k-1) blocks), 2046 entries in all
-__host__ __device__ constexpr uint32_t task_base(uint32_t k) { return 2 * (kTile - (kTile >> (k - 1))); }
-constexpr uint32_t kTaskCap = 2 * (kTile - 1);
+template <uint32_t TL = kTile>
+__host__ __device__ constexpr uint32_t task_base(uint32_t k) { return 2 * (TL - (TL >> (k - 1))); }
+template <uint32_t TL = kTile>
+constexpr uint32_t kTaskCap = 2 * (TL - 1);
 constexpr uint16_t kNoMsg = 0xFFFF;
 
 __device__ __forceinline__ uint32_t enc_task(uint32_t l, uint32_t r, uint32_t msg, bool root) {
@@ -337,15 +347,15 @@ __device__ __forceinline__ uint32_t leaf_bin(uint64_t len, uint64_t j) {
 // per bin per 64-slot group, the 17 x 16 group counts are scanned by one wave,
 // and lane i of the leaf loop takes slot order[i]. The tree and the node
 // layout do not change: a leaf still writes its CV at its own slot.
-constexpr uint32_t kGroups = kTile / 64;
 
-template <int WG, uint32_t NB = 17>
-__device__ __forceinline__ void leaf_order(uint32_t tid, const uint32_t (&bin)[kTile / WG], uint16_t* __restrict__ order,
+template <int WG, uint32_t NB = 17, uint32_t TL = kTile>
+__device__ __forceinline__ void leaf_order(uint32_t tid, const uint32_t (&bin)[TL / WG], uint16_t* __restrict__ order,
                                            uint16_t* __restrict__ gcnt) {
+  constexpr uint32_t kGroups = TL / 64;
   const uint32_t lane = tid & 63;
-  uint32_t rk[kTile / WG];
+  uint32_t rk[TL / WG];
 #pragma unroll
-  for (uint32_t r = 0; r < kTile / WG; ++r) {
+  for (uint32_t r = 0; r < TL / WG; ++r) {
     const uint32_t g = (tid + r * WG) >> 6;
     uint32_t mine = 0, cnt_l = 0;
 #pragma unroll 1
@@ -384,7 +394,7 @@ __device__ __forceinline__ void leaf_order(uint32_t tid, const uint32_t (&bin)[k
   }
   __syncthreads();
 #pragma unroll
-  for (uint32_t r = 0; r < kTile / WG; ++r) {
+  for (uint32_t r = 0; r < TL / WG; ++r) {
     const uint32_t s = tid + r * WG;
     order[gcnt[bin[r] * kGroups + (s >> 6)] + rk[r]] = (uint16_t)s;
   }
@@ -393,7 +403,8 @@ __device__ __forceinline__ void leaf_order(uint32_t tid, const uint32_t (&bin)[k
 
 // MINW: waves per SIMD the register allocation must allow (0: 6 with the
 // leaf order, else 1)
-template <int WG, int PF, int TR = 1, int ORD = 0, int DYN = 0, int CA = 0, int MINW = 0>
+// TL: chunk slots per tile (kTile; kSmallTile for the small-batch kernel)
+template <int WG, int PF, int TR = 1, int ORD = 0, int DYN = 0, int CA = 0, int MINW = 0, uint32_t TL = kTile>
 __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ offs,
                                                    const uint64_t* __restrict__ lens, uint32_t n,
                                                    const uint64_t* __restrict__ S,
@@ -401,17 +412,17 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
                                                    const uint64_t* __restrict__ total_p, uint64_t cap_chunks,
                                                    uint32_t* __restrict__ nodes, uint8_t* __restrict__ out32,
                                                    uint64_t* __restrict__ out_keys, const uint32_t* __restrict__ perm) {
-  __shared__ uint32_t cvs[kTile][8];   // chunk / node chaining values, by slot
-  __shared__ uint64_t sS[kTile + 1];   // S[] of the tile's messages
-  __shared__ uint16_t smsg[kTile];     // slot -> message index in the tile (kNoMsg: past the end)
-  __shared__ uint32_t task[kTaskCap];  // tree tasks by level (enc_task)
+  __shared__ uint32_t cvs[TL][8];   // chunk / node chaining values, by slot
+  __shared__ uint64_t sS[TL + 1];   // S[] of the tile's messages
+  __shared__ uint16_t smsg[TL];     // slot -> message index in the tile (kNoMsg: past the end)
+  __shared__ uint32_t task[kTaskCap<TL>];  // tree tasks by level (enc_task)
   __shared__ uint32_t ntask[12];
-  __shared__ uint16_t order[ORD ? kTile : 1];  // leaf loop position -> slot
+  __shared__ uint16_t order[ORD ? TL : 1];  // leaf loop position -> slot
   __shared__ uint64_t next_tile;
 
   const uint64_t total = *total_p;
   if (total > cap_chunks) return;  // reported by sdcas_dev_sync
-  const uint64_t ntiles = (total + kTile - 1) / kTile;
+  const uint64_t ntiles = (total + TL - 1) / TL;
   const uint32_t tid = threadIdx.x;
   // DYN 1: tiles after the first are handed out by a global counter
   // (total_p[2], zeroed by k_tile_first) instead of round-robin, so a
@@ -422,10 +433,10 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
   // workspace can hold; the hardware dispatcher is the schedule).
   unsigned long long* tile_ctr = reinterpret_cast<unsigned long long*>(const_cast<uint64_t*>(total_p) + 2);
   for (uint64_t tile = blockIdx.x; tile < ntiles;) {
-    const uint64_t tbase = tile * kTile;
+    const uint64_t tbase = tile * TL;
     const uint32_t m0 = tile_first[tile];
     const uint32_t m1 = (tile + 1 < ntiles) ? tile_first[tile + 1] : n - 1;
-    const uint32_t cnt = m1 - m0 + 1;  // <= kTile + 1
+    const uint32_t cnt = m1 - m0 + 1;  // <= TL + 1
     for (uint32_t i = tid; i < cnt; i += WG) sS[i] = S[m0 + i];
     if (tid < 12) ntask[tid] = 0;
     if (DYN == 1 && tid == 0) next_tile = gridDim.x + atomicAdd(tile_ctr, 1ull);
@@ -441,7 +452,7 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
     // counter (CA 2: the first slot's only) are kept in registers from here — the message's offset is
     // loaded now, its latency hidden behind the schedule and the barrier,
     // instead of on the leaf phase's critical path
-    constexpr uint32_t R = kTile / WG;
+    constexpr uint32_t R = TL / WG;
     const uint8_t* c_p[R];
     uint64_t c_j[R];
     uint32_t c_clen[R], c_m[R];
@@ -450,7 +461,7 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
     for (uint32_t r = 0; r < R; ++r) c_ok[r] = false;
     constexpr uint32_t kPhase1Unroll = CA ? R : 1;
 #pragma unroll kPhase1Unroll
-    for (uint32_t s = tid; s < kTile; s += WG) {
+    for (uint32_t s = tid; s < TL; s += WG) {
       const uint64_t g = tbase + s;
       if (g >= total) {
         smsg[s] = kNoMsg;
@@ -477,20 +488,20 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
         c_p[r] = blob + offs[m0 + lo] + j * CHUNK_LEN;
       }
       if (!TR || C == 1) continue;
-      const uint32_t K = node_level(j, C, s);
+      const uint32_t K = node_level_t<TL>(j, C, s);
       for (uint32_t k = 1; k <= K; ++k)
-        task[task_base(k) + atomicAdd(&ntask[k], 1u)] = enc_task(s, s + (1u << (k - 1)), 0, false);
+        task[task_base<TL>(k) + atomicAdd(&ntask[k], 1u)] = enc_task(s, s + (1u << (k - 1)), 0, false);
     }
 #pragma unroll 1
     for (uint32_t i = tid; TR && i < cnt; i += WG) {
       const uint64_t S0 = sS[i];
       if (S0 < tbase) continue;
       const uint64_t C = chunk_count(lens[m0 + i]);
-      if (C == 1 || S0 + C > tbase + kTile) continue;
+      if (C == 1 || S0 + C > tbase + TL) continue;
       const uint32_t s0 = (uint32_t)(S0 - tbase), c = (uint32_t)C;
       if (!(c & (c - 1))) {
         const uint32_t k = 31 - __clz(c);
-        task[task_base(k) + atomicAdd(&ntask[k], 1u)] = enc_task(s0, s0 + (c >> 1), i, true);
+        task[task_base<TL>(k) + atomicAdd(&ntask[k], 1u)] = enc_task(s0, s0 + (c >> 1), i, true);
       } else {
         uint32_t rem = c, part = rem & (0u - rem);
         uint32_t pos = c - part, acc = pos;
@@ -499,7 +510,7 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
           part = rem & (0u - rem);
           pos -= part;
           const uint32_t k = 32 - __clz(part);  // log2(part) + 1
-          task[task_base(k) + atomicAdd(&ntask[k], 1u)] = enc_task(s0 + pos, s0 + acc, i, rem == part);
+          task[task_base<TL>(k) + atomicAdd(&ntask[k], 1u)] = enc_task(s0 + pos, s0 + acc, i, rem == part);
           acc = pos;
           rem -= part;
         }
@@ -517,9 +528,9 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
     const bool ord17 = ORD && cnt > 64 && chunk_count(lens[m0 + cnt - 1]) > 1;
     const bool ord = ord17 || ORD == 2;
     if (ord) {
-      uint32_t bin[kTile / WG];
+      uint32_t bin[TL / WG];
 #pragma unroll
-      for (uint32_t r = 0; r < kTile / WG; ++r) {
+      for (uint32_t r = 0; r < TL / WG; ++r) {
         const uint32_t s = tid + r * WG;
         const uint32_t mi = smsg[s];
         if (ord17) {
@@ -533,8 +544,8 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
       }
       // the per (bin, 64-slot group) counts borrow cvs, which no one reads
       // between the previous tile's last barrier and this tile's leaves
-      if (ord17) leaf_order<WG>(tid, bin, order, reinterpret_cast<uint16_t*>(&cvs[0][0]));
-      else leaf_order<WG, 3>(tid, bin, order, reinterpret_cast<uint16_t*>(&cvs[0][0]));
+      if (ord17) leaf_order<WG, 17, TL>(tid, bin, order, reinterpret_cast<uint16_t*>(&cvs[0][0]));
+      else leaf_order<WG, 3, TL>(tid, bin, order, reinterpret_cast<uint16_t*>(&cvs[0][0]));
     }
     if (CA && !ord) {
 #pragma unroll
@@ -554,7 +565,7 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
     // (CA 2 keeps the first slot only: the second one's state would live in
     // registers across the first one's block loop, where they spill)
 #pragma unroll 1
-    for (uint32_t i = (CA == 2 && !ord) ? tid + WG : tid; (CA != 1 || ord) && i < kTile; i += WG) {
+    for (uint32_t i = (CA == 2 && !ord) ? tid + WG : tid; (CA != 1 || ord) && i < TL; i += WG) {
       const uint32_t s = ord ? order[i] : i;
       const uint32_t mi = smsg[s];
       if (mi == kNoMsg) continue;
@@ -581,7 +592,7 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
 
     // (3) the tree, level by level: every task of a level is independent
     // (TR 3: DIAGNOSTIC, wrong digests — levels 5-10 skipped, what they cost)
-    for (uint32_t k = 1; TR && k <= (TR == 3 ? 4u : 10u); ++k) {
+    for (uint32_t k = 1; TR && (1u << k) <= TL && k <= (TR == 3 ? 4u : 10u); ++k) {
       const uint32_t T = ntask[k];
       if (T == 0) continue;
       // TR 2 (diagnostic, still bit-exact): every lane of a wave that holds
@@ -590,7 +601,7 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
       const uint32_t TT = TR == 2 ? (T + 63u) & ~63u : T;
 #pragma unroll 1
       for (uint32_t t = tid; t < TT; t += WG) {
-        const uint32_t e = task[task_base(k) + (TR == 2 ? min(t, T - 1) : t)];
+        const uint32_t e = task[task_base<TL>(k) + (TR == 2 ? min(t, T - 1) : t)];
         const uint32_t l = e & 1023u, r = (e >> 10) & 1023u;
         const bool root = e >> 31;
         uint32_t a[8], b[8], o[8];
@@ -615,15 +626,15 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
     // (4) messages crossing a tile boundary: their maximal in-tile nodes go to
     // HBM at their first slot, for k_finish
 #pragma unroll 1
-    for (uint32_t s = tid; TR && s < kTile; s += WG) {
+    for (uint32_t s = tid; TR && s < TL; s += WG) {
       const uint32_t mi = smsg[s];
       if (mi == kNoMsg) continue;
       const uint64_t S0 = sS[mi];
       const uint64_t C = chunk_count(lens[m0 + mi]);
-      if (C == 1 || (S0 >= tbase && S0 + C <= tbase + kTile)) continue;  // single chunk / spine done in (3)
+      if (C == 1 || (S0 >= tbase && S0 + C <= tbase + TL)) continue;  // single chunk / spine done in (3)
       const uint64_t j = tbase + s - S0;
-      const uint32_t k = node_level(j, C, s);
-      if (parent_in_tile(j, C, s, k)) continue;
+      const uint32_t k = node_level_t<TL>(j, C, s);
+      if (parent_in_tile_t<TL>(j, C, s, k)) continue;
       uint4* o = reinterpret_cast<uint4*>(nodes + 8ull * (tbase + s));
       o[0] = make_uint4(cvs[s][0], cvs[s][1], cvs[s][2], cvs[s][3]);
       o[1] = make_uint4(cvs[s][4], cvs[s][5], cvs[s][6], cvs[s][7]);
@@ -633,12 +644,6 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
   }
 }
 
-template <uint32_t TILE>
-__host__ __device__ inline bool parent_in_tile_t(uint64_t j, uint64_t C, uint32_t s, uint32_t k) {
-  uint64_t w = 1ull << k;
-  if (!((j >> k) & 1)) return false;
-  return j + w <= C && 2 * w < C && s >= w && (uint64_t)s + w <= TILE;
-}
 
 // Messages crossing tile boundaries: one lane per tile boundary t (the
 // message holding slot t*kTile, when it started in tile t-1 — its first
@@ -1352,9 +1357,16 @@ struct LeafVariant {
   int wg;
   int quad = 0;      // 1: quad slot layout (k_leaf_quad / k_finish_t<kQTile>, needs the shape-sorted order)
   int one_tile = 0;  // 1: one tile per workgroup (DYN 2): the grid covers the workspace's tiles
+  uint32_t tile = kTile;  // chunk slots per tile (kSmallTile: the small-batch kernel)
 };
 #define PROD(wg, ...) {(const void*)__VA_ARGS__, wg}
 #define PROD1(wg, ...) {(const void*)__VA_ARGS__, wg, 0, 1}
+#define PRODS(wg, ...) {(const void*)__VA_ARGS__, wg, 0, 1, kSmallTile}
+#ifdef SDCAS_ABLATIONS
+#define ABLS(wg, ...) {(const void*)__VA_ARGS__, wg, 0, 1, kSmallTile}
+#else
+#define ABLS(wg, ...) {nullptr, wg, 0, 1, kSmallTile}
+#endif
 #ifdef SDCAS_ABLATIONS
 #define ABL(wg, ...) {(const void*)__VA_ARGS__, wg}
 #define ABLQ(wg, ...) {(const void*)__VA_ARGS__, wg, 1}
@@ -1438,9 +1450,17 @@ static const LeafVariant kLeafVariants[] = {
     ABL1(512, k_leaf_tree<512, 289, 1, 1, 2, 2>),   // 68: 65 with the tail masks from a table
     ABL1(512, k_leaf_tree<512, 279, 3, 1, 2, 2>),   // 69 DIAGNOSTIC (wrong digests): 67 without the tree levels 5-10
     ABL1(512, k_leaf_tree<512, 279, 0, 1, 2, 2>),   // 70 DIAGNOSTIC (wrong digests): 67 without the in-tile tree
+    // 71 (product, the small-batch kernel): tiles of kSmallTile slots, one
+    // slot per lane, the compiler-scheduled G (a lone wave issues the four
+    // independent G chains of a half-round together; the asm blocks issue one
+    // chain at a time) and the tail-mask table
+    PRODS(kSmallTile, k_leaf_tree<kSmallTile, 79, 1, 1, 2, 2, 0, kSmallTile>),
+    ABLS(kSmallTile, k_leaf_tree<kSmallTile, 279, 1, 1, 2, 2, 0, kSmallTile>),  // 72: 71 with the asm G blocks (slower: 1-100 files +6-12 %)
 };
 #undef PROD
 #undef PROD1
+#undef PRODS
+#undef ABLS
 #undef ABL1
 #undef ABL
 #undef ABLQ
@@ -1449,6 +1469,15 @@ constexpr int kNumLeafVariants = sizeof(kLeafVariants) / sizeof(kLeafVariants[0]
 constexpr int kDefaultLeafVariant = 67;
 
 int leaf_variant_count() { return kNumLeafVariants; }
+// SDCAS_LEAF_VARIANT names a variant this build holds (then every batch runs it)
+bool leaf_variant_forced() {
+  static int f = -1;
+  if (f < 0) {
+    const char* e = getenv("SDCAS_LEAF_VARIANT");
+    f = e && leaf_variant_available(atoi(e)) ? 1 : 0;
+  }
+  return f == 1;
+}
 bool leaf_variant_available(int v) { return v >= 0 && v < kNumLeafVariants && kLeafVariants[v].fn != nullptr; }
 
 // SDCAS_LEAF_VARIANT selects a variant for A/B runs; a variant this build
@@ -1497,12 +1526,24 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
     lens = ws.slens;
     perm = ws.perm;
   }
+  const bool forced = leaf_variant_available(ws.variant) || leaf_variant_forced();
   int v = leaf_variant_available(ws.variant) ? ws.variant : leaf_variant();
   bool quad = false;
 #ifdef SDCAS_ABLATIONS
   quad = kLeafVariants[v].quad && (perm || n == 1);
   if (kLeafVariants[v].quad && !quad) v = kDefaultLeafVariant;  // the quad layout needs the shape-sorted order
 #endif
+  // slots the batch may fill: a grid sized to the workspace instead costs a
+  // small batch ~45 us of empty workgroups (8449 of them at 256 MiB staging)
+  const uint64_t slots =
+      max_chunks ? std::min<uint64_t>(ws.cap_slots, max_chunks + (quad ? 3ull * n + 8 : 0)) : ws.cap_slots;
+  // A small batch fills a few 1 MiB tiles, each hashed by one CU while the
+  // rest idle: unless a variant was chosen, it takes the small-batch kernel,
+  // whose tiles of kSmallTile slots spread it over the chip.
+  if (!forced && !quad && slots <= ws.small_slots && slots / kSmallTile + 2 <= ws.cap_small_tiles)
+    v = leaf_variant_available(ws.small_variant) && kLeafVariants[ws.small_variant].tile == kSmallTile ? ws.small_variant
+                                                                                                        : kSmallVariant;
+  const uint32_t tile = kLeafVariants[v].tile;
   size_t tmp = ws.scan_tmp_bytes;
   if (quad) {
 #ifdef SDCAS_ABLATIONS
@@ -1514,18 +1555,18 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
   } else {
     hipcub::TransformInputIterator<uint64_t, ChunkCountOp, const uint64_t*> it(lens, ChunkCountOp());
     if ((e = hipcub::DeviceScan::ExclusiveSum(ws.scan_tmp, tmp, it, ws.S, (int)n, st))) return e;
-    hipLaunchKernelGGL(k_tile_first, dim3((n + tb - 1) / tb), dim3(tb), 0, st, lens, ws.S, n, ws.cap_slots,
-                       ws.tile_first, ws.total);
+    if (tile == kSmallTile)
+      hipLaunchKernelGGL(k_tile_first<kSmallTile>, dim3((n + tb - 1) / tb), dim3(tb), 0, st, lens, ws.S, n,
+                         ws.cap_slots, ws.tile_first, ws.total);
+    else
+      hipLaunchKernelGGL(k_tile_first<kTile>, dim3((n + tb - 1) / tb), dim3(tb), 0, st, lens, ws.S, n, ws.cap_slots,
+                         ws.tile_first, ws.total);
   }
-  // slots the batch may fill: a grid sized to the workspace instead costs a
-  // small batch ~45 us of empty workgroups (8449 of them at 256 MiB staging)
-  const uint64_t slots =
-      max_chunks ? std::min<uint64_t>(ws.cap_slots, max_chunks + (quad ? 3ull * n + 8 : 0)) : ws.cap_slots;
   if (ev0) (void)hipEventRecord(ev0, st);
   {
     int dev = 0;
     (void)hipGetDevice(&dev);
-    const int grid = kLeafVariants[v].one_tile ? (int)std::min<uint64_t>(slots / kTile + 1, 0x7FFFFFFF)
+    const int grid = kLeafVariants[v].one_tile ? (int)std::min<uint64_t>(slots / tile + 1, 0x7FFFFFFF)
                                                : batch_grid(dev, v);
     void* args[] = {(void*)&blob,     (void*)&offs,          (void*)&lens,       (void*)&n,
                     (void*)&ws.S,     (void*)&ws.tile_first, (void*)&ws.total,   (void*)&ws.cap_slots,
@@ -1540,6 +1581,10 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
     hipLaunchKernelGGL(k_finish_t<kQTile>, dim3((uint32_t)((tiles + kFinishWG - 1) / kFinishWG)), dim3(kFinishWG), 0,
                        st, lens, n, ws.S, ws.tile_first, ws.total, ws.cap_slots, ws.nodes, perm, out32, out_keys);
 #endif
+  } else if (tile == kSmallTile) {
+    const uint64_t tiles = slots / kSmallTile + 1;
+    hipLaunchKernelGGL(k_finish_t<kSmallTile>, dim3((uint32_t)((tiles + kFinishWG - 1) / kFinishWG)), dim3(kFinishWG),
+                       0, st, lens, n, ws.S, ws.tile_first, ws.total, ws.cap_slots, ws.nodes, perm, out32, out_keys);
   } else {
     const uint64_t tiles = slots / kTile + 1;
     hipLaunchKernelGGL(k_finish_t<kTile>, dim3((uint32_t)((tiles + kFinishWG - 1) / kFinishWG)), dim3(kFinishWG), 0,

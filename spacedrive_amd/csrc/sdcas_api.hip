@@ -93,6 +93,7 @@ struct Slot {
   uint64_t content = 0;  // input bytes whose results this slot's batch makes final (progress)
   std::vector<size_t> idx;  // caller index of message k
   const uint8_t* src = nullptr;  // message bytes DMA'd from here instead of h (a pinned caller buffer)
+  bool blob_uploaded = false;    // the bytes went up in parts while the slot was being read (slot_submit skips them)
   uint64_t* offs() { return hm; }
   uint64_t* lens() { return hm + cap_n; }
   uint8_t* res() { return reinterpret_cast<uint8_t*>(hm + 2 * cap_n); }
@@ -155,6 +156,7 @@ struct sdcas_ctx {
   hipEvent_t scratch_ev = nullptr;
   hipStream_t scratch_st = nullptr;
   bool scratch_pending = false;
+  uint32_t upload_parts = 4;  // sdcas_cas_ids: a lone slot's reads and upload overlapped in this many parts (0/1: off)
 
   // progress / cancellation of the path APIs (sdcas_options, sdcas_set_progress)
   sdcas_progress_fn progress = nullptr;
@@ -223,8 +225,11 @@ int reserve_ws(sdcas_ctx* c, size_t max_msgs, uint64_t max_chunks) {
   // (rounded up, +3: cap_chunks below comes out >= max_chunks, so that
   // slots_prepare's check holds on the next call instead of re-reserving)
   const uint64_t tiles = (max_chunks + 3 * (uint64_t)(c->ws_S.cap - 1) + 8 + kTile - 1) / kTile + 3;
+  // tile_first also serves the small-batch kernel's tiles (kSmallTile slots)
+  const uint64_t small_tiles = (std::min<uint64_t>(max_chunks, kSmallSlots) + kSmallTile - 1) / kSmallTile + 3;
   if ((e = c->ws_total.ensure(4))) return c->hip_fail(e, "workspace total");
-  if ((e = c->ws_tile_first.ensure(tiles))) return c->hip_fail(e, "workspace tile_first");
+  if ((e = c->ws_tile_first.ensure(std::max<uint64_t>(tiles, small_tiles))))
+    return c->hip_fail(e, "workspace tile_first");
   if ((e = c->ws_nodes.ensure(8 * (tiles * kTile)))) return c->hip_fail(e, "workspace nodes");
   size_t tb = batch_scan_temp_bytes((uint32_t)std::max<size_t>(max_msgs, 1));
   if ((e = c->ws_scan.ensure(tb))) return c->hip_fail(e, "workspace scan");
@@ -245,6 +250,7 @@ int reserve_ws(sdcas_ctx* c, size_t max_msgs, uint64_t max_chunks) {
   c->ws.sort_keys = c->ws_sort_keys.p;
   // every tile the leaf kernel may touch needs a tile_first entry and its node slots
   c->ws.cap_slots = std::min<uint64_t>((c->ws_tile_first.cap - 1) * kTile, c->ws_nodes.cap / 8 - 2 * kTile);
+  c->ws.cap_small_tiles = c->ws_tile_first.cap;
   const uint64_t pad = 3 * (uint64_t)(c->ws_S.cap - 1) + 8;
   c->ws.cap_chunks = c->ws.cap_slots > pad ? c->ws.cap_slots - pad : 0;
   return SDCAS_OK;
@@ -354,6 +360,8 @@ hipError_t slot_upload(sdcas_ctx* c, Slot& s, Copies copies) {
 // cas keys) once s.ev has fired.
 int slot_submit(sdcas_ctx* c, Slot& s, bool res32) {
   s.res32 = res32;
+  const bool uploaded = s.blob_uploaded;  // this batch's bytes only: the flag never outlives its submit
+  s.blob_uploaded = false;
   if (!s.n) return SDCAS_OK;
   int rc;
   hipStream_t st = c->stream;
@@ -372,7 +380,7 @@ int slot_submit(sdcas_ctx* c, Slot& s, bool res32) {
   const uint64_t* d_lens = s.d_meta.p + (packed ? s.n : s.cap_n);
   if ((e = slot_upload(c, s, [&](hipStream_t cs) {
          hipError_t r;
-         if ((r = hipMemcpyAsync(s.d_blob.p, s.src ? s.src : s.h, s.used, hipMemcpyHostToDevice, cs)) ||
+         if ((!uploaded && (r = hipMemcpyAsync(s.d_blob.p, s.src ? s.src : s.h, s.used, hipMemcpyHostToDevice, cs))) ||
              (r = hipMemcpyAsync(s.d_meta.p, s.hm, 8 * (packed ? 2 * s.n : s.n), hipMemcpyHostToDevice, cs)))
            return r;
          return packed ? hipSuccess
@@ -589,6 +597,11 @@ int sdcas_init(const sdcas_options* opts, sdcas_ctx** out) {
     delete c;
     return SDCAS_E_NO_DEVICE;
   }
+  // the largest batch (chunk slots) the default leaf kernel hands to the
+  // small-batch kernel (b3_batch.h kSmallSlots; 0: never), for A/B runs
+  if (const char* e = getenv("SDCAS_SMALL_SLOTS")) c->ws.small_slots = strtoull(e, nullptr, 0);
+  if (const char* e = getenv("SDCAS_SMALL_VARIANT")) c->ws.small_variant = atoi(e);
+  if (const char* e = getenv("SDCAS_UPLOAD_PARTS")) c->upload_parts = (uint32_t)std::min(atoi(e) > 0 ? atoi(e) : 0, 16);
   c->device = dev;
   if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess) {
@@ -850,6 +863,9 @@ struct PathCall {
 // 3000 files per call 9.4 -> 7.8 ms, 10000 per call 22.6 -> 20.7 ms; calls
 // of up to 16 MiB (the reference's 100-file step) unchanged.
 constexpr uint64_t kSplit = 8, kMinSlot = 16ull << 20;
+// a lone slot's reads and upload overlapped in parts (sdcas_cas_ids;
+// sdcas_ctx::upload_parts, SDCAS_UPLOAD_PARTS) from this many slot bytes
+constexpr uint64_t kUploadSplitMin = 1ull << 20;
 static uint64_t split_cap(const uint64_t* need, const size_t* order, size_t n, uint64_t cap) {
   uint64_t total = 0;
   for (size_t i = 0; i < n; ++i) total += sdcas_io::align_line(need[order ? order[i] : i]);
@@ -1050,11 +1066,39 @@ int sdcas_cas_ids(sdcas_ctx* c, const char* const* paths, const uint64_t* sizes,
       std::vector<uint64_t> mlen(m), retry_len(m);
       std::vector<int32_t> st(m);
       tr.lap(1);
-      c->pool->run(m, [&](size_t k) {
-        const size_t i = todo[p + k];
-        st[k] = read_cas_message(paths[i], sizes[i], s.h + slot_off[k], align16(want[i]), &mlen[k], &retry_len[k],
-                                 c->direct_io);
-      });
+      auto read_files = [&](size_t k0, size_t k1) {
+        c->pool->run(k1 - k0, [&](size_t kk) {
+          const size_t k = k0 + kk, i = todo[p + k];
+          st[k] = read_cas_message(paths[i], sizes[i], s.h + slot_off[k], align16(want[i]), &mlen[k], &retry_len[k],
+                                   c->direct_io);
+        });
+      };
+      // A call that fits one slot is latency-bound: read -> upload -> hash in
+      // series. Its files are then read in upload_parts parts of about equal
+      // bytes, each part's bytes going up while the next part is read, so that
+      // only the last part's upload stands between the reads and the kernels.
+      const Slot& other = &s == &c->slots[0] ? c->slots[1] : c->slots[0];
+      // (only for a call that fits this one slot: in a call of several slots
+      // the next slot's reads already overlap this one's upload and kernels,
+      // and the parts measured slower there, profiles/r03_small_calls.json)
+      const uint32_t parts = c->upload_parts;
+      s.blob_uploaded = parts > 1 && !other.busy && p == 0 && q == todo.size() && round == 0 &&
+                        used >= kUploadSplitMin && m >= parts;
+      if (s.blob_uploaded) {
+        size_t k0 = 0;
+        for (uint32_t part = 1; part <= parts && k0 < m; ++part) {
+          size_t k1 = k0 + 1;
+          const uint64_t edge = used / parts * part;
+          while (k1 < m && (part == parts || slot_off[k1] < edge)) ++k1;
+          read_files(k0, k1);
+          const uint64_t b0 = slot_off[k0], b1 = k1 < m ? slot_off[k1] : used;
+          hipError_t e = hipMemcpyAsync(s.d_blob.p + b0, s.h + b0, b1 - b0, hipMemcpyHostToDevice, c->stream);
+          if (e) return c->hip_fail(e, "H2D part");
+          k0 = k1;
+        }
+      } else {
+        read_files(0, m);
+      }
       tr.lap(2);
       s.n = 0, s.chunks = 0, s.used = used, s.content = 0;
       s.idx.clear();

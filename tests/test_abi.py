@@ -70,14 +70,16 @@ def _kernel_stubs(path):
 
 
 def test_product_library_holds_only_product_kernels():
-    """libsdcas.so carries only the product kernels — leaf 67 (default) and
-    52, piece 17 (default) and 15, all bit-exact and GPU-tested — and no
+    """libsdcas.so carries only the product kernels — leaf 67 (default), 52
+    and the small-batch kernel 71, piece 17 (default) and 15, all bit-exact
+    and GPU-tested — and no
     ablation or
     DIAGNOSTIC variant (those produce wrong digests and live only in
     libsdcas_ablate.so)"""
     stubs = _kernel_stubs(N.LIB_PATH)
     leaf = [s for s in stubs if s.startswith("k_leaf")]
-    assert leaf == ["k_leaf_tree<512, 209, 1, 1, 2, 2, 0>", "k_leaf_tree<512, 279, 1, 1, 2, 2, 0>"], leaf
+    assert leaf == ["k_leaf_tree<128, 79, 1, 1, 2, 2, 0, 128u>", "k_leaf_tree<512, 209, 1, 1, 2, 2, 0, 1024u>",
+                    "k_leaf_tree<512, 279, 1, 1, 2, 2, 0, 1024u>"], leaf
     assert not [s for s in stubs if "slim" in s or "quad" in s]
     pieces = [s for s in stubs if s.startswith("k_piece")]
     assert sorted(pieces) == ["k_piece_tree<208, 6, 1, 0, 10>", "k_piece_tree<259, 6, 1, 0, 10>"], pieces

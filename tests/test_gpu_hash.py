@@ -181,10 +181,12 @@ def test_tile_straddles_vs_oracle(eng, oracle):
         assert bytes(d).hex() == oracle.hash(m), len(m)
 
 
-@pytest.mark.parametrize("variant", [52, 67])
+@pytest.mark.parametrize("variant", [52, 67, 71])
 def test_tile_straddles_per_variant(oracle, variant):
     """the straddle corpus through each product leaf variant, in caller
-    order (shape sort off) so messages straddle tiles at every level"""
+    order (shape sort off) so messages straddle tiles at every level (71, the
+    small-batch kernel, selected explicitly: its 128-slot tiles for the whole
+    batch, so messages of up to 2049 chunks cross dozens of them)"""
     from spacedrive_amd import Engine
     rng = np.random.default_rng(70 + variant)
     lens = []
@@ -205,14 +207,15 @@ def test_tile_straddles_per_variant(oracle, variant):
     assert not bad, [len(msgs[i]) for i in bad[:10]]
 
 
-@pytest.mark.parametrize("variant", [52, 67])
+@pytest.mark.parametrize("variant", [52, 67, 71])
 def test_many_short_multichunk_messages(oracle, variant):
     """C5-shaped batches — mostly 2..5-chunk messages, so tiles hold far more
     partial last chunks than a wave has lanes and the leaf kernel's block-count
     order is taken — next to runs of single-chunk messages and a few long
-    ones; every digest against the oracle, for both product kernels (52:
+    ones; every digest against the oracle, for every product kernel (52:
     one tile per workgroup, the last-block-index loop, the first chunk kept
-    from phase 1; 67, the default: 52 with the tail masks from a table)"""
+    from phase 1; 67, the default: 52 with the tail masks from a table; 71:
+    the small-batch kernel, 128-slot tiles)"""
     from spacedrive_amd import Engine
     rng = np.random.default_rng(55 + variant)
     lens = np.concatenate([rng.integers(1025, 5 * 1024 + 1, 12000), rng.integers(0, 1025, 3000),
@@ -290,6 +293,43 @@ def test_device_api_synthetic_c2_sample(eng, oracle):
     o = int(offs[i])
     assert bytes(d_blob[o:o + int(lens[i])].cpu().numpy()) == bytes(
         oracle.synth_cas_message(int(keys[i]), int(sizes[i])))
+
+
+def test_small_and_big_batch_kernels(oracle):
+    """the default leaf kernel is chosen by batch size: a device batch whose
+    workspace holds at most 2^14 chunk slots runs the small-batch kernel
+    (128-slot tiles, b3_batch.h kSmallSlots), a larger one the 1 MiB-tile
+    kernel; the same C2-shaped corpus through both, every key against the
+    oracle"""
+    import torch
+    from spacedrive_amd import Engine
+    from tests._oracle import content_key
+    n = 250
+    seed = 0x5D0002
+    idx = np.arange(n, dtype=np.uint64)
+    sizes = np.array([1024 + int(x) % (102400 - 1024 + 1) for x in _c2_raw(seed, idx)], np.uint64)
+    keys = np.array([content_key(seed, 7000 + i) for i in range(n)], np.uint64)
+    lens = sizes + 8
+    chunks = int(((lens + 1023) // 1024).sum())
+    assert chunks + 3 * n + 2048 < (1 << 14)  # the small kernel's side of the threshold
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum((lens[:-1] + 15) // 16 * 16)
+    total = int(offs[-1] + (lens[-1] + 15) // 16 * 16) + 64
+    dev = torch.device("cuda:0")
+    d_blob = torch.empty(total, dtype=torch.uint8, device=dev)
+    t = lambda a: torch.from_numpy(a.view(np.int64)).to(dev)
+    d_keys, d_sizes, d_offs, d_lens = t(keys), t(sizes), t(offs), t(lens)
+    want = [oracle.synth_cas_key(int(keys[i]), int(sizes[i])) for i in range(n)]
+    for reserve in (chunks, 4 * (1 << 14)):
+        with Engine() as eng:
+            d_out = torch.zeros(n, dtype=torch.int64, device=dev)
+            eng.dev_reserve(n, reserve)
+            eng.dev_synth_cas_messages(d_keys.data_ptr(), d_sizes.data_ptr(), d_offs.data_ptr(), n, d_blob.data_ptr())
+            eng.dev_hash_messages(d_blob.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), n, 0, d_out.data_ptr())
+            eng.dev_sync()
+            got = d_out.cpu().numpy().view(np.uint64)
+        bad = [i for i in range(n) if int(got[i]) != want[i]]
+        assert not bad, (reserve, bad[:10])
 
 
 def _c2_raw(seed, idx):

@@ -78,8 +78,8 @@ def main():
         }
     json.dump(out, open(dst, "w"), indent=1)
     # the kernel name bench.load_traffic matches against its default kernel
-    kernel = {51: "k_leaf_tree<512, 109, 1, 1, 2, 2, 0>", 52: "k_leaf_tree<512, 209, 1, 1, 2, 2, 0>",
-              67: "k_leaf_tree<512, 279, 1, 1, 2, 2, 0>"}[variant]
+    kernel = {51: "k_leaf_tree<512, 109, 1, 1, 2, 2, 0>", 52: "k_leaf_tree<512, 209, 1, 1, 2, 2, 0, 1024u>",
+              67: "k_leaf_tree<512, 279, 1, 1, 2, 2, 0, 1024u>"}[variant]
     for w in ("c3", "c5"):
         d = out["workloads"].get(w)
         if not d:

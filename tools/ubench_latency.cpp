@@ -11,6 +11,9 @@
 // call, and the keys must agree. Prints one JSON line per (library, B).
 // "@N" sets the context's reader threads (sdcas_options.io_threads; default
 // 0 = the library's 8); the same library may be named twice with different N.
+// ",NAME=VALUE[,NAME=VALUE]" sets environment variables while the context is created
+// (e.g. ",SDCAS_SMALL_SLOTS=0": that context never uses the small-batch
+// kernel), so one library can be compared with itself under two settings.
 #include <dlfcn.h>
 
 #include <algorithm>
@@ -35,8 +38,14 @@ struct Lib {
   void (*destroy)(sdcas_ctx*) = nullptr;
   int (*cas_ids)(sdcas_ctx*, const char* const*, const uint64_t*, size_t, uint64_t*, int32_t*) = nullptr;
   sdcas_ctx* ctx = nullptr;
-  bool open(const std::string& spec) {
-    path = spec;
+  bool open(const std::string& spec_in) {
+    path = spec_in;
+    std::string spec = spec_in, env;
+    const size_t comma = spec.find(',');
+    if (comma != std::string::npos) {
+      env = spec.substr(comma + 1);
+      spec = spec.substr(0, comma);
+    }
     const size_t at = spec.rfind('@');
     const std::string p = at == std::string::npos ? spec : spec.substr(0, at);
     if (at != std::string::npos) io_threads = (uint32_t)std::stoul(spec.substr(at + 1));
@@ -49,7 +58,20 @@ struct Lib {
     sdcas_options o = SDCAS_OPTIONS_INIT;
     o.device = 0;
     o.io_threads = io_threads;
-    return init(&o, &ctx) == SDCAS_OK;
+    std::vector<std::string> names;  // ",A=1,B=2": several variables
+    for (size_t pos = 0; !env.empty() && pos != std::string::npos;) {
+      const size_t next = env.find(',', pos);
+      const std::string kv = env.substr(pos, next == std::string::npos ? std::string::npos : next - pos);
+      const size_t eq = kv.find('=');
+      if (eq != std::string::npos) {
+        names.push_back(kv.substr(0, eq));
+        setenv(names.back().c_str(), kv.substr(eq + 1).c_str(), 1);
+      }
+      pos = next == std::string::npos ? next : next + 1;
+    }
+    const bool ok = init(&o, &ctx) == SDCAS_OK;
+    for (const auto& nm : names) unsetenv(nm.c_str());
+    return ok;
   }
 };
 
