@@ -31,7 +31,7 @@ if [ "$PART" = a ]; then
 else
   for w in c2 c3 c5; do
     (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$OUT/prof_$w -o $w --output-format csv -- \
-       python $R/bench.py --workload $w --steps 10 --warmup 2 --no-cpu-baseline --no-e2e > $R/$OUT/prof_$w.log 2>&1) || exit 7
+       python $R/bench.py --workload $w --steps 20 --warmup 2 --no-cpu-baseline --no-e2e > $R/$OUT/prof_$w.log 2>&1) || exit 7
   done
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$OUT/prof_c4 -o c4 --output-format csv -- \
      python $R/bench.py --workload c4 --steps 2 --warmup 1 --no-cpu-baseline > $R/$OUT/prof_c4.log 2>&1) || exit 8
