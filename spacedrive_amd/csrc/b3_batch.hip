@@ -38,6 +38,8 @@
 // live in b3_ablate_*.inc and are compiled only with -DSDCAS_ABLATIONS into
 // libsdcas_ablate.so, which only tools/ab_leaf.py loads.
 #include <hip/hip_runtime.h>
+
+#include <atomic>
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
 #include <cstdio>
@@ -1471,37 +1473,37 @@ constexpr int kDefaultLeafVariant = 67;
 int leaf_variant_count() { return kNumLeafVariants; }
 // SDCAS_LEAF_VARIANT names a variant this build holds (then every batch runs it)
 bool leaf_variant_forced() {
-  static int f = -1;
-  if (f < 0) {
+  static const bool f = [] {  // read once, thread-safe (the path calls run on the callers' threads)
     const char* e = getenv("SDCAS_LEAF_VARIANT");
-    f = e && leaf_variant_available(atoi(e)) ? 1 : 0;
-  }
-  return f == 1;
+    return e && leaf_variant_available(atoi(e));
+  }();
+  return f;
 }
 bool leaf_variant_available(int v) { return v >= 0 && v < kNumLeafVariants && kLeafVariants[v].fn != nullptr; }
 
 // SDCAS_LEAF_VARIANT selects a variant for A/B runs; a variant this build
 // does not hold (every diagnostic one in libsdcas.so) falls back to the default
 int leaf_variant() {
-  static int v = -2;
-  if (v == -2) {
+  static const int v = [] {
     const char* e = getenv("SDCAS_LEAF_VARIANT");
-    v = e ? atoi(e) : kDefaultLeafVariant;
-    if (!leaf_variant_available(v)) v = kDefaultLeafVariant;
-  }
+    const int x = e ? atoi(e) : kDefaultLeafVariant;
+    return leaf_variant_available(x) ? x : kDefaultLeafVariant;
+  }();
   return v;
 }
 
 int batch_grid(int device, int variant) {
-  static int cached[64][64] = {{0}};
-  if (device >= 0 && device < 64 && cached[device][variant]) return cached[device][variant];
+  static std::atomic<int> cached[64][kNumLeafVariants];  // zero-initialised (static storage)
+  const bool cacheable = device >= 0 && device < 64 && variant >= 0 && variant < kNumLeafVariants;
+  if (cacheable && cached[device][variant].load(std::memory_order_relaxed))
+    return cached[device][variant].load(std::memory_order_relaxed);
   int cus = 256, per = 1;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
   (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kLeafVariants[variant].fn, kLeafVariants[variant].wg, 0);
   if (per < 1) per = 1;
   if (getenv("SDCAS_DEBUG_GRID")) fprintf(stderr, "leaf variant %d: %d workgroups/CU\n", variant, per);
   int g = cus * per;
-  if (device >= 0 && device < 64) cached[device][variant] = g;
+  if (cacheable) cached[device][variant].store(g, std::memory_order_relaxed);
   return g;
 }
 
@@ -1620,12 +1622,11 @@ bool piece_variant_available(int v) {
 }
 
 int piece_variant() {
-  static int v = -2;
-  if (v == -2) {
+  static const int v = [] {
     const char* e = getenv("SDCAS_PIECE_VARIANT");
-    v = e ? atoi(e) : kDefaultPieceVariant;
-    if (!piece_variant_available(v)) v = kDefaultPieceVariant;
-  }
+    const int x = e ? atoi(e) : kDefaultPieceVariant;
+    return piece_variant_available(x) ? x : kDefaultPieceVariant;
+  }();
   return v;
 }
 
