@@ -149,7 +149,7 @@ def compressions(lens):
 # the library's default kernels (spacedrive_amd/csrc/b3_batch.hip
 # kDefaultLeafVariant / kDefaultPieceVariant): the PMC traffic files are per kernel
 DEFAULT_LEAF_KERNEL = "k_leaf_tree<512, 279, 1, 1, 2, 2, 0, 1024u>"
-DEFAULT_PIECE_VARIANT = 17
+DEFAULT_PIECE_VARIANT = 19
 
 
 def load_traffic(workload, kernel="k_leaf_tree"):
@@ -564,7 +564,9 @@ def run_c4(args, torch, dist, dev, rank, world, distributed, out_f):
         "blake3_gbps": gbs,
         "hash_kernel_gbps": total / hash_s / 1e9 if hash_s > 0 else None,
         "roofline": {
-            "bound": "valu", "kernel": "k_piece_tree (1 MiB pieces -> level-10 nodes)",
+            "bound": "valu", "kernel": ("k_piece_l4 + k_piece_top (1 MiB pieces -> level-4 nodes -> level-10 nodes)"
+                                   if (DEFAULT_PIECE_VARIANT if args.piece_variant < 0 else args.piece_variant) == 19
+                                   else "k_piece_tree (1 MiB pieces -> level-10 nodes)"),
             "achieved": comp / hash_s / world * OPS_PER_COMPRESSION / 1e12 if hash_s > 0 else None,
             "peak": VALU_PEAK_OPS / 1e12, "unit": TOPS_UNIT,
             "traffic": None, "algorithmic_bytes_per_launch": my_bytes,
@@ -589,7 +591,7 @@ def run_c4(args, torch, dist, dev, rank, world, distributed, out_f):
     hb["frac"] = hb["achieved"] / HBM_PEAK_GBS if hb["achieved"] else None
     # PMC traffic of the kernel this run launched (the default piece kernel
     # unless --piece-variant chose another)
-    piece_kernels = {15: "k_piece_tree<208, 6, 1, 0, 10>", 17: "k_piece_tree<259, 6, 1, 0, 10>"}
+    piece_kernels = {17: "k_piece_tree<259, 6, 1, 0, 10>", 19: "k_piece_l4<259, 6>"}
     pv = DEFAULT_PIECE_VARIANT if args.piece_variant < 0 else args.piece_variant
     tr = load_traffic("c4", piece_kernels[pv]) if pv in piece_kernels else None
     if tr and resident and tr.get("algorithmic_bytes_per_launch") == my_bytes:

@@ -81,10 +81,16 @@ struct FileDesc {
 inline uint64_t bigfile_node_count(uint64_t C) {
   return C / kTile + (uint64_t)__builtin_popcountll(C % kTile);
 }
+// Piece variant 19 stops a full piece's tree at this level and finishes the
+// levels above it over many pieces at once (k_piece_top).
+constexpr uint32_t kPieceDeferLevel = 4;
+// device scratch of piece_hash's l4 argument: u32 words per piece
+constexpr uint64_t kPieceL4Words = 8ull * (kTile >> kPieceDeferLevel);
 // ctr: one u32 of device scratch (the persistent variants' piece counter);
+// l4: kPieceL4Words * npieces u32 of device scratch (variant 19);
 // variant: piece kernel variant (-1: default / SDCAS_PIECE_VARIANT)
 hipError_t piece_hash(const uint8_t* blob, const PieceDesc* pieces, uint32_t npieces, uint32_t* file_nodes,
-                      uint32_t* ctr, int variant, hipStream_t st);
+                      uint32_t* ctr, uint32_t* l4, int variant, hipStream_t st);
 hipError_t bigfile_finish(const FileDesc* files, uint32_t nfiles, const uint32_t* file_nodes, uint8_t* out32,
                           hipStream_t st);
 

@@ -996,10 +996,14 @@ __global__ void __launch_bounds__(256) k_shape_scatter(const uint64_t* __restric
 // may arrive over many launches (streamed windows); k_bigfile_finish merges a
 // file's list once all of it is there.
 
-template <int PF, int MINW, int DIRECT = 0, int ROT = 0, int TOP = 10>
-__global__ void __launch_bounds__(kWG, MINW) k_piece_tree(const uint8_t* __restrict__ blob,
-                                                          const PieceDesc* __restrict__ pieces, uint32_t npieces,
-                                                          uint32_t* __restrict__ file_nodes) {
+// One workgroup's pass over its pieces (the body of k_piece_tree and
+// k_piece_l4). DEFER: a full piece stops at tree level 4 and writes its 64
+// level-4 nodes to l4[64 pi ..] for k_piece_top, which runs the one-wave
+// levels 5-10 of eight pieces at once; a tail piece completes here.
+template <int PF, int DIRECT, int ROT, int TOP, int DEFER>
+__device__ __forceinline__ void piece_pass(const uint8_t* __restrict__ blob, const PieceDesc* __restrict__ pieces,
+                                           uint32_t npieces, uint32_t* __restrict__ file_nodes,
+                                           uint32_t* __restrict__ l4) {
   __shared__ uint32_t cvs[kTile][8];
   __shared__ uint16_t task[kTile / 2];
   __shared__ uint32_t ntask[16];
@@ -1023,7 +1027,9 @@ __global__ void __launch_bounds__(kWG, MINW) k_piece_tree(const uint8_t* __restr
       for (int i = 0; i < 8; ++i) cvs[s][i] = cv[i];
     }
     __syncthreads();
-    for (uint32_t k = 1; (1u << k) <= kTile && k <= TOP; ++k) {  // TOP < 10: DIAGNOSTIC (wrong digests)
+    const bool defer = DEFER && nchunks == kTile;
+    const uint32_t top = defer ? kPieceDeferLevel : TOP;
+    for (uint32_t k = 1; (1u << k) <= kTile && k <= top; ++k) {  // TOP < 10: DIAGNOSTIC (wrong digests)
       const uint32_t w = 1u << k;
       uint32_t T;
       if (DIRECT) {
@@ -1053,6 +1059,16 @@ __global__ void __launch_bounds__(kWG, MINW) k_piece_tree(const uint8_t* __restr
       }
       __syncthreads();
     }
+    if (defer) {
+      for (uint32_t t = tid; t < kTile >> kPieceDeferLevel; t += kWG) {
+        const uint32_t s = t << kPieceDeferLevel;
+        uint4* o = reinterpret_cast<uint4*>(l4 + 8ull * ((uint64_t)pi * (kTile >> kPieceDeferLevel) + t));
+        o[0] = make_uint4(cvs[s][0], cvs[s][1], cvs[s][2], cvs[s][3]);
+        o[1] = make_uint4(cvs[s][4], cvs[s][5], cvs[s][6], cvs[s][7]);
+      }
+      __syncthreads();
+      continue;
+    }
     // maximal nodes: the binary decomposition of nchunks (one node for a full piece)
     for (uint32_t s = tid; s < nchunks; s += kWG) {
       const uint32_t rest = nchunks - s;
@@ -1065,6 +1081,69 @@ __global__ void __launch_bounds__(kWG, MINW) k_piece_tree(const uint8_t* __restr
       o[1] = make_uint4(cvs[s][4], cvs[s][5], cvs[s][6], cvs[s][7]);
     }
     __syncthreads();
+  }
+}
+
+template <int PF, int MINW, int DIRECT = 0, int ROT = 0, int TOP = 10>
+__global__ void __launch_bounds__(kWG, MINW) k_piece_tree(const uint8_t* __restrict__ blob,
+                                                          const PieceDesc* __restrict__ pieces, uint32_t npieces,
+                                                          uint32_t* __restrict__ file_nodes) {
+  piece_pass<PF, DIRECT, ROT, TOP, 0>(blob, pieces, npieces, file_nodes, nullptr);
+}
+
+// k_piece_tree whose full pieces stop at level 4 (piece_pass DEFER)
+template <int PF, int MINW>
+__global__ void __launch_bounds__(kWG, MINW) k_piece_l4(const uint8_t* __restrict__ blob,
+                                                        const PieceDesc* __restrict__ pieces, uint32_t npieces,
+                                                        uint32_t* __restrict__ file_nodes, uint32_t* __restrict__ l4) {
+  piece_pass<PF, 1, 0, 10, 1>(blob, pieces, npieces, file_nodes, l4);
+}
+
+// Levels 5-10 of kTopPieces full pieces per workgroup, one thread per level-4
+// node: the levels' tasks (256, 128, 64, 32, 16, 8) fill 10 wave-issues for
+// the 504 parents of 8 pieces, where one piece per workgroup spends 6 nearly
+// empty wave-issues on its 63. A piece's 64 nodes are 64-aligned in the
+// group's array, so the in-place levels never cross pieces. Tail pieces'
+// entries of l4 are never written and their results never stored.
+constexpr uint32_t kTopPieces = kWG / (kTile >> kPieceDeferLevel);
+template <int PF>
+__global__ void __launch_bounds__(kWG) k_piece_top(const PieceDesc* __restrict__ pieces, uint32_t npieces,
+                                                   const uint32_t* __restrict__ l4, uint32_t* __restrict__ file_nodes) {
+  constexpr uint32_t kN = kTile >> kPieceDeferLevel;  // level-4 nodes per piece
+  __shared__ uint32_t cvs[kTopPieces * kN][8];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t p0 = blockIdx.x * kTopPieces;
+  if (p0 + tid / kN < npieces) {
+    const uint4* src = reinterpret_cast<const uint4*>(l4 + 8ull * ((uint64_t)p0 * kN + tid));
+    const uint4 a = src[0], b = src[1];
+    cvs[tid][0] = a.x; cvs[tid][1] = a.y; cvs[tid][2] = a.z; cvs[tid][3] = a.w;
+    cvs[tid][4] = b.x; cvs[tid][5] = b.y; cvs[tid][6] = b.z; cvs[tid][7] = b.w;
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (uint32_t k = 1; (1u << k) <= kN; ++k) {
+    if (tid < (kTopPieces * kN) >> k) {
+      const uint32_t s = tid << k, h = 1u << (k - 1);
+      uint32_t l[8], r[8], o[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        l[i] = cvs[s][i];
+        r[i] = cvs[s + h][i];
+      }
+      parent<kGA<PF>>(l, r, false, o);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) cvs[s][i] = o[i];
+    }
+    __syncthreads();
+  }
+  if (tid < kTopPieces && p0 + tid < npieces) {
+    const PieceDesc pd = pieces[p0 + tid];
+    if (pd.len == kTile * CHUNK_LEN) {
+      const uint32_t s = tid * kN;
+      uint4* o = reinterpret_cast<uint4*>(file_nodes + 8ull * (pd.node_base + pd.j0 / kTile));
+      o[0] = make_uint4(cvs[s][0], cvs[s][1], cvs[s][2], cvs[s][3]);
+      o[1] = make_uint4(cvs[s][4], cvs[s][5], cvs[s][6], cvs[s][7]);
+    }
   }
 }
 
@@ -1595,13 +1674,19 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
   return hipGetLastError();
 }
 
-// Piece kernel variants. Product: 15 = one workgroup per 1 MiB piece, the
+// Piece kernel variants. Product: 17 = one workgroup per 1 MiB piece, whole
+// chunks through hash_chunk_full (no per-block length, flag or tail-mask work
+// on a lane; the block index is wave-uniform), partial chunks through the
 // leaf kernel's line-pair block loop, 6 waves/SIMD, every G step a B3_G_ASM
 // block with the copy-free first column steps (b3_device.h, compress<2>);
-// 17 (default since round 3) = 15 with whole chunks through hash_chunk_full
-// (no per-block length, flag or tail-mask work on a lane; the block index is
-// wave-uniform): 1.7 % faster in a same-process A/B
-// (profiles/r03_ab_piece_15_17.txt). Ablation library only: 14 = 15 without
+// 19 (default since round 3) = 17 whose full pieces stop at tree level 4
+// (k_piece_l4) and k_piece_top runs levels 5-10 of eight pieces per
+// workgroup: those levels are one nearly empty wave-issue each when one
+// piece owns the workgroup (1.0 % faster in a same-process A/B, bit-exact,
+// profiles/r03_ab_piece_17_19.txt; the DIAGNOSTIC 18 bounded the gain at
+// 1.1 %). Ablation library only: 15 = 17 with whole chunks through the
+// line-pair loop (round 3's first-session product pair, 1.7 % slower,
+// profiles/r03_ab_piece_15_17.txt), 14 = 15 without
 // the copy-free first column steps (round 2's product pair), 4 = ping-pong
 // block loop (round 1's default), 6 = 14 with the compiler-scheduled G (round
 // 2's default before B3_G_ASM: 10 % slower), 11 = persistent grid on a global
@@ -1611,12 +1696,12 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
 // orders, a round-robin persistent grid, and the DIAGNOSTIC 7 (no memory
 // reads), 16 and 18 (15 and 17 without the in-piece tree levels 5-10: what
 // the one-wave levels cost).
-constexpr int kDefaultPieceVariant = 17;
+constexpr int kDefaultPieceVariant = 19;
 
 bool piece_variant_available(int v) {
-  if (v == 15 || v == 17) return true;
+  if (v == 17 || v == 19) return true;
 #ifdef SDCAS_ABLATIONS
-  if (v >= 0 && v <= 18) return true;
+  if (v >= 0 && v <= 19) return true;
 #endif
   return false;
 }
@@ -1664,6 +1749,8 @@ static hipError_t piece_hash_ablation(int v, const uint8_t* blob, const PieceDes
   else if (v == 18)  // DIAGNOSTIC (wrong digests): 17 without the in-piece tree levels 5-10
     hipLaunchKernelGGL((k_piece_tree<259, 6, 1, 0, 4>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces,
                        file_nodes);
+  else if (v == 15)  // 17 with whole chunks through the line-pair loop
+    hipLaunchKernelGGL((k_piece_tree<208, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   if (v >= 14) return hipGetLastError();
   if (v == 0) hipLaunchKernelGGL((k_piece_tree<0, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
   else if (v == 1)
@@ -1694,11 +1781,14 @@ static hipError_t piece_hash_ablation(int v, const uint8_t* blob, const PieceDes
 #endif
 
 hipError_t piece_hash(const uint8_t* blob, const PieceDesc* pieces, uint32_t npieces, uint32_t* file_nodes,
-                      uint32_t* ctr, int variant, hipStream_t st) {
+                      uint32_t* ctr, uint32_t* l4, int variant, hipStream_t st) {
   if (!npieces) return hipSuccess;
   const int v = piece_variant_available(variant) ? variant : piece_variant();
-  if (v == 15) {
-    hipLaunchKernelGGL((k_piece_tree<208, 6, 1>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes);
+  if (v == 19) {
+    if (!l4) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_piece_l4<259, 6>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes, l4);
+    hipLaunchKernelGGL((k_piece_top<259>), dim3((npieces + kTopPieces - 1) / kTopPieces), dim3(kWG), 0, st, pieces,
+                       npieces, l4, file_nodes);
     return hipGetLastError();
   }
 #ifdef SDCAS_ABLATIONS

@@ -145,6 +145,7 @@ struct sdcas_ctx {
   bool sm_active = false;
   uint64_t sm_node_bytes = 0;
   DevBuf<uint32_t> piece_ctr;  // the persistent piece kernels' work counter
+  DevBuf<uint32_t> piece_l4;   // piece variant 19's level-4 nodes (kPieceL4Words per piece)
   int piece_variant = -1;
 
   // Every call that enqueues work on the context's device scratch (the
@@ -461,6 +462,7 @@ int run_big(sdcas_ctx* c, const std::vector<BigItem>& items, uint8_t* out32_host
   if ((e = c->d_files.ensure(items.size()))) return c->hip_fail(e, "file descs");
   if ((e = c->d_out32.ensure(32 * items.size()))) return c->hip_fail(e, "device digests");
   if ((e = c->piece_ctr.ensure(1))) return c->hip_fail(e, "piece counter");
+  if ((e = c->piece_l4.ensure(kPieceL4Words * 2 * max_pieces))) return c->hip_fail(e, "piece level-4 nodes");
   hipStream_t st = c->stream;
   int cur = 0;
   struct Job {
@@ -500,13 +502,16 @@ int run_big(sdcas_ctx* c, const std::vector<BigItem>& items, uint8_t* out32_host
       hp[k] = pd;  // a failed item's pieces are hashed too: its digest is never returned
     }
     PieceDesc* dp = reinterpret_cast<PieceDesc*>(s.d_meta.p);
+    if (kPieceL4Words * jobs.size() > c->piece_l4.cap)  // a window holds at most 2 pieces per MiB
+      return c->fail(SDCAS_E_CAPACITY, "piece window: %zu pieces", jobs.size());
     hipError_t ee;
     if ((ee = slot_upload(c, s, [&](hipStream_t cs) {
            hipError_t r = hipMemcpyAsync(s.d_blob.p, s.h, used, hipMemcpyHostToDevice, cs);
            return r ? r : hipMemcpyAsync(dp, hp, sizeof(PieceDesc) * jobs.size(), hipMemcpyHostToDevice, cs);
          })))
       return c->hip_fail(ee, "H2D pieces");
-    if ((ee = piece_hash(s.d_blob.p, dp, (uint32_t)jobs.size(), c->d_file_nodes.p, c->piece_ctr.p, c->piece_variant,
+    if ((ee = piece_hash(s.d_blob.p, dp, (uint32_t)jobs.size(), c->d_file_nodes.p, c->piece_ctr.p, c->piece_l4.p,
+                         c->piece_variant,
                          st)))
       return c->hip_fail(ee, "piece_hash");
     if ((ee = hipEventRecord(s.ev, st))) return c->hip_fail(ee, "event");
@@ -621,7 +626,7 @@ void sdcas_destroy(sdcas_ctx* c) {
   if (c->scratch_ev) (void)hipEventSynchronize(c->scratch_ev);
   for (auto* b : {&c->ws_S, &c->ws_total, &c->ws_soffs, &c->ws_slens, &c->dd_keys, &c->dd_ekeys, &c->dd_ids})
     b->release();
-  for (auto* b : {&c->ws_tile_first, &c->ws_nodes, &c->ws_perm, &c->ws_sort_keys, &c->d_file_nodes, &c->piece_ctr})
+  for (auto* b : {&c->ws_tile_first, &c->ws_nodes, &c->ws_perm, &c->ws_sort_keys, &c->d_file_nodes, &c->piece_ctr, &c->piece_l4})
     b->release();
   for (auto* b : {&c->ws_scan, &c->d_out32, &c->dd_has}) b->release();
   c->d_files.release();
@@ -1593,6 +1598,7 @@ int sdcas_dev_stream_update(sdcas_ctx* c, size_t nseg, const uint64_t* h_file, c
   hipStream_t st = call.st;
   hipError_t e;
   if ((e = c->sm_pieces.ensure(pieces.size()))) return c->hip_fail(e, "piece descs");
+  if ((e = c->piece_l4.ensure(kPieceL4Words * pieces.size()))) return c->hip_fail(e, "piece level-4 nodes");
   // stream-ordered: a previous update's kernel on `st` has finished reading
   // the descriptor buffer before this copy lands
   if ((e = hipMemcpyAsync(c->sm_pieces.p, pieces.data(), sizeof(PieceDesc) * pieces.size(), hipMemcpyHostToDevice,
@@ -1606,7 +1612,7 @@ int sdcas_dev_stream_update(sdcas_ctx* c, size_t nseg, const uint64_t* h_file, c
     (void)hipEventRecord(a, st);
   }
   e = piece_hash(reinterpret_cast<const uint8_t*>(base), c->sm_pieces.p, (uint32_t)pieces.size(), c->sm_nodes.p,
-                 c->piece_ctr.p, c->piece_variant, st);
+                 c->piece_ctr.p, c->piece_l4.p, c->piece_variant, st);
   if (c->profile) {
     (void)hipEventRecord(b, st);
     c->ev_leaf.push_back({a, b});

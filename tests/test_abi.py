@@ -71,7 +71,7 @@ def _kernel_stubs(path):
 
 def test_product_library_holds_only_product_kernels():
     """libsdcas.so carries only the product kernels — leaf 67 (default), 52
-    and the small-batch kernel 71, piece 17 (default) and 15, all bit-exact
+    and the small-batch kernel 71, piece 19 (default: k_piece_l4 + k_piece_top) and 17, all bit-exact
     and GPU-tested — and no
     ablation or
     DIAGNOSTIC variant (those produce wrong digests and live only in
@@ -82,7 +82,7 @@ def test_product_library_holds_only_product_kernels():
                     "k_leaf_tree<512, 279, 1, 1, 2, 2, 0, 1024u>"], leaf
     assert not [s for s in stubs if "slim" in s or "quad" in s]
     pieces = [s for s in stubs if s.startswith("k_piece")]
-    assert sorted(pieces) == ["k_piece_tree<208, 6, 1, 0, 10>", "k_piece_tree<259, 6, 1, 0, 10>"], pieces
+    assert sorted(pieces) == ["k_piece_l4<259, 6>", "k_piece_top<259>", "k_piece_tree<259, 6, 1, 0, 10>"], pieces
 
 
 def test_ablation_build_is_separate():

@@ -242,7 +242,7 @@ def test_diagnostic_variants_unreachable(eng, oracle):
     import sys
     for v in (4, 5, 6, 7, 26, 27, 28, 39, 40, 41, 1, 25, 29, 36, 43, 46, 47, 48, 49, 50, 51, 64, 65, 66, 68):
         assert not eng.dev_set_leaf_variant(v), v
-    for v in (4, 6, 7, 11, 14, 16, 18):
+    for v in (4, 6, 7, 11, 14, 15, 16, 18):
         assert not eng.dev_set_piece_variant(v), v
     code = (
         "import numpy as np, sys; sys.path.insert(0, %r)\n"

@@ -134,10 +134,11 @@ def test_stream_over_4tib_golden(eng):
         assert bytes(out.cpu().numpy()[0]).hex() == c["checksum"], n
 
 
-@pytest.mark.parametrize("variant", [15, 17])
+@pytest.mark.parametrize("variant", [17, 19])
 def test_piece_variants_vs_oracle(oracle, variant):
-    """every product piece kernel (15: one workgroup per piece, the line-pair
-    block loop; 17: 15 with whole chunks through the full-chunk loop) over
+    """every product piece kernel (17: one workgroup per piece, whole chunks
+    through the full-chunk loop; 19: 17 with the full pieces' tree levels
+    5-10 in k_piece_top, eight pieces per workgroup) over
     multi-window files whose windows hold many pieces and a ragged tail,
     against the oracle"""
     from spacedrive_amd import Engine
