@@ -1103,8 +1103,8 @@ __global__ void __launch_bounds__(kWG, MINW) k_piece_l4(const uint8_t* __restric
 // node: the levels' tasks (256, 128, 64, 32, 16, 8) fill 10 wave-issues for
 // the 504 parents of 8 pieces, where one piece per workgroup spends 6 nearly
 // empty wave-issues on its 63. A piece's 64 nodes are 64-aligned in the
-// group's array, so the in-place levels never cross pieces. Tail pieces'
-// entries of l4 are never written and their results never stored.
+// group's array, so the in-place levels never cross pieces. Pieces of fewer
+// than kTile chunks have no l4 entries and no result here.
 constexpr uint32_t kTopPieces = kWG / (kTile >> kPieceDeferLevel);
 template <int PF>
 __global__ void __launch_bounds__(kWG) k_piece_top(const PieceDesc* __restrict__ pieces, uint32_t npieces,
@@ -1138,7 +1138,7 @@ __global__ void __launch_bounds__(kWG) k_piece_top(const PieceDesc* __restrict__
   }
   if (tid < kTopPieces && p0 + tid < npieces) {
     const PieceDesc pd = pieces[p0 + tid];
-    if (pd.len == kTile * CHUNK_LEN) {
+    if ((pd.len + CHUNK_LEN - 1) / CHUNK_LEN == kTile) {  // piece_pass deferred it (a file's last piece too)
       const uint32_t s = tid * kN;
       uint4* o = reinterpret_cast<uint4*>(file_nodes + 8ull * (pd.node_base + pd.j0 / kTile));
       o[0] = make_uint4(cvs[s][0], cvs[s][1], cvs[s][2], cvs[s][3]);

@@ -143,8 +143,10 @@ def test_piece_variants_vs_oracle(oracle, variant):
     against the oracle"""
     from spacedrive_amd import Engine
     rng = np.random.default_rng(40 + variant)
-    sizes = [MiB + 1, 5 * MiB + 17, 16 * MiB, 9 * MiB + 4095, 2 * MiB - 1, 40 * MiB + 3]
-    keys = [content_key(0x5D0004, 300 + i) for i in range(len(sizes))]
+    sizes = [MiB + 1, 5 * MiB + 17, 16 * MiB, 9 * MiB + 4095, 2 * MiB - 1, 40 * MiB + 3, 3 * MiB - 1000]
+    # contents differ per variant: a node a kernel failed to write must not
+    # be found intact in memory an earlier case freed
+    keys = [content_key(0x5D0004, 300 + 16 * variant + i) for i in range(len(sizes))]
     with Engine(staging_bytes=8 * MiB) as e:
         assert e.dev_set_piece_variant(variant)
         from tests._oracle import content
