@@ -1701,7 +1701,7 @@ constexpr int kDefaultPieceVariant = 19;
 bool piece_variant_available(int v) {
   if (v == 17 || v == 19) return true;
 #ifdef SDCAS_ABLATIONS
-  if (v >= 0 && v <= 19) return true;
+  if (v >= 0 && v <= 20) return true;
 #endif
   return false;
 }
@@ -1737,7 +1737,14 @@ static hipError_t launch_piece_dyn(const uint8_t* blob, const PieceDesc* pieces,
 }
 
 static hipError_t piece_hash_ablation(int v, const uint8_t* blob, const PieceDesc* pieces, uint32_t npieces,
-                                      uint32_t* file_nodes, uint32_t* ctr, hipStream_t st) {
+                                      uint32_t* file_nodes, uint32_t* ctr, uint32_t* l4, hipStream_t st) {
+  if (v == 20) {  // 19 at 8 waves/SIMD (64 VGPRs; the spills are outside the full-chunk loop)
+    if (!l4) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_piece_l4<259, 8>), dim3(npieces), dim3(kWG), 0, st, blob, pieces, npieces, file_nodes, l4);
+    hipLaunchKernelGGL((k_piece_top<259>), dim3((npieces + kTopPieces - 1) / kTopPieces), dim3(kWG), 0, st, pieces,
+                       npieces, l4, file_nodes);
+    return hipGetLastError();
+  }
   if (v == 11) return launch_piece_dyn<6, 0>(blob, pieces, npieces, file_nodes, ctr, st);
   if (v == 12) return launch_piece_dyn<6, 1>(blob, pieces, npieces, file_nodes, ctr, st);
   if (v == 13) return launch_piece_dyn<8, 0>(blob, pieces, npieces, file_nodes, ctr, st);
@@ -1792,7 +1799,7 @@ hipError_t piece_hash(const uint8_t* blob, const PieceDesc* pieces, uint32_t npi
     return hipGetLastError();
   }
 #ifdef SDCAS_ABLATIONS
-  if (v != 17) return piece_hash_ablation(v, blob, pieces, npieces, file_nodes, ctr, st);
+  if (v != 17) return piece_hash_ablation(v, blob, pieces, npieces, file_nodes, ctr, l4, st);
 #else
   (void)ctr;
 #endif
