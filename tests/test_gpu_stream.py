@@ -64,6 +64,49 @@ def test_stream_synth_vs_oracle(eng, oracle):
         assert bytes(got[i]).hex() == oracle.synth_checksum(k, n), n
 
 
+@pytest.mark.parametrize("variant", [17, 19])
+def test_stream_piece_boundaries_vs_oracle(oracle, variant):
+    """every product piece kernel over files whose lengths sit at and around
+    1 MiB-piece, 1 KiB-chunk and 64-byte-block boundaries (a last piece of
+    exactly 1024 chunks with a partial last chunk among them: piece 19 must
+    store its deferred node too), delivered as random 1 MiB-aligned segments
+    in shuffled order over three update calls, against the oracle"""
+    from spacedrive_amd import Engine
+    rng = np.random.default_rng(70 + variant)
+    deltas = [-1025, -1024, -1023, -65, -64, -1, 0, 1, 63, 64, 1023, 1024, 1025]
+    sizes = sorted({int(k) * MiB + d for k in (2, 3, 5, 8) for d in deltas} |
+                   {MiB + d for d in deltas if d > 0})
+    sizes = [int(x) for x in rng.permutation(sizes)]
+    keys = [content_key(0x5D0004, 1000 + 64 * variant + i) for i in range(len(sizes))]
+    segs = [(f, o, l) for f, n in enumerate(sizes) for o, l in _segments(rng, n, 3)]
+    rng.shuffle(segs)
+    boffs, used = [], 0
+    for _, _, l in segs:
+        boffs.append(used)
+        used += (l + MiB - 1) // MiB * MiB
+    blob = torch.empty(used + 4096, dtype=torch.uint8, device="cuda")
+    base = blob.data_ptr()
+    t = lambda a: torch.from_numpy(np.array(a, np.uint64).view(np.int64)).cuda()
+    out = torch.zeros((len(sizes), 32), dtype=torch.uint8, device="cuda")
+    with Engine() as e:
+        assert e.dev_set_piece_variant(variant)
+        s = torch.cuda.Stream()
+        args = [t([keys[f] for f, _, _ in segs]), t([o for _, o, _ in segs]), t([l for _, _, l in segs]), t(boffs)]
+        torch.cuda.synchronize()
+        e.dev_synth_content(*(a.data_ptr() for a in args), len(segs), base, s.cuda_stream)
+        e.dev_stream_begin(sizes)
+        cuts = [0, len(segs) // 3, 2 * len(segs) // 3, len(segs)]
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            sg = segs[a:b]
+            e.dev_stream_update([f for f, _, _ in sg], [o for _, o, _ in sg], [l for _, _, l in sg],
+                                [base + x for x in boffs[a:b]], stream=s.cuda_stream)
+        e.dev_stream_finish(out.data_ptr(), s.cuda_stream)
+        e.dev_sync(s.cuda_stream)
+    got = out.cpu().numpy()
+    bad = [n for i, (k, n) in enumerate(zip(keys, sizes)) if bytes(got[i]).hex() != oracle.synth_checksum(k, n)]
+    assert not bad, (variant, bad)
+
+
 def test_stream_4gib_plus_1_golden(eng):
     c = [c for c in golden("checksums.json") if c["size"] == (4 << 30) + 1][0]
     n = c["size"]
