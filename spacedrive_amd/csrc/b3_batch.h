@@ -53,6 +53,27 @@ bool leaf_variant_available(int v);  // compiled into this build (the diagnostic
 bool leaf_variant_forced();          // SDCAS_LEAF_VARIANT names an available variant
 bool piece_variant_available(int v);
 
+// A small batch's slot plan, computed by a caller that has the lengths on the
+// host (the staging path) and uploaded with them: what the scan and
+// k_tile_first would write for tiles of `tile` slots, so that batch_hash
+// launches neither; `crossing` = some message spans a tile boundary (else
+// k_finish_t has nothing to do and is not launched either). Used only for a
+// batch the kernel takes in caller order (fewer than kSortMinMsgs messages)
+// with that tile size; any other batch plans on the device.
+constexpr uint32_t kSortMinMsgs = 128;  // smaller batches keep the caller's order
+struct BatchPlan {
+  const uint64_t* S = nullptr;           // device: first slot of each message
+  const uint32_t* tile_first = nullptr;  // device: message owning each tile's first slot
+  uint64_t* total = nullptr;             // device: [4] total slots, 0, 0 (leaf tile counter), 0
+  uint32_t tile = 0;
+  bool crossing = true;
+};
+// Host side of BatchPlan: S[n], tile_first[tiles] and total[4] for tiles of
+// `tile` slots (tile_first entries below cap_slots only, as k_tile_first);
+// returns the tile count and sets *crossing.
+uint64_t batch_plan_host(const uint64_t* lens, uint32_t n, uint32_t tile, uint64_t cap_slots, uint64_t* S,
+                         uint32_t* tile_first, uint64_t* total, bool* crossing);
+
 // Hash n messages (blob + offs[i], lens[i] bytes; offsets 16-byte aligned),
 // all pointers device pointers. Writes 32-byte digests to out32 and/or cas
 // keys (digest bytes 0..7 big-endian) to out_keys (either may be null).
@@ -63,7 +84,7 @@ bool piece_variant_available(int v);
 // sees).
 hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint64_t* offs, const uint64_t* lens,
                       uint32_t n, uint8_t* out32, uint64_t* out_keys, hipStream_t st, uint64_t max_chunks = 0,
-                      hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+                      hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, const BatchPlan* plan = nullptr);
 
 // ---- big files (C > kTile chunks), hashed as 1 MiB pieces -------------------
 struct PieceDesc {

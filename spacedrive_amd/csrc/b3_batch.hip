@@ -833,7 +833,6 @@ __global__ void __launch_bounds__(kFinishWG) k_finish_t(const uint64_t* __restri
 constexpr uint32_t kShapeBins = 256;
 static_assert(kSortKeyWords == 2 * kShapeBins * kBinStride, "ws.sort_keys holds counts and cursors");
 constexpr uint32_t kScatterPerWG = 4096;
-constexpr uint32_t kSortMinMsgs = 128;  // smaller batches keep the caller's order
 constexpr uint32_t kHistPerThread = 8;
 constexpr uint32_t kScatterR = kScatterPerWG / 256;  // messages per scatter thread
 constexpr uint32_t kShapeManyChunks = 15 << 4;  // first shape key of messages of 15+ chunks
@@ -1586,9 +1585,27 @@ int batch_grid(int device, int variant) {
   return g;
 }
 
+uint64_t batch_plan_host(const uint64_t* lens, uint32_t n, uint32_t tile, uint64_t cap_slots, uint64_t* S,
+                         uint32_t* tile_first, uint64_t* total, bool* crossing) {
+  uint64_t s = 0, tiles = 0;
+  bool cross = false;
+  for (uint32_t m = 0; m < n; ++m) {
+    const uint64_t C = chunk_count(lens[m]);
+    S[m] = s;
+    for (uint64_t t = (s + tile - 1) / tile; t * tile < s + C && t * tile < cap_slots; ++t) tile_first[t] = m;
+    cross |= s / tile != (s + C - 1) / tile;
+    s += C;
+  }
+  tiles = (s + tile - 1) / tile;
+  total[0] = s;
+  total[1] = total[2] = total[3] = 0;
+  *crossing = cross;
+  return tiles;
+}
+
 hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint64_t* offs, const uint64_t* lens,
                       uint32_t n, uint8_t* out32, uint64_t* out_keys, hipStream_t st, uint64_t max_chunks,
-                      hipEvent_t ev0, hipEvent_t ev1) {
+                      hipEvent_t ev0, hipEvent_t ev1, const BatchPlan* plan) {
   if (n == 0) return hipSuccess;
   if (n > ws.cap_msgs) return hipErrorInvalidValue;
   const uint32_t tb = 256;
@@ -1625,8 +1642,15 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
     v = leaf_variant_available(ws.small_variant) && kLeafVariants[ws.small_variant].tile == kSmallTile ? ws.small_variant
                                                                                                         : kSmallVariant;
   const uint32_t tile = kLeafVariants[v].tile;
+  // the caller's host plan stands in for the scan and k_tile_first when it
+  // was made for this order and tile size
+  const bool planned = plan && !perm && !quad && plan->tile == tile;
+  uint64_t* const S = planned ? const_cast<uint64_t*>(plan->S) : ws.S;
+  uint32_t* const tile_first = planned ? const_cast<uint32_t*>(plan->tile_first) : ws.tile_first;
+  uint64_t* const total = planned ? plan->total : ws.total;
   size_t tmp = ws.scan_tmp_bytes;
-  if (quad) {
+  if (planned) {
+  } else if (quad) {
 #ifdef SDCAS_ABLATIONS
     QuadIt qit(hipcub::CountingInputIterator<uint32_t>(0), QuadSlotsOp{lens, n});
     if ((e = hipcub::DeviceScan::ExclusiveSum(ws.scan_tmp, tmp, qit, ws.S, (int)n, st))) return e;
@@ -1649,9 +1673,9 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
     (void)hipGetDevice(&dev);
     const int grid = kLeafVariants[v].one_tile ? (int)std::min<uint64_t>(slots / tile + 1, 0x7FFFFFFF)
                                                : batch_grid(dev, v);
-    void* args[] = {(void*)&blob,     (void*)&offs,          (void*)&lens,       (void*)&n,
-                    (void*)&ws.S,     (void*)&ws.tile_first, (void*)&ws.total,   (void*)&ws.cap_slots,
-                    (void*)&ws.nodes, (void*)&out32,         (void*)&out_keys,   (void*)&perm};
+    void* args[] = {(void*)&blob,     (void*)&offs,       (void*)&lens,     (void*)&n,
+                    (void*)&S,        (void*)&tile_first, (void*)&total,    (void*)&ws.cap_slots,
+                    (void*)&ws.nodes, (void*)&out32,      (void*)&out_keys, (void*)&perm};
     hipError_t le = hipLaunchKernel(kLeafVariants[v].fn, dim3(grid), dim3(kLeafVariants[v].wg), args, 0, st);
     if (le != hipSuccess) return le;
   }
@@ -1662,14 +1686,16 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
     hipLaunchKernelGGL(k_finish_t<kQTile>, dim3((uint32_t)((tiles + kFinishWG - 1) / kFinishWG)), dim3(kFinishWG), 0,
                        st, lens, n, ws.S, ws.tile_first, ws.total, ws.cap_slots, ws.nodes, perm, out32, out_keys);
 #endif
+  } else if (planned && !plan->crossing) {
+    // every message ended inside its tile: the leaf kernel wrote them all
   } else if (tile == kSmallTile) {
     const uint64_t tiles = slots / kSmallTile + 1;
     hipLaunchKernelGGL(k_finish_t<kSmallTile>, dim3((uint32_t)((tiles + kFinishWG - 1) / kFinishWG)), dim3(kFinishWG),
-                       0, st, lens, n, ws.S, ws.tile_first, ws.total, ws.cap_slots, ws.nodes, perm, out32, out_keys);
+                       0, st, lens, n, S, tile_first, total, ws.cap_slots, ws.nodes, perm, out32, out_keys);
   } else {
     const uint64_t tiles = slots / kTile + 1;
     hipLaunchKernelGGL(k_finish_t<kTile>, dim3((uint32_t)((tiles + kFinishWG - 1) / kFinishWG)), dim3(kFinishWG), 0,
-                       st, lens, n, ws.S, ws.tile_first, ws.total, ws.cap_slots, ws.nodes, perm, out32, out_keys);
+                       st, lens, n, S, tile_first, total, ws.cap_slots, ws.nodes, perm, out32, out_keys);
   }
   return hipGetLastError();
 }

@@ -157,7 +157,8 @@ struct sdcas_ctx {
   hipEvent_t scratch_ev = nullptr;
   hipStream_t scratch_st = nullptr;
   bool scratch_pending = false;
-  uint32_t upload_parts = 4;  // sdcas_cas_ids: a lone slot's reads and upload overlapped in this many parts (0/1: off)
+  uint32_t upload_parts = 4;
+  bool plan_small = true;  // small batches planned on the host (SDCAS_PLAN_SMALL=0: on the device)  // sdcas_cas_ids: a lone slot's reads and upload overlapped in this many parts (0/1: off)
 
   // progress / cancellation of the path APIs (sdcas_options, sdcas_set_progress)
   sdcas_progress_fn progress = nullptr;
@@ -260,17 +261,18 @@ int reserve_ws(sdcas_ctx* c, size_t max_msgs, uint64_t max_chunks) {
 // Enqueue the hash of n device messages (the one launch sequence every API
 // ends in), with optional HIP-event profiling of the leaf kernel.
 int launch_batch(sdcas_ctx* c, const uint8_t* blob, const uint64_t* offs, const uint64_t* lens, uint32_t n,
-                 uint8_t* out32, uint64_t* keys, hipStream_t st, uint64_t max_chunks = 0) {
+                 uint8_t* out32, uint64_t* keys, hipStream_t st, uint64_t max_chunks = 0,
+                 const BatchPlan* plan = nullptr) {
   hipError_t e;
   if (c->profile) {
     hipEvent_t a = c->event(), b = c->event(), la = c->event(), lb = c->event();
     (void)hipEventRecord(a, st);
-    e = batch_hash(c->ws, blob, offs, lens, n, out32, keys, st, max_chunks, la, lb);
+    e = batch_hash(c->ws, blob, offs, lens, n, out32, keys, st, max_chunks, la, lb, plan);
     (void)hipEventRecord(b, st);
     c->ev_all.push_back({a, b});
     c->ev_leaf.push_back({la, lb});
   } else {
-    e = batch_hash(c->ws, blob, offs, lens, n, out32, keys, st, max_chunks);
+    e = batch_hash(c->ws, blob, offs, lens, n, out32, keys, st, max_chunks, nullptr, nullptr, plan);
   }
   if (e) return c->hip_fail(e, "batch_hash");
   return SDCAS_OK;
@@ -379,17 +381,38 @@ int slot_submit(sdcas_ctx* c, Slot& s, bool res32) {
   const bool packed = 2 * s.n <= s.cap_n;
   if (packed) memcpy(s.hm + s.n, s.lens(), 8 * s.n);
   const uint64_t* d_lens = s.d_meta.p + (packed ? s.n : s.cap_n);
+  // A batch for the small kernel in caller order is planned here and its
+  // plan goes up behind the lengths in the same copy: the scan, k_tile_first
+  // and (when no message crosses a tile) k_finish_t are not launched.
+  uint64_t meta_words = packed ? 2 * s.n : s.n;
+  BatchPlan plan;
+  const uint64_t plan_tiles = s.chunks / kSmallTile + 2;
+  const uint64_t plan_words = s.n + (plan_tiles + 1) / 2 + 4;
+  const bool use_plan = c->plan_small && packed && s.n < kSortMinMsgs && s.chunks <= c->ws.small_slots &&
+                        2 * s.n + plan_words <= s.cap_n;
+  if (use_plan) {
+    uint64_t* hS = s.hm + 2 * s.n;
+    uint32_t* htf = reinterpret_cast<uint32_t*>(hS + s.n);
+    uint64_t* htot = hS + s.n + (plan_tiles + 1) / 2;
+    batch_plan_host(s.lens(), (uint32_t)s.n, kSmallTile, c->ws.cap_slots, hS, htf, htot, &plan.crossing);
+    plan.S = s.d_meta.p + 2 * s.n;
+    plan.tile_first = reinterpret_cast<const uint32_t*>(plan.S + s.n);
+    plan.total = s.d_meta.p + 2 * s.n + s.n + (plan_tiles + 1) / 2;
+    plan.tile = kSmallTile;
+    meta_words = 2 * s.n + plan_words;
+  }
   if ((e = slot_upload(c, s, [&](hipStream_t cs) {
          hipError_t r;
          if ((!uploaded && (r = hipMemcpyAsync(s.d_blob.p, s.src ? s.src : s.h, s.used, hipMemcpyHostToDevice, cs))) ||
-             (r = hipMemcpyAsync(s.d_meta.p, s.hm, 8 * (packed ? 2 * s.n : s.n), hipMemcpyHostToDevice, cs)))
+             (r = hipMemcpyAsync(s.d_meta.p, s.hm, 8 * meta_words, hipMemcpyHostToDevice, cs)))
            return r;
          return packed ? hipSuccess
                        : hipMemcpyAsync(s.d_meta.p + s.cap_n, s.hm + s.cap_n, 8 * s.n, hipMemcpyHostToDevice, cs);
        })))
     return c->hip_fail(e, "H2D");
   if ((rc = launch_batch(c, s.d_blob.p, s.d_meta.p, d_lens, (uint32_t)s.n, res32 ? s.d_res.p : nullptr,
-                         res32 ? nullptr : reinterpret_cast<uint64_t*>(s.d_res.p), st, s.chunks)))
+                         res32 ? nullptr : reinterpret_cast<uint64_t*>(s.d_res.p), st, s.chunks,
+                         use_plan ? &plan : nullptr)))
     return rc;
   if ((e = hipMemcpyAsync(s.res(), s.d_res.p, (res32 ? 32 : 8) * s.n, hipMemcpyDeviceToHost, st)) ||
       (e = hipEventRecord(s.ev, st)))
@@ -607,6 +630,7 @@ int sdcas_init(const sdcas_options* opts, sdcas_ctx** out) {
   if (const char* e = getenv("SDCAS_SMALL_SLOTS")) c->ws.small_slots = strtoull(e, nullptr, 0);
   if (const char* e = getenv("SDCAS_SMALL_VARIANT")) c->ws.small_variant = atoi(e);
   if (const char* e = getenv("SDCAS_UPLOAD_PARTS")) c->upload_parts = (uint32_t)std::min(atoi(e) > 0 ? atoi(e) : 0, 16);
+  if (const char* e = getenv("SDCAS_PLAN_SMALL")) c->plan_small = atoi(e) != 0;
   c->device = dev;
   if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess) {

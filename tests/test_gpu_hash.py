@@ -332,6 +332,31 @@ def test_small_and_big_batch_kernels(oracle):
         assert not bad, (reserve, bad[:10])
 
 
+def test_host_planned_small_batches(oracle, monkeypatch):
+    """a staging-path batch of fewer than kSortMinMsgs messages for the small
+    kernel is planned on the host (b3_batch.h BatchPlan: no scan, no
+    k_tile_first, no k_finish_t when no message crosses a 128-slot tile):
+    batches of 1-127 messages with empty, one-block, whole-chunk, 128-chunk
+    and tile-crossing lengths give the oracle's digests, planned and with the
+    plan turned off (SDCAS_PLAN_SMALL=0)"""
+    from spacedrive_amd import Engine
+    rng = np.random.default_rng(128)
+    special = [0, 1, 63, 64, 65, 1023, 1024, 1025, 2048, 127 * 1024, 128 * 1024 - 1, 128 * 1024, 128 * 1024 + 1,
+               129 * 1024 + 7, 300 * 1024 + 5]
+    batches = [[L] for L in special]
+    for n in (2, 3, 7, 40, 100, 127):
+        batches.append([int(x) for x in rng.choice(special, n // 3)] +
+                       [int(x) for x in rng.integers(0, 140 * 1024, n - n // 3)])
+    for env in ("1", "0"):
+        monkeypatch.setenv("SDCAS_PLAN_SMALL", env)
+        with Engine(staging_bytes=16 << 20) as e:
+            for lens in batches:
+                msgs = [rng.integers(0, 256, L, dtype=np.uint8).tobytes() for L in lens]
+                out = e.hash_messages(*e.pack(msgs))
+                bad = [len(m) for m, d in zip(msgs, out) if bytes(d).hex() != oracle.hash(m)]
+                assert not bad, (env, len(lens), bad[:10])
+
+
 def _c2_raw(seed, idx):
     from tests._oracle import mix64
     with np.errstate(over="ignore"):
