@@ -1105,6 +1105,8 @@ __global__ void __launch_bounds__(kWG, MINW) k_piece_l4(const uint8_t* __restric
 // group's array, so the in-place levels never cross pieces. Pieces of fewer
 // than kTile chunks have no l4 entries and no result here.
 constexpr uint32_t kTopPieces = kWG / (kTile >> kPieceDeferLevel);
+static_assert(kTopPieces * (kTile >> kPieceDeferLevel) == kWG, "k_piece_top: one thread per level-4 node");
+static_assert(kPieceDeferLevel < 10 && (kTile >> kPieceDeferLevel) <= kWG, "a piece's level-4 nodes fit one workgroup");
 template <int PF>
 __global__ void __launch_bounds__(kWG) k_piece_top(const PieceDesc* __restrict__ pieces, uint32_t npieces,
                                                    const uint32_t* __restrict__ l4, uint32_t* __restrict__ file_nodes) {
