@@ -396,6 +396,76 @@ def e2e_c3(args, eng, torch, dev, d_blob, offs, lens, sizes, gpu_keys):
     return out
 
 
+def e2e_c4(args, torch, dev, blob, sizes, win, out32, local):
+    """End-to-end C4 (file_checksum, hash.rs:11-25) on a bounded sample of the
+    corpus (the first whole files of the resident window up to --c4-e2e-gib),
+    timed outside the on-device passes (never `value`):
+      messages_pinned  sdcas_hash_messages from a page-locked host buffer
+                       (the files' bytes DMA'd slot by slot, 1 MiB pieces)
+      files            sdcas_checksums over the same files written to TMPDIR
+                       and read back from the page cache (1 MiB pieces read in
+                       parallel by the library's I/O threads)
+    Digests are compared with the resident passes' out32."""
+    import shutil
+    import tempfile
+    from spacedrive_amd import Engine
+    pick, acc = [], 0
+    for f, moff, ln, boff in win:
+        if moff != 0 or ln != int(sizes[f]):
+            continue
+        if acc and acc + ln > (int(args.c4_e2e_gib) << 30):
+            break
+        pick.append((f, boff, ln))
+        acc += ln
+    if not pick:
+        return None
+    lens = np.array([ln for _, _, ln in pick], np.uint64)
+    offs = np.zeros(len(pick), np.uint64)
+    offs[1:] = np.cumsum((lens[:-1] + np.uint64(4095)) // np.uint64(4096) * np.uint64(4096))
+    total = int(offs[-1] + lens[-1])
+    pin = torch.empty(total + 4096, dtype=torch.uint8).pin_memory()
+    for (f, boff, ln), ho in zip(pick, offs):
+        pin[int(ho):int(ho) + ln].copy_(blob[boff:boff + ln])
+    torch.cuda.synchronize()
+    host = pin.numpy()
+    want = out32.cpu().numpy()[[local[f] for f, _, _ in pick]]
+    out = {"workload": f"C4 files {[f for f, _, _ in pick]} ({len(pick)} files, {acc / 2**30:.2f} GiB)",
+           "files": len(pick), "bytes": acc, "io_threads": args.cpu_threads, "staging_bytes_per_slot": 256 << 20}
+    with Engine(device=dev.index, io_threads=args.cpu_threads, staging_bytes=256 << 20) as e:
+        best, got = None, None
+        for _ in range(2):
+            t0 = time.perf_counter()
+            got = e.hash_messages(host, offs, lens)
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        out["messages_pinned"] = {"gbps": acc / best / 1e9, "seconds": best,
+                                  "mismatches": int((got != want).any(axis=1).sum())}
+        del host, pin
+        if args.no_faithful:
+            return out
+        root = tempfile.mkdtemp(prefix="sdcas_e2e_c4_", dir=os.environ.get("TMPDIR", "/tmp"))
+        try:
+            paths = []
+            t0 = time.perf_counter()
+            for f, boff, ln in pick:
+                p = os.path.join(root, f"c4_{f:03d}")
+                blob[boff:boff + ln].cpu().numpy().tofile(p)
+                paths.append(p)
+            out["files_written_s"] = time.perf_counter() - t0
+            best = None
+            for _ in range(2):
+                t0 = time.perf_counter()
+                got, st = e.file_checksums(paths)
+                dt = time.perf_counter() - t0
+                best = dt if best is None else min(best, dt)
+            out["files"] = {"gbps": acc / best / 1e9, "seconds": best,
+                            "mismatches": int((got != want).any(axis=1).sum()), "errors": int((st != 0).sum()),
+                            "storage": "page cache (files just written)"}
+        finally:
+            shutil.rmtree(root, ignore_errors=True)
+    return out
+
+
 def c4_assign(sizes, world):
     """largest-first greedy assignment of files to ranks"""
     load = [0] * world
@@ -623,6 +693,8 @@ def run_c4(args, torch, dist, dev, rank, world, distributed, out_f):
         checked, bad = sum_over_ranks(torch, dist, dev, [checked, bad])
         out["parity"].update({"checked_files": checked, "mismatches": bad, "ranks": world,
                               "sample": "each rank: its smallest file, whole-file checksum vs the oracle"})
+    if rank == 0 and world == 1 and resident and split == "files" and not args.no_e2e:
+        out["e2e"] = e2e_c4(args, torch, dev, blob, sizes, wins[0], out32, local)
     if args.c4_full_parity:
         # every file this rank holds a digest of, against the oracle's
         # checksum of the same synthetic content (scalar restatement, one
@@ -663,7 +735,84 @@ def emit(out_f, obj):
     out_f.flush()
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv, script=None):
+    """`bench.py --gpus N` started without a launcher (no WORLD_SIZE in the
+    environment): start N rank processes of this same script, one per GPU,
+    with the torchrun environment (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_*),
+    and return the worst exit status. This parent never touches the GPU (it
+    has not imported torch); rank 0's JSON line reaches stdout through the
+    inherited descriptor. If a rank fails, the others are stopped."""
+    import signal
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=os.environ.get("MASTER_PORT") or str(_free_port()))
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    procs = []
+    for r in range(n):
+        e = dict(env, RANK=str(r), LOCAL_RANK=str(r), GROUP_RANK="0")
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + argv, env=e))
+
+    def stop(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+    old = {s: signal.signal(s, lambda sig, fr: (stop(), sys.exit(128 + sig))) for s in (signal.SIGTERM, signal.SIGINT)}
+    worst = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                rc = p.poll()
+                if rc is None:
+                    continue
+                live.remove(p)
+                if rc != 0:
+                    worst = worst or (rc if rc > 0 else 128 - rc)
+                    print(f"bench.py: rank {procs.index(p)} exited with {rc}; stopping the other ranks",
+                          file=sys.stderr)
+                    stop()
+            time.sleep(0.05)
+        for p in procs:
+            p.wait(timeout=60)
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
+    return worst
+
+
+def check_world(gpus, env):
+    """The launch must agree with --gpus: None when this process is a rank of
+    an N = --gpus job (or the one process of N = 1), 'spawn' when bench.py
+    must start the ranks itself, else the error to exit with."""
+    ws = env.get("WORLD_SIZE")
+    if gpus < 1:
+        return f"--gpus must be >= 1 (got {gpus})"
+    if ws is None:
+        return "spawn" if gpus > 1 else None
+    if int(ws) != gpus:
+        return f"--gpus {gpus} but WORLD_SIZE={ws}: the launch and the flag disagree"
+    return None
+
+
 def main():
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("--gpus", type=int, default=1)
+    known, _ = pre.parse_known_args()
+    how = check_world(known.gpus, os.environ)
+    if how == "spawn":
+        sys.exit(launch_ranks(known.gpus, sys.argv[1:]))
+    if how is not None:
+        print(f"bench.py: {how}", file=sys.stderr)
+        sys.exit(2)
     out_f = _json_stdout()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -677,6 +826,7 @@ def main():
     ap.add_argument("--c4-total-gib", type=int, default=256)
     ap.add_argument("--window-gib", type=int, default=0, help="c4: HBM window (0: the whole share when it fits)")
     ap.add_argument("--c4-cpu-gib", type=int, default=16, help="C4 CPU-baseline sample size")
+    ap.add_argument("--c4-e2e-gib", type=int, default=8, help="C4 end-to-end sample size (pinned buffer, files)")
     ap.add_argument("--e2e-files", type=int, default=200_000, help="c2: files in the end-to-end / faithful leg")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-faithful", action="store_true", help="e2e without the page-cache files legs")

@@ -334,6 +334,13 @@ int sdcas_dev_dedup_plan(sdcas_ctx *ctx, const uint64_t *d_stays, size_t n_stays
 int sdcas_dev_dedup_combine(sdcas_ctx *ctx, const uint64_t *d_keys, const uint8_t *d_has_key,
                             const int32_t *d_status, const uint64_t *d_ids, size_t n, uint32_t world,
                             uint64_t *d_rec, uint32_t *d_slot, uint64_t *out_starts, void *stream);
+/* combine without the host synchronisation: the owner ranges go to
+ * d_starts[0..world] (device u32) instead of out_starts, so that a caller
+ * driving several GPUs enqueues every GPU's combine before it reads any
+ * (sdcas_node_dedup_window) */
+int sdcas_dev_dedup_combine_async(sdcas_ctx *ctx, const uint64_t *d_keys, const uint8_t *d_has_key,
+                                  const int32_t *d_status, const uint64_t *d_ids, size_t n, uint32_t world,
+                                  uint64_t *d_rec, uint32_t *d_slot, uint32_t *d_starts, void *stream);
 int sdcas_dev_dedup_resolve(sdcas_ctx *ctx, const uint64_t *d_frec, size_t nf, const uint64_t *d_erec,
                             size_t ne, int64_t *d_result, void *stream);
 int sdcas_dev_dedup_apply(sdcas_ctx *ctx, const uint64_t *d_ids, const uint32_t *d_slot, size_t n,
@@ -375,10 +382,11 @@ int sdcas_dev_dedup_local(sdcas_ctx *ctx, const uint64_t *d_keys, const uint8_t 
  * sd-core is one process (Node::new, apps/server/src/main.rs:40; jobs run
  * in-process, job/manager.rs:32). A node is one context per entry of
  * `devices` (a device may repeat: two contexts on one GPU), with the batch
- * calls sharded over them and the dedup's exchange run in this process —
- * RCCL (ncclCommInitAll, grouped ncclSend / ncclRecv) when every device is
- * distinct, device-to-device copies otherwise (or with the environment
- * variable SDCAS_NODE_EXCHANGE=copy). Results are those of the single-context
+ * calls sharded over them and the dedup's exchange run in this process as
+ * device-to-device copies (hipMemcpyPeerAsync; over xGMI between distinct
+ * GPUs), or over RCCL (ncclCommInitAll, grouped ncclSend / ncclRecv) when every
+ * device is distinct and the environment sets SDCAS_NODE_EXCHANGE=rccl (opt-in
+ * until measured on a multi-GPU box). Results are those of the single-context
  * calls. opts (may be NULL) applies to every context; its progress function
  * receives the node's sums and may run on any of the node's threads (one at a
  * time). Calls on one node serialise. */

@@ -37,7 +37,8 @@ ABI_SYMBOLS = [
     "sdcas_checksums", "sdcas_hash_messages", "sdcas_cas_ids_from_messages", "sdcas_dev_reserve",
     "sdcas_dev_hash_messages", "sdcas_dev_sync", "sdcas_dedup", "sdcas_dedup_window", "sdcas_job_plan",
     "sdcas_key_to_hex",
-    "sdcas_digest_to_hex", "sdcas_cas_message_len", "sdcas_dev_dedup_combine", "sdcas_dev_dedup_resolve",
+    "sdcas_digest_to_hex", "sdcas_cas_message_len", "sdcas_dev_dedup_combine", "sdcas_dev_dedup_combine_async",
+    "sdcas_dev_dedup_resolve",
     "sdcas_dev_dedup_apply", "sdcas_dev_dedup_local", "sdcas_dev_dedup_combine_buckets",
     "sdcas_dev_dedup_resolve_buckets", "sdcas_dev_dedup_stays", "sdcas_dev_dedup_plan", "sdcas_dev_stream_begin", "sdcas_dev_stream_update",
     "sdcas_dev_stream_finish", "sdcas_dev_stream_node_bytes", "sdcas_dev_stream_export", "sdcas_dev_stream_import",
@@ -159,6 +160,7 @@ def load():
                                                   _vp, _vp, _vp]
     L.sdcas_dev_dedup_resolve_buckets.argtypes = [_vp, _vp, _sz, _vp, _vp, _sz, _vp, ctypes.c_uint32, _vp, _vp]
     L.sdcas_dev_dedup_combine.argtypes = [_vp, _vp, _vp, _vp, _vp, _sz, ctypes.c_uint32, _vp, _vp, _vp, _vp]
+    L.sdcas_dev_dedup_combine_async.argtypes = [_vp, _vp, _vp, _vp, _vp, _sz, ctypes.c_uint32, _vp, _vp, _vp, _vp]
     L.sdcas_dev_dedup_resolve.argtypes = [_vp, _vp, _sz, _vp, _sz, _vp, _vp]
     L.sdcas_dev_dedup_apply.argtypes = [_vp, _vp, _vp, _sz, _vp, _sz, _vp, _vp, _vp, _vp]
     L.sdcas_dev_dedup_local.argtypes = [_vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp, _sz, _sz, _u64, _u64,

@@ -94,6 +94,17 @@ struct PieceDesc {
   uint32_t len;        // bytes (<= 1 MiB; < 1 MiB only for a file's last piece)
   uint32_t pad;
 };
+// A segment of a device-resident stream update (sdcas_dev_stream_update): a
+// run of whole 1 MiB pieces of one message, expanded into PieceDescs on the
+// device (expand_pieces) so that the host never builds or uploads the
+// per-piece list.
+struct SegDesc {
+  uint64_t off;          // byte offset of the segment in the blob
+  uint64_t j0;           // first chunk index (multiple of kTile)
+  uint64_t node_base;    // message's first entry in the node list
+  uint64_t len;          // bytes (a multiple of 1 MiB unless the segment ends the message)
+  uint64_t piece_first;  // index of the segment's first piece in the update (exclusive scan)
+};
 struct FileDesc {
   uint64_t C;          // file chunk count (> kTile)
   uint64_t node_base;  // first entry in the file-node list (Q + popcount(C mod kTile) entries)
@@ -112,6 +123,8 @@ constexpr uint64_t kPieceL4Words = 8ull * (kTile >> kPieceDeferLevel);
 // variant: piece kernel variant (-1: default / SDCAS_PIECE_VARIANT)
 hipError_t piece_hash(const uint8_t* blob, const PieceDesc* pieces, uint32_t npieces, uint32_t* file_nodes,
                       uint32_t* ctr, uint32_t* l4, int variant, hipStream_t st);
+// pieces[piece_first(k) ..] of every segment k; one thread per piece
+hipError_t expand_pieces(const SegDesc* segs, uint32_t nseg, PieceDesc* pieces, uint32_t npieces, hipStream_t st);
 hipError_t bigfile_finish(const FileDesc* files, uint32_t nfiles, const uint32_t* file_nodes, uint8_t* out32,
                           hipStream_t st);
 

@@ -105,6 +105,14 @@ hipError_t dd_combine(DistWs& w, const uint64_t* keys, const uint8_t* has_key, c
                       const uint64_t* ids, uint32_t n, uint32_t world, uint64_t* rec, uint32_t* slot,
                       uint64_t* h_starts, uint64_t* h_u, hipStream_t st);
 
+// Stage 1 with the owner ranges left on the device: starts[0..world] (u32,
+// device) instead of the host copy, no host synchronisation, so that a
+// process driving several GPUs enqueues every GPU's combine before it waits
+// for any (sdcas_node_dedup_window).
+hipError_t dd_combine_dev(DistWs& w, const uint64_t* keys, const uint8_t* has_key, const int32_t* status,
+                          const uint64_t* ids, uint32_t n, uint32_t world, uint64_t* rec, uint32_t* slot,
+                          uint32_t* d_starts, hipStream_t st);
+
 // Stage 1 into fixed-capacity owner buckets, without a host synchronisation:
 // send[(r * cap + p) * 2 ..] = record p of owner r (p < counts[r] <= cap),
 // counts[world] (device int64), slot[i] = bucket position r * cap + p of file

@@ -415,6 +415,16 @@ hipError_t dd_combine(DistWs& w, const uint64_t* keys, const uint8_t* has_key, c
   return hipGetLastError();
 }
 
+hipError_t dd_combine_dev(DistWs& w, const uint64_t* keys, const uint8_t* has_key, const int32_t* status,
+                          const uint64_t* ids, uint32_t n, uint32_t world, uint64_t* rec, uint32_t* slot,
+                          uint32_t* d_starts, hipStream_t st) {
+  if (n == 0) return hipMemsetAsync(d_starts, 0, sizeof(uint32_t) * (world + 1), st);
+  hipError_t e;
+  if ((e = combine_core(w, keys, has_key, status, ids, n, world, rec, slot, st))) return e;
+  // w.starts is the context's scratch: the next combine on it rewrites it
+  return hipMemcpyAsync(d_starts, w.starts.p, sizeof(uint32_t) * (world + 1), hipMemcpyDeviceToDevice, st);
+}
+
 // ---- the combine into fixed-capacity owner buckets (no host sync) ---------------
 //
 // RCCL's all-to-all through torch needs every split size on the host, i.e.

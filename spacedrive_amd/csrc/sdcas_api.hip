@@ -99,6 +99,49 @@ struct Slot {
   uint8_t* res() { return reinterpret_cast<uint8_t*>(hm + 2 * cap_n); }
 };
 
+// Small host arrays (the device stream's message and segment descriptors)
+// sent to the device in stream order without a host wait: each put copies
+// into the next of kN page-locked buffers and enqueues the upload from it; a
+// buffer is reused only after the event recorded behind its last upload.
+struct HostStage {
+  static constexpr int kN = 4;
+  uint8_t* h[kN] = {};
+  size_t cap[kN] = {};
+  hipEvent_t ev[kN] = {};
+  bool recorded[kN] = {};
+  int next = 0;
+  hipError_t put(const void* src, size_t bytes, void* d_dst, hipStream_t st) {
+    if (!bytes) return hipSuccess;
+    const int i = next;
+    next = (next + 1) % kN;
+    hipError_t e;
+    if (recorded[i] && (e = hipEventSynchronize(ev[i]))) return e;
+    recorded[i] = false;
+    if (bytes > cap[i]) {
+      if (h[i]) (void)hipHostFree(h[i]);
+      h[i] = nullptr;
+      cap[i] = 0;
+      const size_t want = std::max<size_t>(bytes + bytes / 4, 64 << 10);
+      if ((e = hipHostMalloc(&h[i], want, hipHostMallocDefault))) return e;
+      cap[i] = want;
+    }
+    if (!ev[i] && (e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming))) return e;
+    memcpy(h[i], src, bytes);
+    if ((e = hipMemcpyAsync(d_dst, h[i], bytes, hipMemcpyHostToDevice, st))) return e;
+    if ((e = hipEventRecord(ev[i], st))) return e;
+    recorded[i] = true;
+    return hipSuccess;
+  }
+  void release() {
+    for (int i = 0; i < kN; ++i) {
+      if (recorded[i]) (void)hipEventSynchronize(ev[i]);
+      if (ev[i]) (void)hipEventDestroy(ev[i]);
+      if (h[i]) (void)hipHostFree(h[i]);
+      h[i] = nullptr, ev[i] = nullptr, cap[i] = 0, recorded[i] = false;
+    }
+  }
+};
+
 }  // namespace
 
 struct sdcas_ctx {
@@ -142,7 +185,10 @@ struct sdcas_ctx {
   DevBuf<FileDesc> sm_d_files;
   DevBuf<uint32_t> sm_nodes;
   DevBuf<PieceDesc> sm_pieces;
+  DevBuf<SegDesc> sm_segs;
+  HostStage sm_stage;             // descriptor uploads without a host wait
   bool sm_active = false;
+  bool sm_begin_pending = false;  // stream_begin's descriptor upload and node-list clear, enqueued by the next call
   uint64_t sm_node_bytes = 0;
   DevBuf<uint32_t> piece_ctr;  // the persistent piece kernels' work counter
   DevBuf<uint32_t> piece_l4;   // piece variant 19's level-4 nodes (kPieceL4Words per piece)
@@ -157,8 +203,8 @@ struct sdcas_ctx {
   hipEvent_t scratch_ev = nullptr;
   hipStream_t scratch_st = nullptr;
   bool scratch_pending = false;
-  uint32_t upload_parts = 4;
-  bool plan_small = true;  // small batches planned on the host (SDCAS_PLAN_SMALL=0: on the device)  // sdcas_cas_ids: a lone slot's reads and upload overlapped in this many parts (0/1: off)
+  uint32_t upload_parts = 4;  // sdcas_cas_ids: a lone slot's reads and upload overlapped in this many parts (0/1: off)
+  bool plan_small = true;      // small batches planned on the host (SDCAS_PLAN_SMALL=0: on the device)
 
   // progress / cancellation of the path APIs (sdcas_options, sdcas_set_progress)
   sdcas_progress_fn progress = nullptr;
@@ -661,6 +707,8 @@ void sdcas_destroy(sdcas_ctx* c) {
   c->sm_d_files.release();
   c->sm_nodes.release();
   c->sm_pieces.release();
+  c->sm_segs.release();
+  c->sm_stage.release();
   for (Slot& s : c->slots) slot_release(s);
   for (auto e : c->ev_free) (void)hipEventDestroy(e);
   for (auto& p : c->ev_leaf) (void)hipEventDestroy(p.first), (void)hipEventDestroy(p.second);
@@ -1111,9 +1159,12 @@ int sdcas_cas_ids(sdcas_ctx* c, const char* const* paths, const uint64_t* sizes,
       // the next slot's reads already overlap this one's upload and kernels,
       // and the parts measured slower there, profiles/r03_small_calls.json)
       const uint32_t parts = c->upload_parts;
-      s.blob_uploaded = parts > 1 && !other.busy && p == 0 && q == todo.size() && round == 0 &&
-                        used >= kUploadSplitMin && m >= parts;
-      if (s.blob_uploaded) {
+      // the flag is set only once every part is enqueued: a failed part
+      // returns with it clear, so no later submit of this slot skips an upload
+      s.blob_uploaded = false;
+      const bool in_parts = parts > 1 && !other.busy && p == 0 && q == todo.size() && round == 0 &&
+                            used >= kUploadSplitMin && m >= parts;
+      if (in_parts) {
         size_t k0 = 0;
         for (uint32_t part = 1; part <= parts && k0 < m; ++part) {
           size_t k1 = k0 + 1;
@@ -1125,6 +1176,7 @@ int sdcas_cas_ids(sdcas_ctx* c, const char* const* paths, const uint64_t* sizes,
           if (e) return c->hip_fail(e, "H2D part");
           k0 = k1;
         }
+        s.blob_uploaded = true;
       } else {
         read_files(0, m);
       }
@@ -1431,6 +1483,18 @@ int sdcas_dev_dedup_combine(sdcas_ctx* c, const uint64_t* d_keys, const uint8_t*
   return e ? c->hip_fail(e, "dedup_combine") : SDCAS_OK;
 }
 
+int sdcas_dev_dedup_combine_async(sdcas_ctx* c, const uint64_t* d_keys, const uint8_t* d_has_key,
+                                  const int32_t* d_status, const uint64_t* d_ids, size_t n, uint32_t world,
+                                  uint64_t* d_rec, uint32_t* d_slot, uint32_t* d_starts, void* stream) {
+  if (!c || world == 0 || !d_starts || (n && (!d_keys || !d_ids || !d_rec))) return SDCAS_E_INVALID;
+  if (n > SDCAS_MAX_BATCH) return c->fail(SDCAS_E_CAPACITY, "dedup_combine: %zu records exceed 2^31 - 1", n);
+  DevCall call(c, stream);
+  if (call.rc) return call.rc;
+  hipError_t e = dd_combine_dev(c->dist, d_keys, d_has_key, d_status, d_ids, (uint32_t)n, world, d_rec, d_slot,
+                                d_starts, call.st);
+  return e ? c->hip_fail(e, "dedup_combine_async") : SDCAS_OK;
+}
+
 int sdcas_dev_dedup_combine_buckets(sdcas_ctx* c, const uint64_t* d_keys, const uint8_t* d_has_key,
                                     const int32_t* d_status, const uint64_t* d_ids, size_t n, uint32_t world,
                                     size_t cap, uint64_t* d_send, uint32_t* d_slot, int64_t* d_counts,
@@ -1530,39 +1594,63 @@ int sdcas_dev_dedup_apply(sdcas_ctx* c, const uint64_t* d_ids, const uint32_t* d
 
 // ---- device-resident big-message stream (C4, file_checksum of huge files) --------
 
+// A device buffer about to grow is freed and reallocated: the context's
+// enqueued work (any stream) must be done with it first. Growth happens on a
+// session larger than every earlier one, so the steady state never waits.
+}  // extern "C"
+template <typename T>
+static hipError_t grow(sdcas_ctx* c, DevBuf<T>& b, size_t n, hipStream_t st = nullptr) {
+  if (n <= b.cap) return hipSuccess;
+  hipError_t e;
+  if (st && (e = hipStreamSynchronize(st))) return e;
+  if (c->scratch_pending && (e = hipEventSynchronize(c->scratch_ev))) return e;
+  return b.ensure(n);
+}
+extern "C" {
+
+// The session's message descriptors go up and its node list is cleared on
+// the stream of the session's first device call (stream_begin names none):
+// no host wait, ordered after the previous session's kernels by the fence.
+static hipError_t stream_flush_begin(sdcas_ctx* c, hipStream_t st) {
+  if (!c->sm_begin_pending) return hipSuccess;
+  c->sm_begin_pending = false;
+  hipError_t e;
+  if (!c->sm_files.empty() &&
+      (e = c->sm_stage.put(c->sm_files.data(), sizeof(FileDesc) * c->sm_files.size(), c->sm_d_files.p, st)))
+    return e;
+  // node entries no segment of this session writes stay zero, so that the
+  // node lists of ranks that hashed disjoint pieces of the same messages add
+  // up to the complete list (sdcas_dev_stream_import)
+  if (c->sm_node_bytes && (e = hipMemsetAsync(c->sm_nodes.p, 0, c->sm_node_bytes, st))) return e;
+  return hipSuccess;
+}
+
 int sdcas_dev_stream_begin(sdcas_ctx* c, const uint64_t* lens, size_t nfiles) {
   if (!c || (nfiles && !lens)) return SDCAS_E_INVALID;
   std::lock_guard<std::mutex> g(c->mu);
   (void)hipSetDevice(c->device);
-  // the session's descriptors and node list are rewritten below: the previous
-  // session's kernels must be done with them
-  if (c->scratch_pending) {
-    hipError_t e = hipEventSynchronize(c->scratch_ev);
-    if (e) return c->hip_fail(e, "sync");
-  }
-  c->sm_files.assign(nfiles, FileDesc{});
+  std::vector<FileDesc> files(nfiles, FileDesc{});
   uint64_t nodes = 0;
   for (size_t i = 0; i < nfiles; ++i) {
     const uint64_t C = chunks_of(lens[i]);
     if (C <= kTile) return c->fail(SDCAS_E_INVALID, "stream message %zu: %llu bytes (must exceed 1 MiB)", i,
                                    (unsigned long long)lens[i]);
-    c->sm_files[i].C = C;
-    c->sm_files[i].node_base = nodes;
-    c->sm_files[i].out_index = i;
+    files[i].C = C;
+    files[i].node_base = nodes;
+    files[i].out_index = i;
     nodes += bigfile_node_count(C);
   }
+  // the descriptors and node list are rewritten in stream order by the
+  // session's first device call (stream_flush_begin); only a buffer that must
+  // grow waits for the previous session here
   hipError_t e;
-  if ((e = c->sm_nodes.ensure(8 * nodes + 8)) || (e = c->sm_d_files.ensure(nfiles + 1)) || (e = c->piece_ctr.ensure(1)))
+  if ((e = grow(c, c->sm_nodes, 8 * nodes + 8)) || (e = grow(c, c->sm_d_files, nfiles + 1)) ||
+      (e = grow(c, c->piece_ctr, 1)))
     return c->hip_fail(e, "stream workspace");
-  if (nfiles && (e = hipMemcpy(c->sm_d_files.p, c->sm_files.data(), sizeof(FileDesc) * nfiles,
-                               hipMemcpyHostToDevice)))
-    return c->hip_fail(e, "stream descs");
-  // node entries no segment of this session writes stay zero, so that the
-  // node lists of ranks that hashed disjoint pieces of the same messages add
-  // up to the complete list (sdcas_dev_stream_import)
+  c->sm_files.swap(files);
   c->sm_node_bytes = 32 * nodes;
-  if (nodes && (e = hipMemset(c->sm_nodes.p, 0, c->sm_node_bytes))) return c->hip_fail(e, "stream nodes");
   c->sm_active = true;
+  c->sm_begin_pending = true;
   return SDCAS_OK;
 }
 
@@ -1575,7 +1663,8 @@ int sdcas_dev_stream_export(sdcas_ctx* c, uint8_t* d_dst, size_t bytes, void* st
   if (!c->sm_active || bytes != c->sm_node_bytes)
     return c->fail(SDCAS_E_INVALID, "stream_export: %zu bytes, the session's node list holds %llu", bytes,
                    (unsigned long long)c->sm_node_bytes);
-  hipError_t e = bytes ? hipMemcpyAsync(d_dst, c->sm_nodes.p, bytes, hipMemcpyDeviceToDevice, call.st) : hipSuccess;
+  hipError_t e = stream_flush_begin(c, call.st);
+  if (!e && bytes) e = hipMemcpyAsync(d_dst, c->sm_nodes.p, bytes, hipMemcpyDeviceToDevice, call.st);
   return e ? c->hip_fail(e, "stream_export") : SDCAS_OK;
 }
 
@@ -1586,7 +1675,8 @@ int sdcas_dev_stream_import(sdcas_ctx* c, const uint8_t* d_src, size_t bytes, vo
   if (!c->sm_active || bytes != c->sm_node_bytes)
     return c->fail(SDCAS_E_INVALID, "stream_import: %zu bytes, the session's node list holds %llu", bytes,
                    (unsigned long long)c->sm_node_bytes);
-  hipError_t e = bytes ? hipMemcpyAsync(c->sm_nodes.p, d_src, bytes, hipMemcpyDeviceToDevice, call.st) : hipSuccess;
+  hipError_t e = stream_flush_begin(c, call.st);
+  if (!e && bytes) e = hipMemcpyAsync(c->sm_nodes.p, d_src, bytes, hipMemcpyDeviceToDevice, call.st);
   return e ? c->hip_fail(e, "stream_import") : SDCAS_OK;
 }
 
@@ -1599,7 +1689,10 @@ int sdcas_dev_stream_update(sdcas_ctx* c, size_t nseg, const uint64_t* h_file, c
   const uint64_t piece_bytes = 1024ull * kTile;
   uint64_t base = ~0ull;
   for (size_t k = 0; k < nseg; ++k) base = std::min(base, h_dev_addr[k]);
-  std::vector<PieceDesc> pieces;
+  // one descriptor per segment (the caller's few hundred); the device expands
+  // them into the per-piece list (expand_pieces)
+  std::vector<SegDesc> segs(nseg);
+  uint64_t npieces = 0;
   for (size_t k = 0; k < nseg; ++k) {
     if (h_file[k] >= c->sm_files.size()) return c->fail(SDCAS_E_INVALID, "segment %zu: no such message", k);
     const FileDesc& fd = c->sm_files[h_file[k]];
@@ -1608,34 +1701,30 @@ int sdcas_dev_stream_update(sdcas_ctx* c, size_t nseg, const uint64_t* h_file, c
     if ((off % piece_bytes) || (h_dev_addr[k] & 15) || !len || off + len > mlen ||
         ((len % piece_bytes) && chunks_of(off + len) != fd.C))
       return c->fail(SDCAS_E_INVALID, "segment %zu: offset/length not on 1 MiB pieces", k);
-    for (uint64_t o = 0; o < len; o += piece_bytes) {
-      PieceDesc pd{};
-      pd.off = h_dev_addr[k] - base + o;
-      pd.j0 = (off + o) / 1024;
-      pd.node_base = fd.node_base;
-      pd.len = (uint32_t)std::min<uint64_t>(piece_bytes, len - o);
-      pieces.push_back(pd);
-    }
+    segs[k] = SegDesc{h_dev_addr[k] - base, off / 1024, fd.node_base, len, npieces};
+    npieces += (len + piece_bytes - 1) / piece_bytes;
   }
-  if (pieces.empty()) return SDCAS_OK;
-  if (pieces.size() > SDCAS_MAX_BATCH) return c->fail(SDCAS_E_CAPACITY, "stream_update: %zu pieces", pieces.size());
   hipStream_t st = call.st;
-  hipError_t e;
-  if ((e = c->sm_pieces.ensure(pieces.size()))) return c->hip_fail(e, "piece descs");
-  if ((e = c->piece_l4.ensure(kPieceL4Words * pieces.size()))) return c->hip_fail(e, "piece level-4 nodes");
-  // stream-ordered: a previous update's kernel on `st` has finished reading
-  // the descriptor buffer before this copy lands
-  if ((e = hipMemcpyAsync(c->sm_pieces.p, pieces.data(), sizeof(PieceDesc) * pieces.size(), hipMemcpyHostToDevice,
-                          st)) ||
-      (e = hipStreamSynchronize(st)))
-    return c->hip_fail(e, "H2D piece descs");
+  hipError_t e = stream_flush_begin(c, st);
+  if (e) return c->hip_fail(e, "stream descs");
+  if (!npieces) return SDCAS_OK;
+  if (npieces > SDCAS_MAX_BATCH) return c->fail(SDCAS_E_CAPACITY, "stream_update: %llu pieces",
+                                                (unsigned long long)npieces);
+  // stream-ordered: a previous update's kernels on any stream are behind the
+  // fence, so the descriptor buffers are free once this call's work starts
+  if ((e = grow(c, c->sm_pieces, npieces, st)) || (e = grow(c, c->sm_segs, nseg, st)) ||
+      (e = grow(c, c->piece_l4, kPieceL4Words * npieces, st)))
+    return c->hip_fail(e, "piece descs");
+  if ((e = c->sm_stage.put(segs.data(), sizeof(SegDesc) * nseg, c->sm_segs.p, st)) ||
+      (e = expand_pieces(c->sm_segs.p, (uint32_t)nseg, c->sm_pieces.p, (uint32_t)npieces, st)))
+    return c->hip_fail(e, "piece descs");
   hipEvent_t a = nullptr, b = nullptr;
   if (c->profile) {
     a = c->event();
     b = c->event();
     (void)hipEventRecord(a, st);
   }
-  e = piece_hash(reinterpret_cast<const uint8_t*>(base), c->sm_pieces.p, (uint32_t)pieces.size(), c->sm_nodes.p,
+  e = piece_hash(reinterpret_cast<const uint8_t*>(base), c->sm_pieces.p, (uint32_t)npieces, c->sm_nodes.p,
                  c->piece_ctr.p, c->piece_l4.p, c->piece_variant, st);
   if (c->profile) {
     (void)hipEventRecord(b, st);
@@ -1653,8 +1742,10 @@ int sdcas_dev_stream_finish(sdcas_ctx* c, uint8_t* d_out32, void* stream) {
   if (call.rc) return call.rc;
   if (!c->sm_active) return c->fail(SDCAS_E_INVALID, "stream_finish without stream_begin");
   hipStream_t st = call.st;
+  hipError_t e = stream_flush_begin(c, st);
+  if (e) return c->hip_fail(e, "stream descs");
   c->sm_active = false;
-  hipError_t e = bigfile_finish(c->sm_d_files.p, (uint32_t)c->sm_files.size(), c->sm_nodes.p, d_out32, st);
+  e = bigfile_finish(c->sm_d_files.p, (uint32_t)c->sm_files.size(), c->sm_nodes.p, d_out32, st);
   return e ? c->hip_fail(e, "bigfile_finish") : SDCAS_OK;
 }
 

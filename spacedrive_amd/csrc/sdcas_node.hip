@@ -93,12 +93,15 @@ struct Rank {
   sdcas_ctx* ctx = nullptr;
   hipStream_t st = nullptr;
   hipEvent_t ev = nullptr;
+  hipEvent_t ev_starts = nullptr;  // the owner ranges are on the host
+  uint32_t* hstarts = nullptr;     // pinned: owner ranges of the files' and the existing Objects' records
+  size_t hstarts_cap = 0;
   // dedup shard: files [lo, hi) and existing Objects [elo, ehi) of the batch
   size_t lo = 0, hi = 0, elo = 0, ehi = 0;
   DBuf<uint64_t> keys, ids, ekeys, eids, rec, erec, frecv, erecv, stays, gstays, plan, counts;
   DBuf<uint8_t> has;
   DBuf<int32_t> status;
-  DBuf<uint32_t> slot;
+  DBuf<uint32_t> slot, dstarts;
   DBuf<int64_t> answer, back, link, scount;
   std::vector<uint64_t> starts, estarts;
   uint64_t done = 0, total = 0;  // progress of this rank's share of a path call
@@ -107,7 +110,11 @@ struct Rank {
     has.release();
     status.release();
     slot.release();
+    dstarts.release();
     for (auto* b : {&answer, &back, &link, &scount}) b->release();
+    if (hstarts) (void)hipHostFree(hstarts);
+    hstarts = nullptr;
+    hstarts_cap = 0;
   }
 };
 
@@ -223,7 +230,20 @@ int exchange(sdcas_node* n, const std::vector<Copy>& copies, const char* what) {
   return SDCAS_OK;
 }
 
+// SDCAS_NODE_TRACE=1: one stderr line per host wait of a node call (the
+// dedup waits once for the owner ranges and once for the results, whatever
+// the number of ranks)
+bool node_trace() {
+  const char* v = getenv("SDCAS_NODE_TRACE");
+  return v && *v && strcmp(v, "0") != 0;
+}
+
+void trace_wait(const sdcas_node* n, const char* phase) {
+  if (node_trace()) fprintf(stderr, "sdcas_node: host wait [%s] over %zu ranks\n", phase, n->ranks.size());
+}
+
 int sync_all(sdcas_node* n, const char* what) {
+  trace_wait(n, what);
   for (Rank& k : n->ranks) {
     (void)hipSetDevice(k.dev);
     hipError_t e = hipStreamSynchronize(k.st);
@@ -277,16 +297,20 @@ int sdcas_node_init(const int32_t* devices, size_t n_devices, const sdcas_option
     if (rc) break;
     (void)hipSetDevice(k.dev);
     if (hipStreamCreateWithFlags(&k.st, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&k.ev, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&k.ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&k.ev_starts, hipEventDisableTiming) != hipSuccess)
       rc = SDCAS_E_NO_DEVICE;
   }
-  // RCCL between distinct devices (it refuses two ranks on one device)
+  // The exchange is device-to-device copies (hipMemcpyPeerAsync: over xGMI
+  // between distinct GPUs, a local copy when a device repeats). RCCL between
+  // distinct devices is opt-in (SDCAS_NODE_EXCHANGE=rccl; it refuses two ranks
+  // on one device) until it has been run against the oracle on a multi-GPU box.
   std::vector<int> devs(devices, devices + n_devices);
   std::vector<int> sorted = devs;
   std::sort(sorted.begin(), sorted.end());
   const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
-  const char* mode = getenv("SDCAS_NODE_EXCHANGE");  // "copy": device copies even between distinct devices
-  if (rc == SDCAS_OK && distinct && n_devices > 1 && !(mode && !strcmp(mode, "copy")) && n->nccl.load()) {
+  const char* mode = getenv("SDCAS_NODE_EXCHANGE");
+  if (rc == SDCAS_OK && distinct && n_devices > 1 && mode && !strcmp(mode, "rccl") && n->nccl.load()) {
     n->comms.resize(n_devices);
     if (n->nccl.comm_init_all(n->comms.data(), (int)n_devices, devs.data()) == ncclSuccess) n->rccl = true;
     else n->comms.clear();
@@ -312,6 +336,7 @@ void sdcas_node_destroy(sdcas_node* n) {
     (void)hipSetDevice(k.dev);
     k.release();
     if (k.ev) (void)hipEventDestroy(k.ev);
+    if (k.ev_starts) (void)hipEventDestroy(k.ev_starts);
     if (k.st) (void)hipStreamDestroy(k.st);
     if (k.ctx) sdcas_destroy(k.ctx);
   }
@@ -479,19 +504,41 @@ int sdcas_node_dedup_window(sdcas_node* n, const uint64_t* keys, const uint8_t* 
         return n->ctx_fail(d, rc, "dedup_plan");
     }
   }
-  // combine (owner ranges to the host)
+  // combine: every rank's files and existing Objects are enqueued before any
+  // owner range is read, so the GPUs sort concurrently and the host waits
+  // once for the phase (the ranges size the exchange exactly)
   std::vector<std::vector<uint64_t>> fcnt(R, std::vector<uint64_t>(R, 0)), ecnt(R, std::vector<uint64_t>(R, 0));
   for (size_t r = 0; r < R; ++r) {
     Rank& k = n->ranks[r];
     const size_t m = k.hi - k.lo, me = k.ehi - k.elo;
-    k.starts.assign(R + 1, 0);
-    k.estarts.assign(R + 1, 0);
-    if (m && (rc = sdcas_dev_dedup_combine(k.ctx, k.keys.p, k.has.p, status ? k.status.p : nullptr, k.ids.p, m, world,
-                                           k.rec.p, k.slot.p, k.starts.data(), k.st)))
+    (void)hipSetDevice(k.dev);
+    if ((e = k.dstarts.ensure(2 * (R + 1)))) return n->hip_fail(e, "node dedup buffers");
+    if (k.hstarts_cap < 2 * (R + 1)) {
+      if (k.hstarts) (void)hipHostFree(k.hstarts);
+      k.hstarts = nullptr;
+      k.hstarts_cap = 0;
+      if ((e = hipHostMalloc(&k.hstarts, sizeof(uint32_t) * 2 * (R + 1), hipHostMallocDefault)))
+        return n->hip_fail(e, "node dedup pinned ranges");
+      k.hstarts_cap = 2 * (R + 1);
+    }
+    if ((rc = sdcas_dev_dedup_combine_async(k.ctx, k.keys.p, k.has.p, status ? k.status.p : nullptr, k.ids.p, m,
+                                            world, k.rec.p, k.slot.p, k.dstarts.p, k.st)))
       return n->ctx_fail(r, rc, "dedup_combine");
-    if (me && (rc = sdcas_dev_dedup_combine(k.ctx, k.ekeys.p, nullptr, nullptr, k.eids.p, me, world, k.erec.p, nullptr,
-                                            k.estarts.data(), k.st)))
+    if ((rc = sdcas_dev_dedup_combine_async(k.ctx, k.ekeys.p, nullptr, nullptr, k.eids.p, me, world, k.erec.p, nullptr,
+                                            k.dstarts.p + (R + 1), k.st)))
       return n->ctx_fail(r, rc, "dedup_combine (existing)");
+    (void)hipSetDevice(k.dev);
+    if ((e = hipMemcpyAsync(k.hstarts, k.dstarts.p, sizeof(uint32_t) * 2 * (R + 1), hipMemcpyDeviceToHost, k.st)) ||
+        (e = hipEventRecord(k.ev_starts, k.st)))
+      return n->hip_fail(e, "node dedup owner ranges");
+  }
+  trace_wait(n, "owner ranges");
+  for (size_t r = 0; r < R; ++r) {
+    Rank& k = n->ranks[r];
+    (void)hipSetDevice(k.dev);
+    if ((e = hipEventSynchronize(k.ev_starts))) return n->hip_fail(e, "node dedup owner ranges");
+    k.starts.assign(k.hstarts, k.hstarts + (R + 1));
+    k.estarts.assign(k.hstarts + (R + 1), k.hstarts + 2 * (R + 1));
     for (size_t d = 0; d < R; ++d) {
       fcnt[r][d] = k.starts[d + 1] - k.starts[d];
       ecnt[r][d] = k.estarts[d + 1] - k.estarts[d];
@@ -559,7 +606,7 @@ int sdcas_node_dedup_window(sdcas_node* n, const uint64_t* keys, const uint8_t* 
         (r == 0 && (e = hipMemcpyAsync(hdr, k.plan.p, sizeof hdr, hipMemcpyDeviceToHost, k.st))))
       return n->hip_fail(e, "node dedup D2H");
   }
-  if ((rc = sync_all(n, "node dedup sync"))) return rc;
+  if ((rc = sync_all(n, "results"))) return rc;
   int64_t created = 0, linked = 0;
   for (auto& c : cnt) created += (int64_t)c[0], linked += (int64_t)c[1];
   if (out_created) *out_created = created;

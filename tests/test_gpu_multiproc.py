@@ -245,23 +245,35 @@ def test_split_checksum_two_processes(oracle):
             assert bytes(got[i]).hex() == oracle.synth_checksum(k, n), n
 
 
+@pytest.mark.parametrize("launcher", ["torchrun", "plain"])
 @pytest.mark.parametrize("workload", ["c2", "c5", "c4"])
-def test_bench_two_ranks(workload):
-    """bench.py as the driver launches it at N > 1 (torch.distributed.run, one
-    process per rank), on the one GPU with gloo standing in for RCCL: the line
-    reports both ranks, every rank's oracle sample matches, and the c5 dedup
-    exchange gives the chunked oracle's links over both ranks' files"""
+def test_bench_two_ranks(workload, launcher):
+    """bench.py as the driver launches it at N > 1 — under
+    torch.distributed.run, or as a plain `python3 bench.py --gpus 2` that
+    starts its two ranks itself — on the one GPU with gloo standing in for
+    RCCL: ONE line that reports both ranks, every rank's oracle sample
+    matches, and the c5 dedup exchange gives the chunked oracle's links over
+    both ranks' files"""
     import json
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, SDCAS_BENCH_BACKEND="gloo", OMP_NUM_THREADS="4")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
-           "--workload", workload, "--files", "20000", "--steps", "2", "--warmup", "1", "--c4-total-gib", "4"]
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    args = ["bench.py", "--gpus", "2", "--workload", workload, "--files", "20000", "--steps", "2", "--warmup", "1",
+            "--c4-total-gib", "4"]
+    if launcher == "torchrun":
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + args
+    else:
+        cmd = [sys.executable] + args
     r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-3000:]
-    line = [l for l in r.stdout.splitlines() if '{"metric"' in l][-1]
+    lines = [l for l in r.stdout.splitlines() if '{"metric"' in l]
+    if launcher == "plain":
+        assert len(lines) == 1 and lines[0].startswith('{"metric"'), r.stdout[-2000:]
+    line = lines[-1]
     d = json.loads(line[line.index('{"metric"'):])  # torchrun may prefix a rank tag
     assert d["n_gpus"] == 2 and d["value"] > 0
     assert d["parity"]["ranks"] == 2 and d["parity"]["checked_files"] >= (2 if workload == "c4" else 2000)

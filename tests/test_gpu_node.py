@@ -2,8 +2,9 @@
 spacedrive_amd.Node) — sd-core is one process (apps/server/src/main.rs:40,
 job/manager.rs:32), so the multi-GPU paths must be reachable without a
 process per GPU. On this one-GPU box the node is [0, 0]: two contexts on one
-device, the exchange as device-to-device copies; between distinct devices
-the same calls exchange over RCCL (ncclCommInitAll), unmeasured here.
+device, the exchange as device-to-device copies — the default between
+distinct devices too (over xGMI); RCCL (ncclCommInitAll) is opt-in with
+SDCAS_NODE_EXCHANGE=rccl and unmeasured here.
 Everything against the oracle."""
 import numpy as np
 import pytest
@@ -42,6 +43,23 @@ def test_node_dedup_vs_oracle(node, oracle):
     got, gc, gl, gw = node.identifier_dedup_window(keys[:1], has[:1], status[:1], 100, existing[:3])
     want, wc, wl, ww = oracle.identifier_job(keys[:1], has[:1], status[:1], 100, existing[:3])
     assert np.array_equal(got, want) and (gc, gl) == (wc, wl)
+
+
+def test_node_dedup_waits_once_per_phase(node, oracle, monkeypatch, capfd):
+    """every context's combine (files and existing Objects) is enqueued before
+    the host reads any owner range: the trace shows ONE host wait for the
+    owner ranges and one for the results, whatever the number of contexts"""
+    keys, has, status, existing = make_corpus(11, 20000, pool=3000, p_none=0.05, p_err=0.05)
+    capfd.readouterr()
+    monkeypatch.setenv("SDCAS_NODE_TRACE", "1")
+    got, gc, gl, gw = node.identifier_dedup_window(keys, has, status, 100, existing)
+    monkeypatch.delenv("SDCAS_NODE_TRACE")
+    err = capfd.readouterr().err
+    waits = [ln for ln in err.splitlines() if ln.startswith("sdcas_node: host wait")]
+    assert waits == [f"sdcas_node: host wait [owner ranges] over {node.size} ranks",
+                     f"sdcas_node: host wait [results] over {node.size} ranks"], err
+    want, wc, wl, ww = oracle.identifier_job(keys, has, status, 100, existing)
+    assert np.array_equal(got, want) and (gc, gl) == (wc, wl) and gw == ww
 
 
 def test_node_cas_ids_and_checksums(node, oracle, tmp_path):

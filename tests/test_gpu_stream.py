@@ -65,6 +65,68 @@ def test_stream_synth_vs_oracle(eng, oracle):
 
 
 @pytest.mark.parametrize("variant", [17, 19])
+def test_stream_sessions_back_to_back(oracle):
+    """sessions enqueued without a host wait between them (stream_begin no
+    longer synchronises; its descriptors and the node-list clear go up on the
+    session's first stream call, the piece list is expanded on the device):
+    three sessions of different shapes — the second smaller, the third larger
+    than the first (its buffers grow) — alternating between two streams, then
+    one sync; every digest exact"""
+    from spacedrive_amd import Engine
+    rng = np.random.default_rng(12)
+    shapes = [[MiB + 1, 5 * MiB + 3, 9 * MiB], [2 * MiB], [3 * MiB + 17, MiB + 1025, 12 * MiB, 4 * MiB + 1, 7 * MiB]]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    with Engine() as e:
+        runs = []
+        for si, sizes in enumerate(shapes):
+            keys = [content_key(0x5D0004, 300 + 10 * si + i) for i in range(len(sizes))]
+            segs = [(f, o, l) for f, n in enumerate(sizes) for o, l in _segments(rng, n, 3)]
+            rng.shuffle(segs)
+            boffs, used = [], 0
+            for _, _, l in segs:
+                boffs.append(used)
+                used += (l + MiB - 1) // MiB * MiB
+            blob = torch.empty(used + 4096, dtype=torch.uint8, device="cuda")
+            t = lambda a: torch.from_numpy(np.array(a, np.uint64).view(np.int64)).cuda()
+            args = [t([keys[f] for f, _, _ in segs]), t([o for _, o, _ in segs]), t([l for _, _, l in segs]), t(boffs)]
+            out = torch.zeros((len(sizes), 32), dtype=torch.uint8, device="cuda")
+            runs.append((keys, sizes, segs, boffs, blob, args, out))
+        torch.cuda.synchronize()
+        for si, (keys, sizes, segs, boffs, blob, args, out) in enumerate(runs):
+            st = streams[si % 2].cuda_stream
+            base = blob.data_ptr()
+            e.dev_synth_content(*(a.data_ptr() for a in args), len(segs), base, st)
+            e.dev_stream_begin(sizes)
+            for part in (slice(0, 1), slice(1, None)):
+                sg = segs[part]
+                e.dev_stream_update([f for f, _, _ in sg], [o for _, o, _ in sg], [l for _, _, l in sg],
+                                    [base + b for b in boffs[part]], stream=st)
+            e.dev_stream_finish(out.data_ptr(), st)
+        for s in streams:
+            e.dev_sync(s.cuda_stream)
+        for keys, sizes, _, _, _, _, out in runs:
+            got = out.cpu().numpy()
+            for i, (k, n) in enumerate(zip(keys, sizes)):
+                assert bytes(got[i]).hex() == oracle.synth_checksum(k, n), n
+        # a session with no update at all still clears its node list: a
+        # message none of whose pieces arrived finishes as the same garbage
+        # every time (zeros in), never as the previous session's nodes
+        out0 = torch.zeros((1, 32), dtype=torch.uint8, device="cuda")
+        out1 = torch.zeros((1, 32), dtype=torch.uint8, device="cuda")
+        e.dev_stream_begin([3 * MiB])
+        e.dev_stream_finish(out0.data_ptr(), streams[0].cuda_stream)
+        keys, sizes, segs, boffs, blob, args, out = runs[1]
+        e.dev_stream_begin(sizes)
+        e.dev_stream_update([f for f, _, _ in segs], [o for _, o, _ in segs], [l for _, _, l in segs],
+                            [blob.data_ptr() + b for b in boffs], stream=streams[0].cuda_stream)
+        e.dev_stream_finish(out.data_ptr(), streams[0].cuda_stream)
+        e.dev_stream_begin([3 * MiB])
+        e.dev_stream_finish(out1.data_ptr(), streams[0].cuda_stream)
+        e.dev_sync(streams[0].cuda_stream)
+        assert torch.equal(out0, out1)
+        assert bytes(out.cpu().numpy()[0]).hex() == oracle.synth_checksum(keys[0], sizes[0])
+
+
 def test_stream_piece_boundaries_vs_oracle(oracle, variant):
     """every product piece kernel over files whose lengths sit at and around
     1 MiB-piece, 1 KiB-chunk and 64-byte-block boundaries (a last piece of
