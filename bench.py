@@ -152,6 +152,31 @@ DEFAULT_LEAF_KERNEL = "k_leaf_tree<512, 279, 1, 1, 2, 2, 0, 1024u>"
 DEFAULT_PIECE_VARIANT = 19
 
 
+def dedup_bytes(n, ne=0):
+    """the bytes the identifier dedup must move at least: each file's 16-byte
+    record (cas key + orphan ordinal) and 1-byte has-key flag read once, its
+    8-byte link written once, and each existing Object's 16-byte record
+    (cas key + DB index) read once; the group-by's table is the
+    implementation's, not the algorithm's"""
+    return 25 * int(n) + 16 * int(ne)
+
+
+def load_dedup_traffic(workload, files):
+    """HBM bytes per dedup call from the committed PMC passes
+    (profiles/*pmc_dedup*.json, tools/pmc_dedup_summary.py), the latest
+    round's for this workload and share size; None if none"""
+    import glob
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_dedup*.json"))):
+        try:
+            d = json.load(open(p))
+        except Exception:
+            continue
+        if d.get("workload") == workload.upper() and d.get("files") == files:
+            best = d
+    return best
+
+
 def load_traffic(workload, kernel="k_leaf_tree"):
     """HBM bytes per launch of the dominant kernel from the committed
     rocprofv3 PMC passes (profiles/*pmc*.json, written by
@@ -904,6 +929,7 @@ def main():
         d_has = (d_sizes != 0).to(torch.uint8)  # mod.rs:78-86: empty files have no cas_id
         d_ids = torch.from_numpy(ids).to(dev)
         stages = DeviceStages(eng, dev.index)
+        stages.time_exchange = distributed
         dd = {"ev": []}
 
     def step():
@@ -1008,6 +1034,32 @@ def main():
         out["dedup"] = {"ms_per_step": ms, "ms_median": med, "objects_created": created, "files_linked": linked,
                         "records_per_gpu": n, "protocol": getattr(stages, "last_protocol", None),
                         "timing": "HIP events around the dedup stages, inside the step"}
+        # the dedup is HBM-bound; priced on the bytes it must
+        # move (dedup_bytes) over its time, the PMC-measured bytes beside them
+        algo = dedup_bytes(n)
+        dr = {"bound": "hbm", "achieved": algo / med / 1e6, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+              "frac": algo / med / 1e6 / HBM_PEAK_GBS, "algorithmic_bytes_per_step": algo,
+              "algorithmic": "25 B per file (16-B record in, 1-B has-key flag in, 8-B link out)",
+              "traffic": None}
+        tr = load_dedup_traffic(args.workload, n) if world == 1 else None
+        if tr:
+            dr["traffic"] = tr["hbm_bytes_per_call"]
+            dr["traffic_over_algorithmic"] = tr["hbm_bytes_per_call"] / algo
+            dr["traffic_gbps"] = tr["hbm_bytes_per_call"] / med / 1e6
+            dr["traffic_frac"] = dr["traffic_gbps"] / HBM_PEAK_GBS
+            dr["traffic_source"] = tr.get("source")
+        out["dedup"]["roofline"] = dr
+        xs = getattr(stages, "last_exchange", None)
+        if xs is not None:
+            # the exchange (RCCL all-to-alls) of the last step: bytes this
+            # rank sent and the HIP-event time of its collectives
+            xms = sum(a.elapsed_time(b) for a, b in xs["events"])
+            xb, xoff, xms = max_over_ranks(torch, dist, dev, [xs["bytes"], xs["bytes_off_rank"], xms])
+            out["dedup"]["exchange"] = {"bytes_per_rank": xb, "bytes_off_rank": xoff, "ms": xms,
+                                        "gbps_off_rank": xoff / xms / 1e6 if xms > 0 else None,
+                                        "timing": "HIP events around the all-to-alls on the step's stream, "
+                                                  "max over ranks",
+                                        "link_peak_gbps_per_peer": 153.6}
     if rank == 0 and world == 1:
         gk = d_out.cpu().numpy().view(np.uint64)
         if args.workload == "c2" and not args.no_cpu_baseline:

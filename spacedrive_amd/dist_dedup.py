@@ -202,9 +202,14 @@ def _exchange(send, send_counts, group, recv_counts=None):
 _META_GROUPS = {}
 
 
-def _meta_group(group):
-    """a gloo group over the same ranks for host-known integers (file and
-    Object counts): exchanging them never waits for the device"""
+def prepare_meta_group(group=None):
+    """Create the gloo group over `group`'s ranks that carries the host-known
+    integers (file and Object counts: exchanging them never waits for the
+    device). dist.new_group is collective over the WHOLE default group, so
+    for a strict subgroup every rank of the default group must call this
+    (members and non-members alike) before the subgroup's first dedup; the
+    default group's own is created on its first dedup, which every rank
+    reaches."""
     if dist.get_backend(group) == "gloo":
         return group
     key = id(group)
@@ -212,6 +217,18 @@ def _meta_group(group):
         ranks = dist.get_process_group_ranks(group) if group is not None else None
         _META_GROUPS[key] = dist.new_group(ranks=ranks, backend="gloo")
     return _META_GROUPS[key]
+
+
+def _meta_group(group):
+    if dist.get_backend(group) == "gloo":
+        return group
+    if id(group) not in _META_GROUPS:
+        whole = group is None or dist.get_world_size(group) == dist.get_world_size()
+        if not whole:
+            raise RuntimeError("identifier_dedup_distributed over a subgroup: call "
+                               "dist_dedup.prepare_meta_group(group) on every rank of the default group first "
+                               "(dist.new_group is collective over all ranks)")
+    return prepare_meta_group(group)
 
 
 def _meta(n, ne, group):
@@ -405,6 +422,33 @@ class _Trace:
             print("dedup buckets ms: " + ", ".join(self.parts), file=sys.stderr, flush=True)
 
 
+class _XTimer:
+    """stages.time_exchange: HIP events around the bucket protocol's
+    all-to-alls on the caller's stream (the collectives are ordered on it; no
+    host synchronisation added) and the bytes this rank sends, left in
+    stages.last_exchange for the caller to read after it synchronises"""
+
+    def __init__(self, stages, dev):
+        self.stages, self.dev = stages, dev
+        self.on = bool(getattr(stages, "time_exchange", False))
+        self.events = []
+
+    def start(self):
+        if self.on:
+            self.events.append([torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)])
+            self.events[-1][0].record(torch.cuda.current_stream(self.dev))
+
+    def stop(self):
+        if self.on:
+            self.events[-1][1].record(torch.cuda.current_stream(self.dev))
+
+    def done(self, world, *tensors):
+        if self.on:
+            b = sum(int(t.numel()) * t.element_size() for t in tensors if t is not None)
+            self.stages.last_exchange = {"bytes": b, "bytes_off_rank": b * (world - 1) // world,
+                                         "events": [tuple(e) for e in self.events]}
+
+
 def _dedup_buckets(stages, world, keys, has_key, status, ids, chunk_size, existing_keys, existing_ids, group, win):
     """the exchange in fixed-capacity buckets: one host synchronisation of the
     device (the totals; the counts agreed before it are host integers); None
@@ -429,6 +473,8 @@ def _dedup_buckets(stages, world, keys, has_key, status, ids, chunk_size, existi
     else:
         sc = fcnt.view(world, 1).contiguous()
     tr.mark("stays+plan+combine")
+    xev = _XTimer(stages, dev)
+    xev.start()
     rc = torch.empty_like(sc)
     dist.all_to_all_single(rc, sc, group=group)  # equal splits: no host sizes
     tr.mark("a2a counts")
@@ -441,10 +487,14 @@ def _dedup_buckets(stages, world, keys, has_key, status, ids, chunk_size, existi
         ercnt = rc[:, 1].contiguous()
     else:
         erecv, ercnt = None, None
+    xev.stop()
     answer = stages.resolve_buckets(frecv, fcap, rc[:, 0].contiguous(), erecv, ecap if has_ex else 0, ercnt, world)
     tr.mark("resolve")
+    xev.start()
     back = torch.empty_like(answer)
     dist.all_to_all_single(back, answer.contiguous(), group=group)
+    xev.stop()
+    xev.done(world, sc, send, esend if has_ex else None, answer)
     tr.mark("a2a answers")
     link, cnt = stages.apply(ids, slot, back, chunk_size, plan)
     tr.mark("apply")
@@ -474,5 +524,5 @@ def owner_of(keys: np.ndarray, world: int) -> np.ndarray:
     return ((k >> np.uint64(52)) * np.uint64(world) >> np.uint64(12)).astype(np.int64)
 
 
-__all__ = ["DeviceStages", "identifier_dedup_distributed", "owner_of"]
+__all__ = ["DeviceStages", "identifier_dedup_distributed", "owner_of", "prepare_meta_group"]
 _ = N  # the C ABI is bound by spacedrive_amd._native.load()

@@ -481,3 +481,47 @@ def test_owner_resolve_with_one_owners_keys(eng, oracle):
         want = np.array([first[k] for k in keys.tolist()], np.int64)
         assert (res.cpu().numpy() == want).all(), name
     assert times["one owner of 8"] < 5 * times["uniform"] + 0.002, times
+
+
+def _subgroup_worker(rank, world, port, outdir):
+    import torch.distributed as dist
+
+    from spacedrive_amd import dist_dedup as D
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        sub = dist.new_group(ranks=[0, 1])
+        real = dist.get_backend
+        # stand in for an RCCL subgroup (the meta group is only built for a
+        # non-gloo group; gloo is all this container has)
+        D.dist.get_backend = lambda g=None: "nccl" if g is sub else real(g)
+        res = []
+        if rank in (0, 1):
+            try:
+                D._meta_group(sub)
+                res.append("no error")
+            except RuntimeError as e:
+                res.append("prepare_meta_group" in str(e))
+        D.prepare_meta_group(sub)  # every rank of the default group
+        if rank in (0, 1):
+            g = D._meta_group(sub)
+            res.append(real(g) == "gloo" and dist.get_world_size(g) == 2)
+            t = torch.tensor([rank + 1])
+            dist.all_reduce(t, group=g)
+            res.append(int(t) == 3)
+        D.dist.get_backend = real
+        np.save(os.path.join(outdir, f"r{rank}.npy"), np.array(res, dtype=object), allow_pickle=True)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_meta_group_of_a_subgroup():
+    """the host-integer group of a strict subgroup: asking for it before it
+    exists raises (dist.new_group would hang: it is collective over every
+    rank), prepare_meta_group on every rank creates it"""
+    import torch.multiprocessing as mp
+    world = 3
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_subgroup_worker, args=(world, _free_port(), d), nprocs=world, join=True,
+                           start_method="spawn")
+        res = [list(np.load(os.path.join(d, f"r{r}.npy"), allow_pickle=True)) for r in range(world)]
+    assert res[0] == [True, True, True] and res[1] == [True, True, True] and res[2] == []

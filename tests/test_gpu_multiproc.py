@@ -282,3 +282,8 @@ def test_bench_two_ranks(workload, launcher):
         assert d["dedup"]["records_per_gpu"] == 20000
         pd = d["parity"]["dedup"]  # both ranks' links against the oracle over the whole corpus
         assert pd["files"] == 40000 and pd["link_mismatches"] == 0 and pd["counts_match"]
+        # the dedup priced: bytes over time against HBM, and the exchange's
+        # bytes and collective time
+        assert d["dedup"]["roofline"]["bound"] == "hbm" and d["dedup"]["roofline"]["frac"] > 0
+        x = d["dedup"]["exchange"]
+        assert x["bytes_per_rank"] >= 20000 * 16 and 0 < x["bytes_off_rank"] < x["bytes_per_rank"] and x["ms"] > 0

@@ -1,0 +1,96 @@
+#!/usr/bin/env python3
+"""Price the identifier dedup (file_identifier/mod.rs:149-254 inside the job's
+steps) on one GPU: the C3 or C5 share bench.py builds, hashed once, then the
+world-of-one dedup (sdcas_dev_dedup_local: stays select, plan walk, table
+memset, k_solo_insert, k_solo_apply) run --reps times, each bracketed by HIP
+events on the stream it runs on. One JSON line: ms per dedup, the bytes it
+must move at least (bench.dedup_bytes) and that figure over the time against
+the HBM peak. Run under rocprofv3 --pmc (tools/pmc_dedup.sh) for the bytes
+it does move: every kernel after the hash belongs to the dedup.
+
+usage: dedup_probe.py [--workload c5] [--files N] [--reps 20] [--existing K]"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="c5", choices=["c3", "c5"])
+    ap.add_argument("--files", type=int, default=0)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--existing", type=int, default=0, help="existing Objects (cas keys of the first K files)")
+    a = ap.parse_args()
+    import torch
+    import torch.distributed as dist
+
+    import bench
+    from spacedrive_amd import Engine
+    from spacedrive_amd import synth as S
+    from spacedrive_amd.dist_dedup import DeviceStages
+    n = a.files or bench.WORKLOADS[a.workload]["files"]
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=dev)
+    sizes, keys, ids = bench.files_of(a.workload, 0, n)
+    lens = S.cas_msg_len(sizes)
+    padded = (lens + np.uint64(127)) // np.uint64(128) * np.uint64(128)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(padded[:-1])
+    total = int(offs[-1] + padded[-1]) + 64
+    chunks = int(np.maximum(np.uint64(1), (lens + np.uint64(1023)) // np.uint64(1024)).sum())
+    eng = Engine(device=0)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    sp = stream.cuda_stream
+    t = lambda x: torch.from_numpy(np.ascontiguousarray(x).view(np.int64)).to(dev)
+    d_blob = torch.empty(total, dtype=torch.uint8, device=dev)
+    d_keys, d_sizes, d_offs, d_lens = t(keys), t(sizes), t(offs), t(lens)
+    d_out = torch.zeros(n, dtype=torch.int64, device=dev)
+    # every device input of the dedup exists before the hash, so that under
+    # rocprofv3 every dispatch after the hash's last kernel is the dedup's
+    d_has = (d_sizes != 0).to(torch.uint8)
+    d_ids = torch.from_numpy(ids).to(dev)
+    ei = torch.arange(a.existing, dtype=torch.int64, device=dev) if a.existing else None
+    ek = torch.empty(a.existing, dtype=torch.int64, device=dev) if a.existing else None
+    eng.dev_reserve(n, chunks)
+    eng.dev_synth_cas_messages(d_keys.data_ptr(), d_sizes.data_ptr(), d_offs.data_ptr(), n, d_blob.data_ptr(), sp)
+    eng.dev_hash_messages(d_blob.data_ptr(), d_offs.data_ptr(), d_lens.data_ptr(), n, 0, d_out.data_ptr(), sp)
+    if a.existing:  # the first K files' keys stand for K existing Objects
+        ek.copy_(d_out[: a.existing])
+    torch.cuda.synchronize()
+    del d_blob
+    stages = DeviceStages(eng, 0)
+    ev = []
+    link = counts = None
+    for r in range(a.reps + 2):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        link, counts = stages.local(d_out, d_has, None, d_ids, 100, ek, ei)
+        e1.record(stream)
+        if r >= 2:
+            ev.append((e0, e1))
+    torch.cuda.synchronize()
+    ms = [x.elapsed_time(y) for x, y in ev]
+    gk = d_out.cpu().numpy().view(np.uint64)
+    distinct = int(np.unique(gk[sizes != 0]).size)
+    algo = bench.dedup_bytes(n, a.existing)
+    med = float(np.median(ms))
+    res = {"workload": a.workload.upper(), "files": n, "existing": a.existing, "distinct_keys": distinct,
+           "reps": a.reps, "ms_median": med, "ms_mean": float(np.mean(ms)), "ms_min": float(np.min(ms)),
+           "algorithmic_bytes": algo, "algorithmic_gbps": algo / med / 1e6,
+           "frac_of_hbm_peak": algo / med / 1e6 / bench.HBM_PEAK_GBS,
+           "created_linked": [int(x) for x in counts.tolist()]}
+    print(json.dumps(res), flush=True)
+    eng.close()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
