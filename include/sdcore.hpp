@@ -258,6 +258,18 @@ class Library {
   // transaction in a database; no-ops in memory
   virtual void begin_batch() {}
   virtual void end_batch() {}
+  // A job about to identify `orphans` rows may let the database keep what
+  // first_objects answers on the host for the job's duration instead of in
+  // an index it would update row by row (SqliteLibrary: the cas_id index is
+  // dropped, its content kept as a cas_id -> first Object map that every
+  // write of the job updates, and the index rebuilt in one pass by
+  // end_bulk_identify). Returns whether it did. Every query answers as
+  // before; the job must be the library's only writer meanwhile.
+  virtual bool begin_bulk_identify(size_t orphans) {
+    (void)orphans;
+    return false;
+  }
+  virtual void end_bulk_identify() {}
 };
 
 // In-memory tables with the reference's query semantics (ids ascending = DB order)
@@ -301,8 +313,12 @@ class SqliteLibrary : public Library {
  public:
   // path of the database file, or ":memory:"; throws std::runtime_error.
   // cas_id_index = false keeps the reference's schema (no index on cas_id),
-  // for comparison
-  static std::unique_ptr<SqliteLibrary> open(const std::string& path, bool cas_id_index = true);
+  // for comparison. object_id_index: an index on file_path(object_id), which
+  // the reference's schema lacks too and the identifier step does not read
+  // (only existing_objects' join does); off by default, since every link
+  // would update it.
+  static std::unique_ptr<SqliteLibrary> open(const std::string& path, bool cas_id_index = true,
+                                             bool object_id_index = false);
   ~SqliteLibrary() override;
 
   // insert rows (ids and pub_ids assigned when 0), one transaction
@@ -330,6 +346,14 @@ class SqliteLibrary : public Library {
   void set_integrity_checksum(int32_t file_path_id, const std::string& checksum) override;
   void begin_batch() override;
   void end_batch() override;
+  // with the cas_id index, when the library holds at most 4x `orphans` rows
+  // with a cas_id (loading them costs less than indexing the job's rows one
+  // by one): the index goes, a host map of its MIN(object_id) per cas_id
+  // stays; a write that could make the map stale (a row with an Object and
+  // a cas_id gets another of either) restores the index first
+  bool begin_bulk_identify(size_t orphans) override;
+  void end_bulk_identify() override;
+  bool bulk_identify_active() const;
 
  private:
   struct Impl;
@@ -403,6 +427,7 @@ struct FileIdentifierJobRunMetadata {
   size_t batches = 0;         // fetches of `batch` rows
   size_t rereads = 0;         // rows two consecutive steps read
   bool early_finish = false;  // JobError::EarlyFinish (file_identifier_job.rs:184-191)
+  bool bulk_identify = false; // the library kept its lookups on the host (FileIdentifierJobInit::bulk_identify)
 };
 
 // FileIdentifierJobInit (file_identifier_job.rs:33-37); batch = orphans
@@ -412,6 +437,10 @@ struct FileIdentifierJobInit {
   Location location;
   std::string sub_materialized_path;  // "" or "/sub/dir/"
   size_t batch = SDCAS_IDENTIFIER_CHUNK_SIZE;
+  // let the library trade its lookup index for a host map during the job
+  // (Library::begin_bulk_identify); the rows and Objects the job leaves are
+  // the same either way
+  bool bulk_identify = false;
 };
 
 // init (count orphans, cursor = first orphan id, task_count = ceil(count /

@@ -653,6 +653,20 @@ FileIdentifierJobRunMetadata run_file_identifier_job_with(Library& db, const Fil
   auto first = db.get_orphan_file_paths(loc, 0, sub, 1);
   meta.cursor = first.empty() ? 0 : first[0].id;
   const uint64_t task_count = (meta.total_orphan_paths + SDCAS_IDENTIFIER_CHUNK_SIZE - 1) / SDCAS_IDENTIFIER_CHUNK_SIZE;
+  // the lookup index traded for a host map for the job's duration, restored
+  // on every way out (Library::begin_bulk_identify)
+  struct Bulk {
+    Library& db;
+    bool on;
+    ~Bulk() {
+      if (!on) return;
+      try {
+        db.end_bulk_identify();
+      } catch (...) {  // unwinding already; the index is rebuilt by the next bulk job or existing_objects
+      }
+    }
+  } bulk{db, init.bulk_identify && db.begin_bulk_identify(meta.total_orphan_paths)};
+  meta.bulk_identify = bulk.on;
   const StepLoop L = run_steps(
       db, task_count, meta.cursor, init.batch,
       [&](int32_t cursor, size_t take) { return db.get_orphan_file_paths(loc, cursor, sub, take); }, metadata,

@@ -5,6 +5,7 @@
 // as prepared statements. See include/sdcore.hpp.
 #include <cstring>
 #include <stdexcept>
+#include <unordered_map>
 
 #include "sdcore.hpp"
 #include "sqlite3_min.h"
@@ -45,9 +46,44 @@ struct SqliteLibrary::Impl {
   Stmt count_orphans_dir, get_orphans_dir;
   Stmt count_orphans, get_orphans, set_cas, want_clear, want_add, existing, new_object, connect, no_checksum,
       set_checksum, add_path, get_path, all_objects, first_object, set_cas_connect;
+  Stmt row_state, set_cas_connect_free, count_cas, load_first;
   int64_t next_object = 1;
   bool cas_index = false;
   int batch_depth = 0;
+  // bulk identify (begin_bulk_identify): the cas_id index is dropped and its
+  // answer to first_objects kept here, cas_id -> MIN(object_id) over the
+  // rows with both
+  bool bulk = false;
+  std::unordered_map<std::string, int32_t> first;
+
+  void first_min(const std::string& cas, int32_t oid) {
+    auto it = first.find(cas);
+    if (it == first.end()) first.emplace(cas, oid);
+    else if (oid < it->second) it->second = oid;
+  }
+  // (cas_id, object_id) of a row before a write
+  std::pair<std::optional<std::string>, std::optional<int32_t>> state(int32_t id) {
+    sqlite3_bind_int64(row_state.s, 1, id);
+    std::pair<std::optional<std::string>, std::optional<int32_t>> r;
+    const int rc = sqlite3_step(row_state.s);
+    if (rc == SQLITE_ROW) {
+      r.first = col_text(row_state.s, 0);
+      if (sqlite3_column_type(row_state.s, 1) != SQLITE_NULL) r.second = (int32_t)sqlite3_column_int64(row_state.s, 1);
+    } else if (rc != SQLITE_DONE) {
+      fail("row state");
+    }
+    sqlite3_reset(row_state.s);
+    sqlite3_clear_bindings(row_state.s);
+    return r;
+  }
+  void index_restore() {
+    if (!bulk) return;
+    if (batch_depth) exec("COMMIT");  // CREATE INDEX in its own transaction
+    exec("CREATE INDEX IF NOT EXISTS file_path_cas_id_idx ON file_path (cas_id)");
+    if (batch_depth) exec("BEGIN IMMEDIATE");
+    bulk = false;
+    first.clear();
+  }
 
   [[noreturn]] void fail(const std::string& what) {
     throw std::runtime_error("sqlite: " + what + ": " + (db ? sqlite3_errmsg(db) : "no database"));
@@ -137,7 +173,7 @@ SqliteLibrary::~SqliteLibrary() {
   if (db) sqlite3_close(db);
 }
 
-std::unique_ptr<SqliteLibrary> SqliteLibrary::open(const std::string& path, bool cas_id_index) {
+std::unique_ptr<SqliteLibrary> SqliteLibrary::open(const std::string& path, bool cas_id_index, bool object_id_index) {
   auto d = std::make_unique<Impl>();
   if (sqlite3_open_v2(path.c_str(), &d->db, SQLITE_OPEN_READWRITE | SQLITE_OPEN_CREATE | SQLITE_OPEN_NOMUTEX,
                       nullptr) != SQLITE_OK) {
@@ -167,7 +203,7 @@ std::unique_ptr<SqliteLibrary> SqliteLibrary::open(const std::string& path, bool
           "materialized_path)");
   // not in the reference's schema: the existing-Object lookup by cas_id
   if (cas_id_index) d->exec("CREATE INDEX IF NOT EXISTS file_path_cas_id_idx ON file_path (cas_id)");
-  d->exec("CREATE INDEX IF NOT EXISTS file_path_object_id_idx ON file_path (object_id)");
+  if (object_id_index) d->exec("CREATE INDEX IF NOT EXISTS file_path_object_id_idx ON file_path (object_id)");
   d->exec("CREATE TEMP TABLE IF NOT EXISTS want_cas (cas_id TEXT PRIMARY KEY)");
   Impl& x = *d;
   x.prepare(x.count_orphans, "SELECT COUNT(*) FROM file_path WHERE " SD_ORPHAN);
@@ -187,12 +223,17 @@ std::unique_ptr<SqliteLibrary> SqliteLibrary::open(const std::string& path, bool
   // (join order and indexes pinned: the planner otherwise walks every
   // identified file_path per step — measured 29 ms per 100-row step at 50 K
   // rows, quadratic over a job)
-  if (cas_id_index)
+  if (cas_id_index && object_id_index)
     x.prepare(x.existing,
               "WITH objs AS (SELECT DISTINCT f2.object_id AS oid FROM want_cas w CROSS JOIN file_path f2"
               " INDEXED BY file_path_cas_id_idx ON f2.cas_id = w.cas_id WHERE f2.object_id IS NOT NULL)"
               " SELECT fp.object_id, fp.cas_id FROM objs CROSS JOIN file_path fp INDEXED BY file_path_object_id_idx"
               " ON fp.object_id = objs.oid WHERE fp.cas_id IS NOT NULL ORDER BY fp.object_id, fp.id");
+  else if (cas_id_index)  // the Objects by index probes, their file_paths by one scan
+    x.prepare(x.existing,
+              "SELECT fp.object_id, fp.cas_id FROM file_path fp WHERE fp.cas_id IS NOT NULL AND fp.object_id IN"
+              " (SELECT f2.object_id FROM want_cas w CROSS JOIN file_path f2 INDEXED BY file_path_cas_id_idx"
+              " ON f2.cas_id = w.cas_id WHERE f2.object_id IS NOT NULL) ORDER BY fp.object_id, fp.id");
   else  // the reference's schema: the same query over an unindexed cas_id
     x.prepare(x.existing,
               "SELECT fp.object_id, fp.cas_id FROM file_path fp WHERE fp.cas_id IS NOT NULL AND fp.object_id IN"
@@ -217,6 +258,14 @@ std::unique_ptr<SqliteLibrary> SqliteLibrary::open(const std::string& path, bool
             " size_in_bytes_bytes, cas_id, object_id, integrity_checksum, date_created, kind_hint, inode, hidden)"
             " VALUES (?1, ?2, ?3, ?4, ?5, ?6, ?7, ?8, ?9, ?10, ?11, ?12, ?13, ?14, ?15)");
   x.prepare(x.get_path, "SELECT " SD_COLS " FROM file_path WHERE id = ?1");
+  x.prepare(x.row_state, "SELECT cas_id, object_id FROM file_path WHERE id = ?1");
+  // bulk identify: the combined write of a row without an Object, which
+  // leaves any other row alone (sqlite3_changes() tells which happened)
+  x.prepare(x.set_cas_connect_free, "UPDATE file_path SET cas_id = ?1, object_id = ?2 WHERE id = ?3 AND object_id IS NULL");
+  x.prepare(x.count_cas, "SELECT COUNT(*) FROM file_path WHERE cas_id IS NOT NULL");
+  x.prepare(x.load_first,
+            "SELECT cas_id, MIN(object_id) FROM file_path WHERE cas_id IS NOT NULL AND object_id IS NOT NULL"
+            " GROUP BY cas_id");
   x.prepare(x.all_objects, "SELECT id, pub_id, kind, date_created FROM object ORDER BY id");
   {
     Stmt mx;
@@ -236,6 +285,7 @@ void SqliteLibrary::end_batch() {
 
 void SqliteLibrary::add_file_paths(std::vector<FilePathRow>& rows) {
   Impl& x = *d_;
+  x.index_restore();  // new rows may carry cas_ids and Objects
   int64_t next = 1;
   {
     Stmt mx;
@@ -335,14 +385,23 @@ std::vector<FilePathRow> SqliteLibrary::get_orphan_file_paths(int32_t location_i
 
 void SqliteLibrary::set_cas_id(int32_t id, const std::optional<std::string>& cas_id) {
   Impl& x = *d_;
+  std::optional<int32_t> oid;
+  if (x.bulk) {
+    auto [old_cas, old_oid] = x.state(id);
+    // a row with an Object leaving a cas_id: its MIN may move, only the index knows
+    if (old_oid && old_cas && old_cas != cas_id) x.index_restore();
+    oid = old_oid;
+  }
   x.opt_text(x.set_cas, 1, cas_id);
   sqlite3_bind_int64(x.set_cas.s, 2, id);
   x.done(x.set_cas);
+  if (x.bulk && oid && cas_id) x.first_min(*cas_id, *oid);
 }
 
 std::vector<std::pair<int32_t, std::vector<std::string>>> SqliteLibrary::existing_objects(
     const std::vector<std::string>& cas_ids) {
   Impl& x = *d_;
+  x.index_restore();  // the join reads the cas_id index
   begin_batch();
   x.done(x.want_clear);
   for (const auto& c : cas_ids) {
@@ -378,6 +437,13 @@ std::vector<std::pair<std::string, int32_t>> SqliteLibrary::first_objects(const 
   Impl& x = *d_;
   if (!x.cas_index) return Library::first_objects(cas_ids);
   std::vector<std::pair<std::string, int32_t>> out;
+  if (x.bulk) {
+    for (const auto& c : cas_ids) {
+      auto it = x.first.find(c);
+      if (it != x.first.end()) out.emplace_back(c, it->second);
+    }
+    return out;
+  }
   begin_batch();
   for (const auto& c : cas_ids) {
     x.text(x.first_object, 1, c);
@@ -394,6 +460,20 @@ std::vector<std::pair<std::string, int32_t>> SqliteLibrary::first_objects(const 
 void SqliteLibrary::set_cas_id_and_connect(int32_t file_path_id, const std::optional<std::string>& cas_id,
                                            int32_t object_id) {
   Impl& x = *d_;
+  if (x.bulk) {
+    // the step's rows have no Object: one write, no read
+    x.opt_text(x.set_cas_connect_free, 1, cas_id);
+    sqlite3_bind_int64(x.set_cas_connect_free.s, 2, object_id);
+    sqlite3_bind_int64(x.set_cas_connect_free.s, 3, file_path_id);
+    x.done(x.set_cas_connect_free);
+    if (sqlite3_changes(x.db) == 1) {
+      if (cas_id) x.first_min(*cas_id, object_id);
+      return;
+    }
+    set_cas_id(file_path_id, cas_id);  // a row with an Object (or none at all): the general path
+    connect(file_path_id, object_id);
+    return;
+  }
   x.opt_text(x.set_cas_connect, 1, cas_id);
   sqlite3_bind_int64(x.set_cas_connect.s, 2, object_id);
   sqlite3_bind_int64(x.set_cas_connect.s, 3, file_path_id);
@@ -402,10 +482,40 @@ void SqliteLibrary::set_cas_id_and_connect(int32_t file_path_id, const std::opti
 
 void SqliteLibrary::connect(int32_t file_path_id, int32_t object_id) {
   Impl& x = *d_;
+  std::optional<std::string> cas;
+  if (x.bulk) {
+    auto [old_cas, old_oid] = x.state(file_path_id);
+    if (old_cas && old_oid && *old_oid != object_id) x.index_restore();  // its cas_id's MIN may move
+    cas = old_cas;
+  }
   sqlite3_bind_int64(x.connect.s, 1, object_id);
   sqlite3_bind_int64(x.connect.s, 2, file_path_id);
   x.done(x.connect);
+  if (x.bulk && cas) x.first_min(*cas, object_id);
 }
+
+bool SqliteLibrary::begin_bulk_identify(size_t orphans) {
+  Impl& x = *d_;
+  if (!x.cas_index || x.bulk || x.batch_depth) return false;
+  if (sqlite3_step(x.count_cas.s) != SQLITE_ROW) x.fail("count cas_ids");
+  const uint64_t with_cas = (uint64_t)sqlite3_column_int64(x.count_cas.s, 0);
+  sqlite3_reset(x.count_cas.s);
+  if (with_cas > 4 * (uint64_t)orphans) return false;
+  x.first.clear();
+  x.first.reserve((size_t)with_cas + orphans);
+  int rc;
+  while ((rc = sqlite3_step(x.load_first.s)) == SQLITE_ROW)
+    x.first.emplace(*Impl::col_text(x.load_first.s, 0), (int32_t)sqlite3_column_int64(x.load_first.s, 1));
+  if (rc != SQLITE_DONE) x.fail("load cas_ids");
+  sqlite3_reset(x.load_first.s);
+  x.exec("DROP INDEX IF EXISTS file_path_cas_id_idx");
+  x.bulk = true;
+  return true;
+}
+
+void SqliteLibrary::end_bulk_identify() { d_->index_restore(); }
+
+bool SqliteLibrary::bulk_identify_active() const { return d_->bulk; }
 
 std::vector<FilePathRow> SqliteLibrary::file_paths_without_checksum(int32_t location_id, const std::string& sub) {
   Impl& x = *d_;

@@ -206,7 +206,7 @@ int main(int argc, char** argv) {
   for (size_t i = 0; i < rows.size(); ++i) rows[i].id = (int32_t)(i + 1);
 
   std::vector<Leg> legs;
-  auto run_leg = [&](const std::string& name, size_t batch, bool reference) {
+  auto run_leg = [&](const std::string& name, size_t batch, bool reference, bool bulk = false) {
     Leg L;
     L.name = name;
     const std::string db = fresh_db();
@@ -217,6 +217,7 @@ int main(int argc, char** argv) {
       ReferenceCalls rc(*sql);
       Library& lib = reference ? static_cast<Library&>(rc) : *sql;
       FileIdentifierJobInit init{loc, "", batch};
+      init.bulk_identify = bulk;
       MetadataFn md;
       GroupBy gb;
       if (!reference) {
@@ -301,6 +302,7 @@ int main(int argc, char** argv) {
   };
   run_leg("gpu_batch10000", 10000, false);
   run_leg("gpu_batch100", 100, false);
+  run_leg("gpu_batch10000_bulk_identify", 10000, false, true);
   // the reference shape over a bounded sample: the first `sample` files only
   // (a fresh location holding just them keeps every leg's job whole)
   const bool sampled = sample < rows.size();
@@ -316,8 +318,8 @@ int main(int argc, char** argv) {
            a.meta.total_objects_created == b.meta.total_objects_created &&
            a.meta.total_objects_linked == b.meta.total_objects_linked;
   };
-  if (!same(legs[0], legs[1])) ++bad;
-  if (!same(legs[2], sampled ? legs[3] : legs[0])) ++bad;
+  if (!same(legs[0], legs[1]) || !same(legs[0], legs[2])) ++bad;
+  if (!same(legs[3], sampled ? legs[4] : legs[0])) ++bad;
   std::string out = "{\"what\": \"the file identifier job end to end on real files (page cache) into SQLite\", ";
   char b[1024];
   std::snprintf(b, sizeof b,
@@ -330,10 +332,10 @@ int main(int argc, char** argv) {
     std::snprintf(b, sizeof b,
                   ", \"%s\": {\"orphans\": %zu, \"seconds\": %.3f, \"orphans_per_s\": %.0f, \"metadata_s\": %.3f, "
                   "\"group_by_s\": %.3f, \"rows_fetched\": %zu, \"steps\": %zu, \"batches\": %zu, "
-                  "\"created\": %zu, \"linked\": %zu}",
+                  "\"created\": %zu, \"linked\": %zu, \"bulk_identify\": %s}",
                   L.name.c_str(), L.meta.total_orphan_paths, L.seconds, L.meta.total_orphan_paths / L.seconds,
                   L.metadata_s, L.group_by_s, L.rows, L.meta.steps, L.meta.batches,
-                  L.meta.total_objects_created, L.meta.total_objects_linked);
+                  L.meta.total_objects_created, L.meta.total_objects_linked, L.meta.bulk_identify ? "true" : "false");
     out += b;
   }
   std::printf("%s}\n", out.c_str());

@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <random>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -105,10 +106,69 @@ static GroupBy oracle_group_by(size_t chunk_size) {
 // the identifier job's loop (run_file_identifier_job_with: the reference's
 // file_identifier_job.rs:125-236 in batches) with the metadata supplied
 // instead of read from files, and the oracle as the group-by
-static FileIdentifierJobRunMetadata run_job(Library& db, int32_t loc, size_t batch, uint64_t pool) {
+static FileIdentifierJobRunMetadata run_job(Library& db, int32_t loc, size_t batch, uint64_t pool, bool bulk = false) {
   FileIdentifierJobInit init{Location{loc, "/nowhere"}, "", batch};
+  init.bulk_identify = bulk;
   return run_file_identifier_job_with(
       db, init, [&](const std::vector<FilePathRow>& rows) { return make_metadata(rows, pool); }, oracle_group_by(100));
+}
+
+// The reference's job restated literally on a Library, as an independent
+// ground truth for run_file_identifier_job_with (which plans steps, defers
+// cas_id writes into the link, probes first_objects and batches): init
+// (file_identifier_job.rs:125-176), then per step the next 100 orphans with
+// id >= cursor (:296-319) through identifier_job_step exactly as mod.rs:98-350
+// orders its calls — every processed row's cas_id written (:157-178), the
+// existing-Object query (:181-188), each row with a cas_id linked to the
+// first such Object (:202-238), a new Object for each row whose cas_id no
+// existing Object carries or that has none (:246-342) — and the cursor moved
+// to the step's last row (mod.rs:401-405). HashMap order is canonicalised to
+// row id order.
+static FileIdentifierJobRunMetadata literal_job(Library& db, int32_t loc, uint64_t pool) {
+  FileIdentifierJobRunMetadata meta;
+  meta.total_orphan_paths = db.count_orphan_file_paths(loc, "");
+  if (!meta.total_orphan_paths) return meta;
+  int32_t cursor = db.get_orphan_file_paths(loc, 0, "", 1)[0].id;
+  const size_t task_count = (meta.total_orphan_paths + 99) / 100;
+  for (size_t step = 0; step < task_count; ++step) {
+    const auto rows = db.get_orphan_file_paths(loc, cursor, "", 100);
+    if (rows.empty()) {
+      meta.early_finish = true;
+      break;
+    }
+    const auto md = make_metadata(rows, pool);
+    std::vector<size_t> ok;  // mod.rs:105-147: rows whose FileMetadata failed drop out
+    for (size_t i = 0; i < rows.size(); ++i)
+      if (md[i].ok()) ok.push_back(i);
+    std::vector<std::string> unique;
+    for (size_t i : ok)
+      if (md[i].value().cas_id && std::find(unique.begin(), unique.end(), *md[i].value().cas_id) == unique.end())
+        unique.push_back(*md[i].value().cas_id);
+    for (size_t i : ok) db.set_cas_id(rows[i].id, md[i].value().cas_id);
+    const auto existing = db.existing_objects(unique);
+    std::set<std::string> existing_cas;
+    for (const auto& [oid, cs] : existing) existing_cas.insert(cs.begin(), cs.end());
+    for (size_t i : ok) {
+      const auto& c = md[i].value().cas_id;
+      if (!c) continue;
+      for (const auto& [oid, cs] : existing)
+        if (std::find(cs.begin(), cs.end(), *c) != cs.end()) {
+          db.connect(rows[i].id, oid);
+          ++meta.total_objects_linked;
+          break;
+        }
+    }
+    for (size_t i : ok) {
+      const auto& c = md[i].value().cas_id;
+      if (c && existing_cas.count(*c)) continue;
+      db.connect(rows[i].id, db.create_object(md[i].value().kind, rows[i].date_created));
+      ++meta.total_objects_created;
+    }
+    ++meta.steps;
+    cursor = rows.back().id;
+  }
+  meta.cursor = cursor;
+  return meta;
 }
 
 static bool same_row(const FilePathRow& a, const FilePathRow& b) {
@@ -286,7 +346,16 @@ static void test_parity(bool cas_index) {
   // result must be the same (a step's last row that stays an orphan — an
   // I/O error, an empty file — is read again by the next step, inside a
   // batch as across fetches)
-  MemoryLibrary mem_b = mem, mem_c = mem;
+  MemoryLibrary mem_b = mem, mem_c = mem, mem_lit = mem;
+  // a second SQLite copy runs the job in 10000-row batches with the lookup
+  // index traded for the host map (bulk identify); the re-identified rows
+  // make it restore the index mid-job
+  auto sql_bulk = SqliteLibrary::open(":memory:", cas_index);
+  {
+    std::vector<FilePathRow> all = mem.file_paths;
+    sql_bulk->add_file_paths(all);
+    for (const auto& o : mem.objects) sql_bulk->create_object(o.kind, o.date_created);
+  }
   size_t rereads = 0;
   for (int32_t loc : {1, 2}) {
     const auto orphans = mem.get_orphan_file_paths(loc, 0, "", 1u << 30);
@@ -294,7 +363,24 @@ static void test_parity(bool cas_index) {
     auto js = run_job(*sql, loc, 100, 400);
     auto jb = run_job(mem_b, loc, 1000, 400);
     auto jc = run_job(mem_c, loc, 10000, 400);
-    for (const auto* j : {&js, &jb, &jc})
+    FileIdentifierJobInit binit{Location{loc, "/nowhere"}, "", 10000};
+    binit.bulk_identify = true;
+    auto jk = run_file_identifier_job_with(
+        *sql_bulk, binit, [&](const std::vector<FilePathRow>& rows) { return make_metadata(rows, 400); },
+        oracle_group_by(100));
+    CHECK(!sql_bulk->bulk_identify_active(), "bulk identify left on after the job");
+    // taken for the first location; the second's 253 orphans are fewer than
+    // a quarter of the rows the first left with a cas_id (probing is cheaper)
+    if (cas_index) CHECK(jk.bulk_identify == (loc == 1), "bulk identify %d at loc %d", (int)jk.bulk_identify, loc);
+    // the literal restatement of the reference's steps: no early finish
+    // here, so it runs the same steps over the same rows
+    auto jl = literal_job(mem_lit, loc, 400);
+    CHECK(jl.total_objects_created == jm.total_objects_created && jl.total_objects_linked == jm.total_objects_linked &&
+              jl.steps == jm.steps && jl.cursor == jm.cursor,
+          "job loc %d vs the literal steps: created %zu/%zu linked %zu/%zu steps %zu/%zu cursor %d/%d", loc,
+          jm.total_objects_created, jl.total_objects_created, jm.total_objects_linked, jl.total_objects_linked,
+          jm.steps, jl.steps, jm.cursor, jl.cursor);
+    for (const auto* j : {&js, &jb, &jc, &jk})
       CHECK(jm.total_objects_created == j->total_objects_created && jm.total_objects_linked == j->total_objects_linked &&
                 jm.steps == j->steps && jm.cursor == j->cursor && jm.rereads == j->rereads,
             "job loc %d: memory/100 %zu/%zu/%zu steps cursor %d rereads %zu, other %zu/%zu/%zu steps cursor %d "
@@ -310,20 +396,34 @@ static void test_parity(bool cas_index) {
   for (const auto& r : mem.file_paths) {
     const FilePathRow* b = mem_b.file_path(r.id);
     const FilePathRow* c = mem_c.file_path(r.id);
+    const FilePathRow* l = mem_lit.file_path(r.id);
     CHECK(b && c && same_row(r, *b) && same_row(r, *c), "row %d: batch 100 / 1000 / 10000 differ", r.id);
+    CHECK(l && same_row(r, *l), "row %d: the job and the literal steps differ", r.id);
   }
-  CHECK(mem_b.objects.size() == mem.objects.size() && mem_c.objects.size() == mem.objects.size(),
-        "objects: %zu %zu %zu", mem.objects.size(), mem_b.objects.size(), mem_c.objects.size());
+  CHECK(mem_b.objects.size() == mem.objects.size() && mem_c.objects.size() == mem.objects.size() &&
+            mem_lit.objects.size() == mem.objects.size(),
+        "objects: %zu %zu %zu %zu", mem.objects.size(), mem_b.objects.size(), mem_c.objects.size(),
+        mem_lit.objects.size());
+  for (size_t i = 0; i < mem.objects.size() && i < mem_lit.objects.size(); ++i)
+    CHECK(mem_lit.objects[i].id == mem.objects[i].id && mem_lit.objects[i].kind == mem.objects[i].kind &&
+              mem_lit.objects[i].date_created == mem.objects[i].date_created,
+          "object %zu vs the literal steps", i);
   for (int32_t id = 1; id <= 3000; ++id) {
     auto s = sql->file_path(id);
     CHECK(s && same_row(*mem.file_path(id), *s), "row %d after the job", id);
+    auto k = sql_bulk->file_path(id);
+    CHECK(k && same_row(*mem.file_path(id), *k), "row %d after the bulk job", id);
   }
-  auto so = sql->objects();
-  CHECK(so.size() == mem.objects.size(), "object count %zu %zu", so.size(), mem.objects.size());
-  for (size_t i = 0; i < so.size() && i < mem.objects.size(); ++i)
-    CHECK(so[i].id == mem.objects[i].id && so[i].kind == mem.objects[i].kind &&
-              so[i].date_created == mem.objects[i].date_created,
-          "object %zu", i);
+  for (auto* lib : {sql.get(), sql_bulk.get()}) {
+    auto so = lib->objects();
+    CHECK(so.size() == mem.objects.size(), "object count %zu %zu", so.size(), mem.objects.size());
+    for (size_t i = 0; i < so.size() && i < mem.objects.size(); ++i)
+      CHECK(so[i].id == mem.objects[i].id && so[i].kind == mem.objects[i].kind &&
+                so[i].date_created == mem.objects[i].date_created,
+            "object %zu", i);
+  }
+  // the bulk job's library answers lookups as before (its index is back)
+  CHECK(sql_bulk->existing_objects(want) == mem.existing_objects(want), "existing objects after the bulk job");
   // validator writes
   for (const auto& r : sql->file_paths_without_checksum(1, "/sub/")) {
     sql->set_integrity_checksum(r.id, std::string(64, 'b'));
@@ -423,6 +523,8 @@ struct Timed : Library {
   void set_integrity_checksum(int32_t i, const std::string& c) override { d.set_integrity_checksum(i, c); }
   void begin_batch() override { tm(6, [&] { d.begin_batch(); }); }
   void end_batch() override { tm(7, [&] { d.end_batch(); }); }
+  bool begin_bulk_identify(size_t n) override { return tm(3, [&] { return d.begin_bulk_identify(n); }); }
+  void end_bulk_identify() override { tm(7, [&] { d.end_bulk_identify(); }); }
 };
 
 static int bench(size_t n) {
@@ -431,13 +533,13 @@ static int bench(size_t n) {
   struct Mode {
     const char* name;
     size_t batch;
-    bool autocommit, cas_index;
+    bool autocommit, cas_index, bulk = false;
   };
   // the reference's shape: 100-row steps, a commit per write, no cas_id index
   // (a bounded sample: it is slow); then this library's batching and index
   for (Mode m : {Mode{"reference_shape_batch100_autocommit_no_cas_index", 100, true, false},
                  Mode{"batch100_autocommit", 100, true, true}, Mode{"batch100_txn", 100, false, true},
-                 Mode{"batch10000_txn", 10000, false, true}}) {
+                 Mode{"batch10000_txn", 10000, false, true}, Mode{"batch10000_txn_bulk_identify", 10000, false, true, true}}) {
     const size_t rows_n = m.autocommit ? std::min<size_t>(n, 20000) : n;
     char path[] = "/tmp/sdcore_dbXXXXXX";
     const int fd = mkstemp(path);
@@ -456,7 +558,7 @@ static int bench(size_t n) {
       Autocommit ac(*sql);
       Timed timed(m.autocommit ? static_cast<Library&>(ac) : *sql, !m.cas_index);
       const double t0 = now();
-      auto meta = run_job(timed, 1, m.batch, rows_n / 3);
+      auto meta = run_job(timed, 1, m.batch, rows_n / 3, m.bulk);
       const double dt = now() - t0;
       char b[512];
       std::snprintf(b, sizeof b,

@@ -64,7 +64,6 @@ def test_stream_synth_vs_oracle(eng, oracle):
         assert bytes(got[i]).hex() == oracle.synth_checksum(k, n), n
 
 
-@pytest.mark.parametrize("variant", [17, 19])
 def test_stream_sessions_back_to_back(oracle):
     """sessions enqueued without a host wait between them (stream_begin no
     longer synchronises; its descriptors and the node-list clear go up on the
@@ -127,6 +126,7 @@ def test_stream_sessions_back_to_back(oracle):
         assert bytes(out.cpu().numpy()[0]).hex() == oracle.synth_checksum(keys[0], sizes[0])
 
 
+@pytest.mark.parametrize("variant", [17, 19])
 def test_stream_piece_boundaries_vs_oracle(oracle, variant):
     """every product piece kernel over files whose lengths sit at and around
     1 MiB-piece, 1 KiB-chunk and 64-byte-block boundaries (a last piece of
