@@ -220,10 +220,15 @@ __device__ __forceinline__ void hash_chunk_pl(const uint8_t* __restrict__ p, uin
   const uint32_t lb = clen <= BLOCK_LEN ? 0u : (clen - 1) / BLOCK_LEN;  // last block index
   const uint32_t lblen = clen - lb * BLOCK_LEN;                          // its length (0 only for an empty message)
   const uint32_t endf = CHUNK_END | (root ? ROOT : 0u);
-  uint32_t m0[16], m1[16];
   const uint8_t* q = p;
 #pragma unroll 1
   for (uint32_t b = 0; b <= lb; b += 2, q += 2 * BS) {
+    // m1 is loaded only when the chunk has the second block; left undefined
+    // otherwise, the compiler zeroed its sixteen registers before the loop
+    // (16 v_mov per chunk). An empty asm defines them as "whatever is there".
+    uint32_t m0[16], m1[16];
+#pragma unroll
+    for (int w = 0; w < 16; ++w) asm volatile("" : "=v"(m1[w]));
     const bool two = b + 1 <= lb;
     if constexpr (NT) {
       load_full_block_nt(q, m0);

@@ -26,21 +26,24 @@ def short(name):
     return n[:60]
 
 
-def rows(src, kind):
-    for f in glob.glob(os.path.join(src, "*", f"*_{kind}.csv")):
+def rows(src, pass_name, kind):
+    for f in glob.glob(os.path.join(src, pass_name, f"*_{kind}.csv")):
         yield from csv.DictReader(open(f))
 
 
 def after_hash(rs):
+    """the dispatches after the hash's last kernel, up to the last dedup
+    apply (the probe's read-back copies after it are not the dedup's)"""
     rs = sorted(rs, key=lambda r: int(r["Dispatch_Id"]))
     last = max((int(r["Dispatch_Id"]) for r in rs if any(h in r["Kernel_Name"] for h in HASH)), default=-1)
-    return [r for r in rs if int(r["Dispatch_Id"]) > last]
+    end = max((int(r["Dispatch_Id"]) for r in rs if "apply" in r["Kernel_Name"]), default=1 << 62)
+    return [r for r in rs if last < int(r["Dispatch_Id"]) <= end]
 
 
 def main():
     src, dst, calls = sys.argv[1], sys.argv[2], int(sys.argv[3])
     # kernel time per call from the trace pass
-    tr = after_hash(list(rows(os.path.join(src, "trace"), "kernel_trace")))
+    tr = after_hash(list(rows(src, "trace", "kernel_trace")))
     per_k = collections.defaultdict(lambda: [0, 0.0])
     for r in tr:
         k = short(r["Kernel_Name"])
@@ -51,7 +54,7 @@ def main():
     byk = collections.defaultdict(lambda: collections.defaultdict(float))
     tot = collections.defaultdict(float)
     for p in ("fetch", "write", "req", "tcc"):
-        for r in after_hash(list(rows(os.path.join(src, p), "counter_collection"))):
+        for r in after_hash(list(rows(src, p, "counter_collection"))):
             v = float(r["Counter_Value"])
             tot[r["Counter_Name"]] += v
             byk[short(r["Kernel_Name"])][r["Counter_Name"]] += v
