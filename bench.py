@@ -852,6 +852,8 @@ def main():
     ap.add_argument("--window-gib", type=int, default=0, help="c4: HBM window (0: the whole share when it fits)")
     ap.add_argument("--c4-cpu-gib", type=int, default=16, help="C4 CPU-baseline sample size")
     ap.add_argument("--c4-e2e-gib", type=int, default=8, help="C4 end-to-end sample size (pinned buffer, files)")
+    ap.add_argument("--msg-align", type=int, default=128, choices=[16, 32, 64, 128],
+                    help="c2/c3/c5: byte alignment of each message in HBM")
     ap.add_argument("--e2e-files", type=int, default=200_000, help="c2: files in the end-to-end / faithful leg")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-faithful", action="store_true", help="e2e without the page-cache files legs")
@@ -899,8 +901,10 @@ def main():
     lens = S.cas_msg_len(sizes)
     offs = np.zeros(n, np.uint64)
     # messages start on 128-byte lines (the L2/HBM line): a chunk then spans
-    # 8 lines instead of 9 (the layout of device memory is ours to choose)
-    padded = (lens + np.uint64(127)) // np.uint64(128) * np.uint64(128)
+    # 8 lines instead of 9 (the layout of device memory is ours to choose);
+    # --msg-align 16 packs them at the ABI's minimum instead (A/B)
+    al = np.uint64(args.msg_align)
+    padded = (lens + al - np.uint64(1)) // al * al
     offs[1:] = np.cumsum(padded[:-1])
     total_bytes = int(offs[-1] + padded[-1]) + 64
     chunks = int(np.maximum(np.uint64(1), (lens + np.uint64(1023)) // np.uint64(1024)).sum())

@@ -270,6 +270,19 @@ class Library {
     return false;
   }
   virtual void end_bulk_identify() {}
+  // The job reads its next batch (orphans past the current batch's last row,
+  // which the current batch never writes) while the current batch's writes
+  // are still open. A database that can serve that read from another
+  // connection without waiting for them (SQLite in WAL mode: a second,
+  // read-only connection) says so here; the job then fetches on its
+  // metadata thread, concurrently with the writes. The concurrent call
+  // answers what get_orphan_file_paths would after the current batch commits.
+  virtual bool concurrent_orphan_reads() { return false; }
+  virtual std::vector<FilePathRow> get_orphan_file_paths_concurrent(int32_t location_id, int32_t cursor,
+                                                                    const std::string& sub_materialized_path,
+                                                                    size_t take) {
+    return get_orphan_file_paths(location_id, cursor, sub_materialized_path, take);
+  }
 };
 
 // In-memory tables with the reference's query semantics (ids ascending = DB order)
@@ -354,6 +367,11 @@ class SqliteLibrary : public Library {
   bool begin_bulk_identify(size_t orphans) override;
   void end_bulk_identify() override;
   bool bulk_identify_active() const;
+  // a file database (not ":memory:") opens a second, read-only connection
+  // for the job's read-ahead (WAL readers do not wait for the writer)
+  bool concurrent_orphan_reads() override;
+  std::vector<FilePathRow> get_orphan_file_paths_concurrent(int32_t location_id, int32_t cursor,
+                                                            const std::string& sub, size_t take) override;
 
  private:
   struct Impl;

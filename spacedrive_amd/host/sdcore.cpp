@@ -563,7 +563,7 @@ struct StepLoop {
 using Fetch = std::function<std::vector<FilePathRow>(int32_t cursor, size_t take)>;
 
 StepLoop run_steps(Library& db, uint64_t task_count, int32_t cursor, size_t batch_rows, const Fetch& fetch,
-                   const MetadataFn& metadata, const GroupBy& group_by) {
+                   const MetadataFn& metadata, const GroupBy& group_by, const Fetch* fetch_ahead = nullptr) {
   StepLoop L;
   L.cursor = cursor;
   const size_t cs = SDCAS_IDENTIFIER_CHUNK_SIZE;
@@ -599,7 +599,8 @@ StepLoop run_steps(Library& db, uint64_t task_count, int32_t cursor, size_t batc
     // FileMetadata computed on another thread after the group-by; the cursor
     // row is fetched again once the writes are done.
     std::vector<FilePathRow> next;
-    std::future<std::vector<Result<FileMetadata>>> next_md;
+    using Ahead = std::pair<std::vector<FilePathRow>, std::vector<Result<FileMetadata>>>;
+    std::future<Ahead> next_md;
     bool stays = false;
     int32_t next_cursor = 0;
     const OnGrouped prefetch = [&](const sdcas_job_window& done) {
@@ -607,12 +608,28 @@ StepLoop run_steps(Library& db, uint64_t task_count, int32_t cursor, size_t batc
       const size_t last = done.rows - 1;
       next_cursor = rows[last].id;
       stays = !md[last].ok() || !md[last].value().cas_id;
-      next = fetch(next_cursor + 1, batch - (stays ? 1 : 0));
-      std::vector<FilePathRow> ahead;
-      if (stays) ahead.push_back(rows[last]);  // the same file; its row is re-read below
+      std::vector<FilePathRow> head;
+      if (stays) head.push_back(rows[last]);  // the same file; its row is re-read below
+      const size_t take = batch - (stays ? 1 : 0);
+      if (fetch_ahead) {
+        // the fetch too runs beside this batch's writes (a second connection)
+        next_md = std::async(std::launch::async, [&metadata, fetch_ahead, head = std::move(head), next_cursor, take] {
+          Ahead a;
+          a.first = (*fetch_ahead)(next_cursor + 1, take);
+          std::vector<FilePathRow> ahead = head;
+          ahead.insert(ahead.end(), a.first.begin(), a.first.end());
+          if (!ahead.empty()) a.second = metadata(ahead);
+          return a;
+        });
+        return;
+      }
+      next = fetch(next_cursor + 1, take);
+      std::vector<FilePathRow> ahead = std::move(head);
       ahead.insert(ahead.end(), next.begin(), next.end());
       if (ahead.empty()) return;
-      next_md = std::async(std::launch::async, [&metadata, ahead = std::move(ahead)] { return metadata(ahead); });
+      next_md = std::async(std::launch::async, [&metadata, ahead = std::move(ahead)] {
+        return Ahead{{}, metadata(ahead)};
+      });
     };
     auto [created, linked] = step_db(db, rows, md, group_by, &w, cs, &prefetch);
     if (w.steps == 0) break;  // cannot happen: a batch of `batch` >= cs rows holds a whole step
@@ -625,7 +642,13 @@ StepLoop run_steps(Library& db, uint64_t task_count, int32_t cursor, size_t batc
     L.cursor = rows[w.rows - 1].id;
     have_md = false;
     if (next_md.valid()) {
-      auto ahead_md = next_md.get();
+      Ahead got = next_md.get();
+      if (fetch_ahead) next = std::move(got.first);
+      auto ahead_md = std::move(got.second);
+      if (ahead_md.empty()) {  // nothing past the cursor, nor a cursor row to read again
+        if (steps_left) rows = fetch(L.cursor, batch);
+        continue;
+      }
       std::vector<FilePathRow> cur;
       if (stays) cur = fetch(L.cursor, 1);
       if (!stays || (cur.size() == 1 && cur[0].id == L.cursor)) {
@@ -667,10 +690,13 @@ FileIdentifierJobRunMetadata run_file_identifier_job_with(Library& db, const Fil
     }
   } bulk{db, init.bulk_identify && db.begin_bulk_identify(meta.total_orphan_paths)};
   meta.bulk_identify = bulk.on;
+  const Fetch ahead = [&](int32_t cursor, size_t take) {
+    return db.get_orphan_file_paths_concurrent(loc, cursor, sub, take);
+  };
   const StepLoop L = run_steps(
       db, task_count, meta.cursor, init.batch,
       [&](int32_t cursor, size_t take) { return db.get_orphan_file_paths(loc, cursor, sub, take); }, metadata,
-      group_by);
+      group_by, db.concurrent_orphan_reads() ? &ahead : nullptr);
   meta.total_objects_created = L.created;
   meta.total_objects_linked = L.linked;
   meta.steps = L.steps;

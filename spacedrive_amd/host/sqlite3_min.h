@@ -37,6 +37,7 @@ constexpr int SQLITE_OK = 0;
 constexpr int SQLITE_ROW = 100;
 constexpr int SQLITE_DONE = 101;
 constexpr int SQLITE_NULL = 5;
+constexpr int SQLITE_OPEN_READONLY = 0x00000001;
 constexpr int SQLITE_OPEN_READWRITE = 0x00000002;
 constexpr int SQLITE_OPEN_CREATE = 0x00000004;
 constexpr int SQLITE_OPEN_NOMUTEX = 0x00008000;

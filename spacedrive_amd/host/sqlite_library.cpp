@@ -4,6 +4,7 @@
 // (file_identifier_job.rs:251-319, mod.rs:157-342, validator_job.rs:107-172)
 // as prepared statements. See include/sdcore.hpp.
 #include <cstring>
+#include <mutex>
 #include <stdexcept>
 #include <unordered_map>
 
@@ -47,6 +48,13 @@ struct SqliteLibrary::Impl {
   Stmt count_orphans, get_orphans, set_cas, want_clear, want_add, existing, new_object, connect, no_checksum,
       set_checksum, add_path, get_path, all_objects, first_object, set_cas_connect;
   Stmt row_state, set_cas_connect_free, count_cas, load_first;
+  // the job's read-ahead connection (concurrent_orphan_reads): read-only, one
+  // statement, used by one thread at a time
+  std::string path;
+  sqlite3* rdb = nullptr;
+  Stmt r_get_orphans;
+  bool reader_tried = false;
+  std::mutex rmu;
   int64_t next_object = 1;
   bool cas_index = false;
   int batch_depth = 0;
@@ -80,6 +88,9 @@ struct SqliteLibrary::Impl {
     if (!bulk) return;
     if (batch_depth) exec("COMMIT");  // CREATE INDEX in its own transaction
     exec("CREATE INDEX IF NOT EXISTS file_path_cas_id_idx ON file_path (cas_id)");
+    // the WAL checkpoints the job deferred, once (begin_bulk_identify)
+    exec("PRAGMA wal_checkpoint(PASSIVE)");
+    exec("PRAGMA wal_autocheckpoint = 1000");
     if (batch_depth) exec("BEGIN IMMEDIATE");
     bulk = false;
     first.clear();
@@ -168,8 +179,10 @@ SqliteLibrary::SqliteLibrary(std::unique_ptr<Impl> d) : d_(std::move(d)) {}
 SqliteLibrary::~SqliteLibrary() {
   if (!d_) return;
   sqlite3* db = d_->db;
+  sqlite3* rdb = d_->rdb;
   Impl* p = d_.release();
-  delete p;  // statements finalize before the database closes
+  delete p;  // statements finalize before the databases close
+  if (rdb) sqlite3_close(rdb);
   if (db) sqlite3_close(db);
 }
 
@@ -206,6 +219,7 @@ std::unique_ptr<SqliteLibrary> SqliteLibrary::open(const std::string& path, bool
   if (object_id_index) d->exec("CREATE INDEX IF NOT EXISTS file_path_object_id_idx ON file_path (object_id)");
   d->exec("CREATE TEMP TABLE IF NOT EXISTS want_cas (cas_id TEXT PRIMARY KEY)");
   Impl& x = *d;
+  x.path = path;
   x.prepare(x.count_orphans, "SELECT COUNT(*) FROM file_path WHERE " SD_ORPHAN);
   // a rowid range scan from the cursor (the location index would make every
   // step rescan the whole location: quadratic over a job)
@@ -509,6 +523,9 @@ bool SqliteLibrary::begin_bulk_identify(size_t orphans) {
   if (rc != SQLITE_DONE) x.fail("load cas_ids");
   sqlite3_reset(x.load_first.s);
   x.exec("DROP INDEX IF EXISTS file_path_cas_id_idx");
+  // no WAL checkpoint after every ~1000 pages of the job's commits: one at
+  // the end (index_restore) writes each page back once
+  x.exec("PRAGMA wal_autocheckpoint = 0");
   x.bulk = true;
   return true;
 }
@@ -516,6 +533,52 @@ bool SqliteLibrary::begin_bulk_identify(size_t orphans) {
 void SqliteLibrary::end_bulk_identify() { d_->index_restore(); }
 
 bool SqliteLibrary::bulk_identify_active() const { return d_->bulk; }
+
+bool SqliteLibrary::concurrent_orphan_reads() {
+  Impl& x = *d_;
+  if (x.rdb) return true;
+  if (x.reader_tried || x.path.empty() || x.path == ":memory:" || x.path.rfind("file:", 0) == 0) return false;
+  x.reader_tried = true;
+  if (sqlite3_open_v2(x.path.c_str(), &x.rdb, SQLITE_OPEN_READONLY | SQLITE_OPEN_NOMUTEX, nullptr) != SQLITE_OK) {
+    if (x.rdb) sqlite3_close(x.rdb);
+    x.rdb = nullptr;
+    return false;
+  }
+  char* err = nullptr;
+  if (sqlite3_exec(x.rdb, "PRAGMA mmap_size = 4294967296", nullptr, nullptr, &err) != SQLITE_OK ||
+      sqlite3_prepare_v2(x.rdb,
+                         "SELECT " SD_COLS " FROM file_path NOT INDEXED WHERE " SD_ORPHAN
+                         " AND id >= ?3 ORDER BY id LIMIT ?4",
+                         -1, &x.r_get_orphans.s, nullptr) != SQLITE_OK) {
+    sqlite3_free(err);
+    if (x.r_get_orphans.s) sqlite3_finalize(x.r_get_orphans.s);
+    x.r_get_orphans.s = nullptr;
+    sqlite3_close(x.rdb);
+    x.rdb = nullptr;
+    return false;
+  }
+  return true;
+}
+
+std::vector<FilePathRow> SqliteLibrary::get_orphan_file_paths_concurrent(int32_t location_id, int32_t cursor,
+                                                                         const std::string& sub, size_t take) {
+  Impl& x = *d_;
+  if (!x.rdb) return get_orphan_file_paths(location_id, cursor, sub, take);
+  std::lock_guard<std::mutex> g(x.rmu);
+  Stmt& st = x.r_get_orphans;
+  sqlite3_bind_int64(st.s, 1, location_id);
+  sqlite3_bind_text(st.s, 2, sub.data(), (int)sub.size(), SQLITE_TRANSIENT);
+  sqlite3_bind_int64(st.s, 3, cursor);
+  sqlite3_bind_int64(st.s, 4, (int64_t)take);
+  std::vector<FilePathRow> out;
+  int rc;
+  while ((rc = sqlite3_step(st.s)) == SQLITE_ROW) out.push_back(Impl::row_of(st.s));
+  sqlite3_reset(st.s);
+  sqlite3_clear_bindings(st.s);
+  if (rc != SQLITE_DONE)
+    throw std::runtime_error(std::string("sqlite: read-ahead: ") + sqlite3_errmsg(x.rdb));
+  return out;
+}
 
 std::vector<FilePathRow> SqliteLibrary::file_paths_without_checksum(int32_t location_id, const std::string& sub) {
   Impl& x = *d_;

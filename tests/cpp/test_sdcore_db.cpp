@@ -356,9 +356,26 @@ static void test_parity(bool cas_index) {
     sql_bulk->add_file_paths(all);
     for (const auto& o : mem.objects) sql_bulk->create_object(o.kind, o.date_created);
   }
+  // and a file database in 1000-row batches: its job reads each next batch
+  // through a second connection while the current batch's writes are open
+  char fpath[] = "/tmp/sdcore_dbfXXXXXX";
+  {
+    const int fd = mkstemp(fpath);
+    if (fd >= 0) close(fd);
+    std::remove(fpath);
+  }
+  auto sql_file = SqliteLibrary::open(fpath, cas_index);
+  {
+    std::vector<FilePathRow> all = mem.file_paths;
+    sql_file->add_file_paths(all);
+    for (const auto& o : mem.objects) sql_file->create_object(o.kind, o.date_created);
+  }
+  CHECK(sql_file->concurrent_orphan_reads(), "a file database offers the read-ahead connection");
+  CHECK(!sql->concurrent_orphan_reads(), "an in-memory database does not");
   size_t rereads = 0;
   for (int32_t loc : {1, 2}) {
     const auto orphans = mem.get_orphan_file_paths(loc, 0, "", 1u << 30);
+    auto jf = run_job(*sql_file, loc, 1000, 400);
     auto jm = run_job(mem, loc, 100, 400);
     auto js = run_job(*sql, loc, 100, 400);
     auto jb = run_job(mem_b, loc, 1000, 400);
@@ -380,7 +397,7 @@ static void test_parity(bool cas_index) {
           "job loc %d vs the literal steps: created %zu/%zu linked %zu/%zu steps %zu/%zu cursor %d/%d", loc,
           jm.total_objects_created, jl.total_objects_created, jm.total_objects_linked, jl.total_objects_linked,
           jm.steps, jl.steps, jm.cursor, jl.cursor);
-    for (const auto* j : {&js, &jb, &jc, &jk})
+    for (const auto* j : {&js, &jb, &jc, &jk, &jf})
       CHECK(jm.total_objects_created == j->total_objects_created && jm.total_objects_linked == j->total_objects_linked &&
                 jm.steps == j->steps && jm.cursor == j->cursor && jm.rereads == j->rereads,
             "job loc %d: memory/100 %zu/%zu/%zu steps cursor %d rereads %zu, other %zu/%zu/%zu steps cursor %d "
@@ -413,8 +430,10 @@ static void test_parity(bool cas_index) {
     CHECK(s && same_row(*mem.file_path(id), *s), "row %d after the job", id);
     auto k = sql_bulk->file_path(id);
     CHECK(k && same_row(*mem.file_path(id), *k), "row %d after the bulk job", id);
+    auto f = sql_file->file_path(id);
+    CHECK(f && same_row(*mem.file_path(id), *f), "row %d after the file database's job", id);
   }
-  for (auto* lib : {sql.get(), sql_bulk.get()}) {
+  for (auto* lib : {sql.get(), sql_bulk.get(), sql_file.get()}) {
     auto so = lib->objects();
     CHECK(so.size() == mem.objects.size(), "object count %zu %zu", so.size(), mem.objects.size());
     for (size_t i = 0; i < so.size() && i < mem.objects.size(); ++i)
@@ -424,6 +443,8 @@ static void test_parity(bool cas_index) {
   }
   // the bulk job's library answers lookups as before (its index is back)
   CHECK(sql_bulk->existing_objects(want) == mem.existing_objects(want), "existing objects after the bulk job");
+  sql_file.reset();
+  for (const char* suf : {"", "-wal", "-shm"}) std::remove((std::string(fpath) + suf).c_str());
   // validator writes
   for (const auto& r : sql->file_paths_without_checksum(1, "/sub/")) {
     sql->set_integrity_checksum(r.id, std::string(64, 'b'));
@@ -525,6 +546,12 @@ struct Timed : Library {
   void end_batch() override { tm(7, [&] { d.end_batch(); }); }
   bool begin_bulk_identify(size_t n) override { return tm(3, [&] { return d.begin_bulk_identify(n); }); }
   void end_bulk_identify() override { tm(7, [&] { d.end_bulk_identify(); }); }
+  // the read-ahead runs beside the writes (not timed: it overlaps them)
+  bool concurrent_orphan_reads() override { return !reference_calls && d.concurrent_orphan_reads(); }
+  std::vector<FilePathRow> get_orphan_file_paths_concurrent(int32_t l, int32_t c, const std::string& s,
+                                                            size_t n) override {
+    return d.get_orphan_file_paths_concurrent(l, c, s, n);
+  }
 };
 
 static int bench(size_t n) {

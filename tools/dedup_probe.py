@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--files", type=int, default=0)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--existing", type=int, default=0, help="existing Objects (cas keys of the first K files)")
+    ap.add_argument("--tables", default="", help="A/B: comma-separated SDCAS_DEDUP_TABLE values, interleaved per rep")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -67,17 +68,25 @@ def main():
     torch.cuda.synchronize()
     del d_blob
     stages = DeviceStages(eng, 0)
-    ev = []
+    tables = [t for t in a.tables.split(",") if t] or [os.environ.get("SDCAS_DEDUP_TABLE", "")]
+    ev = {t: [] for t in tables}
+    links = {}
     link = counts = None
     for r in range(a.reps + 2):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        link, counts = stages.local(d_out, d_has, None, d_ids, 100, ek, ei)
-        e1.record(stream)
-        if r >= 2:
-            ev.append((e0, e1))
+        for t in tables:
+            if t:
+                os.environ["SDCAS_DEDUP_TABLE"] = t
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            link, counts = stages.local(d_out, d_has, None, d_ids, 100, ek, ei)
+            e1.record(stream)
+            if r >= 2:
+                ev[t].append((e0, e1))
+            if r == a.reps + 1 and len(tables) > 1:
+                links[t] = (link.clone(), counts.clone())
     torch.cuda.synchronize()
-    ms = [x.elapsed_time(y) for x, y in ev]
+    per = {t: [x.elapsed_time(y) for x, y in v] for t, v in ev.items()}
+    ms = per[tables[-1]]
     gk = d_out.cpu().numpy().view(np.uint64)
     distinct = int(np.unique(gk[sizes != 0]).size)
     algo = bench.dedup_bytes(n, a.existing)
@@ -87,6 +96,10 @@ def main():
            "algorithmic_bytes": algo, "algorithmic_gbps": algo / med / 1e6,
            "frac_of_hbm_peak": algo / med / 1e6 / bench.HBM_PEAK_GBS,
            "created_linked": [int(x) for x in counts.tolist()]}
+    if len(tables) > 1:
+        res["ab"] = {t: {"ms_median": float(np.median(v)), "ms_min": float(np.min(v))} for t, v in per.items()}
+        l0, c0 = links[tables[0]]
+        res["ab_equal"] = all(torch.equal(l0, l) and torch.equal(c0, c) for l, c in links.values())
     print(json.dumps(res), flush=True)
     eng.close()
     dist.destroy_process_group()
