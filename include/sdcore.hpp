@@ -246,6 +246,14 @@ class Library {
   }
   // mod.rs:290-327: object::create_unchecked(kind, date_created) -> object id
   virtual int32_t create_object(ObjectKind kind, int64_t date_created) = 0;
+  // object::create_many (mod.rs:314-327): Objects created in this order, ids
+  // returned in the same order (the default creates them one by one)
+  virtual std::vector<int32_t> create_objects(const std::vector<std::pair<ObjectKind, int64_t>>& kinds_dates) {
+    std::vector<int32_t> ids;
+    ids.reserve(kinds_dates.size());
+    for (const auto& [k, d] : kinds_dates) ids.push_back(create_object(k, d));
+    return ids;
+  }
   // connect_file_path_to_object (mod.rs:352-377)
   virtual void connect(int32_t file_path_id, int32_t object_id) = 0;
   // validator_job.rs:107-123: location_id = ? AND is_dir = false AND
@@ -354,6 +362,8 @@ class SqliteLibrary : public Library {
   void set_cas_id_and_connect(int32_t file_path_id, const std::optional<std::string>& cas_id,
                               int32_t object_id) override;
   int32_t create_object(ObjectKind kind, int64_t date_created) override;
+  // multi-row INSERTs of up to 64 Objects each
+  std::vector<int32_t> create_objects(const std::vector<std::pair<ObjectKind, int64_t>>& kinds_dates) override;
   void connect(int32_t file_path_id, int32_t object_id) override;
   std::vector<FilePathRow> file_paths_without_checksum(int32_t location_id, const std::string& sub) override;
   void set_integrity_checksum(int32_t file_path_id, const std::string& checksum) override;

@@ -706,48 +706,69 @@ __global__ void k_solo_apply(const uint64_t* __restrict__ ids, const uint32_t* _
   add_counts(c, l, sc, counts);
 }
 
-// The compact table of a world of one without existing Objects: one u32 per
-// slot, the lowest file index carrying the slot's key — 4 bytes a slot
-// instead of 16, so the table (and its clearing) is a quarter of the kv
-// table's and stays resident in the Infinity Cache (C5: 67 MB against 268 MB).
-// A slot's key is read back from keys[] (the index it holds), never stored:
-// every index ever written to a slot carries the same key, so the slot's key
-// never changes, and the atomicMin of later inserters leaves the lowest. ids
-// are ascending, so the lowest index has the lowest ordinal.
+// The compact table of a world of one: one u32 per slot, the lowest index
+// carrying the slot's key in a combined index space — file i is i, existing
+// Object j is n + j — so 4 bytes a slot instead of 16, a table (and its
+// clearing) a quarter of the kv table's that stays resident in the Infinity
+// Cache (C5: 67 MB against 268 MB). A slot's key is read back through the
+// index it holds, never stored: every index ever written to a slot carries
+// the same key, so the slot's key never changes, and the atomicMin of later
+// inserters leaves the lowest — a file whenever a file carries the key (ids
+// are ascending, so the lowest file index has the lowest ordinal). Existing
+// Objects fold their DB index into a u64 side array (emin) by slot, which
+// exists only when there are existing Objects.
 constexpr uint32_t kIdxEmpty = 0xFFFFFFFFu;
 
-__global__ void k_solo_insert_idx(const uint64_t* __restrict__ keys, const uint8_t* __restrict__ has_key,
-                                  const int32_t* __restrict__ status, uint32_t n, uint32_t* __restrict__ tab,
-                                  uint32_t mask, uint32_t shift, uint32_t* __restrict__ pos) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const bool ok = status == nullptr || status[i] == 0;  // mod.rs:125-141
-  const bool has = has_key == nullptr || has_key[i];    // mod.rs:83-86
-  if (!(ok && has)) {
-    pos[i] = !ok ? kSlotDropped : kSlotNoKey;
-    return;
+__device__ __forceinline__ uint64_t idx_key(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ ekeys,
+                                            uint32_t n, uint32_t x) {
+  return x < n ? keys[x] : ekeys[x - n];
+}
+
+// files (emin null, base 0): pos[i] = slot, or the code of a file without
+// one; existing Objects (emin set, base n): min-fold eids[j] into emin[slot]
+__global__ void k_solo_insert_idx(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ ekeys, uint32_t n,
+                                  const uint8_t* __restrict__ has_key, const int32_t* __restrict__ status,
+                                  const uint64_t* __restrict__ eids, uint32_t count, uint32_t base,
+                                  uint32_t* __restrict__ tab, unsigned long long* __restrict__ emin, uint32_t mask,
+                                  uint32_t shift, uint32_t* __restrict__ pos) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= count) return;
+  const uint32_t x = base + q;
+  if (!emin) {
+    const bool ok = status == nullptr || status[q] == 0;  // mod.rs:125-141
+    const bool has = has_key == nullptr || has_key[q];    // mod.rs:83-86
+    if (!(ok && has)) {
+      pos[q] = !ok ? kSlotDropped : kSlotNoKey;
+      return;
+    }
   }
-  const uint64_t key = keys[i];
+  const uint64_t key = idx_key(keys, ekeys, n, x);
   uint32_t h = (uint32_t)(key >> shift) & mask;
   for (;;) {
     uint32_t cur = __hip_atomic_load(&tab[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (cur == kIdxEmpty) {
-      const uint32_t prev = atomicCAS(&tab[h], kIdxEmpty, i);
+      const uint32_t prev = atomicCAS(&tab[h], kIdxEmpty, x);
       if (prev == kIdxEmpty) break;
       cur = prev;
     }
-    if (keys[cur] == key) {
-      if (cur > i) atomicMin(&tab[h], i);
+    if (idx_key(keys, ekeys, n, cur) == key) {
+      if (cur > x) atomicMin(&tab[h], x);
       break;
     }
     h = (h + 1) & mask;
   }
-  pos[i] = h;
+  if (emin) {
+    const unsigned long long v = eids[q];
+    if (__hip_atomic_load(&emin[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > v) atomicMin(&emin[h], v);
+  } else {
+    pos[q] = h;
+  }
 }
 
 __global__ void k_solo_apply_idx(const uint64_t* __restrict__ ids, const uint32_t* __restrict__ pos, uint32_t n,
-                                 const uint32_t* __restrict__ tab, uint64_t cs, const uint64_t* __restrict__ plan,
-                                 int64_t* __restrict__ link, unsigned long long* __restrict__ counts) {
+                                 const uint32_t* __restrict__ tab, const uint64_t* __restrict__ emin, uint64_t cs,
+                                 const uint64_t* __restrict__ plan, int64_t* __restrict__ link,
+                                 unsigned long long* __restrict__ counts) {
   __shared__ unsigned long long sc[2];
   if (threadIdx.x < 2) sc[threadIdx.x] = 0;
   __syncthreads();
@@ -758,16 +779,18 @@ __global__ void k_solo_apply_idx(const uint64_t* __restrict__ ids, const uint32_
     const int kind = h == kSlotDropped ? kFileDropped : h == kSlotNoKey ? kFileNoKey : kFileKeyed;
     int64_t r = 0;
     if (kind == kFileKeyed) {
-      const uint32_t f = tab[h];  // mod.rs:246-254: the key's first file
-      r = (int64_t)(f == i ? ids[i] : ids[f]);
+      // mod.rs:202-238: the first existing Object; else (mod.rs:246-254) the
+      // key's first file — a file, as this one carries the key
+      const uint64_t e = emin ? emin[h] : ~0ull;
+      const uint32_t f = tab[h];
+      r = e != ~0ull ? -(int64_t)e - 1 : (int64_t)(f == i ? ids[i] : ids[f]);
     }
     link[i] = step_link(kind, (int64_t)ids[i], r, cs, pv, c, l);
   }
   add_counts(c, l, sc, counts);
 }
 
-// SDCAS_DEDUP_TABLE=kv: the 16-byte (key, minimum) table for every call (the
-// compact table is the default when there are no existing Objects)
+// SDCAS_DEDUP_TABLE=kv: the 16-byte (key, minimum) table (round 3's; A/B)
 static bool dedup_compact_table() {
   const char* v = getenv("SDCAS_DEDUP_TABLE");
   return !(v && strcmp(v, "kv") == 0);
@@ -844,17 +867,25 @@ hipError_t dd_local(DistWs& w, const uint64_t* keys, const uint8_t* has_key, con
   uint64_t cap = 1024;
   while (cap < 2 * ((uint64_t)n + ne)) cap <<= 1;
   if (cap > (1ull << 31)) return hipErrorInvalidValue;
-  if (ne == 0 && dedup_compact_table()) {
+  if (dedup_compact_table()) {
     const uint32_t mask = (uint32_t)(cap - 1);
     const uint32_t shift = 64u - (uint32_t)__builtin_ctzll(cap);
-    // the u32 table borrows tmin's storage (cap u32 = cap / 4 of its u64)
-    if ((e = w.tmin.ensure(cap / 2 + 1)) || (e = w.tpos.ensure(n))) return e;
+    // the u32 table borrows tmin's storage (cap u32 = cap / 4 of its u64);
+    // the existing Objects' minima live in tkey (cap u64), when there are any
+    if ((e = w.tmin.ensure(cap / 2 + 1)) || (e = w.tpos.ensure(n)) || (ne && (e = w.tkey.ensure(cap + 1)))) return e;
     auto* tab = reinterpret_cast<uint32_t*>(w.tmin.p);
-    if ((e = hipMemsetAsync(tab, 0xFF, sizeof(uint32_t) * cap, st))) return e;
-    hipLaunchKernelGGL(k_solo_insert_idx, dim3(blocks(n)), dim3(TB), 0, st, keys, has_key, status, n, tab, mask, shift,
-                       w.tpos.p);
+    auto* em = ne ? reinterpret_cast<unsigned long long*>(w.tkey.p) : nullptr;
+    if ((e = hipMemsetAsync(tab, 0xFF, sizeof(uint32_t) * cap, st)) ||
+        (ne && (e = hipMemsetAsync(em, 0xFF, sizeof(uint64_t) * cap, st))))
+      return e;
+    if (ne)
+      hipLaunchKernelGGL(k_solo_insert_idx, dim3(blocks(ne)), dim3(TB), 0, st, keys, ekeys, n,
+                         (const uint8_t*)nullptr, (const int32_t*)nullptr, eids, ne, n, tab, em, mask, shift,
+                         (uint32_t*)nullptr);
+    hipLaunchKernelGGL(k_solo_insert_idx, dim3(blocks(n)), dim3(TB), 0, st, keys, ekeys, n, has_key, status,
+                       (const uint64_t*)nullptr, n, 0u, tab, (unsigned long long*)nullptr, mask, shift, w.tpos.p);
     hipLaunchKernelGGL(k_solo_apply_idx, dim3(blocks(n) < 1024 ? blocks(n) : 1024), dim3(TB), 0, st, ids, w.tpos.p, n,
-                       tab, chunk_size, w.plan.p, link, counts);
+                       tab, ne ? w.tkey.p : nullptr, chunk_size, w.plan.p, link, counts);
     return hipGetLastError();
   }
   // (key, file minimum) pairs in tmin, existing minima in tkey (when ne > 0)

@@ -7,11 +7,15 @@
 
 #include <algorithm>
 #include <cerrno>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <future>
 #include <set>
 #include <thread>
 #include <unordered_map>
+#include <unordered_set>
 
 namespace sdcore {
 
@@ -211,10 +215,15 @@ std::vector<FilePathRow> walk_location(const Location& location, std::vector<IoE
 
 // ---- MemoryLibrary ------------------------------------------------------------------
 
-static PubId pub_id_of(uint32_t tag, int32_t id) {
+// pub_ids in creation order: a tag, then the id big-endian in the last 8
+// bytes, so that consecutive rows sort together (memcmp order) — the
+// reference draws them at random (Uuid::new_v4, mod.rs:273), which is why it
+// cannot be matched byte for byte, and an ordered id keeps the UNIQUE index
+// on pub_id appending instead of inserting at random (as UUIDv7 does)
+static PubId pub_id_of(uint32_t tag, int64_t id) {
   PubId p{};
   std::memcpy(p.data(), &tag, 4);
-  std::memcpy(p.data() + 4, &id, 4);
+  for (int i = 0; i < 8; ++i) p[8 + i] = (uint8_t)((uint64_t)id >> (56 - 8 * i));
   return p;
 }
 
@@ -424,6 +433,43 @@ static bool reidentified(const FilePathRow& r, const Result<FileMetadata>& md) {
   return r.object_id && !r.cas_id && md.ok() && md.value().cas_id;
 }
 
+// SDCORE_TRACE_JOB=1: where the identifier job's wall time goes, per phase
+// of its main thread, summed over the job and printed to stderr at its end
+// (a diagnostic; the phases of the read-ahead thread overlap them)
+namespace {
+struct JobTrace {
+  enum { kMetadata, kWaitAhead, kFetch, kPlan, kCasWrites, kLookup, kGroupBy, kObjects, kIndex, kN };
+  bool on = [] {
+    const char* v = getenv("SDCORE_TRACE_JOB");
+    return v && *v && strcmp(v, "0") != 0;
+  }();
+  double t[kN] = {};
+  std::chrono::steady_clock::time_point m = std::chrono::steady_clock::now();
+  void mark() { m = std::chrono::steady_clock::now(); }
+  void lap(int k) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    t[k] += std::chrono::duration<double>(now - m).count();
+    m = now;
+  }
+  void print() const {
+    if (!on) return;
+    fprintf(stderr,
+            "sdcore job trace s: metadata %.3f wait_ahead %.3f fetch %.3f plan %.3f cas_writes %.3f lookup %.3f "
+            "group_by %.3f objects_links %.3f index %.3f\n",
+            t[kMetadata], t[kWaitAhead], t[kFetch], t[kPlan], t[kCasWrites], t[kLookup], t[kGroupBy], t[kObjects],
+            t[kIndex]);
+  }
+};
+thread_local JobTrace* g_trace = nullptr;
+void trace_lap(int k) {
+  if (g_trace) g_trace->lap(k);
+}
+void trace_mark() {
+  if (g_trace) g_trace->mark();
+}
+}  // namespace
+
 // after the group-by, before the Objects are written: the job's loop reads
 // its next batch there (run_steps)
 using OnGrouped = std::function<void(const sdcas_job_window& done)>;
@@ -449,6 +495,7 @@ static std::pair<size_t, size_t> step_db(Library& db, const std::vector<FilePath
     win.more = window->more;
   }
   // which rows the steps read: only theirs are written (mod.rs:157-178)
+  trace_mark();
   const StepPlan plan = plan_steps(md, chunk_size, win);
   const auto& step = plan.step;
   for (size_t i = 0; i < n; ++i)
@@ -458,7 +505,8 @@ static std::pair<size_t, size_t> step_db(Library& db, const std::vector<FilePath
   std::vector<uint8_t> has_key(n, 0);
   std::vector<int32_t> status(n, 0);
   std::vector<std::string> unique;
-  std::set<std::string> seen;
+  std::unordered_set<uint64_t> seen;  // by cas key: cas_ids are canonical 16-hex (cas.rs:61)
+  seen.reserve(n);
   // cas_id writes (mod.rs:157-178): a row with an Object now, since the
   // lookup below can find its Object by it; a row without one together with
   // its link (set_cas_id_and_connect), the same end state in one write
@@ -475,11 +523,12 @@ static std::pair<size_t, size_t> step_db(Library& db, const std::vector<FilePath
       has_key[i] = 1;
     }
     if (step[i] == UINT64_MAX) continue;  // no step reads it: it stays as it is
-    if (cas && seen.insert(*cas).second) unique.push_back(*cas);
+    if (cas && seen.insert(keys[i]).second) unique.push_back(*cas);
     if (file_paths[i].object_id) db.set_cas_id(file_paths[i].id, cas);
     else cas_pending[i] = 1;
   }
   db.end_batch();
+  trace_lap(JobTrace::kCasWrites);
   // the first existing Object carrying each cas_id, DB order (mod.rs:181-188
   // and the find of :214-224): one existing-key entry per cas_id
   std::vector<uint64_t> ekeys;
@@ -488,14 +537,17 @@ static std::pair<size_t, size_t> step_db(Library& db, const std::vector<FilePath
     ekeys.push_back(hex_to_key(c));
     eobj.push_back(oid);
   }
+  trace_lap(JobTrace::kLookup);
   sdcas_job_window gw{};
   gw.max_steps = win.max_steps;
   gw.more = win.more;
   auto d = group_by(keys, has_key, status, ekeys, gw);
+  trace_lap(JobTrace::kGroupBy);
   if (d.link.size() != n) throw std::logic_error("identifier_step_db: group-by returned a wrong link count");
   if (gw.steps != win.steps || gw.rows != win.rows)
     throw std::logic_error("identifier_step_db: the group-by ran other steps than the plan");
   if (on_grouped) (*on_grouped)(win);
+  trace_lap(JobTrace::kFetch);
   // new Objects (mod.rs:246-342) in the order the steps create them: step by
   // step, rows in id order within a step; a row without cas_id that several
   // steps read gets an Object from each, the last one its link. They take
@@ -518,9 +570,18 @@ static std::pair<size_t, size_t> step_db(Library& db, const std::vector<FilePath
     }
   };
   db.begin_batch();
-  for (const auto& [s, i] : creates) {
-    created_object[i] = db.create_object(md[i].value().kind, file_paths[i].date_created);
-    link_row(i, created_object[i]);
+  {
+    // object::create_many (mod.rs:314-327), then the links of :331-342
+    std::vector<std::pair<ObjectKind, int64_t>> kd;
+    kd.reserve(creates.size());
+    for (const auto& [s, i] : creates) kd.emplace_back(md[i].value().kind, file_paths[i].date_created);
+    const std::vector<int32_t> oids = db.create_objects(kd);
+    if (oids.size() != creates.size()) throw std::logic_error("identifier_step_db: create_objects returned a wrong count");
+    for (size_t k = 0; k < creates.size(); ++k) {
+      const size_t i = creates[k].second;
+      created_object[i] = oids[k];
+      link_row(i, created_object[i]);
+    }
   }
   // links to the first Object carrying the cas_id (mod.rs:202-238)
   for (size_t i = 0; i < n; ++i) {
@@ -531,6 +592,7 @@ static std::pair<size_t, size_t> step_db(Library& db, const std::vector<FilePath
   for (size_t i = 0; i < n; ++i)  // read but not linked (none such today)
     if (cas_pending[i]) db.set_cas_id(file_paths[i].id, md[i].value().cas_id);
   db.end_batch();
+  trace_lap(JobTrace::kObjects);
   if (window) *window = win;
   return {(size_t)d.created, (size_t)d.linked};
 }
@@ -577,7 +639,9 @@ StepLoop run_steps(Library& db, uint64_t task_count, int32_t cursor, size_t batc
       L.ran_dry = true;
       break;
     }
+    trace_mark();
     if (!have_md) md = metadata(rows);
+    trace_lap(JobTrace::kMetadata);
     if (L.batches && rows[0].id == L.cursor) ++L.rereads;  // the cursor row is still an orphan
     sdcas_job_window w{};
     w.max_steps = steps_left;
@@ -642,7 +706,9 @@ StepLoop run_steps(Library& db, uint64_t task_count, int32_t cursor, size_t batc
     L.cursor = rows[w.rows - 1].id;
     have_md = false;
     if (next_md.valid()) {
+      trace_mark();
       Ahead got = next_md.get();
+      trace_lap(JobTrace::kWaitAhead);
       if (fetch_ahead) next = std::move(got.first);
       auto ahead_md = std::move(got.second);
       if (ahead_md.empty()) {  // nothing past the cursor, nor a cursor row to read again
@@ -659,7 +725,9 @@ StepLoop run_steps(Library& db, uint64_t task_count, int32_t cursor, size_t batc
         continue;
       }
     }
+    trace_mark();
     if (steps_left) rows = fetch(L.cursor, batch);
+    trace_lap(JobTrace::kFetch);
   }
   return L;
 }
@@ -676,6 +744,15 @@ FileIdentifierJobRunMetadata run_file_identifier_job_with(Library& db, const Fil
   auto first = db.get_orphan_file_paths(loc, 0, sub, 1);
   meta.cursor = first.empty() ? 0 : first[0].id;
   const uint64_t task_count = (meta.total_orphan_paths + SDCAS_IDENTIFIER_CHUNK_SIZE - 1) / SDCAS_IDENTIFIER_CHUNK_SIZE;
+  JobTrace trace;
+  struct TraceScope {
+    JobTrace* t;
+    explicit TraceScope(JobTrace* x) : t(x) { g_trace = x->on ? x : nullptr; }
+    ~TraceScope() {
+      t->print();
+      g_trace = nullptr;
+    }
+  } trace_scope(&trace);
   // the lookup index traded for a host map for the job's duration, restored
   // on every way out (Library::begin_bulk_identify)
   struct Bulk {
@@ -683,8 +760,10 @@ FileIdentifierJobRunMetadata run_file_identifier_job_with(Library& db, const Fil
     bool on;
     ~Bulk() {
       if (!on) return;
+      trace_mark();
       try {
         db.end_bulk_identify();
+        trace_lap(JobTrace::kIndex);
       } catch (...) {  // unwinding already; the index is rebuilt by the next bulk job or existing_objects
       }
     }

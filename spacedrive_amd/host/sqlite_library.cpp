@@ -33,10 +33,12 @@ uint64_t from_be64(const void* p, int n) {
   return v;
 }
 
+// as MemoryLibrary's (sdcore.cpp pub_id_of): tag, then the id big-endian in
+// the last 8 bytes, so the UNIQUE pub_id index appends in creation order
 PubId pub_id(uint32_t tag, int64_t id) {
   PubId p{};
   std::memcpy(p.data(), &tag, 4);
-  std::memcpy(p.data() + 4, &id, 8);
+  for (int i = 0; i < 8; ++i) p[8 + i] = (uint8_t)((uint64_t)id >> (56 - 8 * i));
   return p;
 }
 
@@ -48,6 +50,8 @@ struct SqliteLibrary::Impl {
   Stmt count_orphans, get_orphans, set_cas, want_clear, want_add, existing, new_object, connect, no_checksum,
       set_checksum, add_path, get_path, all_objects, first_object, set_cas_connect;
   Stmt row_state, set_cas_connect_free, count_cas, load_first;
+  static constexpr int kManyObjects = 64;
+  Stmt new_objects;  // kManyObjects rows of (id, pub_id, kind, date_created)
   // the job's read-ahead connection (concurrent_orphan_reads): read-only, one
   // statement, used by one thread at a time
   std::string path;
@@ -87,7 +91,10 @@ struct SqliteLibrary::Impl {
   void index_restore() {
     if (!bulk) return;
     if (batch_depth) exec("COMMIT");  // CREATE INDEX in its own transaction
+    // the sorter may use helper threads for the one big sort (PRAGMA threads)
+    exec("PRAGMA threads = 4");
     exec("CREATE INDEX IF NOT EXISTS file_path_cas_id_idx ON file_path (cas_id)");
+    exec("PRAGMA threads = 0");
     // the WAL checkpoints the job deferred, once (begin_bulk_identify)
     exec("PRAGMA wal_checkpoint(PASSIVE)");
     exec("PRAGMA wal_autocheckpoint = 1000");
@@ -254,6 +261,11 @@ std::unique_ptr<SqliteLibrary> SqliteLibrary::open(const std::string& path, bool
               " (SELECT f2.object_id FROM file_path f2 WHERE f2.object_id IS NOT NULL AND f2.cas_id IN"
               " (SELECT cas_id FROM want_cas)) ORDER BY fp.object_id, fp.id");
   x.prepare(x.new_object, "INSERT INTO object (pub_id, kind, date_created) VALUES (?1, ?2, ?3)");
+  {
+    std::string q = "INSERT INTO object (id, pub_id, kind, date_created) VALUES ";
+    for (int k = 0; k < Impl::kManyObjects; ++k) q += k ? ", (?, ?, ?, ?)" : "(?, ?, ?, ?)";
+    x.prepare(x.new_objects, q.c_str());
+  }
   x.prepare(x.connect, "UPDATE file_path SET object_id = ?1 WHERE id = ?2");
   x.prepare(x.set_cas_connect, "UPDATE file_path SET cas_id = ?1, object_id = ?2 WHERE id = ?3");
   // first_objects: the smallest object id among the file_paths with the
@@ -445,6 +457,33 @@ int32_t SqliteLibrary::create_object(ObjectKind kind, int64_t date_created) {
   const int64_t id = sqlite3_last_insert_rowid(x.db);
   x.next_object = id + 1;
   return (int32_t)id;
+}
+
+std::vector<int32_t> SqliteLibrary::create_objects(const std::vector<std::pair<ObjectKind, int64_t>>& kinds_dates) {
+  Impl& x = *d_;
+  std::vector<int32_t> ids;
+  ids.reserve(kinds_dates.size());
+  size_t k = 0;
+  // whole groups of kManyObjects in one statement each, ids given explicitly
+  // (the ids the table would assign: one past its largest), the rest one by one
+  begin_batch();
+  for (; k + Impl::kManyObjects <= kinds_dates.size(); k += Impl::kManyObjects) {
+    sqlite3_stmt* st = x.new_objects.s;
+    for (int r = 0; r < Impl::kManyObjects; ++r) {
+      const int64_t id = x.next_object + r;
+      const PubId p = pub_id(0x4F424A54u, id);
+      sqlite3_bind_int64(st, 4 * r + 1, id);
+      sqlite3_bind_blob(st, 4 * r + 2, p.data(), 16, SQLITE_TRANSIENT);
+      sqlite3_bind_int64(st, 4 * r + 3, kinds_dates[k + r].first);
+      sqlite3_bind_int64(st, 4 * r + 4, kinds_dates[k + r].second);
+      ids.push_back((int32_t)id);
+    }
+    x.done(x.new_objects);
+    x.next_object += Impl::kManyObjects;
+  }
+  for (; k < kinds_dates.size(); ++k) ids.push_back(create_object(kinds_dates[k].first, kinds_dates[k].second));
+  end_batch();
+  return ids;
 }
 
 std::vector<std::pair<std::string, int32_t>> SqliteLibrary::first_objects(const std::vector<std::string>& cas_ids) {

@@ -537,6 +537,10 @@ struct Timed : Library {
     tm(8, [&] { d.set_cas_id_and_connect(i, c, o); });
   }
   int32_t create_object(ObjectKind k, int64_t t_) override { return tm(4, [&] { return d.create_object(k, t_); }); }
+  std::vector<int32_t> create_objects(const std::vector<std::pair<ObjectKind, int64_t>>& kd) override {
+    if (reference_calls) return Library::create_objects(kd);  // one insert per Object
+    return tm(4, [&] { return d.create_objects(kd); });
+  }
   void connect(int32_t f, int32_t o) override { tm(5, [&] { d.connect(f, o); }); }
   std::vector<FilePathRow> file_paths_without_checksum(int32_t l, const std::string& s) override {
     return d.file_paths_without_checksum(l, s);
