@@ -369,6 +369,11 @@ std::vector<Result<FileMetadata>> file_metadata_batch(Engine& engine,
       md[i].len = (uint64_t)sb.st_size;
     }
   };
+  static const bool trace = [] {
+    const char* v = getenv("SDCORE_TRACE_JOB");
+    return v && *v && strcmp(v, "0") != 0;
+  }();
+  const auto t0 = std::chrono::steady_clock::now();
   const size_t threads = std::min<size_t>(16, n / 512);
   if (threads < 2) {
     stat_range(0, n);
@@ -387,7 +392,12 @@ std::vector<Result<FileMetadata>> file_metadata_batch(Engine& engine,
       hashed_index.push_back(i);
     }
   }
+  const auto t1 = std::chrono::steady_clock::now();
   auto cas = engine.generate_cas_ids(to_hash);
+  if (trace)
+    fprintf(stderr, "sdcore file_metadata_batch: %zu files, stat+kind %.2f ms, cas_ids %.2f ms\n", n,
+            std::chrono::duration<double, std::milli>(t1 - t0).count(),
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count());
   for (size_t k = 0; k < cas.size(); ++k) {
     const size_t i = hashed_index[k];
     if (cas[k].ok()) md[i].cas_id = cas[k].value();
@@ -470,8 +480,8 @@ void trace_mark() {
 }
 }  // namespace
 
-// after the group-by, before the Objects are written: the job's loop reads
-// its next batch there (run_steps)
+// once the batch's steps are planned, before any of its writes: the job's
+// loop starts reading its next batch there (run_steps)
 using OnGrouped = std::function<void(const sdcas_job_window& done)>;
 
 static std::pair<size_t, size_t> step_db(Library& db, const std::vector<FilePathRow>& file_paths,
@@ -498,6 +508,11 @@ static std::pair<size_t, size_t> step_db(Library& db, const std::vector<FilePath
   trace_mark();
   const StepPlan plan = plan_steps(md, chunk_size, win);
   const auto& step = plan.step;
+  // the plan fixes which rows the steps read, so the job's read-ahead of its
+  // next batch (rows past the last of them) starts now, beside this batch's
+  // writes, lookup and group-by
+  if (on_grouped) (*on_grouped)(win);
+  trace_lap(JobTrace::kFetch);
   for (size_t i = 0; i < n; ++i)
     if (step[i] != UINT64_MAX && step[i] > 0 && reidentified(file_paths[i], md[i]))
       throw std::invalid_argument("identifier_step_db: a row to re-identify past the batch's first step");
@@ -546,8 +561,6 @@ static std::pair<size_t, size_t> step_db(Library& db, const std::vector<FilePath
   if (d.link.size() != n) throw std::logic_error("identifier_step_db: group-by returned a wrong link count");
   if (gw.steps != win.steps || gw.rows != win.rows)
     throw std::logic_error("identifier_step_db: the group-by ran other steps than the plan");
-  if (on_grouped) (*on_grouped)(win);
-  trace_lap(JobTrace::kFetch);
   // new Objects (mod.rs:246-342) in the order the steps create them: step by
   // step, rows in id order within a step; a row without cas_id that several
   // steps read gets an Object from each, the last one its link. They take

@@ -1,0 +1,18 @@
+#!/bin/bash
+# round 4: the job with its phase traces, then rocprofv3 kernel stats of the
+# four bench workloads at HEAD (the bench's own line is written beside each)
+set -o pipefail
+cd "$(dirname "$0")/.."
+OUT=${1:-gpurun_out/r04e}
+R=$(pwd)
+mkdir -p $OUT
+export TMPDIR=/tmp
+SDCORE_TRACE_JOB=1 SDCAS_TRACE_IO=1 timeout -k 10 300 tests/cpp/build/job_bench 100000 > $OUT/job_bench.json 2> $OUT/job_bench.err || exit 1
+echo "job ok"
+for w in c2 c3 c5; do
+  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$OUT/prof_$w -o $w --output-format csv -- \
+     python3 $R/bench.py --workload $w --steps 20 --warmup 2 --no-cpu-baseline --no-e2e > $R/$OUT/prof_$w.json 2> $R/$OUT/prof_$w.err) || exit 2
+done
+(cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$OUT/prof_c4 -o c4 --output-format csv -- \
+   python3 $R/bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline --no-e2e > $R/$OUT/prof_c4.json 2> $R/$OUT/prof_c4.err) || exit 3
+echo done
