@@ -27,9 +27,11 @@ def main():
                       "--no-cpu-baseline --no-e2e (C4: --steps 2 --warmup 1)"}
     for w, steps in (("c2", 20), ("c3", 20), ("c5", 20), ("c4", 2)):
         tr = glob.glob(os.path.join(src, f"prof_{w}", "**", f"{w}_kernel_trace.csv"), recursive=True)
-        b = bench_line(os.path.join(src, f"prof_{w}.log"))
+        logs = [os.path.join(src, f"prof_{w}.{x}") for x in ("log", "json")]
+        b = next((bench_line(x) for x in logs if os.path.exists(x)), None)
         if not tr or not b:
             continue
+        steps = int(b.get("steps", steps))
         rows = list(csv.DictReader(open(tr[0])))
         def launches(sub):
             return [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in
