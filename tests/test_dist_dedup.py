@@ -322,12 +322,18 @@ def test_rccl_world1(eng, oracle):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("table", ["idx", "kv"])
 @pytest.mark.parametrize("corpus,chunk_size", [("default", 100), ("default", 7), ("default", 1),
                                                ("collisions", 100), ("clustered", 100)])
-def test_device_local_vs_oracle(eng, oracle, corpus, chunk_size):
+def test_device_local_vs_oracle(eng, oracle, corpus, chunk_size, table, monkeypatch):
     """the fused single-rank path (sdcas_dev_dedup_local: no combine, files and
-    existing Objects straight into the resolve table) against the oracle"""
+    existing Objects straight into the resolve table) against the oracle, with
+    both tables (the compact u32 default, round 3's 16-byte kv table), and the
+    existing Objects passed in DB order and shuffled (their DB indices then
+    not ascending: the first Object is the lowest DB index, not the first
+    entry)"""
     from spacedrive_amd.dist_dedup import DeviceStages
+    monkeypatch.setenv("SDCAS_DEDUP_TABLE", table)
     if corpus == "default":
         keys, has, status, existing = make_corpus(91, 40000, pool=6000)
         keys[:2] = np.uint64(2**64 - 1)  # the table's empty marker is a legal key
@@ -347,9 +353,11 @@ def test_device_local_vs_oracle(eng, oracle, corpus, chunk_size):
     ek = torch.from_numpy(existing.view(np.int64)).cuda()
     eids = torch.arange(existing.size, dtype=torch.int64, device="cuda")
     st = DeviceStages(eng)
-    for with_existing in (True, False):
-        link, cnt = st.local(k, h, s, ids, chunk_size, ek if with_existing else None,
-                             eids if with_existing else None)
+    order = torch.from_numpy(np.random.default_rng(5).permutation(existing.size)).cuda()
+    for with_existing in (True, "shuffled", False):
+        e_k, e_i = (ek, eids) if with_existing is True else (ek[order], eids[order])
+        link, cnt = st.local(k, h, s, ids, chunk_size, e_k if with_existing else None,
+                             e_i if with_existing else None)
         want, wc, wl = oracle.identifier_dedup(keys, has, status, chunk_size,
                                                existing if with_existing else np.zeros(0, np.uint64))
         assert np.array_equal(link.cpu().numpy(), want)

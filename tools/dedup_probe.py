@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--existing", type=int, default=0, help="existing Objects (cas keys of the first K files)")
     ap.add_argument("--tables", default="", help="A/B: comma-separated SDCAS_DEDUP_TABLE values, interleaved per rep")
+    ap.add_argument("--world", type=int, default=1,
+                    help="> 1: one rank's device stages of the bucket protocol at this world size (combine_buckets, "
+                         "resolve_buckets over its own buckets as if received, apply), each timed; no exchange")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -68,6 +71,29 @@ def main():
     torch.cuda.synchronize()
     del d_blob
     stages = DeviceStages(eng, 0)
+    if a.world > 1:
+        W = a.world
+        cap = int(n / W * 1.125) + 256
+        tm = {"combine_buckets": [], "resolve_buckets": [], "apply": []}
+        for r in range(a.reps + 2):
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            ev[0].record(stream)
+            send, slot, cnt, ovf = stages.combine_buckets(d_out, d_has, None, d_ids, W, cap)
+            ev[1].record(stream)
+            res = stages.resolve_buckets(send, cap, cnt, None, 0, None, W)
+            ev[2].record(stream)
+            link, counts = stages.apply(d_ids, slot, res, 100)
+            ev[3].record(stream)
+            if r >= 2:
+                for k, (x, y) in zip(tm, zip(ev[:-1], ev[1:])):
+                    tm[k].append((x, y))
+        torch.cuda.synchronize()
+        out = {k: float(np.median([x.elapsed_time(y) for x, y in v])) for k, v in tm.items()}
+        print(json.dumps({"workload": a.workload.upper(), "files": n, "world": W, "bucket_cap": cap,
+                          "overflow": int(ovf.item()), "ms_median": out, "ms_total": sum(out.values())}), flush=True)
+        eng.close()
+        dist.destroy_process_group()
+        return
     tables = [t for t in a.tables.split(",") if t] or [os.environ.get("SDCAS_DEDUP_TABLE", "")]
     ev = {t: [] for t in tables}
     links = {}
