@@ -481,12 +481,122 @@ __global__ void k_dd_slot_remap(const uint64_t* __restrict__ rec, const uint32_t
   slot[i] = p < cap ? r * cap + p : kSlotNoKey;
 }
 
+// (defined with the world-of-one path below)
+__global__ void k_solo_insert_idx(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ ekeys, uint32_t n,
+                                  const uint8_t* __restrict__ has_key, const int32_t* __restrict__ status,
+                                  const uint64_t* __restrict__ eids, uint32_t count, uint32_t base,
+                                  uint32_t* __restrict__ tab, unsigned long long* __restrict__ emin, uint32_t mask,
+                                  uint32_t shift, uint32_t* __restrict__ pos);
+
+// ---- the bucket combine through a hash table (SDCAS_COMBINE=hash) -------------
+//
+// The same outputs as the sort-based combine below — one (key, min ordinal)
+// record per distinct key in its owner's bucket, each file's bucket position
+// — from the compact table of the world-of-one path: insert (the lowest file
+// index per key), then each key's lowest file emits the record into its
+// owner's bucket at a position taken by a wave-aggregated atomicAdd (one per
+// owner present in the wave), then every file reads its key's position. No
+// sort; the records of a bucket are in no particular order, which neither the
+// exchange nor the owner's resolve needs.
+__global__ void k_cb_emit(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ ids, uint32_t n,
+                          const uint32_t* __restrict__ pos, const uint32_t* __restrict__ tab, uint32_t world,
+                          uint32_t cap, uint32_t* __restrict__ fill, uint64_t* __restrict__ send,
+                          uint32_t* __restrict__ bpos, uint32_t* __restrict__ overflow) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  bool mine = false;
+  uint32_t r = 0;
+  uint64_t key = 0;
+  if (i < n) {
+    const uint32_t h = pos[i];
+    if (h < kSlotDropped && tab[h] == i) {  // the key's lowest file carries its record
+      key = keys[i];
+      r = dd_owner(key, world);
+      mine = true;
+    }
+  }
+  // one atomicAdd per owner present in the wave
+  uint64_t pending = __ballot(mine);
+  uint32_t p = 0;
+  while (pending) {
+    const int leader = __ffsll((long long)pending) - 1;
+    const uint32_t r0 = __shfl(r, leader);
+    const uint64_t grp = __ballot(mine && r == r0);
+    uint32_t base = 0;
+    if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(&fill[r0], (uint32_t)__popcll(grp));
+    base = __shfl(base, leader);
+    if (mine && r == r0) {
+      p = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(grp >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)grp, 0u));
+      mine = false;
+    }
+    pending &= ~grp;
+  }
+  if (i >= n) return;
+  const uint32_t h = pos[i];
+  if (h >= kSlotDropped || tab[h] != i) return;
+  if (p >= cap) {
+    atomicOr(overflow, 1u);  // the caller reruns the exact stages
+    bpos[i] = kSlotNoKey;
+    return;
+  }
+  const uint64_t q = (uint64_t)r * cap + p;
+  send[2 * q] = key;
+  send[2 * q + 1] = ids[i];
+  bpos[i] = (uint32_t)q;
+}
+
+__global__ void k_cb_slot(const uint32_t* __restrict__ pos, const uint32_t* __restrict__ tab,
+                          const uint32_t* __restrict__ bpos, uint32_t n, uint32_t* __restrict__ slot) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t h = pos[i];
+  slot[i] = h >= kSlotDropped ? h : bpos[tab[h]];
+}
+
+__global__ void k_cb_counts(const uint32_t* __restrict__ fill, uint32_t world, uint32_t cap,
+                            int64_t* __restrict__ counts) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < world) counts[r] = fill[r] < cap ? fill[r] : cap;
+}
+
+static bool combine_by_hash() {
+  const char* v = getenv("SDCAS_COMBINE");
+  return v && strcmp(v, "hash") == 0;
+}
+
+static hipError_t combine_buckets_hash(DistWs& w, const uint64_t* keys, const uint8_t* has_key,
+                                       const int32_t* status, const uint64_t* ids, uint32_t n, uint32_t world,
+                                       uint32_t cap, uint64_t* send, uint32_t* slot, int64_t* counts,
+                                       uint32_t* overflow, hipStream_t st) {
+  uint64_t tcap = 1024;
+  while (tcap < 2 * (uint64_t)n) tcap <<= 1;
+  if (tcap > (1ull << 31)) return hipErrorInvalidValue;
+  hipError_t e;
+  if ((e = w.idx_a.ensure(tcap)) || (e = w.idx_b.ensure(n)) || (e = w.tpos.ensure(n)) ||
+      (e = w.starts.ensure(world + 1)))
+    return e;
+  const uint32_t mask = (uint32_t)(tcap - 1);
+  const uint32_t shift = 64u - (uint32_t)__builtin_ctzll(tcap);
+  if ((e = hipMemsetAsync(w.idx_a.p, 0xFF, sizeof(uint32_t) * tcap, st)) ||
+      (e = hipMemsetAsync(w.starts.p, 0, sizeof(uint32_t) * (world + 1), st)))
+    return e;
+  hipLaunchKernelGGL(k_solo_insert_idx, dim3(blocks(n)), dim3(TB), 0, st, keys, (const uint64_t*)nullptr, n, has_key,
+                     status, (const uint64_t*)nullptr, n, 0u, w.idx_a.p, (unsigned long long*)nullptr, mask, shift,
+                     w.idx_b.p);
+  hipLaunchKernelGGL(k_cb_emit, dim3(blocks(n)), dim3(TB), 0, st, keys, ids, n, w.idx_b.p, w.idx_a.p, world, cap,
+                     w.starts.p, send, w.tpos.p, overflow);
+  hipLaunchKernelGGL(k_cb_counts, dim3(blocks(world)), dim3(TB), 0, st, w.starts.p, world, cap, counts);
+  if (slot) hipLaunchKernelGGL(k_cb_slot, dim3(blocks(n)), dim3(TB), 0, st, w.idx_b.p, w.idx_a.p, w.tpos.p, n, slot);
+  return hipGetLastError();
+}
+
 hipError_t dd_combine_buckets(DistWs& w, const uint64_t* keys, const uint8_t* has_key, const int32_t* status,
                               const uint64_t* ids, uint32_t n, uint32_t world, uint32_t cap, uint64_t* send,
                               uint32_t* slot, int64_t* counts, uint32_t* overflow, hipStream_t st) {
   hipError_t e;
   if ((e = hipMemsetAsync(overflow, 0, sizeof(uint32_t), st))) return e;
   if (n == 0) return hipMemsetAsync(counts, 0, sizeof(int64_t) * world, st);
+  if (combine_by_hash())
+    return combine_buckets_hash(w, keys, has_key, status, ids, n, world, cap, send, slot, counts, overflow, st);
   if ((e = w.ukey.ensure(2 * (size_t)n))) return e;
   if ((e = combine_core(w, keys, has_key, status, ids, n, world, w.ukey.p, slot, st))) return e;
   hipLaunchKernelGGL(k_dd_pack, dim3(blocks(n)), dim3(TB), 0, st, w.ukey.p, w.scan.p, w.nvalid.p, w.starts.p, world,

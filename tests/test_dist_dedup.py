@@ -533,3 +533,34 @@ def test_meta_group_of_a_subgroup():
                            start_method="spawn")
         res = [list(np.load(os.path.join(d, f"r{r}.npy"), allow_pickle=True)) for r in range(world)]
     assert res[0] == [True, True, True] and res[1] == [True, True, True] and res[2] == []
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("combine", ["sort", "hash"])
+@pytest.mark.parametrize("R,chunk_size", [(2, 100), (8, 100), (5, 7)])
+def test_device_bucket_protocol_vs_oracle(eng, oracle, R, chunk_size, combine, monkeypatch):
+    """the bucket protocol's device stages (combine_buckets -> equal-split
+    exchange -> resolve_buckets -> apply) over R virtual ranks with existing
+    Objects, both combines: the radix-sort one and the hash-table one
+    (SDCAS_COMBINE=hash); then buckets one record too small, which must raise
+    the overflow flag (the caller then reruns the exact stages)"""
+    from spacedrive_amd.dist_dedup import DeviceStages
+    from tests._dist_stages import dedup_virtual_buckets
+    monkeypatch.setenv("SDCAS_COMBINE", combine)
+    keys, has, status, existing = make_corpus(700 + R, 24000, pool=5000, p_none=0.05, p_err=0.05)
+    want, wc, wl = oracle.identifier_dedup(keys, has, status, chunk_size, existing)
+    shards, ex = shard(keys, has, status, existing, R, device="cuda")
+    st = DeviceStages(eng)
+    n = max(int(s[3].numel()) for s in shards)
+    caps = (n + 1, max(int(e[0].numel()) for e in ex) + 1)
+    links, c, l, over = dedup_virtual_buckets(lambda r: st, shards, chunk_size, ex, caps)
+    assert not over
+    assert np.array_equal(np.concatenate([x.cpu().numpy() for x in links]), want)
+    assert (c, l) == (wc, wl)
+    # the largest bucket's fill, then one less capacity: overflow
+    fills = []
+    for (k, h, s, ids) in shards:
+        _, _, cnt, _ = st.combine_buckets(k, h, s, ids, R, caps[0])
+        fills.append(int(cnt.max()))
+    _, _, _, over = dedup_virtual_buckets(lambda r: st, shards, chunk_size, ex, (max(fills) - 1, caps[1]))
+    assert over

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--existing", type=int, default=0, help="existing Objects (cas keys of the first K files)")
     ap.add_argument("--tables", default="", help="A/B: comma-separated SDCAS_DEDUP_TABLE values, interleaved per rep")
+    ap.add_argument("--combines", default="sort", help="--world > 1: comma-separated SDCAS_COMBINE values (A/B)")
     ap.add_argument("--world", type=int, default=1,
                     help="> 1: one rank's device stages of the bucket protocol at this world size (combine_buckets, "
                          "resolve_buckets over its own buckets as if received, apply), each timed; no exchange")
@@ -74,23 +75,34 @@ def main():
     if a.world > 1:
         W = a.world
         cap = int(n / W * 1.125) + 256
-        tm = {"combine_buckets": [], "resolve_buckets": [], "apply": []}
+        combines = [c for c in a.combines.split(",") if c]
+        tm = {c: {"combine_buckets": [], "resolve_buckets": [], "apply": []} for c in combines}
+        links = {}
+        ovf = None
         for r in range(a.reps + 2):
-            ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-            ev[0].record(stream)
-            send, slot, cnt, ovf = stages.combine_buckets(d_out, d_has, None, d_ids, W, cap)
-            ev[1].record(stream)
-            res = stages.resolve_buckets(send, cap, cnt, None, 0, None, W)
-            ev[2].record(stream)
-            link, counts = stages.apply(d_ids, slot, res, 100)
-            ev[3].record(stream)
-            if r >= 2:
-                for k, (x, y) in zip(tm, zip(ev[:-1], ev[1:])):
-                    tm[k].append((x, y))
+            for c in combines:
+                os.environ["SDCAS_COMBINE"] = c
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+                ev[0].record(stream)
+                send, slot, cnt, ovf = stages.combine_buckets(d_out, d_has, None, d_ids, W, cap)
+                ev[1].record(stream)
+                res = stages.resolve_buckets(send, cap, cnt, None, 0, None, W)
+                ev[2].record(stream)
+                link, counts = stages.apply(d_ids, slot, res, 100)
+                ev[3].record(stream)
+                if r >= 2:
+                    for k, (x, y) in zip(tm[c], zip(ev[:-1], ev[1:])):
+                        tm[c][k].append((x, y))
+                if r == a.reps + 1:
+                    links[c] = (link.clone(), counts.clone())
         torch.cuda.synchronize()
-        out = {k: float(np.median([x.elapsed_time(y) for x, y in v])) for k, v in tm.items()}
+        out = {c: {k: float(np.median([x.elapsed_time(y) for x, y in v])) for k, v in t.items()} for c, t in tm.items()}
+        l0, c0 = links[combines[0]]
         print(json.dumps({"workload": a.workload.upper(), "files": n, "world": W, "bucket_cap": cap,
-                          "overflow": int(ovf.item()), "ms_median": out, "ms_total": sum(out.values())}), flush=True)
+                          "overflow": int(ovf.item()), "ms_median": out,
+                          "ms_total": {c: sum(v.values()) for c, v in out.items()},
+                          "equal": all(torch.equal(l0, l) and torch.equal(c0, x) for l, x in links.values())}),
+              flush=True)
         eng.close()
         dist.destroy_process_group()
         return
