@@ -932,7 +932,8 @@ def main():
     if W["dedup"]:
         d_has = (d_sizes != 0).to(torch.uint8)  # mod.rs:78-86: empty files have no cas_id
         d_ids = torch.from_numpy(ids).to(dev)
-        stages = DeviceStages(eng, dev.index)
+        # the dedup's stages on the step's own stream (no cross-stream waits)
+        stages = DeviceStages(eng, dev.index, same_stream=True)
         stages.time_exchange = distributed
         dd = {"ev": []}
 

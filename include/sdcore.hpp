@@ -373,7 +373,9 @@ class SqliteLibrary : public Library {
   // with a cas_id (loading them costs less than indexing the job's rows one
   // by one): the index goes, a host map of its MIN(object_id) per cas_id
   // stays; a write that could make the map stale (a row with an Object and
-  // a cas_id gets another of either) restores the index first
+  // a cas_id gets another of either) restores the index first — inside a
+  // batch that commits the batch's writes so far and opens a new
+  // transaction for the rest (CREATE INDEX runs in its own)
   bool begin_bulk_identify(size_t orphans) override;
   void end_bulk_identify() override;
   bool bulk_identify_active() const;

@@ -494,54 +494,63 @@ __global__ void k_solo_insert_idx(const uint64_t* __restrict__ keys, const uint6
 // record per distinct key in its owner's bucket, each file's bucket position
 // — from the compact table of the world-of-one path: insert (the lowest file
 // index per key), then each key's lowest file emits the record into its
-// owner's bucket at a position taken by a wave-aggregated atomicAdd (one per
-// owner present in the wave), then every file reads its key's position. No
+// owner's bucket at a position taken per workgroup (LDS counters, one global
+// atomicAdd per owner present), then every file reads its key's position. No
 // sort; the records of a bucket are in no particular order, which neither the
 // exchange nor the owner's resolve needs.
-__global__ void k_cb_emit(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ ids, uint32_t n,
-                          const uint32_t* __restrict__ pos, const uint32_t* __restrict__ tab, uint32_t world,
-                          uint32_t cap, uint32_t* __restrict__ fill, uint64_t* __restrict__ send,
-                          uint32_t* __restrict__ bpos, uint32_t* __restrict__ overflow) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  bool mine = false;
-  uint32_t r = 0;
-  uint64_t key = 0;
-  if (i < n) {
-    const uint32_t h = pos[i];
-    if (h < kSlotDropped && tab[h] == i) {  // the key's lowest file carries its record
-      key = keys[i];
-      r = dd_owner(key, world);
-      mine = true;
+constexpr uint32_t kEmitR = 16;          // files per thread: 4096 per workgroup
+constexpr uint32_t kEmitMaxWorld = 256;  // owners a workgroup counts in LDS (more: the sort combine)
+
+__global__ void __launch_bounds__(TB) k_cb_emit(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ ids,
+                                                uint32_t n, const uint32_t* __restrict__ pos,
+                                                const uint32_t* __restrict__ tab, uint32_t world, uint32_t cap,
+                                                uint32_t* __restrict__ fill, uint64_t* __restrict__ send,
+                                                uint32_t* __restrict__ bpos, uint32_t* __restrict__ overflow) {
+  // positions are taken per workgroup: LDS counters per owner, then ONE
+  // global atomicAdd per owner present in the workgroup (a wave-level
+  // aggregate left ~ 8 atomics per wave on `world` addresses: 7.5 ms for
+  // C5's 6.25 M files at world 8, profiles/r04_dedup_world.json)
+  __shared__ uint32_t s_cnt[kEmitMaxWorld], s_base[kEmitMaxWorld];
+  for (uint32_t t = threadIdx.x; t < world; t += TB) s_cnt[t] = 0;
+  __syncthreads();
+  const uint64_t i0 = (uint64_t)blockIdx.x * TB * kEmitR + threadIdx.x;
+  uint32_t h[kEmitR], lp[kEmitR], rr[kEmitR];
+#pragma unroll
+  for (uint32_t k = 0; k < kEmitR; ++k) {
+    const uint64_t i = i0 + (uint64_t)k * TB;
+    h[k] = i < n ? pos[i] : kSlotDropped;
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < kEmitR; ++k) {
+    const uint64_t i = i0 + (uint64_t)k * TB;
+    // the key's lowest file carries its record
+    lp[k] = h[k] < kSlotDropped && tab[h[k]] == (uint32_t)i ? 0u : ~0u;
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < kEmitR; ++k) {
+    rr[k] = 0;
+    if (lp[k] == ~0u) continue;
+    rr[k] = dd_owner(keys[i0 + (uint64_t)k * TB], world);
+    lp[k] = atomicAdd(&s_cnt[rr[k]], 1u);
+  }
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t < world; t += TB) s_base[t] = s_cnt[t] ? atomicAdd(&fill[t], s_cnt[t]) : 0u;
+  __syncthreads();
+#pragma unroll
+  for (uint32_t k = 0; k < kEmitR; ++k) {
+    if (lp[k] == ~0u) continue;
+    const uint64_t i = i0 + (uint64_t)k * TB;
+    const uint32_t p = s_base[rr[k]] + lp[k];
+    if (p >= cap) {
+      atomicOr(overflow, 1u);  // the caller reruns the exact stages
+      bpos[i] = kSlotNoKey;
+      continue;
     }
+    const uint64_t q = (uint64_t)rr[k] * cap + p;
+    send[2 * q] = keys[i];
+    send[2 * q + 1] = ids[i];
+    bpos[i] = (uint32_t)q;
   }
-  // one atomicAdd per owner present in the wave
-  uint64_t pending = __ballot(mine);
-  uint32_t p = 0;
-  while (pending) {
-    const int leader = __ffsll((long long)pending) - 1;
-    const uint32_t r0 = __shfl(r, leader);
-    const uint64_t grp = __ballot(mine && r == r0);
-    uint32_t base = 0;
-    if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(&fill[r0], (uint32_t)__popcll(grp));
-    base = __shfl(base, leader);
-    if (mine && r == r0) {
-      p = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(grp >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)grp, 0u));
-      mine = false;
-    }
-    pending &= ~grp;
-  }
-  if (i >= n) return;
-  const uint32_t h = pos[i];
-  if (h >= kSlotDropped || tab[h] != i) return;
-  if (p >= cap) {
-    atomicOr(overflow, 1u);  // the caller reruns the exact stages
-    bpos[i] = kSlotNoKey;
-    return;
-  }
-  const uint64_t q = (uint64_t)r * cap + p;
-  send[2 * q] = key;
-  send[2 * q + 1] = ids[i];
-  bpos[i] = (uint32_t)q;
 }
 
 __global__ void k_cb_slot(const uint32_t* __restrict__ pos, const uint32_t* __restrict__ tab,
@@ -582,7 +591,8 @@ static hipError_t combine_buckets_hash(DistWs& w, const uint64_t* keys, const ui
   hipLaunchKernelGGL(k_solo_insert_idx, dim3(blocks(n)), dim3(TB), 0, st, keys, (const uint64_t*)nullptr, n, has_key,
                      status, (const uint64_t*)nullptr, n, 0u, w.idx_a.p, (unsigned long long*)nullptr, mask, shift,
                      w.idx_b.p);
-  hipLaunchKernelGGL(k_cb_emit, dim3(blocks(n)), dim3(TB), 0, st, keys, ids, n, w.idx_b.p, w.idx_a.p, world, cap,
+  hipLaunchKernelGGL(k_cb_emit, dim3((uint32_t)((n + TB * kEmitR - 1) / (TB * kEmitR))), dim3(TB), 0, st, keys, ids,
+                     n, w.idx_b.p, w.idx_a.p, world, cap,
                      w.starts.p, send, w.tpos.p, overflow);
   hipLaunchKernelGGL(k_cb_counts, dim3(blocks(world)), dim3(TB), 0, st, w.starts.p, world, cap, counts);
   if (slot) hipLaunchKernelGGL(k_cb_slot, dim3(blocks(n)), dim3(TB), 0, st, w.idx_b.p, w.idx_a.p, w.tpos.p, n, slot);
@@ -595,7 +605,7 @@ hipError_t dd_combine_buckets(DistWs& w, const uint64_t* keys, const uint8_t* ha
   hipError_t e;
   if ((e = hipMemsetAsync(overflow, 0, sizeof(uint32_t), st))) return e;
   if (n == 0) return hipMemsetAsync(counts, 0, sizeof(int64_t) * world, st);
-  if (combine_by_hash())
+  if (combine_by_hash() && world <= kEmitMaxWorld)
     return combine_buckets_hash(w, keys, has_key, status, ids, n, world, cap, send, slot, counts, overflow, st);
   if ((e = w.ukey.ensure(2 * (size_t)n))) return e;
   if ((e = combine_core(w, keys, has_key, status, ids, n, world, w.ukey.p, slot, st))) return e;

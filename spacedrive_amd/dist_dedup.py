@@ -59,16 +59,30 @@ class DeviceStages:
     "the context's non-blocking stream", so it is never handed over as is).
     """
 
-    def __init__(self, engine, device=None):
+    def __init__(self, engine, device=None, same_stream=False):
         self.eng = engine
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
         self.stream = torch.cuda.Stream(self.device)
+        # same_stream: enqueue on the caller's current stream when it is a
+        # real stream (not the legacy NULL stream) — no cross-stream event
+        # wait on either side of every stage (≈ 20 µs each, measured in the
+        # C5 step's trace)
+        self.same_stream = same_stream
+
+    def _current(self):
+        cur = torch.cuda.current_stream(self.device)
+        return cur if self.same_stream and cur.cuda_stream else None
 
     def _enter(self):
+        cur = self._current()
+        if cur is not None:
+            return cur.cuda_stream
         self.stream.wait_stream(torch.cuda.current_stream(self.device))
         return self.stream.cuda_stream
 
     def _leave(self, *tensors):
+        if self._current() is not None:
+            return
         for t in tensors:
             if t is not None and t.is_cuda:
                 t.record_stream(self.stream)
