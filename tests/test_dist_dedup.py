@@ -217,6 +217,25 @@ def test_device_stages_virtual_vs_oracle(eng, oracle, R, chunk_size):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("R", [1, 3])
+def test_device_stages_on_callers_stream(eng, oracle, R):
+    """same_stream=True (the bench's setting): the stages enqueue on the
+    caller's current stream, with no cross-stream waits; same links"""
+    from spacedrive_amd.dist_dedup import DeviceStages
+    keys, has, status, existing = make_corpus(70 + R, 30000, pool=5000)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        shards, ex = shard(keys, has, status, existing, R, device="cuda")
+        st = DeviceStages(eng, same_stream=True)
+        assert st._current() is not None and st._enter() == s.cuda_stream
+        links, c, l = dedup_virtual(lambda r: st, shards, 100, ex)
+        got = np.concatenate([x.cpu().numpy() for x in links])
+    want, wc, wl = oracle.identifier_dedup(keys, has, status, 100, existing)
+    assert np.array_equal(got, want)
+    assert (c, l) == (wc, wl)
+
+
+@pytest.mark.gpu
 def test_device_stages_match_numpy_stages(eng):
     """stage by stage, device vs numpy restatement (records, slots, answers)"""
     from spacedrive_amd.dist_dedup import DeviceStages
