@@ -488,7 +488,7 @@ __global__ void k_solo_insert_idx(const uint64_t* __restrict__ keys, const uint6
                                   uint32_t* __restrict__ tab, unsigned long long* __restrict__ emin, uint32_t mask,
                                   uint32_t shift, uint32_t* __restrict__ pos);
 
-// ---- the bucket combine through a hash table (SDCAS_COMBINE=hash) -------------
+// ---- the bucket combine through a hash table (default; SDCAS_COMBINE=sort: radix sort) --
 //
 // The same outputs as the sort-based combine below — one (key, min ordinal)
 // record per distinct key in its owner's bucket, each file's bucket position
@@ -567,9 +567,12 @@ __global__ void k_cb_counts(const uint32_t* __restrict__ fill, uint32_t world, u
   if (r < world) counts[r] = fill[r] < cap ? fill[r] : cap;
 }
 
+// the default since round 4 (one rank's bucket stages, profiles/r04_dedup_world.json:
+// C5 at world 8 1.41 -> 1.08 ms, C3 0.57 -> 0.44 ms); SDCAS_COMBINE=sort: the
+// radix-sort combine (A/B)
 static bool combine_by_hash() {
   const char* v = getenv("SDCAS_COMBINE");
-  return v && strcmp(v, "hash") == 0;
+  return !(v && strcmp(v, "sort") == 0);
 }
 
 static hipError_t combine_buckets_hash(DistWs& w, const uint64_t* keys, const uint8_t* has_key,

@@ -560,8 +560,8 @@ def test_meta_group_of_a_subgroup():
 def test_device_bucket_protocol_vs_oracle(eng, oracle, R, chunk_size, combine, monkeypatch):
     """the bucket protocol's device stages (combine_buckets -> equal-split
     exchange -> resolve_buckets -> apply) over R virtual ranks with existing
-    Objects, both combines: the radix-sort one and the hash-table one
-    (SDCAS_COMBINE=hash); then buckets one record too small, which must raise
+    Objects, both combines: the hash-table one (the default) and the
+    radix-sort one (SDCAS_COMBINE=sort); then buckets one record too small, which must raise
     the overflow flag (the caller then reruns the exact stages)"""
     from spacedrive_amd.dist_dedup import DeviceStages
     from tests._dist_stages import dedup_virtual_buckets

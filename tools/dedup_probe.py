@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--existing", type=int, default=0, help="existing Objects (cas keys of the first K files)")
     ap.add_argument("--tables", default="", help="A/B: comma-separated SDCAS_DEDUP_TABLE values, interleaved per rep")
-    ap.add_argument("--combines", default="sort", help="--world > 1: comma-separated SDCAS_COMBINE values (A/B)")
+    ap.add_argument("--combines", default="hash", help="--world > 1: comma-separated SDCAS_COMBINE values (A/B)")
     ap.add_argument("--world", type=int, default=1,
                     help="> 1: one rank's device stages of the bucket protocol at this world size (combine_buckets, "
                          "resolve_buckets over its own buckets as if received, apply), each timed; no exchange")
