@@ -43,6 +43,7 @@
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
 #include <cstdio>
+#include <cstring>
 
 #include "b3_device.h"
 #include "b3_batch.h"
@@ -825,7 +826,9 @@ __device__ __forceinline__ void merge_nodes(const uint32_t* __restrict__ nodes, 
 // the merge of the stack's top two nodes or a fold of the final node into
 // the stack. merge_nodes' nested loops, run by 64 lanes whose node lists
 // differ, execute the union of their compression sequences instead.
-template <uint32_t TILE, class At>
+// QUAD: the four lanes of a quad run the same message's merges (identical
+// bookkeeping) and each parent compression together (compress_quad)
+template <uint32_t TILE, bool QUAD = false, class At>
 __device__ __forceinline__ void merge_nodes_flat(const uint32_t* __restrict__ nodes, uint64_t s0, uint64_t C, At at,
                                                  uint32_t (&cv)[8]) {
   int depth = 0, keep = 0;
@@ -878,7 +881,8 @@ __device__ __forceinline__ void merge_nodes_flat(const uint32_t* __restrict__ no
         l[i] = pl[i];
         r[i] = op == 1 ? pr[i] : v[i];
       }
-      parent(l, r, op == 2 && depth == 1, o);
+      if constexpr (QUAD) parent_quad(l, r, op == 2 && depth == 1, o);
+      else parent(l, r, op == 2 && depth == 1, o);
       if (op == 1) {
         uint32_t* po = at(depth - 2);
 #pragma unroll
@@ -933,6 +937,58 @@ __global__ void __launch_bounds__(kFinishWG) k_finish_t(const uint64_t* __restri
   else
     merge_nodes_deep<TILE>(nodes, s0, C, cv);
   store_digest(perm ? perm[m] : m, cv, out32, out_keys);
+}
+
+// The same with a quad per tile boundary: the boundary's merges run on four
+// lanes (merge_nodes_flat<QUAD>), each parent compression a quad's chain of
+// ~180 dependent instructions instead of one lane's 680, and four times the
+// lanes in flight. C2's 50 K boundaries: 0.07 ms as k_finish_t.
+constexpr int kFinishQWG = 64, kFinishQPerWG = kFinishQWG / 4;
+template <uint32_t TILE>
+__global__ void __launch_bounds__(kFinishQWG) k_finish_q(const uint64_t* __restrict__ lens, uint32_t n,
+                                                        const uint64_t* __restrict__ S,
+                                                        const uint32_t* __restrict__ tile_first,
+                                                        const uint64_t* __restrict__ total_p, uint64_t cap_slots,
+                                                        const uint32_t* __restrict__ nodes,
+                                                        const uint32_t* __restrict__ perm, uint8_t* __restrict__ out32,
+                                                        uint64_t* __restrict__ out_keys) {
+  constexpr uint32_t kFinishRow = kFinishDepth * 8 + 1;
+  __shared__ uint32_t lstack[kFinishQPerWG][kFinishRow];
+  const uint32_t b = threadIdx.x >> 2;  // the quad's boundary in the workgroup
+  const uint64_t t = (uint64_t)blockIdx.x * kFinishQPerWG + b;
+  const uint64_t total = *total_p;
+  // every test below depends on t only: a quad's lanes leave together
+  if (total > cap_slots || t == 0 || t * TILE >= total) return;
+  const uint32_t m = tile_first[t];
+  const uint64_t s0 = S[m];
+  if (s0 >= t * TILE || s0 / TILE != t - 1) return;
+  const uint64_t C = chunk_count(lens[m]);
+  if (s0 + C <= t * TILE) return;
+  uint32_t cv[8];
+  if (C < (1ull << (kFinishDepth - 2)))
+    merge_nodes_flat<TILE, true>(nodes, s0, C, [&](int d) { return &lstack[b][8 * d]; }, cv);
+  else
+    merge_nodes_deep<TILE>(nodes, s0, C, cv);
+  if ((threadIdx.x & 3) == 0) store_digest(perm ? perm[m] : m, cv, out32, out_keys);
+}
+
+// SDCAS_FINISH=lane: k_finish_t (a lane per boundary) instead of k_finish_q (A/B)
+static bool finish_by_quad() {
+  const char* v = getenv("SDCAS_FINISH");
+  return !(v && strcmp(v, "lane") == 0);
+}
+
+template <uint32_t TILE>
+static void launch_finish(uint64_t tiles, hipStream_t st, const uint64_t* lens, uint32_t n, const uint64_t* S,
+                          const uint32_t* tile_first, const uint64_t* total, uint64_t cap_slots, const uint32_t* nodes,
+                          const uint32_t* perm, uint8_t* out32, uint64_t* out_keys) {
+  if (finish_by_quad())
+    hipLaunchKernelGGL(k_finish_q<TILE>, dim3((uint32_t)((tiles + kFinishQPerWG - 1) / kFinishQPerWG)),
+                       dim3(kFinishQWG), 0, st, lens, n, S, tile_first, total, cap_slots, nodes, perm, out32,
+                       out_keys);
+  else
+    hipLaunchKernelGGL(k_finish_t<TILE>, dim3((uint32_t)((tiles + kFinishWG - 1) / kFinishWG)), dim3(kFinishWG), 0,
+                       st, lens, n, S, tile_first, total, cap_slots, nodes, perm, out32, out_keys);
 }
 
 #ifdef SDCAS_ABLATIONS
@@ -1812,13 +1868,11 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
   } else if (planned && !plan->crossing) {
     // every message ended inside its tile: the leaf kernel wrote them all
   } else if (tile == kSmallTile) {
-    const uint64_t tiles = slots / kSmallTile + 1;
-    hipLaunchKernelGGL(k_finish_t<kSmallTile>, dim3((uint32_t)((tiles + kFinishWG - 1) / kFinishWG)), dim3(kFinishWG),
-                       0, st, lens, n, S, tile_first, total, ws.cap_slots, ws.nodes, perm, out32, out_keys);
+    launch_finish<kSmallTile>(slots / kSmallTile + 1, st, lens, n, S, tile_first, total, ws.cap_slots, ws.nodes, perm,
+                              out32, out_keys);
   } else {
-    const uint64_t tiles = slots / kTile + 1;
-    hipLaunchKernelGGL(k_finish_t<kTile>, dim3((uint32_t)((tiles + kFinishWG - 1) / kFinishWG)), dim3(kFinishWG), 0,
-                       st, lens, n, S, tile_first, total, ws.cap_slots, ws.nodes, perm, out32, out_keys);
+    launch_finish<kTile>(slots / kTile + 1, st, lens, n, S, tile_first, total, ws.cap_slots, ws.nodes, perm, out32,
+                         out_keys);
   }
   return hipGetLastError();
 }

@@ -168,6 +168,86 @@ __device__ __forceinline__ void parent(const uint32_t (&l)[8], const uint32_t (&
   compress<GA>(out, m, 0, BLOCK_LEN, PARENT | (root ? ROOT : 0u));
 }
 
+// ---- quad-cooperative compression, for chains that wait on each compression --
+//
+// One compression by the four lanes of a quad (q = lane & 3): lane q holds
+// column q of the state (v[q], v[4+q], v[8+q], v[12+q]) and runs the column
+// step's G for column q, then — its rows rotated within the quad by DPP
+// (b from lane q+1, c from q+2, d from q+3) — the diagonal step's G for
+// diagonal q, and rotates back. Every lane holds the whole message block and
+// picks its round's four words by q. Per lane ~7 × (24 ARX + 6 DPP + 12
+// selects) instructions, of which the dependent chain is ~7 × 26, against 680
+// for one lane alone: where one compression waits on the previous one
+// (k_finish_t's merges of a message's tile-crossing nodes) and nothing else
+// fills the SIMD, the chain is what costs. Every lane of an active quad must
+// be active (DPP reads the quad's other lanes).
+template <int P>
+__device__ __forceinline__ uint32_t qperm(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, P, 0xF, 0xF, false);
+}
+// quad_perm controls: lane q reads lane (q+1)&3 / (q+2)&3 / (q+3)&3 of its quad
+constexpr int kQ1 = 0x39, kQ2 = 0x4E, kQ3 = 0x93;
+
+__device__ __forceinline__ uint32_t qsel(bool q1, bool q2, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  return q2 ? (q1 ? d : c) : (q1 ? b : a);
+}
+
+#define B3_QROUND(s0, s1, s2, s3, s4, s5, s6, s7, s8, s9, s10, s11, s12, s13, s14, s15) \
+  do {                                                                                 \
+    const uint32_t x0 = qsel(q1, q2, m[s0], m[s2], m[s4], m[s6]);                      \
+    const uint32_t y0 = qsel(q1, q2, m[s1], m[s3], m[s5], m[s7]);                      \
+    const uint32_t x1 = qsel(q1, q2, m[s8], m[s10], m[s12], m[s14]);                   \
+    const uint32_t y1 = qsel(q1, q2, m[s9], m[s11], m[s13], m[s15]);                   \
+    B3_G(a, b, c, d, x0, y0);                                                          \
+    b = qperm<kQ1>(b);                                                                 \
+    c = qperm<kQ2>(c);                                                                 \
+    d = qperm<kQ3>(d);                                                                 \
+    B3_G(a, b, c, d, x1, y1);                                                          \
+    b = qperm<kQ3>(b);                                                                 \
+    c = qperm<kQ2>(c);                                                                 \
+    d = qperm<kQ1>(d);                                                                 \
+  } while (0)
+
+// out <- compress(cv, m, counter, block_len, flags)'s first 8 words, in every
+// lane of the quad (cv and m identical across the quad)
+__device__ __forceinline__ void compress_quad(const uint32_t (&cv)[8], const uint32_t (&m)[16], uint64_t counter,
+                                              uint32_t block_len, uint32_t flags, uint32_t (&out)[8]) {
+  const uint32_t q = __lane_id() & 3u;
+  const bool q1 = q & 1u, q2 = q & 2u;
+  uint32_t a = qsel(q1, q2, cv[0], cv[1], cv[2], cv[3]);
+  uint32_t b = qsel(q1, q2, cv[4], cv[5], cv[6], cv[7]);
+  uint32_t c = qsel(q1, q2, IV0, IV1, IV2, IV3);
+  uint32_t d = qsel(q1, q2, (uint32_t)counter, (uint32_t)(counter >> 32), block_len, flags);
+  B3_QROUND(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+  B3_QROUND(2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8);
+  B3_QROUND(3, 4, 10, 12, 13, 2, 7, 14, 6, 5, 9, 0, 11, 15, 8, 1);
+  B3_QROUND(10, 7, 12, 9, 14, 3, 13, 15, 4, 0, 11, 2, 5, 8, 1, 6);
+  B3_QROUND(12, 13, 9, 11, 15, 10, 14, 8, 7, 2, 5, 3, 0, 1, 6, 4);
+  B3_QROUND(9, 14, 11, 5, 8, 12, 15, 1, 13, 3, 0, 10, 2, 6, 4, 7);
+  B3_QROUND(11, 15, 5, 0, 1, 9, 8, 6, 14, 10, 2, 12, 3, 4, 7, 13);
+  const uint32_t lo = a ^ c, hi = b ^ d;  // words q and 4 + q of the output
+  out[0] = qperm<0x00>(lo);
+  out[1] = qperm<0x55>(lo);
+  out[2] = qperm<0xAA>(lo);
+  out[3] = qperm<0xFF>(lo);
+  out[4] = qperm<0x00>(hi);
+  out[5] = qperm<0x55>(hi);
+  out[6] = qperm<0xAA>(hi);
+  out[7] = qperm<0xFF>(hi);
+}
+
+__device__ __forceinline__ void parent_quad(const uint32_t (&l)[8], const uint32_t (&r)[8], bool root,
+                                            uint32_t (&out)[8]) {
+  uint32_t m[16], iv[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    m[i] = l[i];
+    m[8 + i] = r[i];
+  }
+  set_iv(iv);
+  compress_quad(iv, m, 0, BLOCK_LEN, PARENT | (root ? ROOT : 0u), out);
+}
+
 // 64 message bytes, 16-byte aligned, fully inside the message
 __device__ __forceinline__ void load_full_block(const uint8_t* p, uint32_t (&m)[16]) {
   const uint4* q = reinterpret_cast<const uint4*>(p);
