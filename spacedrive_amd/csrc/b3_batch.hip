@@ -376,6 +376,29 @@ __device__ __forceinline__ void hash_chunk_pl(const uint8_t* __restrict__ p, uin
 #include "b3_ablate_loops.inc"
 #endif
 
+// One chunk by the four lanes of a quad (compress_quad), for batches whose
+// chunks are so few that each chunk's 16-compression chain is the kernel's
+// time (a lone file of the watcher or of browse): every lane loads the same
+// block, the chain is ~1/3 of one lane's.
+__device__ __forceinline__ void hash_chunk_quad(const uint8_t* __restrict__ p, uint32_t clen, uint64_t j, bool root,
+                                                uint32_t (&cv)[8]) {
+  set_iv(cv);
+  const uint32_t lb = clen <= BLOCK_LEN ? 0u : (clen - 1) / BLOCK_LEN;  // last block index
+  const uint32_t lblen = clen - lb * BLOCK_LEN;
+  const uint32_t endf = CHUNK_END | (root ? ROOT : 0u);
+  const uint8_t* q = p;
+#pragma unroll 1
+  for (uint32_t b = 0; b <= lb; ++b, q += BLOCK_LEN) {
+    uint32_t m[16], o[8];
+    load_full_block(q, m);
+    const bool last = b == lb;
+    if (last && lblen < BLOCK_LEN) mask_tail_table(m, lblen);
+    compress_quad(cv, m, j, last ? lblen : BLOCK_LEN, (b == 0 ? CHUNK_START : 0u) | (last ? endf : 0u), o);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) cv[i] = o[i];
+  }
+}
+
 // Block loop of a leaf chunk: PF 8 = hash_chunk_ps, 9 = hash_chunk_pl, 4 =
 // hash_chunk_pp, 59 = hash_chunk_full for a whole non-root chunk (per lane)
 // else hash_chunk_ps, 69 = hash_chunk_full when every active lane of the wave
@@ -523,7 +546,12 @@ __device__ __forceinline__ void leaf_order(uint32_t tid, const uint32_t (&bin)[T
 // MINW: waves per SIMD the register allocation must allow (0: 6 with the
 // leaf order, else 1)
 // TL: chunk slots per tile (kTile; kSmallTile for the small-batch kernel)
-template <int WG, int PF, int TR = 1, int ORD = 0, int DYN = 0, int CA = 0, int MINW = 0, uint32_t TL = kTile>
+// QD: a quad of lanes per slot (WG = 4 x the slots a pass covers): each
+// chunk and each tree node by compress_quad; the quad's lead lane alone
+// writes shared state (task lists, chaining values, digests). Needs ORD 0 and
+// CA 0.
+template <int WG, int PF, int TR = 1, int ORD = 0, int DYN = 0, int CA = 0, int MINW = 0, uint32_t TL = kTile,
+          int QD = 0>
 __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ offs,
                                                    const uint64_t* __restrict__ lens, uint32_t n,
                                                    const uint64_t* __restrict__ S,
@@ -543,6 +571,10 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
   if (total > cap_chunks) return;  // reported by sdcas_dev_sync
   const uint64_t ntiles = (total + TL - 1) / TL;
   const uint32_t tid = threadIdx.x;
+  static_assert(!QD || (ORD == 0 && CA == 0 && WG % 4 == 0), "quad slots: no leaf order, no cached chunk");
+  constexpr uint32_t SW = QD ? WG / 4 : WG;  // slot workers: lanes, or quads of lanes
+  const uint32_t sid = QD ? tid >> 2 : tid;
+  const bool lead = !QD || (tid & 3u) == 0;
   // DYN 1: tiles after the first are handed out by a global counter
   // (total_p[2], zeroed by k_tile_first) instead of round-robin, so a
   // workgroup that drew cheap tiles takes more and the grid drains within
@@ -571,7 +603,7 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
     // counter (CA 2: the first slot's only) are kept in registers from here — the message's offset is
     // loaded now, its latency hidden behind the schedule and the barrier,
     // instead of on the leaf phase's critical path
-    constexpr uint32_t R = TL / WG;
+    constexpr uint32_t R = TL / SW;
     const uint8_t* c_p[R];
     uint64_t c_j[R];
     uint32_t c_clen[R], c_m[R];
@@ -580,7 +612,7 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
     for (uint32_t r = 0; r < R; ++r) c_ok[r] = false;
     constexpr uint32_t kPhase1Unroll = CA ? R : 1;
 #pragma unroll kPhase1Unroll
-    for (uint32_t s = tid; s < TL; s += WG) {
+    for (uint32_t s = sid; s < TL; s += SW) {
       const uint64_t g = tbase + s;
       if (g >= total) {
         smsg[s] = kNoMsg;
@@ -606,13 +638,13 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
         c_root[r] = C == 1;
         c_p[r] = blob + offs[m0 + lo] + j * CHUNK_LEN;
       }
-      if (!TR || C == 1) continue;
+      if (!TR || C == 1 || !lead) continue;
       const uint32_t K = node_level_t<TL>(j, C, s);
       for (uint32_t k = 1; k <= K; ++k)
         task[task_base<TL>(k) + atomicAdd(&ntask[k], 1u)] = enc_task(s, s + (1u << (k - 1)), 0, false);
     }
 #pragma unroll 1
-    for (uint32_t i = tid; TR && i < cnt; i += WG) {
+    for (uint32_t i = sid; TR && lead && i < cnt; i += SW) {
       const uint64_t S0 = sS[i];
       if (S0 < tbase) continue;
       const uint64_t C = chunk_count(lens[m0 + i]);
@@ -646,7 +678,7 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
     // waves over whole chunks take the full-chunk loop (PF % 100 == 6)
     const bool ord17 = ORD && cnt > 64 && chunk_count(lens[m0 + cnt - 1]) > 1;
     const bool ord = ord17 || ORD == 2;
-    if (ord) {
+    if constexpr (ORD != 0) if (ord) {
       uint32_t bin[TL / WG];
 #pragma unroll
       for (uint32_t r = 0; r < TL / WG; ++r) {
@@ -684,7 +716,7 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
     // (CA 2 keeps the first slot only: the second one's state would live in
     // registers across the first one's block loop, where they spill)
 #pragma unroll 1
-    for (uint32_t i = (CA == 2 && !ord) ? tid + WG : tid; (CA != 1 || ord) && i < TL; i += WG) {
+    for (uint32_t i = (CA == 2 && !ord) ? tid + WG : sid; (CA != 1 || ord) && i < TL; i += SW) {
       const uint32_t s = ord ? order[i] : i;
       const uint32_t mi = smsg[s];
       if (mi == kNoMsg) continue;
@@ -695,7 +727,9 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
       const uint32_t clen = len == 0 ? 0u : (uint32_t)min<uint64_t>(CHUNK_LEN, len - j * CHUNK_LEN);
       const bool root = (C == 1);
       uint32_t cv[8];
-      leaf_hash<PF>(leaf_ptr<PF>(blob, blob + offs[m] + j * CHUNK_LEN), clen, j, root, cv);
+      if constexpr (QD) hash_chunk_quad(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
+      else leaf_hash<PF>(leaf_ptr<PF>(blob, blob + offs[m] + j * CHUNK_LEN), clen, j, root, cv);
+      if (!lead) continue;
       if (root) {
         store_digest(perm ? perm[m] : m, cv, out32, out_keys);
       } else {
@@ -719,7 +753,7 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
       // do not store — to price masked lanes against active ones
       const uint32_t TT = TR == 2 ? (T + 63u) & ~63u : T;
 #pragma unroll 1
-      for (uint32_t t = tid; t < TT; t += WG) {
+      for (uint32_t t = sid; t < TT; t += SW) {
         const uint32_t e = task[task_base<TL>(k) + (TR == 2 ? min(t, T - 1) : t)];
         const uint32_t l = e & 1023u, r = (e >> 10) & 1023u;
         const bool root = e >> 31;
@@ -729,8 +763,9 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
           a[q] = cvs[l][q];
           b[q] = cvs[r][q];
         }
-        parent<kGA<PF>>(a, b, root, o);
-        if (TR == 2 && t >= T) continue;
+        if constexpr (QD) parent_quad(a, b, root, o);
+        else parent<kGA<PF>>(a, b, root, o);
+        if ((TR == 2 && t >= T) || !lead) continue;
         if (root) {
           const uint32_t mm = m0 + ((e >> 20) & 2047u);
           store_digest(perm ? perm[mm] : mm, o, out32, out_keys);
@@ -745,7 +780,7 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
     // (4) messages crossing a tile boundary: their maximal in-tile nodes go to
     // HBM at their first slot, for k_finish
 #pragma unroll 1
-    for (uint32_t s = tid; TR && s < TL; s += WG) {
+    for (uint32_t s = sid; TR && lead && s < TL; s += SW) {
       const uint32_t mi = smsg[s];
       if (mi == kNoMsg) continue;
       const uint64_t S0 = sS[mi];
@@ -1712,6 +1747,9 @@ static const LeafVariant kLeafVariants[] = {
     // chain at a time) and the tail-mask table
     PRODS(kSmallTile, k_leaf_tree<kSmallTile, 79, 1, 1, 2, 2, 0, kSmallTile>),
     ABLS(kSmallTile, k_leaf_tree<kSmallTile, 279, 1, 1, 2, 2, 0, kSmallTile>),  // 72: 71 with the asm G blocks (slower: 1-100 files +6-12 %)
+    // 73 (product): 71 with a quad of lanes per slot (compress_quad), no leaf
+    // order, 512 threads for the 128 slots
+    PRODS(4 * kSmallTile, k_leaf_tree<4 * kSmallTile, 79, 1, 0, 2, 0, 0, kSmallTile, 1>),
 };
 #undef PROD
 #undef PROD1

@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 4: the quad-lane finish kernel (k_finish_q): the whole GPU suite, then
 # rocprofv3 kernel stats of the C2 and C5 lines with it and with the lane
-# kernel (SDCAS_FINISH=lane)
+# kernel (SDCAS_FINISH=lane); then the quad-slot small kernel (tools/r04_p.sh)
 set -o pipefail
 cd "$(dirname "$0")/.."
 OUT=${1:-gpurun_out/r04o}
@@ -17,4 +17,5 @@ for fin in quad lane; do
        > $R/$OUT/prof_${w}_$fin.json 2> $R/$OUT/prof_${w}_$fin.err) || exit 2
   done
 done
+bash tools/r04_p.sh $OUT/p || exit 3
 echo done
