@@ -11,10 +11,13 @@ constexpr uint32_t kWG = 512;     // threads per workgroup: 2 slots per lane
 // Batches of at most kSmallSlots chunk slots (the staging slots of a path call
 // that small, e.g. the reference's 100-file step) run the small-batch kernel:
 // tiles of kSmallTile slots, so that they spread over many CUs instead of
-// running a few 1 MiB tiles one CU each (leaf variant kSmallVariant).
+// running a few 1 MiB tiles one CU each (leaf variant kSmallVariant: since
+// round 4 variant 73, a quad of lanes per slot — sdcas_cas_ids of 1 / 10 /
+// 100 / 300 files 68.3 / 124.8 / 291.9 / 545.7 us -> 53.1 / 112.0 / 280.1 /
+// 521.6 us against 71, profiles/r04_small_quad.json).
 constexpr uint32_t kSmallTile = 128;
 constexpr uint64_t kSmallSlots = 1ull << 14;
-constexpr int kSmallVariant = 71;
+constexpr int kSmallVariant = 73;
 // The shape sort's 256 bin counters and 256 bin cursors, each alone in a
 // 128-byte line: every workgroup adds to most of them, and packed into 8 lines
 // those atomics queued at 8 L2 channels.
