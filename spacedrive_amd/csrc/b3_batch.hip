@@ -863,17 +863,12 @@ __device__ __forceinline__ void merge_nodes(const uint32_t* __restrict__ nodes, 
 // differ, execute the union of their compression sequences instead.
 // QUAD: the four lanes of a quad run the same message's merges (identical
 // bookkeeping) and each parent compression together (compress_quad)
-// Pre: the node list already fetched (k_finish_q): node number ni of the walk
-// comes from pre(ni, v) when pre(ni, v) returns true, else from `nodes`.
-struct NoPrefetch {
-  __device__ bool operator()(uint32_t, uint32_t (&)[8]) const { return false; }
-};
-template <uint32_t TILE, bool QUAD = false, class At, class Pre = NoPrefetch>
+template <uint32_t TILE, bool QUAD = false, class At>
 __device__ __forceinline__ void merge_nodes_flat(const uint32_t* __restrict__ nodes, uint64_t s0, uint64_t C, At at,
-                                                 uint32_t (&cv)[8], Pre pre = Pre{}) {
+                                                 uint32_t (&cv)[8]) {
   int depth = 0, keep = 0;
   uint64_t j = 0;
-  uint32_t k = 0, ni = 0;
+  uint32_t k = 0;
   bool have = false, done = false;
   uint32_t v[8];
   for (;;) {
@@ -882,12 +877,10 @@ __device__ __forceinline__ void merge_nodes_flat(const uint32_t* __restrict__ no
       if (!have) {
         const uint64_t g = s0 + j;
         k = node_level_t<TILE>(j, C, (uint32_t)(g % TILE));
-        if (!pre(ni++, v)) {
-          const uint4* p = reinterpret_cast<const uint4*>(nodes + 8ull * g);
-          const uint4 a = p[0], b = p[1];
-          v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-          v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-        }
+        const uint4* p = reinterpret_cast<const uint4*>(nodes + 8ull * g);
+        const uint4 a = p[0], b = p[1];
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+        v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
         keep = __popcll(j);  // subtrees completed by the first j chunks merge first
         have = true;
       }
@@ -986,7 +979,6 @@ __global__ void __launch_bounds__(kFinishWG) k_finish_t(const uint64_t* __restri
 // ~180 dependent instructions instead of one lane's 680, and four times the
 // lanes in flight. C2's 50 K boundaries: 0.07 ms as k_finish_t.
 constexpr int kFinishQWG = 64, kFinishQPerWG = kFinishQWG / 4;
-constexpr uint32_t kFinishNodes = 32;  // nodes a quad loads before merging (a <= 1 MiB message has <= ~20)
 template <uint32_t TILE>
 __global__ void __launch_bounds__(kFinishQWG) k_finish_q(const uint64_t* __restrict__ lens, uint32_t n,
                                                         const uint64_t* __restrict__ S,
@@ -996,9 +988,7 @@ __global__ void __launch_bounds__(kFinishQWG) k_finish_q(const uint64_t* __restr
                                                         const uint32_t* __restrict__ perm, uint8_t* __restrict__ out32,
                                                         uint64_t* __restrict__ out_keys) {
   constexpr uint32_t kFinishRow = kFinishDepth * 8 + 1;
-  constexpr uint32_t kNodeRow = kFinishNodes * 8 + 4;
   __shared__ uint32_t lstack[kFinishQPerWG][kFinishRow];
-  __shared__ uint32_t nbuf[kFinishQPerWG][kNodeRow];  // the boundary's message's first kFinishNodes nodes
   const uint32_t b = threadIdx.x >> 2;  // the quad's boundary in the workgroup
   const uint64_t t = (uint64_t)blockIdx.x * kFinishQPerWG + b;
   const uint64_t total = *total_p;
@@ -1010,37 +1000,10 @@ __global__ void __launch_bounds__(kFinishQWG) k_finish_q(const uint64_t* __restr
   const uint64_t C = chunk_count(lens[m]);
   if (s0 + C <= t * TILE) return;
   uint32_t cv[8];
-  if (C < (1ull << (kFinishDepth - 2))) {
-    // the message's node list, left to right, is a closed form of (s0, C):
-    // its first kFinishNodes nodes are loaded up front, spread over the
-    // quad's lanes, instead of one dependent load per merge step
-    const uint32_t q = threadIdx.x & 3u;
-    uint32_t nn = 0;
-    for (uint64_t j = 0; j < C && nn < kFinishNodes; ++nn) {
-      const uint64_t g = s0 + j;
-      if ((nn & 3u) == q) {
-        const uint4* p = reinterpret_cast<const uint4*>(nodes + 8ull * g);
-        const uint4 x = p[0], y = p[1];
-        uint32_t* o = &nbuf[b][8 * nn];
-        o[0] = x.x; o[1] = x.y; o[2] = x.z; o[3] = x.w;
-        o[4] = y.x; o[5] = y.y; o[6] = y.z; o[7] = y.w;
-      }
-      j += 1ull << node_level_t<TILE>(j, C, (uint32_t)(g % TILE));
-    }
-    // the quad's other lanes wrote part of the list: order those LDS writes
-    // before the reads below (one wave per workgroup, so no barrier)
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    auto pre = [&](uint32_t ni, uint32_t (&v)[8]) {
-      if (ni >= nn) return false;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = nbuf[b][8 * ni + i];
-      return true;
-    };
-    merge_nodes_flat<TILE, true>(nodes, s0, C, [&](int d) { return &lstack[b][8 * d]; }, cv, pre);
-  } else {
+  if (C < (1ull << (kFinishDepth - 2)))
+    merge_nodes_flat<TILE, true>(nodes, s0, C, [&](int d) { return &lstack[b][8 * d]; }, cv);
+  else
     merge_nodes_deep<TILE>(nodes, s0, C, cv);
-  }
   if ((threadIdx.x & 3) == 0) store_digest(perm ? perm[m] : m, cv, out32, out_keys);
 }
 
