@@ -50,6 +50,7 @@ struct DistWs {
   Buf<uint32_t> tpos;        // table entry of each received file record
   Buf<uint8_t> valid, temp;
   Buf<uint32_t> stay_idx, nstay;  // the batch's stay-orphan rows (dd_local's plan)
+  Buf<uint32_t> stay_cnt;         // per-workgroup stays counts, then offsets (select_stays)
   Buf<uint64_t> plan, stay_sorted;
   void release();
 };

@@ -213,14 +213,111 @@ __global__ void k_dd_apply(const uint64_t* __restrict__ ids, const uint32_t* __r
   add_counts(c, l, sc, counts);
 }
 
-// stays rows: their step leaves them orphans (file_identifier_job.rs:258-264)
-struct StayPred {
-  const uint8_t* has_key;
-  const int32_t* status;
-  __host__ __device__ __forceinline__ bool operator()(const uint32_t& i) const {
-    return (status && status[i] != 0) || (has_key && !has_key[i]);
+// Stays rows — their step leaves them orphans (file_identifier_job.rs:258-264)
+// — in order (what hipcub::DeviceSelect::If gave, without its look-back
+// scan): (1) each workgroup counts its 4096 rows' stays, (2) one
+// workgroup turns the counts into offsets and writes the total, (3) only the
+// workgroups that hold a stays row write their indices, in order. A batch
+// with none (C3 / C5: every file has a key) costs two streaming passes over
+// the flags and an empty third launch. C5: ~50 us -> ~15 us per call.
+constexpr uint32_t kStayWG = 256, kStayR = 16, kStayPer = kStayWG * kStayR;
+
+__device__ __forceinline__ bool stays_row(const uint8_t* __restrict__ has_key, const int32_t* __restrict__ status,
+                                          uint64_t i) {
+  return (status && status[i] != 0) || (has_key && !has_key[i]);
+}
+
+__global__ void __launch_bounds__(kStayWG) k_stays_count(const uint8_t* __restrict__ has_key,
+                                                         const int32_t* __restrict__ status, uint32_t n,
+                                                         uint32_t* __restrict__ bcnt) {
+  __shared__ uint32_t ws[kStayWG / 64];
+  const uint64_t lo = (uint64_t)blockIdx.x * kStayPer;
+  uint32_t c = 0;
+#pragma unroll
+  for (uint32_t r = 0; r < kStayR; ++r) {
+    const uint64_t i = lo + r * kStayWG + threadIdx.x;
+    c += i < n && stays_row(has_key, status, i);
   }
-};
+#pragma unroll
+  for (uint32_t d = 32; d; d >>= 1) c += __shfl_xor(c, d);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) bcnt[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+// one workgroup: bcnt[b] <- its exclusive prefix; *total <- the sum
+__global__ void __launch_bounds__(1024) k_stays_scan(uint32_t* __restrict__ bcnt, uint32_t nb,
+                                                     uint32_t* __restrict__ total) {
+  __shared__ uint32_t ws[16];
+  __shared__ uint32_t carry;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t base = 0; base < nb; base += 1024) {
+    const uint32_t i = base + tid;
+    const uint32_t v = i < nb ? bcnt[i] : 0u;
+    uint32_t inc = v;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint32_t t = __shfl_up(inc, d);
+      if (lane >= d) inc += t;
+    }
+    if (lane == 63) ws[wave] = inc;
+    __syncthreads();
+    uint32_t before = carry;
+    for (uint32_t w = 0; w < wave; ++w) before += ws[w];
+    if (i < nb) bcnt[i] = before + inc - v;
+    __syncthreads();
+    if (tid == 1023) carry = before + inc;
+    __syncthreads();
+  }
+  if (tid == 0) *total = carry;
+}
+
+__global__ void __launch_bounds__(kStayWG) k_stays_write(const uint8_t* __restrict__ has_key,
+                                                         const int32_t* __restrict__ status, uint32_t n,
+                                                         const uint32_t* __restrict__ boff,
+                                                         const uint32_t* __restrict__ total,
+                                                         uint32_t* __restrict__ out) {
+  __shared__ uint32_t ws[kStayWG / 64];
+  const uint32_t b = blockIdx.x;
+  const uint32_t mine = (b + 1 < gridDim.x ? boff[b + 1] : *total) - boff[b];
+  if (mine == 0) return;  // uniform over the workgroup
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint64_t lo = (uint64_t)b * kStayPer;
+  uint32_t run = boff[b];
+#pragma unroll 1
+  for (uint32_t r = 0; r < kStayR; ++r) {
+    const uint64_t i = lo + r * kStayWG + tid;
+    const bool f = i < n && stays_row(has_key, status, i);
+    const uint64_t bal = __ballot(f);
+    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+    if (lane == 0) ws[wave] = (uint32_t)__popcll(bal);
+    __syncthreads();
+    uint32_t before = run, all = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kStayWG / 64; ++w) {
+      if (w < wave) before += ws[w];
+      all += ws[w];
+    }
+    __syncthreads();
+    if (f) out[before + below] = (uint32_t)i;
+    run += all;
+  }
+}
+
+// the stays rows of [0, n) in order into w.stay_idx, their count into w.nstay
+static hipError_t select_stays(DistWs& w, const uint8_t* has_key, const int32_t* status, uint32_t n,
+                               hipStream_t st) {
+  hipError_t e;
+  const uint32_t nb = (n + kStayPer - 1) / kStayPer;
+  if ((e = w.stay_idx.ensure(n)) || (e = w.stay_cnt.ensure(nb + 1))) return e;
+  hipLaunchKernelGGL(k_stays_count, dim3(nb), dim3(kStayWG), 0, st, has_key, status, n, w.stay_cnt.p);
+  hipLaunchKernelGGL(k_stays_scan, dim3(1), dim3(1024), 0, st, w.stay_cnt.p, nb, w.nstay.p);
+  hipLaunchKernelGGL(k_stays_write, dim3(nb), dim3(kStayWG), 0, st, has_key, status, n, w.stay_cnt.p, w.nstay.p,
+                     w.stay_idx.p);
+  return hipGetLastError();
+}
 
 __global__ void k_stays_gather(const uint32_t* __restrict__ idx, const uint32_t* __restrict__ m_p,
                                const uint64_t* __restrict__ ids, uint32_t cap, uint64_t* __restrict__ out,
@@ -358,7 +455,7 @@ void DistWs::release() {
   idx_a.release(); idx_b.release(); scan.release(); nvalid.release(); starts.release(); hi_a.release();
   hi_b.release(); tkey.release(); tmin.release(); tpos.release();
   valid.release(); temp.release();
-  stay_idx.release(); nstay.release(); plan.release(); stay_sorted.release();
+  stay_idx.release(); nstay.release(); stay_cnt.release(); plan.release(); stay_sorted.release();
 }
 
 // the combine up to its device outputs: rec, slot, w.starts[0..world] (n > 0)
@@ -926,15 +1023,7 @@ hipError_t dd_stays(DistWs& w, const uint8_t* has_key, const int32_t* status, co
   if (n == 0 || (!has_key && !status)) {
     if ((e = hipMemsetAsync(w.nstay.p, 0, sizeof(uint32_t), st))) return e;
   } else {
-    if ((e = w.stay_idx.ensure(n))) return e;
-    size_t need = 0;
-    (void)hipcub::DeviceSelect::If(nullptr, need, hipcub::CountingInputIterator<uint32_t>(0), w.stay_idx.p,
-                                   w.nstay.p, (int)n, StayPred{has_key, status}, st);
-    if ((e = w.temp.ensure(need + 256))) return e;
-    size_t tmp = w.temp.cap;
-    if ((e = hipcub::DeviceSelect::If(w.temp.p, tmp, hipcub::CountingInputIterator<uint32_t>(0), w.stay_idx.p,
-                                      w.nstay.p, (int)n, StayPred{has_key, status}, st)))
-      return e;
+    if ((e = select_stays(w, has_key, status, n, st))) return e;
   }
   const uint32_t g = cap ? cap : 1;
   hipLaunchKernelGGL(k_stays_gather, dim3(blocks(g)), dim3(TB), 0, st, w.stay_idx.p, w.nstay.p, ids, cap, out, count);
@@ -972,15 +1061,7 @@ hipError_t dd_local(DistWs& w, const uint64_t* keys, const uint8_t* has_key, con
   // the steps' plan from this batch's stays rows (all of the job's: a world of one)
   if ((e = w.nstay.ensure(1)) || (e = w.plan.ensure(kPlanHeader + (uint64_t)n + 1))) return e;
   if (n && (has_key || status)) {
-    if ((e = w.stay_idx.ensure(n))) return e;
-    size_t need = 0;
-    (void)hipcub::DeviceSelect::If(nullptr, need, hipcub::CountingInputIterator<uint32_t>(0), w.stay_idx.p,
-                                   w.nstay.p, (int)n, StayPred{has_key, status}, st);
-    if ((e = w.temp.ensure(need + 256))) return e;
-    size_t tmp = w.temp.cap;
-    if ((e = hipcub::DeviceSelect::If(w.temp.p, tmp, hipcub::CountingInputIterator<uint32_t>(0), w.stay_idx.p,
-                                      w.nstay.p, (int)n, StayPred{has_key, status}, st)))
-      return e;
+    if ((e = select_stays(w, has_key, status, n, st))) return e;
   } else if ((e = hipMemsetAsync(w.nstay.p, 0, sizeof(uint32_t), st))) {
     return e;
   }
