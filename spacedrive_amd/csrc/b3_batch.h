@@ -18,11 +18,11 @@ constexpr uint32_t kWG = 512;     // threads per workgroup: 2 slots per lane
 constexpr uint32_t kSmallTile = 128;
 constexpr uint64_t kSmallSlots = 1ull << 14;
 constexpr int kSmallVariant = 73;
-// The shape sort's 256 bin counters and 256 bin cursors, each alone in a
-// 128-byte line: every workgroup adds to most of them, and packed into 8 lines
-// those atomics queued at 8 L2 channels.
-constexpr uint32_t kBinStride = 32;
-constexpr uint32_t kSortKeyWords = 2 * 256 * kBinStride;
+// The shape sort's workspace: the 256 bin totals, then each scatter
+// workgroup's (kSortPerWG messages) count per bin, bin-major.
+constexpr uint32_t kSortTotalsWords = 256;
+constexpr uint32_t kSortPerWG = 4096;
+inline size_t sort_key_words(size_t max_msgs) { return kSortTotalsWords + 256 * (max_msgs / kSortPerWG + 1); }
 
 // Device workspace owned by the library context (caller never sees it).
 struct BatchWorkspace {
@@ -46,7 +46,7 @@ struct BatchWorkspace {
   uint32_t* perm = nullptr;        // [cap_msgs]
   uint64_t* soffs = nullptr;       // [cap_msgs]
   uint64_t* slens = nullptr;       // [cap_msgs]
-  uint32_t* sort_keys = nullptr;   // [kSortKeyWords] shape-bin counts and cursors, one 128-byte line each
+  uint32_t* sort_keys = nullptr;   // [sort_key_words(cap_msgs)] shape-bin totals and per-workgroup counts
 };
 
 size_t batch_scan_temp_bytes(uint32_t max_msgs);

@@ -1034,15 +1034,21 @@ static void launch_finish(uint64_t tiles, hipStream_t st, const uint64_t* lens, 
 // last chunk - 1). Single-chunk messages — whose lanes otherwise run 1..16
 // blocks side by side in one wave — end up grouped by block count;
 // multi-chunk messages have one short chunk each and are merely clustered.
-// A counting sort over the 256 shape bins (histogram, then a scatter that
-// reserves each workgroup's range per bin): order inside a bin is not
-// specified, which changes nothing but the slot a message lands in.
+// A counting sort over the 256 shape bins in three launches and no global
+// atomics: (1) each workgroup's histogram of its 4096 messages, stored
+// bin-major (wcnt[bin][wg]); (2) one workgroup per bin: the bin's total and
+// each workgroup's start inside the bin; (3) the scatter: each workgroup
+// scans the bin totals, orders its messages by shape in LDS and writes them
+// run by run. Round 3's version reserved each workgroup's range per bin with
+// a global atomicAdd on one counter per bin — on C5, ~300 K atomics on ~200
+// addresses, serialised at their L2 channels (hist 20 us + scatter 104 us).
+// Order inside a bin: by workgroup, then unspecified — it changes nothing
+// but the slot a message lands in.
 constexpr uint32_t kShapeBins = 256;
-static_assert(kSortKeyWords == 2 * kShapeBins * kBinStride, "ws.sort_keys holds counts and cursors");
 constexpr uint32_t kScatterPerWG = 4096;
-constexpr uint32_t kHistPerThread = 8;
 constexpr uint32_t kScatterR = kScatterPerWG / 256;  // messages per scatter thread
 constexpr uint32_t kShapeManyChunks = 15 << 4;  // first shape key of messages of 15+ chunks
+static_assert(kSortTotalsWords == kShapeBins && kSortPerWG == kScatterPerWG, "ws.sort_keys layout");
 
 __device__ __forceinline__ uint32_t shape_key(uint64_t L) {
   const uint64_t C = chunk_count(L);
@@ -1051,49 +1057,77 @@ __device__ __forceinline__ uint32_t shape_key(uint64_t L) {
   return ((uint32_t)min<uint64_t>(C, 15) << 4) | (blocks - 1);
 }
 
+// (1) wcnt[bin * nwg + wg] = messages of workgroup wg's 4096 in bin
 __global__ void __launch_bounds__(256) k_shape_hist(const uint64_t* __restrict__ lens, uint32_t n,
-                                                    uint32_t* __restrict__ counts) {
+                                                    uint32_t* __restrict__ wcnt) {
   __shared__ uint32_t h[kShapeBins];
-  h[threadIdx.x] = 0;
+  const uint32_t t = threadIdx.x;
+  h[t] = 0;
   __syncthreads();
-  // kHistPerThread loads in flight before their LDS atomics (one load per
-  // iteration had each thread wait out the HBM latency once per message)
-  for (uint64_t base = (uint64_t)blockIdx.x * 256 * kHistPerThread; base < n;
-       base += (uint64_t)gridDim.x * 256 * kHistPerThread) {
-    uint64_t L[kHistPerThread];
+  const uint64_t lo = (uint64_t)blockIdx.x * kScatterPerWG;
+  uint64_t L[kScatterR];
 #pragma unroll
-    for (uint32_t r = 0; r < kHistPerThread; ++r) {
-      const uint64_t i = base + r * 256 + threadIdx.x;
-      L[r] = i < n ? lens[i] : 0;
-    }
-#pragma unroll
-    for (uint32_t r = 0; r < kHistPerThread; ++r)
-      if (base + r * 256 + threadIdx.x < n) atomicAdd(&h[shape_key(L[r])], 1u);
+  for (uint32_t r = 0; r < kScatterR; ++r) {
+    const uint64_t i = lo + r * 256 + t;
+    L[r] = i < n ? lens[i] : 0;
   }
+#pragma unroll
+  for (uint32_t r = 0; r < kScatterR; ++r)
+    if (lo + r * 256 + t < n) atomicAdd(&h[shape_key(L[r])], 1u);
   __syncthreads();
-  if (h[threadIdx.x]) atomicAdd(&counts[threadIdx.x * kBinStride], h[threadIdx.x]);
+  wcnt[(uint64_t)t * gridDim.x + blockIdx.x] = h[t];
 }
 
-// Scatter in two steps so that the global writes are coalesced: the
+// (2) one workgroup per bin: totals[bin], and wcnt[bin][wg] <- the exclusive
+// prefix over the workgroups (the workgroup's first position inside the bin)
+__global__ void __launch_bounds__(256) k_shape_bins(uint32_t* __restrict__ wcnt, uint32_t nwg,
+                                                    uint32_t* __restrict__ totals) {
+  __shared__ uint32_t ws[4];
+  __shared__ uint32_t carry;
+  const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  uint32_t* col = wcnt + (uint64_t)blockIdx.x * nwg;
+  if (t == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t base = 0; base < nwg; base += 256) {
+    const uint32_t i = base + t;
+    const uint32_t v = i < nwg ? col[i] : 0u;
+    uint32_t inc = v;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint32_t x = __shfl_up(inc, d);
+      if (lane >= d) inc += x;
+    }
+    if (lane == 63) ws[wave] = inc;
+    __syncthreads();
+    uint32_t before = carry;
+    for (uint32_t w = 0; w < wave; ++w) before += ws[w];
+    if (i < nwg) col[i] = before + inc - v;
+    __syncthreads();
+    if (t == 255) carry = before + inc;
+    __syncthreads();
+  }
+  if (t == 0) totals[blockIdx.x] = carry;
+}
+
+// (3) Scatter in two steps so that the global writes are coalesced: the
 // workgroup's 4096 messages are first ordered by shape in LDS (2-byte local
 // indices), then written run by run — consecutive threads to consecutive
 // addresses of a bin's range. The second read of offs/lens (in LDS order) hits
 // the L2 lines the first read brought in. Each thread's kScatterR global
-// loads of a pass are issued together, ahead of their use: the workgroups
-// all fit the chip at once, so the kernel takes one workgroup's latency, and
-// a load per loop iteration made that kScatterR HBM round trips per pass.
+// loads of a pass are issued together, ahead of their use.
 __global__ void __launch_bounds__(256) k_shape_scatter(const uint64_t* __restrict__ offs,
                                                        const uint64_t* __restrict__ lens, uint32_t n,
-                                                       const uint32_t* __restrict__ counts,
-                                                       uint32_t* __restrict__ cursor, uint32_t* __restrict__ perm,
-                                                       uint64_t* __restrict__ soffs, uint64_t* __restrict__ slens) {
+                                                       const uint32_t* __restrict__ totals,
+                                                       const uint32_t* __restrict__ wstart,
+                                                       uint32_t* __restrict__ perm, uint64_t* __restrict__ soffs,
+                                                       uint64_t* __restrict__ slens) {
   __shared__ uint32_t gstart[kShapeBins], lstart[kShapeBins], h[kShapeBins];
   __shared__ uint16_t order[kScatterPerWG];
   __shared__ uint8_t keyof[kScatterPerWG];
   __shared__ uint32_t few_chunks;
   const uint32_t t = threadIdx.x;
-  // exclusive scan of the global bin counts (256 entries, one per thread)
-  const uint32_t bin_count = counts[t * kBinStride];
+  // exclusive scan of the bin totals (256 entries, one per thread)
+  const uint32_t bin_count = totals[t];
   gstart[t] = bin_count;
   h[t] = 0;
   __syncthreads();
@@ -1112,7 +1146,7 @@ __global__ void __launch_bounds__(256) k_shape_scatter(const uint64_t* __restric
   // chunks are full whatever the order and sorting gains nothing (measured:
   // C2 leaf 15.34 ms unsorted vs 15.38 sorted, C3 / C5 2-3 % faster sorted):
   // keep the caller's order, as a coalesced copy. Every workgroup decides the
-  // same from the same counts.
+  // same from the same totals.
   if ((uint64_t)(n - few_chunks) * 10 > (uint64_t)n * 6) {
     uint64_t o[kScatterR], l[kScatterR];
 #pragma unroll
@@ -1148,9 +1182,10 @@ __global__ void __launch_bounds__(256) k_shape_scatter(const uint64_t* __restric
     }
   }
   __syncthreads();
-  // this workgroup's range in bin t, and the bin's start in the local order
+  // this workgroup's range in bin t (from k_shape_bins), and the bin's start
+  // in the local order
   const uint32_t cnt = h[t];
-  if (cnt) gstart[t] += atomicAdd(&cursor[t * kBinStride], cnt);
+  gstart[t] += wstart[(uint64_t)t * gridDim.x + blockIdx.x];
   lstart[t] = cnt;
   __syncthreads();
   for (uint32_t d = 1; d < kShapeBins; d <<= 1) {
@@ -1822,17 +1857,19 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
                       hipEvent_t ev0, hipEvent_t ev1, const BatchPlan* plan) {
   if (n == 0) return hipSuccess;
   if (n > ws.cap_msgs) return hipErrorInvalidValue;
-  hipError_t e;
+  [[maybe_unused]] hipError_t e;  // (the quad-layout ablation's scan)
   const uint32_t* perm = nullptr;
   // A batch of a few messages fills a tile or two whatever their order: its
   // three sort launches would only add latency (the reference's 100-file step).
   if (ws.sort && n >= kSortMinMsgs && ws.perm) {
-    uint32_t* counts = ws.sort_keys;  // 256 bin sizes, then 256 per-bin cursors (kBinStride apart)
-    if ((e = hipMemsetAsync(counts, 0, kSortKeyWords * sizeof(uint32_t), st))) return e;
-    const uint32_t hb = std::min<uint32_t>((n + 256 * kHistPerThread - 1) / (256 * kHistPerThread), 1024u);
-    hipLaunchKernelGGL(k_shape_hist, dim3(hb), dim3(256), 0, st, lens, n, counts);
-    hipLaunchKernelGGL(k_shape_scatter, dim3((n + kScatterPerWG - 1) / kScatterPerWG), dim3(256), 0, st, offs, lens,
-                       n, counts, counts + kShapeBins * kBinStride, ws.perm, ws.soffs, ws.slens);
+    // the bin totals, then each workgroup's count per bin (bin-major)
+    const uint32_t nwg = (n + kScatterPerWG - 1) / kScatterPerWG;
+    uint32_t* totals = ws.sort_keys;
+    uint32_t* wcnt = ws.sort_keys + kSortTotalsWords;
+    hipLaunchKernelGGL(k_shape_hist, dim3(nwg), dim3(256), 0, st, lens, n, wcnt);
+    hipLaunchKernelGGL(k_shape_bins, dim3(kShapeBins), dim3(256), 0, st, wcnt, nwg, totals);
+    hipLaunchKernelGGL(k_shape_scatter, dim3(nwg), dim3(256), 0, st, offs, lens, n, totals, wcnt, ws.perm, ws.soffs,
+                       ws.slens);
     offs = ws.soffs;
     lens = ws.slens;
     perm = ws.perm;

@@ -282,7 +282,7 @@ int reserve_ws(sdcas_ctx* c, size_t max_msgs, uint64_t max_chunks) {
   size_t tb = batch_scan_temp_bytes((uint32_t)std::max<size_t>(max_msgs, 1));
   if ((e = c->ws_scan.ensure(tb))) return c->hip_fail(e, "workspace scan");
   if ((e = c->ws_perm.ensure(max_msgs + 1)) || (e = c->ws_soffs.ensure(max_msgs + 1)) ||
-      (e = c->ws_slens.ensure(max_msgs + 1)) || (e = c->ws_sort_keys.ensure(kSortKeyWords)))
+      (e = c->ws_slens.ensure(max_msgs + 1)) || (e = c->ws_sort_keys.ensure(sort_key_words(max_msgs + 1))))
     return c->hip_fail(e, "workspace sort");
   c->ws.S = c->ws_S.p;
   c->ws.total = c->ws_total.p;
