@@ -1785,6 +1785,7 @@ static const LeafVariant kLeafVariants[] = {
     // 73 (product): 71 with a quad of lanes per slot (compress_quad), no leaf
     // order, 512 threads for the 128 slots
     PRODS(4 * kSmallTile, k_leaf_tree<4 * kSmallTile, 79, 1, 0, 2, 0, 0, kSmallTile, 1>),
+    ABL1(512, k_leaf_tree<512, 299, 1, 1, 2, 2>),  // 74: 67 with the split line-pair loop (hash_chunk_split)
 };
 #undef PROD
 #undef PROD1
