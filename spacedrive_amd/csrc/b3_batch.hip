@@ -1892,6 +1892,9 @@ hipError_t batch_hash(const BatchWorkspace& ws, const uint8_t* blob, const uint6
   if (!forced && !quad && slots <= ws.small_slots && slots / kSmallTile + 2 <= ws.cap_small_tiles)
     v = leaf_variant_available(ws.small_variant) && kLeafVariants[ws.small_variant].tile == kSmallTile ? ws.small_variant
                                                                                                         : kSmallVariant;
+  // a small-tile kernel chosen by hand (A/B) for a batch whose 128-slot tiles
+  // outnumber the workspace's tile_first entries runs the default instead
+  if (kLeafVariants[v].tile == kSmallTile && slots / kSmallTile + 2 > ws.cap_small_tiles) v = kDefaultLeafVariant;
   const uint32_t tile = kLeafVariants[v].tile;
   // the caller's host plan stands in for the scan and k_tile_first when it
   // was made for this order and tile size

@@ -181,13 +181,18 @@ def test_tile_straddles_vs_oracle(eng, oracle):
         assert bytes(d).hex() == oracle.hash(m), len(m)
 
 
-@pytest.mark.parametrize("variant", [52, 67, 71])
-def test_tile_straddles_per_variant(oracle, variant):
+@pytest.mark.parametrize("variant,finish", [(52, "quad"), (67, "quad"), (71, "quad"), (73, "quad"), (67, "lane"),
+                                            (73, "lane")])
+def test_tile_straddles_per_variant(oracle, variant, finish, monkeypatch):
     """the straddle corpus through each product leaf variant, in caller
-    order (shape sort off) so messages straddle tiles at every level (71, the
-    small-batch kernel, selected explicitly: its 128-slot tiles for the whole
-    batch, so messages of up to 2049 chunks cross dozens of them)"""
+    order (shape sort off) so messages straddle tiles at every level (71 and
+    73, the small-batch kernels — a lane / a quad of lanes per slot — selected
+    explicitly: their 128-slot tiles for the whole batch, so messages of up to
+    2049 chunks cross dozens of them), the crossing messages finished by
+    k_finish_q (default) or k_finish_t (SDCAS_FINISH=lane)"""
     from spacedrive_amd import Engine
+    if finish == "lane":
+        monkeypatch.setenv("SDCAS_FINISH", "lane")
     rng = np.random.default_rng(70 + variant)
     lens = []
     for c in [1, 2, 3, 7, 8, 9, 16, 17, 31, 32, 33, 64, 65, 127, 128, 129, 255, 256, 257, 511, 512, 513, 1000,
@@ -207,15 +212,15 @@ def test_tile_straddles_per_variant(oracle, variant):
     assert not bad, [len(msgs[i]) for i in bad[:10]]
 
 
-@pytest.mark.parametrize("variant", [52, 67, 71])
+@pytest.mark.parametrize("variant", [52, 67, 71, 73])
 def test_many_short_multichunk_messages(oracle, variant):
     """C5-shaped batches — mostly 2..5-chunk messages, so tiles hold far more
     partial last chunks than a wave has lanes and the leaf kernel's block-count
     order is taken — next to runs of single-chunk messages and a few long
     ones; every digest against the oracle, for every product kernel (52:
     one tile per workgroup, the last-block-index loop, the first chunk kept
-    from phase 1; 67, the default: 52 with the tail masks from a table; 71:
-    the small-batch kernel, 128-slot tiles)"""
+    from phase 1; 67, the default: 52 with the tail masks from a table; 71 and
+    73: the small-batch kernels, 128-slot tiles, a lane / a quad per slot)"""
     from spacedrive_amd import Engine
     rng = np.random.default_rng(55 + variant)
     lens = np.concatenate([rng.integers(1025, 5 * 1024 + 1, 12000), rng.integers(0, 1025, 3000),
