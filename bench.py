@@ -148,7 +148,8 @@ def compressions(lens):
 
 # the library's default kernels (spacedrive_amd/csrc/b3_batch.hip
 # kDefaultLeafVariant / kDefaultPieceVariant): the PMC traffic files are per kernel
-DEFAULT_LEAF_KERNEL = "k_leaf_tree<512, 279, 1, 1, 2, 2, 0, 1024u>"
+# (a name prefix: round 4 added a last template argument, QD = 0, to the same kernel)
+DEFAULT_LEAF_KERNEL = "k_leaf_tree<512, 279, 1, 1, 2, 2, 0, 1024u"
 DEFAULT_PIECE_VARIANT = 19
 
 
