@@ -93,10 +93,26 @@ def c2_files(seed, lo, hi):
     return S.c2_files(lo, hi, seed)
 
 
-C5_STRIDE = 8  # the C5 corpus spans 8 GPUs: GPU r's share is files r, r+8, r+16, ...
+C5_CORPUS = 50_000_000  # 50 M files (the first 20 M distinct contents, then Zipf draws)
 
 
-def files_of(workload, rank, n):
+def c5_share(rank, n, world):
+    """C5 corpus file indices of rank `rank`'s n files in a world of `world`:
+    the world's n * world files sampled evenly over the whole corpus (global
+    sample g -> file floor(g * 50 M / (n * world))), rank r taking samples r,
+    r + world, r + 2 * world, ... So every rank's mix — 40 % first copies,
+    60 % Zipf draws, the Zipf head (content 0) among them — is the corpus'
+    at ANY n and world: 20 000 files per rank still carry duplicates, within
+    a rank and across ranks. At n * world = 50 M (6.25 M files per GPU at
+    N = 8) the sample is the corpus itself, file 8i + r, as before; a world
+    asking more than the corpus takes files [0, n * world), the Zipf part
+    continuing past 50 M."""
+    g = np.arange(n, dtype=np.int64) * world + rank
+    tot = n * world
+    return g * C5_CORPUS // tot if tot < C5_CORPUS else g
+
+
+def files_of(workload, rank, n, world=1):
     """(sizes, content keys, global orphan ordinals) of this rank's files"""
     if workload == "c2":
         s, k = S.c2_files(rank * n, (rank + 1) * n)
@@ -105,10 +121,9 @@ def files_of(workload, rank, n):
         s, k, _ = S.c3_files(rank * n, (rank + 1) * n)
         return s, k, np.arange(rank * n, (rank + 1) * n, dtype=np.int64)
     if workload == "c5":
-        # a strided share of the corpus keeps each GPU's mix (40% first
-        # copies, 60% Zipf draws) equal to the whole corpus' at any N <= 8;
-        # the orphan ordinals (the job's id order) are contiguous per rank
-        fi = np.arange(n, dtype=np.int64) * C5_STRIDE + rank % C5_STRIDE + (rank // C5_STRIDE) * n * C5_STRIDE
+        # an even sample of the corpus per rank (c5_share); the orphan
+        # ordinals (the job's id order) are contiguous per rank
+        fi = c5_share(rank, n, world)
         cid = S.c5_content_ids_at(fi.astype(np.uint64))
         return S.c5_sizes_of(cid), S.content_key(S.SEED_C5, cid), np.arange(rank * n, (rank + 1) * n, dtype=np.int64)
     raise ValueError(workload)
@@ -898,7 +913,7 @@ def main():
     from spacedrive_amd.dist_dedup import DeviceStages, identifier_dedup_distributed
 
     n = args.files or W["files"]
-    sizes, keys, ids = files_of(args.workload, rank, n)
+    sizes, keys, ids = files_of(args.workload, rank, n, world)
     lens = S.cas_msg_len(sizes)
     offs = np.zeros(n, np.uint64)
     # messages start on 128-byte lines (the L2/HBM line): a chunk then spans
@@ -1116,7 +1131,7 @@ def main():
                 from tests._oracle import load_oracle
                 allk = np.concatenate([x.cpu().numpy()[:n] for x in parts]).view(np.uint64)
                 alll = np.concatenate([x.cpu().numpy()[n:] for x in parts])
-                has = np.concatenate([(files_of(args.workload, r, n)[0] != 0) for r in range(world)]).astype(np.uint8)
+                has = np.concatenate([(files_of(args.workload, r, n, world)[0] != 0) for r in range(world)]).astype(np.uint8)
                 want, wc, wl = load_oracle().identifier_dedup(allk, has, None, 100)
                 out["parity"]["dedup"] = {"files": int(alll.size), "link_mismatches": int((alll != want).sum()),
                                           "counts_match": (wc, wl) == (dd["last"][1], dd["last"][2]),

@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -341,9 +342,19 @@ __global__ void k_stays_gather(const uint32_t* __restrict__ idx, const uint32_t*
 __global__ __launch_bounds__(64) void k_plan_walk(const uint64_t* __restrict__ stays, const uint32_t* __restrict__ idx,
                                                   const uint64_t* __restrict__ ids, uint32_t cap,
                                                   const uint32_t* __restrict__ m_p, uint64_t n_total, uint64_t cs,
-                                                  uint64_t max_steps, uint32_t more, uint64_t* __restrict__ plan) {
+                                                  uint64_t max_steps, uint32_t more, uint64_t* __restrict__ plan,
+                                                  const uint32_t* __restrict__ tile_cnt = nullptr, uint32_t ntiles = 0) {
   const int lane = (int)threadIdx.x;
-  const uint32_t m = m_p ? min(*m_p, cap) : cap;
+  uint32_t m;
+  if (tile_cnt) {  // the tiled insert's per-tile stays counts: their sum
+    uint32_t s = 0;
+    for (uint32_t t = (uint32_t)lane; t < ntiles; t += 64) s += tile_cnt[t];
+#pragma unroll
+    for (int d = 32; d; d >>= 1) s += __shfl_xor(s, d);
+    m = min(s, cap);
+  } else {
+    m = m_p ? min(*m_p, cap) : cap;
+  }
   uint64_t* rr = plan + kPlanHeader;
   uint64_t r = 0;
   uint64_t first = ~0ull, last_stay = ~0ull;  // smallest / largest valid stays ordinal
@@ -583,7 +594,7 @@ __global__ void k_solo_insert_idx(const uint64_t* __restrict__ keys, const uint6
                                   const uint8_t* __restrict__ has_key, const int32_t* __restrict__ status,
                                   const uint64_t* __restrict__ eids, uint32_t count, uint32_t base,
                                   uint32_t* __restrict__ tab, unsigned long long* __restrict__ emin, uint32_t mask,
-                                  uint32_t shift, uint32_t* __restrict__ pos);
+                                  uint32_t shift, uint32_t* __restrict__ pos, uint32_t* __restrict__ stay_cnt);
 
 // ---- the bucket combine through a hash table (default; SDCAS_COMBINE=sort: radix sort) --
 //
@@ -670,51 +681,6 @@ __global__ void k_cb_counts(const uint32_t* __restrict__ fill, uint32_t world, u
 static bool combine_by_hash() {
   const char* v = getenv("SDCAS_COMBINE");
   return !(v && strcmp(v, "sort") == 0);
-}
-
-static hipError_t combine_buckets_hash(DistWs& w, const uint64_t* keys, const uint8_t* has_key,
-                                       const int32_t* status, const uint64_t* ids, uint32_t n, uint32_t world,
-                                       uint32_t cap, uint64_t* send, uint32_t* slot, int64_t* counts,
-                                       uint32_t* overflow, hipStream_t st) {
-  uint64_t tcap = 1024;
-  while (tcap < 2 * (uint64_t)n) tcap <<= 1;
-  if (tcap > (1ull << 31)) return hipErrorInvalidValue;
-  hipError_t e;
-  if ((e = w.idx_a.ensure(tcap)) || (e = w.idx_b.ensure(n)) || (e = w.tpos.ensure(n)) ||
-      (e = w.starts.ensure(world + 1)))
-    return e;
-  const uint32_t mask = (uint32_t)(tcap - 1);
-  const uint32_t shift = 64u - (uint32_t)__builtin_ctzll(tcap);
-  if ((e = hipMemsetAsync(w.idx_a.p, 0xFF, sizeof(uint32_t) * tcap, st)) ||
-      (e = hipMemsetAsync(w.starts.p, 0, sizeof(uint32_t) * (world + 1), st)))
-    return e;
-  hipLaunchKernelGGL(k_solo_insert_idx, dim3(blocks(n)), dim3(TB), 0, st, keys, (const uint64_t*)nullptr, n, has_key,
-                     status, (const uint64_t*)nullptr, n, 0u, w.idx_a.p, (unsigned long long*)nullptr, mask, shift,
-                     w.idx_b.p);
-  hipLaunchKernelGGL(k_cb_emit, dim3((uint32_t)((n + TB * kEmitR - 1) / (TB * kEmitR))), dim3(TB), 0, st, keys, ids,
-                     n, w.idx_b.p, w.idx_a.p, world, cap,
-                     w.starts.p, send, w.tpos.p, overflow);
-  hipLaunchKernelGGL(k_cb_counts, dim3(blocks(world)), dim3(TB), 0, st, w.starts.p, world, cap, counts);
-  if (slot) hipLaunchKernelGGL(k_cb_slot, dim3(blocks(n)), dim3(TB), 0, st, w.idx_b.p, w.idx_a.p, w.tpos.p, n, slot);
-  return hipGetLastError();
-}
-
-hipError_t dd_combine_buckets(DistWs& w, const uint64_t* keys, const uint8_t* has_key, const int32_t* status,
-                              const uint64_t* ids, uint32_t n, uint32_t world, uint32_t cap, uint64_t* send,
-                              uint32_t* slot, int64_t* counts, uint32_t* overflow, hipStream_t st) {
-  hipError_t e;
-  if ((e = hipMemsetAsync(overflow, 0, sizeof(uint32_t), st))) return e;
-  if (n == 0) return hipMemsetAsync(counts, 0, sizeof(int64_t) * world, st);
-  if (combine_by_hash() && world <= kEmitMaxWorld)
-    return combine_buckets_hash(w, keys, has_key, status, ids, n, world, cap, send, slot, counts, overflow, st);
-  if ((e = w.ukey.ensure(2 * (size_t)n))) return e;
-  if ((e = combine_core(w, keys, has_key, status, ids, n, world, w.ukey.p, slot, st))) return e;
-  hipLaunchKernelGGL(k_dd_pack, dim3(blocks(n)), dim3(TB), 0, st, w.ukey.p, w.scan.p, w.nvalid.p, w.starts.p, world,
-                     cap, send, overflow);
-  hipLaunchKernelGGL(k_dd_bucket_counts, dim3(blocks(world)), dim3(TB), 0, st, w.starts.p, world, cap, counts);
-  if (slot)
-    hipLaunchKernelGGL(k_dd_slot_remap, dim3(blocks(n)), dim3(TB), 0, st, w.ukey.p, w.starts.p, world, cap, n, slot);
-  return hipGetLastError();
 }
 
 // ---- resolve: per-key minima in an open-addressing hash table -----------------
@@ -829,6 +795,96 @@ __global__ void k_ht_answer_b(const uint32_t* __restrict__ pos, uint32_t total, 
   result[q] = e != ~0ull ? -(int64_t)e - 1 : (int64_t)tmin[2 * (uint64_t)h];
 }
 
+// Round 5: the owner's table sized from the records that arrived, not from
+// the buckets' capacity, in one 16-byte (key, files' minimum) entry per slot
+// — an insert is one line (its CAS and its atomicMin), an answer one line —
+// plus the existing Objects' minima in a side array only when some arrived.
+// The valid counts live on the device (the exchange carried them), so a
+// one-wave kernel turns them into the table's mask and shift (cfg) and the
+// other kernels read those: no host synchronisation, and only the table
+// that is used is cleared. C5 at world 8 before: world x cap = 7.03 M slots
+// of records, 2^24 slots x 24 B = 402 MB cleared per call for 3.04 M valid
+// records; now 2^23 x 16 B = 134 MB.
+__global__ void k_rb_size(const int64_t* __restrict__ fcounts, const int64_t* __restrict__ ecounts, uint32_t world,
+                          uint32_t* __restrict__ cfg) {
+  const uint32_t lane = threadIdx.x;
+  uint64_t s = 0;
+  for (uint32_t r = lane; r < world; r += 64) s += (uint64_t)fcounts[r] + (ecounts ? (uint64_t)ecounts[r] : 0ull);
+#pragma unroll
+  for (int d = 32; d; d >>= 1) s += __shfl_xor(s, d);
+  if (lane == 0) {
+    uint64_t cap = 1024;
+    while (cap < 2 * s) cap <<= 1;
+    cfg[0] = (uint32_t)(cap - 1);
+    cfg[1] = 64u - (uint32_t)__builtin_ctzll(cap);
+  }
+}
+
+// entries 0..mask+1 (the all-ones key's extra entry included) of the table
+// and of the existing minima (when present) to all ones
+__global__ void k_rb_clear(ulonglong2* __restrict__ tab, unsigned long long* __restrict__ emin,
+                           const uint32_t* __restrict__ cfg) {
+  const uint64_t m = (uint64_t)cfg[0] + 2;
+  const ulonglong2 ones = make_ulonglong2(~0ull, ~0ull);
+  for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < m; q += (uint64_t)gridDim.x * blockDim.x) {
+    tab[q] = ones;
+    if (emin) emin[q] = ~0ull;
+  }
+}
+
+__global__ void k_rb_insert(const uint64_t* __restrict__ rec, uint32_t bcap, const int64_t* __restrict__ counts,
+                            uint32_t total, unsigned long long* __restrict__ tab,
+                            unsigned long long* __restrict__ emin, const uint32_t* __restrict__ cfg,
+                            uint32_t* __restrict__ pos_out) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= total) return;
+  const uint32_t r = q / bcap, p = q - r * bcap;
+  if ((int64_t)p >= counts[r]) {
+    if (pos_out) pos_out[q] = kNoEntry;
+    return;
+  }
+  const uint32_t mask = cfg[0], shift = cfg[1];
+  const uint64_t key = rec[2 * (uint64_t)q];
+  const unsigned long long v = rec[2 * (uint64_t)q + 1];
+  uint32_t h = mask + 1;  // the all-ones key's own entry
+  if (key != kEmptyKey) {
+    h = (uint32_t)((key << kOwnerBits) >> shift) & mask;  // below the owner bits (ht_find)
+    for (;;) {
+      const unsigned long long cur =
+          __hip_atomic_load(&tab[2 * (uint64_t)h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cur == key) break;
+      if (cur == kEmptyKey) {
+        const unsigned long long prev =
+            atomicCAS(&tab[2 * (uint64_t)h], (unsigned long long)kEmptyKey, (unsigned long long)key);
+        if (prev == kEmptyKey || prev == key) break;
+      }
+      h = (h + 1) & mask;
+    }
+  }
+  unsigned long long* m = emin ? &emin[h] : &tab[2 * (uint64_t)h + 1];
+  if (__hip_atomic_load(m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > v) atomicMin(m, v);
+  if (pos_out) pos_out[q] = h;
+}
+
+__global__ void k_rb_answer(const uint32_t* __restrict__ pos, uint32_t total, const uint64_t* __restrict__ tab,
+                            const uint64_t* __restrict__ emin, int64_t* __restrict__ result) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= total) return;
+  const uint32_t h = pos[q];
+  if (h == kNoEntry) return;  // padding: nobody reads its answer
+  const uint64_t e = emin ? emin[h] : ~0ull;
+  // mod.rs:202-238: the first existing Object carrying the key; else the
+  // key's first file (mod.rs:246-254)
+  result[q] = e != ~0ull ? -(int64_t)e - 1 : (int64_t)tab[2 * (uint64_t)h + 1];
+}
+
+// SDCAS_RESOLVE=split: round 4's resolve (key array + minima pairs sized from
+// the buckets' capacity; A/B)
+static bool resolve_split() {
+  const char* v = getenv("SDCAS_RESOLVE");
+  return v && strcmp(v, "split") == 0;
+}
+
 hipError_t dd_resolve_buckets(DistWs& w, const uint64_t* frec, uint32_t fcap, const int64_t* fcounts,
                               const uint64_t* erec, uint32_t ecap, const int64_t* ecounts, uint32_t world,
                               int64_t* result, hipStream_t st) {
@@ -838,6 +894,26 @@ hipError_t dd_resolve_buckets(DistWs& w, const uint64_t* frec, uint32_t fcap, co
   uint64_t cap = 1024;
   while (cap < 2 * ((uint64_t)nf + ne)) cap <<= 1;
   if (cap > (1ull << 31)) return hipErrorInvalidValue;
+  if (!resolve_split()) {
+    // cap bounds the table the valid counts ask for; allocate that, clear what they ask
+    if ((e = w.tmin.ensure(2 * (cap + 1))) || (ne && (e = w.tkey.ensure(cap + 1))) || (e = w.tpos.ensure(nf)) ||
+        (e = w.starts.ensure(2)))
+      return e;
+    auto* tab = reinterpret_cast<unsigned long long*>(w.tmin.p);
+    auto* em = ne ? reinterpret_cast<unsigned long long*>(w.tkey.p) : nullptr;
+    hipLaunchKernelGGL(k_rb_size, dim3(1), dim3(64), 0, st, fcounts, ne ? ecounts : nullptr, world, w.starts.p);
+    const uint64_t slots = cap + 1;
+    const uint32_t cg = (uint32_t)std::min<uint64_t>((slots + TB - 1) / TB, 2048);
+    hipLaunchKernelGGL(k_rb_clear, dim3(cg), dim3(TB), 0, st, reinterpret_cast<ulonglong2*>(tab), em, w.starts.p);
+    if (ne)
+      hipLaunchKernelGGL(k_rb_insert, dim3(blocks(ne)), dim3(TB), 0, st, erec, ecap, ecounts, ne, tab, em, w.starts.p,
+                         (uint32_t*)nullptr);
+    hipLaunchKernelGGL(k_rb_insert, dim3(blocks(nf)), dim3(TB), 0, st, frec, fcap, fcounts, nf, tab,
+                       (unsigned long long*)nullptr, w.starts.p, w.tpos.p);
+    hipLaunchKernelGGL(k_rb_answer, dim3(blocks(nf)), dim3(TB), 0, st, w.tpos.p, nf, w.tmin.p,
+                       ne ? w.tkey.p : nullptr, result);
+    return hipGetLastError();
+  }
   if ((e = w.tkey.ensure(cap + 1)) || (e = w.tmin.ensure(2 * (cap + 1))) || (e = w.tpos.ensure(nf))) return e;
   const uint32_t mask = (uint32_t)(cap - 1);
   const uint32_t shift = 64u - (uint32_t)__builtin_ctzll(cap);
@@ -946,17 +1022,24 @@ __device__ __forceinline__ uint64_t idx_key(const uint64_t* __restrict__ keys, c
 
 // files (emin null, base 0): pos[i] = slot, or the code of a file without
 // one; existing Objects (emin set, base n): min-fold eids[j] into emin[slot]
+// stay_cnt (files, may be null): += the rows of each 1024-row tile that stay
+// orphans, one atomicAdd per wave holding one
 __global__ void k_solo_insert_idx(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ ekeys, uint32_t n,
                                   const uint8_t* __restrict__ has_key, const int32_t* __restrict__ status,
                                   const uint64_t* __restrict__ eids, uint32_t count, uint32_t base,
                                   uint32_t* __restrict__ tab, unsigned long long* __restrict__ emin, uint32_t mask,
-                                  uint32_t shift, uint32_t* __restrict__ pos) {
+                                  uint32_t shift, uint32_t* __restrict__ pos, uint32_t* __restrict__ stay_cnt) {
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= count) return;
   const uint32_t x = base + q;
   if (!emin) {
     const bool ok = status == nullptr || status[q] == 0;  // mod.rs:125-141
     const bool has = has_key == nullptr || has_key[q];    // mod.rs:83-86
+    if (stay_cnt) {
+      const uint64_t bal = __ballot(!(ok && has));
+      if (bal && (threadIdx.x & 63) == (uint32_t)(__ffsll((long long)bal) - 1))
+        atomicAdd(&stay_cnt[q / 1024], (uint32_t)__popcll(bal));  // a wave's 64 rows share a tile
+    }
     if (!(ok && has)) {
       pos[q] = !ok ? kSlotDropped : kSlotNoKey;
       return;
@@ -1010,10 +1093,123 @@ __global__ void k_solo_apply_idx(const uint64_t* __restrict__ ids, const uint32_
   add_counts(c, l, sc, counts);
 }
 
-// SDCAS_DEDUP_TABLE=kv: the 16-byte (key, minimum) table (round 3's; A/B)
-static bool dedup_compact_table() {
+// ---- round 5: the world-of-one path in fewer launches -----------------------------
+//
+// The files' insert also counts, per 1024-row tile, the rows that stay
+// orphans (one atomicAdd per wave that holds one; C3 / C5 have none), so
+// the stays pass loses its counting launch and its one-workgroup scan: the
+// writer sums the counts of the tiles before its own, and the plan walk sums
+// them all. One clear kernel empties the table, the existing Objects'
+// minima and the tile counts. Five launches where round 4 had eight (C3:
+// 0.181 -> 0.168 ms per call in the same process, profiles/r05_ab_dedup.json).
+// Measured and not kept (same-process A/Bs, bit-identical links): tiles of
+// 1024 / 4096 files issuing each probe phase for 4 or 16 files per thread
+// together, and tiles that first group their files by key in LDS so that only
+// a key's lowest file per tile touches the table (C5's 4096-file tiles hold
+// 71 % distinct keys) — every shape was slower on C5, 0.43-0.67 ms against
+// 0.40, the barrier a tile needs holding its workgroup until its slowest
+// probe chain ends.
+constexpr uint32_t kStayTile = 1024;  // rows per stays count (a multiple of the wave)
+
+__global__ void k_local_clear(uint4* __restrict__ tab, uint64_t tab_q, uint4* __restrict__ em, uint64_t em_q,
+                              uint32_t* __restrict__ cnt, uint32_t nt) {
+  const uint4 ones = make_uint4(~0u, ~0u, ~0u, ~0u);
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (uint64_t q = t0; q < tab_q; q += stride) tab[q] = ones;
+  for (uint64_t q = t0; q < em_q; q += stride) em[q] = ones;
+  for (uint64_t q = t0; q < nt; q += stride) cnt[q] = 0;
+}
+
+// the stays rows of tile blockIdx.x (PER rows) in order, at the offset the
+// tiles before it add up to (only tiles holding one do any work)
+template <uint32_t PER>
+__global__ void __launch_bounds__(TB) k_stays_write_t(const uint8_t* __restrict__ has_key,
+                                                      const int32_t* __restrict__ status, uint32_t n,
+                                                      const uint32_t* __restrict__ cnt, uint32_t* __restrict__ out) {
+  __shared__ uint32_t ws[TB / 64];
+  const uint32_t b = blockIdx.x;
+  if (cnt[b] == 0) return;  // uniform over the workgroup
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint32_t s = 0;
+  for (uint32_t t = tid; t < b; t += TB) s += cnt[t];
+#pragma unroll
+  for (uint32_t d = 32; d; d >>= 1) s += __shfl_xor(s, d);
+  if (lane == 0) ws[wave] = s;
+  __syncthreads();
+  uint32_t run = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < TB / 64; ++w) run += ws[w];
+  __syncthreads();
+  const uint64_t lo = (uint64_t)b * PER;
+#pragma unroll 1
+  for (uint32_t r = 0; r < PER / TB; ++r) {
+    const uint64_t i = lo + r * TB + tid;
+    const bool f = i < n && stays_row(has_key, status, i);
+    const uint64_t bal = __ballot(f);
+    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+    if (lane == 0) ws[wave] = (uint32_t)__popcll(bal);
+    __syncthreads();
+    uint32_t before = run, all = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < TB / 64; ++w) {
+      if (w < wave) before += ws[w];
+      all += ws[w];
+    }
+    __syncthreads();
+    if (f) out[before + below] = (uint32_t)i;
+    run += all;
+  }
+}
+
+// SDCAS_DEDUP_TABLE: "idx" (the default) = the compact u32 table, the
+// world-of-one path in five launches (above); "idx4" = the same table
+// behind round 4's eight launches; "kv" = round 3's 16-byte (key, minimum)
+// table (A/B)
+enum DedupTable { kTableIdx = 0, kTableIdx4 = 1, kTableKv = 2 };
+static DedupTable dedup_table() {
   const char* v = getenv("SDCAS_DEDUP_TABLE");
-  return !(v && strcmp(v, "kv") == 0);
+  if (v && strcmp(v, "kv") == 0) return kTableKv;
+  if (v && strcmp(v, "idx4") == 0) return kTableIdx4;
+  return kTableIdx;
+}
+
+static hipError_t local_fused(DistWs& w, const uint64_t* keys, const uint8_t* has_key, const int32_t* status,
+                              const uint64_t* ids, uint32_t n, const uint64_t* ekeys, const uint64_t* eids,
+                              uint32_t ne, uint64_t cs, const StepWindow& win, int64_t* link,
+                              unsigned long long* counts, uint64_t cap, hipStream_t st) {
+  hipError_t e;
+  const uint32_t nt = (n + kStayTile - 1) / kStayTile;
+  const bool stays = has_key || status;
+  const uint32_t mask = (uint32_t)(cap - 1);
+  const uint32_t shift = 64u - (uint32_t)__builtin_ctzll(cap);
+  // the u32 table borrows tmin's storage (cap u32 = cap / 4 of its u64);
+  // the existing Objects' minima live in tkey (cap u64), when there are any
+  if ((e = w.tmin.ensure(cap / 2 + 1)) || (e = w.tpos.ensure(n)) || (ne && (e = w.tkey.ensure(cap + 1))) ||
+      (e = w.stay_cnt.ensure(nt + 1)) || (stays && (e = w.stay_idx.ensure(n))))
+    return e;
+  auto* tab = reinterpret_cast<uint32_t*>(w.tmin.p);
+  auto* em = ne ? reinterpret_cast<unsigned long long*>(w.tkey.p) : nullptr;
+  const uint64_t tab_q = cap / 4, em_q = ne ? cap / 2 : 0;  // uint4 stores (cap >= 1024)
+  const uint32_t cg = (uint32_t)std::min<uint64_t>((tab_q + em_q + TB - 1) / TB, 2048);
+  hipLaunchKernelGGL(k_local_clear, dim3(cg), dim3(TB), 0, st, reinterpret_cast<uint4*>(tab), tab_q,
+                     reinterpret_cast<uint4*>(em), em_q, w.stay_cnt.p, stays ? nt : 0u);
+  if (ne)
+    hipLaunchKernelGGL(k_solo_insert_idx, dim3(blocks(ne)), dim3(TB), 0, st, keys, ekeys, n, (const uint8_t*)nullptr,
+                       (const int32_t*)nullptr, eids, ne, n, tab, em, mask, shift, (uint32_t*)nullptr,
+                       (uint32_t*)nullptr);
+  hipLaunchKernelGGL(k_solo_insert_idx, dim3(blocks(n)), dim3(TB), 0, st, keys, ekeys, n, has_key, status,
+                     (const uint64_t*)nullptr, n, 0u, tab, (unsigned long long*)nullptr, mask, shift, w.tpos.p,
+                     stays ? w.stay_cnt.p : (uint32_t*)nullptr);
+  if (stays)
+    hipLaunchKernelGGL(k_stays_write_t<kStayTile>, dim3(nt), dim3(TB), 0, st, has_key, status, n, w.stay_cnt.p,
+                       w.stay_idx.p);
+  hipLaunchKernelGGL(k_plan_walk, dim3(1), dim3(64), 0, st, (const uint64_t*)nullptr, w.stay_idx.p, ids,
+                     stays ? n : 0u, (const uint32_t*)nullptr, win.n_total ? win.n_total : (uint64_t)n, cs,
+                     win.max_steps, win.more, w.plan.p, stays ? w.stay_cnt.p : (const uint32_t*)nullptr, nt);
+  hipLaunchKernelGGL(k_solo_apply_idx, dim3(blocks(n) < 1024 ? blocks(n) : 1024), dim3(TB), 0, st, ids, w.tpos.p, n,
+                     tab, ne ? w.tkey.p : nullptr, cs, w.plan.p, link, counts);
+  return hipGetLastError();
 }
 
 hipError_t dd_stays(DistWs& w, const uint8_t* has_key, const int32_t* status, const uint64_t* ids, uint32_t n,
@@ -1060,6 +1256,13 @@ hipError_t dd_local(DistWs& w, const uint64_t* keys, const uint8_t* has_key, con
   if (chunk_size == 0) chunk_size = 100;
   // the steps' plan from this batch's stays rows (all of the job's: a world of one)
   if ((e = w.nstay.ensure(1)) || (e = w.plan.ensure(kPlanHeader + (uint64_t)n + 1))) return e;
+  const DedupTable table = dedup_table();
+  if (n && table == kTableIdx) {
+    uint64_t cap = 1024;
+    while (cap < 2 * ((uint64_t)n + ne)) cap <<= 1;
+    if (cap > (1ull << 31)) return hipErrorInvalidValue;
+    return local_fused(w, keys, has_key, status, ids, n, ekeys, eids, ne, chunk_size, win, link, counts, cap, st);
+  }
   if (n && (has_key || status)) {
     if ((e = select_stays(w, has_key, status, n, st))) return e;
   } else if ((e = hipMemsetAsync(w.nstay.p, 0, sizeof(uint32_t), st))) {
@@ -1071,7 +1274,7 @@ hipError_t dd_local(DistWs& w, const uint64_t* keys, const uint8_t* has_key, con
   uint64_t cap = 1024;
   while (cap < 2 * ((uint64_t)n + ne)) cap <<= 1;
   if (cap > (1ull << 31)) return hipErrorInvalidValue;
-  if (dedup_compact_table()) {
+  if (table == kTableIdx4) {
     const uint32_t mask = (uint32_t)(cap - 1);
     const uint32_t shift = 64u - (uint32_t)__builtin_ctzll(cap);
     // the u32 table borrows tmin's storage (cap u32 = cap / 4 of its u64);
@@ -1085,9 +1288,10 @@ hipError_t dd_local(DistWs& w, const uint64_t* keys, const uint8_t* has_key, con
     if (ne)
       hipLaunchKernelGGL(k_solo_insert_idx, dim3(blocks(ne)), dim3(TB), 0, st, keys, ekeys, n,
                          (const uint8_t*)nullptr, (const int32_t*)nullptr, eids, ne, n, tab, em, mask, shift,
-                         (uint32_t*)nullptr);
+                         (uint32_t*)nullptr, (uint32_t*)nullptr);
     hipLaunchKernelGGL(k_solo_insert_idx, dim3(blocks(n)), dim3(TB), 0, st, keys, ekeys, n, has_key, status,
-                       (const uint64_t*)nullptr, n, 0u, tab, (unsigned long long*)nullptr, mask, shift, w.tpos.p);
+                       (const uint64_t*)nullptr, n, 0u, tab, (unsigned long long*)nullptr, mask, shift, w.tpos.p,
+                       (uint32_t*)nullptr);
     hipLaunchKernelGGL(k_solo_apply_idx, dim3(blocks(n) < 1024 ? blocks(n) : 1024), dim3(TB), 0, st, ids, w.tpos.p, n,
                        tab, ne ? w.tkey.p : nullptr, chunk_size, w.plan.p, link, counts);
     return hipGetLastError();
@@ -1116,6 +1320,51 @@ hipError_t dd_apply(const uint64_t* ids, const uint32_t* slot, uint32_t n, const
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_dd_apply, dim3(blocks(n) < 1024 ? blocks(n) : 1024), dim3(TB), 0, st, ids, slot, n, result,
                      chunk_size ? chunk_size : 100, plan, link, counts);
+  return hipGetLastError();
+}
+
+static hipError_t combine_buckets_hash(DistWs& w, const uint64_t* keys, const uint8_t* has_key,
+                                       const int32_t* status, const uint64_t* ids, uint32_t n, uint32_t world,
+                                       uint32_t cap, uint64_t* send, uint32_t* slot, int64_t* counts,
+                                       uint32_t* overflow, hipStream_t st) {
+  uint64_t tcap = 1024;
+  while (tcap < 2 * (uint64_t)n) tcap <<= 1;
+  if (tcap > (1ull << 31)) return hipErrorInvalidValue;
+  hipError_t e;
+  if ((e = w.idx_a.ensure(tcap)) || (e = w.idx_b.ensure(n)) || (e = w.tpos.ensure(n)) ||
+      (e = w.starts.ensure(world + 1)))
+    return e;
+  const uint32_t mask = (uint32_t)(tcap - 1);
+  const uint32_t shift = 64u - (uint32_t)__builtin_ctzll(tcap);
+  if ((e = hipMemsetAsync(w.idx_a.p, 0xFF, sizeof(uint32_t) * tcap, st)) ||
+      (e = hipMemsetAsync(w.starts.p, 0, sizeof(uint32_t) * (world + 1), st)))
+    return e;
+  hipLaunchKernelGGL(k_solo_insert_idx, dim3(blocks(n)), dim3(TB), 0, st, keys, (const uint64_t*)nullptr, n, has_key,
+                     status, (const uint64_t*)nullptr, n, 0u, w.idx_a.p, (unsigned long long*)nullptr, mask, shift,
+                     w.idx_b.p, (uint32_t*)nullptr);
+  hipLaunchKernelGGL(k_cb_emit, dim3((uint32_t)((n + TB * kEmitR - 1) / (TB * kEmitR))), dim3(TB), 0, st, keys, ids,
+                     n, w.idx_b.p, w.idx_a.p, world, cap,
+                     w.starts.p, send, w.tpos.p, overflow);
+  hipLaunchKernelGGL(k_cb_counts, dim3(blocks(world)), dim3(TB), 0, st, w.starts.p, world, cap, counts);
+  if (slot) hipLaunchKernelGGL(k_cb_slot, dim3(blocks(n)), dim3(TB), 0, st, w.idx_b.p, w.idx_a.p, w.tpos.p, n, slot);
+  return hipGetLastError();
+}
+
+hipError_t dd_combine_buckets(DistWs& w, const uint64_t* keys, const uint8_t* has_key, const int32_t* status,
+                              const uint64_t* ids, uint32_t n, uint32_t world, uint32_t cap, uint64_t* send,
+                              uint32_t* slot, int64_t* counts, uint32_t* overflow, hipStream_t st) {
+  hipError_t e;
+  if ((e = hipMemsetAsync(overflow, 0, sizeof(uint32_t), st))) return e;
+  if (n == 0) return hipMemsetAsync(counts, 0, sizeof(int64_t) * world, st);
+  if (combine_by_hash() && world <= kEmitMaxWorld)
+    return combine_buckets_hash(w, keys, has_key, status, ids, n, world, cap, send, slot, counts, overflow, st);
+  if ((e = w.ukey.ensure(2 * (size_t)n))) return e;
+  if ((e = combine_core(w, keys, has_key, status, ids, n, world, w.ukey.p, slot, st))) return e;
+  hipLaunchKernelGGL(k_dd_pack, dim3(blocks(n)), dim3(TB), 0, st, w.ukey.p, w.scan.p, w.nvalid.p, w.starts.p, world,
+                     cap, send, overflow);
+  hipLaunchKernelGGL(k_dd_bucket_counts, dim3(blocks(world)), dim3(TB), 0, st, w.starts.p, world, cap, counts);
+  if (slot)
+    hipLaunchKernelGGL(k_dd_slot_remap, dim3(blocks(n)), dim3(TB), 0, st, w.ukey.p, w.starts.p, world, cap, n, slot);
   return hipGetLastError();
 }
 

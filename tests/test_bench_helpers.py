@@ -47,3 +47,29 @@ def test_committed_traffic_passes_are_found():
     for w, n in (("c5", 6_250_000), ("c3", 1_250_000)):
         d = bench.load_dedup_traffic(w, n)
         assert d is not None, w
+
+
+def test_c5_shares_keep_the_corpus_mix_at_any_size():
+    """bench.c5_share: the full-size shares are the corpus' files 8i + r (the
+    committed C5 lines' workload), and a small share still carries the
+    corpus' duplicates — the Zipf head on every rank, links within a rank and
+    across ranks"""
+    from spacedrive_amd import synth as S
+    n = 6_250_000
+    for world, rank in ((1, 0), (8, 0), (8, 5)):
+        got = bench.c5_share(rank, 1000, world) if world == 1 else None
+        full = bench.c5_share(rank, n, world)
+        assert np.array_equal(full[:1000], np.arange(1000) * 8 + (rank if world == 8 else 0))
+        if got is not None:
+            assert got[0] == 0 and np.all(np.diff(got) > 0)
+    for world in (2, 8):
+        cids = [S.c5_content_ids_at(bench.c5_share(r, 20_000, world).astype(np.uint64)) for r in range(world)]
+        for c in cids:
+            assert (c == 0).any()  # the Zipf head
+            assert np.unique(c).size < c.size  # duplicates inside a rank
+            first = (bench.c5_share(0, 20_000, world) < 20_000_000).mean()
+            assert 0.35 < first < 0.45  # ~40 % first copies, as the corpus
+        assert np.intersect1d(cids[0], cids[1]).size > 0  # duplicates across ranks
+    # shares are disjoint and inside the corpus
+    allf = np.concatenate([bench.c5_share(r, 20_000, 8) for r in range(8)])
+    assert np.unique(allf).size == allf.size and allf.max() < bench.C5_CORPUS

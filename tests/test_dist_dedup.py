@@ -314,6 +314,17 @@ def test_device_stages_empty_and_degenerate(eng, oracle):
     assert (c, l) == (wc, wl)
 
 
+def _mismatches(got, want, keys, has, status, k=8):
+    """the first k mismatching files, for an assertion message"""
+    bad = np.nonzero(got != want)[0]
+    rows = [f"{bad.size} mismatches"]
+    for b in bad[:k]:
+        first = int(np.nonzero(keys == keys[b])[0][0])
+        rows.append(f"i={b} key={int(keys[b]):016x} has={int(has[b])} status={int(status[b])} got={got[b]} "
+                    f"want={want[b]} first_with_key={first}")
+    return "\n".join(rows)
+
+
 @pytest.mark.gpu
 def test_rccl_world1(eng, oracle):
     """the real collective path (backend nccl = RCCL) at world size 1"""
@@ -334,20 +345,24 @@ def test_rccl_world1(eng, oracle):
     finally:
         dist.destroy_process_group()
     want, wc, wl = oracle.identifier_dedup(keys, has, status, 100, existing)
-    assert np.array_equal(link.cpu().numpy(), want)
+    got = link.cpu().numpy()
+    assert np.array_equal(got, want), _mismatches(got, want, keys, has, status)
     assert (c, l) == (wc, wl)
     assert cnt.is_cuda and cnt.tolist() == [wc, wl]
     assert np.array_equal(link2.cpu().numpy(), want)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("table", ["idx", "kv"])
+@pytest.mark.parametrize("table", ["idx", "idx4", "kv"])
 @pytest.mark.parametrize("corpus,chunk_size", [("default", 100), ("default", 7), ("default", 1),
                                                ("collisions", 100), ("clustered", 100)])
 def test_device_local_vs_oracle(eng, oracle, corpus, chunk_size, table, monkeypatch):
     """the fused single-rank path (sdcas_dev_dedup_local: no combine, files and
     existing Objects straight into the resolve table) against the oracle, with
-    both tables (the compact u32 default, round 3's 16-byte kv table), and the
+    every table: the compact u32 table (the default; since round 5 the
+    insert also counts the stays rows per 1024-row tile, five launches),
+    the same table behind round 4's eight launches, round 3's 16-byte kv
+    table; and the
     existing Objects passed in DB order and shuffled (their DB indices then
     not ascending: the first Object is the lowest DB index, not the first
     entry)"""
@@ -372,6 +387,13 @@ def test_device_local_vs_oracle(eng, oracle, corpus, chunk_size, table, monkeypa
     ek = torch.from_numpy(existing.view(np.int64)).cuda()
     eids = torch.arange(existing.size, dtype=torch.int64, device="cuda")
     st = DeviceStages(eng)
+    # dirty the workspace first: a larger batch with dense stays rows leaves
+    # its stays list and tile counts behind (round 5: a tiled insert counted
+    # its last tile's lanes past n as stays rows, and the walk read that
+    # call's stale entries)
+    dk, dh, ds, _ = make_corpus(3, 3 * keys.size + 1000, p_none=0.3, p_err=0.3)
+    (dk, dh, ds, dids), = shard(dk, dh, ds, existing, 1, device="cuda")[0]
+    st.local(dk, dh, ds, dids, chunk_size)
     order = torch.from_numpy(np.random.default_rng(5).permutation(existing.size)).cuda()
     for with_existing in (True, "shuffled", False):
         e_k, e_i = (ek, eids) if with_existing is True else (ek[order], eids[order])
@@ -555,17 +577,22 @@ def test_meta_group_of_a_subgroup():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("combine", ["sort", "hash"])
+@pytest.mark.parametrize("combine", ["sort", "hash", "hash-split"])
 @pytest.mark.parametrize("R,chunk_size", [(2, 100), (8, 100), (5, 7)])
 def test_device_bucket_protocol_vs_oracle(eng, oracle, R, chunk_size, combine, monkeypatch):
     """the bucket protocol's device stages (combine_buckets -> equal-split
     exchange -> resolve_buckets -> apply) over R virtual ranks with existing
-    Objects, both combines: the hash-table one (the default) and the
-    radix-sort one (SDCAS_COMBINE=sort); then buckets one record too small, which must raise
-    the overflow flag (the caller then reruns the exact stages)"""
+    Objects, every combine and resolve: the hash-table combine (the
+    default), the radix-sort one (SDCAS_COMBINE=sort); the owner's resolve
+    in a table sized on the device from the valid counts (the default) and
+    round 4's sized from the buckets' capacity (SDCAS_RESOLVE=split); then
+    buckets one record too small, which must raise the overflow flag (the
+    caller then reruns the exact stages)"""
     from spacedrive_amd.dist_dedup import DeviceStages
     from tests._dist_stages import dedup_virtual_buckets
-    monkeypatch.setenv("SDCAS_COMBINE", combine)
+    monkeypatch.setenv("SDCAS_COMBINE", combine.split("-")[0])
+    if combine == "hash-split":
+        monkeypatch.setenv("SDCAS_RESOLVE", "split")
     keys, has, status, existing = make_corpus(700 + R, 24000, pool=5000, p_none=0.05, p_err=0.05)
     want, wc, wl = oracle.identifier_dedup(keys, has, status, chunk_size, existing)
     shards, ex = shard(keys, has, status, existing, R, device="cuda")

@@ -282,6 +282,9 @@ def test_bench_two_ranks(workload, launcher):
         assert d["dedup"]["records_per_gpu"] == 20000
         pd = d["parity"]["dedup"]  # both ranks' links against the oracle over the whole corpus
         assert pd["files"] == 40000 and pd["link_mismatches"] == 0 and pd["counts_match"]
+        # the shares carry the corpus' duplicates at this size (bench.c5_share):
+        # the exchange links files, the Zipf head's among them
+        assert d["dedup"]["files_linked"] > 0
         # the dedup priced: bytes over time against HBM, and the exchange's
         # bytes and collective time
         assert d["dedup"]["roofline"]["bound"] == "hbm" and d["dedup"]["roofline"]["frac"] > 0

@@ -20,6 +20,18 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def settings(spec):
+    """'N=v1,v2' -> [{N: v1}, {N: v2}]; 'N1=a+N2=b,N1=c' -> [{N1: a, N2: b}, {N1: c}]"""
+    if spec.count("=") == 1:
+        name, vals = spec.split("=")
+        return [{name: v} for v in vals.split(",")]
+    return [dict(kv.split("=") for kv in part.split("+")) for part in spec.split(",")]
+
+
+def label(env):
+    return "+".join(f"{k}={v}" for k, v in env.items())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="c5", choices=["c3", "c5"])
@@ -28,6 +40,9 @@ def main():
     ap.add_argument("--existing", type=int, default=0, help="existing Objects (cas keys of the first K files)")
     ap.add_argument("--tables", default="", help="A/B: comma-separated SDCAS_DEDUP_TABLE values, interleaved per rep")
     ap.add_argument("--combines", default="hash", help="--world > 1: comma-separated SDCAS_COMBINE values (A/B)")
+    ap.add_argument("--ab", default="",
+                    help="A/B of settings, interleaved per rep: 'NAME=v1,v2' or 'N1=a+N2=b,N1=c+N2=d' (environment "
+                         "values each library call reads), e.g. SDCAS_DEDUP_TABLE=tile,idx")
     ap.add_argument("--world", type=int, default=1,
                     help="> 1: one rank's device stages of the bucket protocol at this world size (combine_buckets, "
                          "resolve_buckets over its own buckets as if received, apply), each timed; no exchange")
@@ -75,13 +90,14 @@ def main():
     if a.world > 1:
         W = a.world
         cap = int(n / W * 1.125) + 256
-        combines = [c for c in a.combines.split(",") if c]
+        combines = settings(a.ab) if a.ab else [{"SDCAS_COMBINE": c} for c in a.combines.split(",") if c]
+        combines = {label(c): c for c in combines}
         tm = {c: {"combine_buckets": [], "resolve_buckets": [], "apply": []} for c in combines}
         links = {}
         ovf = None
         for r in range(a.reps + 2):
-            for c in combines:
-                os.environ["SDCAS_COMBINE"] = c
+            for c, env in combines.items():
+                os.environ.update(env)
                 ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
                 ev[0].record(stream)
                 send, slot, cnt, ovf = stages.combine_buckets(d_out, d_has, None, d_ids, W, cap)
@@ -97,7 +113,7 @@ def main():
                     links[c] = (link.clone(), counts.clone())
         torch.cuda.synchronize()
         out = {c: {k: float(np.median([x.elapsed_time(y) for x, y in v])) for k, v in t.items()} for c, t in tm.items()}
-        l0, c0 = links[combines[0]]
+        l0, c0 = links[next(iter(combines))]
         print(json.dumps({"workload": a.workload.upper(), "files": n, "world": W, "bucket_cap": cap,
                           "overflow": int(ovf.item()), "ms_median": out,
                           "ms_total": {c: sum(v.values()) for c, v in out.items()},
@@ -106,14 +122,16 @@ def main():
         eng.close()
         dist.destroy_process_group()
         return
-    tables = [t for t in a.tables.split(",") if t] or [os.environ.get("SDCAS_DEDUP_TABLE", "")]
+    if a.ab:
+        tables = {label(c): c for c in settings(a.ab)}
+    else:
+        tables = {t: {"SDCAS_DEDUP_TABLE": t} for t in a.tables.split(",") if t} or {"": {}}
     ev = {t: [] for t in tables}
     links = {}
     link = counts = None
     for r in range(a.reps + 2):
-        for t in tables:
-            if t:
-                os.environ["SDCAS_DEDUP_TABLE"] = t
+        for t, env in tables.items():
+            os.environ.update(env)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
             link, counts = stages.local(d_out, d_has, None, d_ids, 100, ek, ei)
@@ -124,7 +142,7 @@ def main():
                 links[t] = (link.clone(), counts.clone())
     torch.cuda.synchronize()
     per = {t: [x.elapsed_time(y) for x, y in v] for t, v in ev.items()}
-    ms = per[tables[-1]]
+    ms = per[list(tables)[-1]]
     gk = d_out.cpu().numpy().view(np.uint64)
     distinct = int(np.unique(gk[sizes != 0]).size)
     algo = bench.dedup_bytes(n, a.existing)
@@ -136,7 +154,7 @@ def main():
            "created_linked": [int(x) for x in counts.tolist()]}
     if len(tables) > 1:
         res["ab"] = {t: {"ms_median": float(np.median(v)), "ms_min": float(np.min(v))} for t, v in per.items()}
-        l0, c0 = links[tables[0]]
+        l0, c0 = links[next(iter(tables))]
         res["ab_equal"] = all(torch.equal(l0, l) and torch.equal(c0, c) for l, c in links.values())
     print(json.dumps(res), flush=True)
     eng.close()
