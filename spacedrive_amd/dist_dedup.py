@@ -213,36 +213,47 @@ def _exchange(send, send_counts, group, recv_counts=None):
     return recv, recv_counts
 
 
-_META_GROUPS = {}
+_META_GROUPS = {}  # sorted ranks -> the gloo group of host integers over them
 
 
-def prepare_meta_group(group=None):
+def _ranks_of(group):
+    return tuple(range(dist.get_world_size())) if group is None else tuple(sorted(dist.get_process_group_ranks(group)))
+
+
+def prepare_meta_group(group=None, ranks=None):
     """Create the gloo group over `group`'s ranks that carries the host-known
     integers (file and Object counts: exchanging them never waits for the
     device). dist.new_group is collective over the WHOLE default group, so
     for a strict subgroup every rank of the default group must call this
-    (members and non-members alike) before the subgroup's first dedup; the
-    default group's own is created on its first dedup, which every rank
-    reaches."""
-    if dist.get_backend(group) == "gloo":
-        return group
-    key = id(group)
+    before the subgroup's first dedup — a member with the subgroup's handle
+    (or its ranks), a rank outside it with `ranks` (its handle of the
+    subgroup is torch's NON_GROUP_MEMBER, which names no ranks); the default
+    group's own is created on its first dedup, which every rank reaches.
+    Every rank creates the same group whatever the subgroup's backend, and
+    groups are kept by their ranks, so two subgroups never share one."""
+    if ranks is None:
+        if group is not None and dist.distributed_c10d._rank_not_in_group(group):
+            raise ValueError("prepare_meta_group: this rank is outside `group`; pass the subgroup's ranks= instead")
+        key = _ranks_of(group)
+    else:
+        key = tuple(sorted(int(r) for r in ranks))
     if key not in _META_GROUPS:
-        ranks = dist.get_process_group_ranks(group) if group is not None else None
-        _META_GROUPS[key] = dist.new_group(ranks=ranks, backend="gloo")
+        _META_GROUPS[key] = dist.new_group(ranks=list(key), backend="gloo")
     return _META_GROUPS[key]
 
 
 def _meta_group(group):
     if dist.get_backend(group) == "gloo":
         return group
-    if id(group) not in _META_GROUPS:
-        whole = group is None or dist.get_world_size(group) == dist.get_world_size()
-        if not whole:
+    key = _ranks_of(group)
+    if key not in _META_GROUPS:
+        if len(key) != dist.get_world_size():
             raise RuntimeError("identifier_dedup_distributed over a subgroup: call "
-                               "dist_dedup.prepare_meta_group(group) on every rank of the default group first "
+                               "dist_dedup.prepare_meta_group(group) on every member and "
+                               "prepare_meta_group(ranks=...) on every other rank of the default group first "
                                "(dist.new_group is collective over all ranks)")
-    return prepare_meta_group(group)
+        _META_GROUPS[key] = dist.new_group(ranks=list(key), backend="gloo")
+    return _META_GROUPS[key]
 
 
 def _meta(n, ne, group):

@@ -31,6 +31,7 @@ const void* sqlite3_column_blob(sqlite3_stmt* s, int i);
 int sqlite3_column_bytes(sqlite3_stmt* s, int i);
 int64_t sqlite3_last_insert_rowid(sqlite3* db);
 int sqlite3_changes(sqlite3* db);
+int sqlite3_busy_timeout(sqlite3* db, int ms);
 }
 
 constexpr int SQLITE_OK = 0;

@@ -3,6 +3,7 @@
 // file_path / object models (core/prisma/schema.prisma) and its queries
 // (file_identifier_job.rs:251-319, mod.rs:157-342, validator_job.rs:107-172)
 // as prepared statements. See include/sdcore.hpp.
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <stdexcept>
@@ -91,13 +92,24 @@ struct SqliteLibrary::Impl {
   void index_restore() {
     if (!bulk) return;
     if (batch_depth) exec("COMMIT");  // CREATE INDEX in its own transaction
-    // the sorter may use helper threads for the one big sort (PRAGMA threads)
-    exec("PRAGMA threads = 4");
-    exec("CREATE INDEX IF NOT EXISTS file_path_cas_id_idx ON file_path (cas_id)");
-    exec("PRAGMA threads = 0");
-    // the WAL checkpoints the job deferred, once (begin_bulk_identify)
-    exec("PRAGMA wal_checkpoint(PASSIVE)");
-    exec("PRAGMA wal_autocheckpoint = 1000");
+    try {
+      // the sorter may use helper threads for the one big sort (PRAGMA threads)
+      exec("PRAGMA threads = 4");
+      if (const char* f = getenv("SDCORE_FAULT"); f && !strcmp(f, "index_restore"))  // tests: a failing rebuild
+        exec("CREATE INDEX file_path_cas_id_idx_fault ON no_such_table (x)");
+      exec("CREATE INDEX IF NOT EXISTS file_path_cas_id_idx ON file_path (cas_id)");
+      exec("PRAGMA threads = 0");
+      // the WAL checkpoints the job deferred, once (begin_bulk_identify)
+      exec("PRAGMA wal_checkpoint(PASSIVE)");
+      exec("PRAGMA wal_autocheckpoint = 1000");
+    } catch (...) {
+      // leave the caller's batch open as it was (its end_batch commits it)
+      // and stay in bulk mode, so that a later restore (end_bulk_identify)
+      // rebuilds the index
+      sqlite3_exec(db, "PRAGMA threads = 0", nullptr, nullptr, nullptr);
+      if (batch_depth) sqlite3_exec(db, "BEGIN IMMEDIATE", nullptr, nullptr, nullptr);
+      throw;
+    }
     if (batch_depth) exec("BEGIN IMMEDIATE");
     bulk = false;
     first.clear();
@@ -294,8 +306,13 @@ std::unique_ptr<SqliteLibrary> SqliteLibrary::open(const std::string& path, bool
             " GROUP BY cas_id");
   x.prepare(x.all_objects, "SELECT id, pub_id, kind, date_created FROM object ORDER BY id");
   {
+    // the id AUTOINCREMENT would assign next: past the largest id the table
+    // ever held (sqlite_sequence keeps it after the top Objects are deleted),
+    // not only past the largest it holds now (create_objects gives ids)
     Stmt mx;
-    x.prepare(mx, "SELECT COALESCE(MAX(id), 0) FROM object");
+    x.prepare(mx,
+              "SELECT MAX(COALESCE((SELECT MAX(id) FROM object), 0),"
+              " COALESCE((SELECT seq FROM sqlite_sequence WHERE name = 'object'), 0))");
     if (sqlite3_step(mx.s) == SQLITE_ROW) x.next_object = sqlite3_column_int64(mx.s, 0) + 1;
   }
   return std::unique_ptr<SqliteLibrary>(new SqliteLibrary(std::move(d)));
@@ -583,6 +600,9 @@ bool SqliteLibrary::concurrent_orphan_reads() {
     x.rdb = nullptr;
     return false;
   }
+  // a WAL recovery or checkpoint of the writer can hold the read a moment:
+  // wait for it rather than fail the job
+  sqlite3_busy_timeout(x.rdb, 5000);
   char* err = nullptr;
   if (sqlite3_exec(x.rdb, "PRAGMA mmap_size = 4294967296", nullptr, nullptr, &err) != SQLITE_OK ||
       sqlite3_prepare_v2(x.rdb,
@@ -602,7 +622,11 @@ bool SqliteLibrary::concurrent_orphan_reads() {
 std::vector<FilePathRow> SqliteLibrary::get_orphan_file_paths_concurrent(int32_t location_id, int32_t cursor,
                                                                          const std::string& sub, size_t take) {
   Impl& x = *d_;
-  if (!x.rdb) return get_orphan_file_paths(location_id, cursor, sub, take);
+  // the writer's connection is opened NOMUTEX: reading through it from
+  // another thread would race with the writes
+  if (!x.rdb)
+    throw std::logic_error("sqlite: get_orphan_file_paths_concurrent without the read-ahead connection "
+                           "(concurrent_orphan_reads() returned false or was not called)");
   std::lock_guard<std::mutex> g(x.rmu);
   Stmt& st = x.r_get_orphans;
   sqlite3_bind_int64(st.s, 1, location_id);

@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "../../oracle/oracle.h"
+#include "../../spacedrive_amd/host/sqlite3_min.h"
 #include "sdcore.hpp"
 
 using namespace sdcore;
@@ -743,6 +744,85 @@ static void test_kind() {
   std::printf("kind: %zu files ok\n", sizeof cases / sizeof cases[0]);
 }
 
+// SqliteLibrary's Object ids, a failing index rebuild and the read-ahead
+// guard (round 5's review findings)
+static void raw_sql(const char* path, const char* sql, int64_t* out = nullptr) {
+  sqlite3* raw = nullptr;
+  sqlite3_open_v2(path, &raw, SQLITE_OPEN_READWRITE, nullptr);
+  sqlite3_stmt* st = nullptr;
+  CHECK(sqlite3_prepare_v2(raw, sql, -1, &st, nullptr) == SQLITE_OK, "raw sql: %s", sql);
+  const int rc = sqlite3_step(st);
+  if (out && rc == SQLITE_ROW) *out = sqlite3_column_int64(st, 0);
+  sqlite3_finalize(st);
+  sqlite3_close(raw);
+}
+
+static void test_library_edges() {
+  char fpath[] = "/tmp/sdcore_idsXXXXXX";
+  {
+    const int fd = mkstemp(fpath);
+    if (fd >= 0) close(fd);
+    std::remove(fpath);
+  }
+  {
+    auto db = SqliteLibrary::open(fpath, true);
+    for (int i = 0; i < 5; ++i) db->create_object(ObjectKindImage, 0);  // ids 1..5
+  }
+  // the top Objects deleted: AUTOINCREMENT never hands out 4 or 5 again, and
+  // neither may the multi-row INSERTs, which give their ids
+  raw_sql(fpath, "DELETE FROM object WHERE id > 3");
+  {
+    auto db = SqliteLibrary::open(fpath, true);
+    const auto ids = db->create_objects(std::vector<std::pair<ObjectKind, int64_t>>(70, {ObjectKindImage, 0}));
+    bool seq = ids.size() == 70;
+    for (size_t i = 0; seq && i < ids.size(); ++i) seq = ids[i] == (int32_t)(6 + i);
+    CHECK(seq, "bulk Object ids after deleted top Objects start at %d", ids.empty() ? -1 : ids[0]);
+    const int32_t one = db->create_object(ObjectKindImage, 0);
+    CHECK(one == 76, "the next single Object %d", one);
+  }
+  // an index rebuild that fails inside a batch: the batch stays usable (its
+  // commit succeeds), bulk identify stays on, and a later restore rebuilds
+  {
+    auto db = SqliteLibrary::open(fpath, true);
+    CHECK(db->begin_bulk_identify(100), "bulk identify on an empty file_path table");
+    db->begin_batch();
+    setenv("SDCORE_FAULT", "index_restore", 1);
+    bool threw = false;
+    try {
+      db->end_bulk_identify();
+    } catch (const std::exception&) {
+      threw = true;
+    }
+    unsetenv("SDCORE_FAULT");
+    CHECK(threw && db->bulk_identify_active(), "a failing rebuild raises and keeps bulk identify on");
+    const int32_t id = db->create_object(ObjectKindText, 0);
+    bool committed = true;
+    try {
+      db->end_batch();
+    } catch (const std::exception&) {
+      committed = false;
+    }
+    CHECK(committed && id == 77, "the batch after a failing rebuild commits (object %d)", id);
+    db->end_bulk_identify();
+    CHECK(!db->bulk_identify_active(), "the second rebuild ends bulk identify");
+  }
+  int64_t idx = 0, objs = 0;
+  raw_sql(fpath, "SELECT COUNT(*) FROM sqlite_master WHERE name = 'file_path_cas_id_idx'", &idx);
+  raw_sql(fpath, "SELECT COUNT(*) FROM object", &objs);
+  CHECK(idx == 1 && objs == 3 + 70 + 1 + 1, "index restored (%lld), objects %lld", (long long)idx, (long long)objs);
+  // the read-ahead call without its connection refuses instead of reading
+  // through the writer's (NOMUTEX) connection
+  auto mem = SqliteLibrary::open(":memory:", true);
+  bool refused = false;
+  try {
+    (void)mem->get_orphan_file_paths_concurrent(1, 0, "", 10);
+  } catch (const std::logic_error&) {
+    refused = !mem->concurrent_orphan_reads();
+  }
+  CHECK(refused, "concurrent read without the read-ahead connection");
+  for (const char* suf : {"", "-wal", "-shm"}) std::remove((std::string(fpath) + suf).c_str());
+}
+
 int main(int argc, char** argv) {
   if (argc > 2 && std::strcmp(argv[1], "--bench") == 0) return bench((size_t)std::atoll(argv[2]));
   test_parity(true);
@@ -756,6 +836,7 @@ int main(int argc, char** argv) {
   g_none_mod = 31;
   test_walk();
   test_kind();
+  test_library_edges();
   std::printf("%s (%d failures)\n", failures ? "FAILED" : "ALL OK", failures);
   return failures ? 1 : 0;
 }

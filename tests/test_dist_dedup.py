@@ -539,21 +539,34 @@ def _subgroup_worker(rank, world, port, outdir):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
         sub = dist.new_group(ranks=[0, 1])
+        sub2 = dist.new_group(ranks=[1, 2])
+        member = rank in (0, 1)
         real = dist.get_backend
-        # stand in for an RCCL subgroup (the meta group is only built for a
-        # non-gloo group; gloo is all this container has)
-        D.dist.get_backend = lambda g=None: "nccl" if g is sub else real(g)
+        # stand in for an RCCL subgroup on its members (the meta group is
+        # only built for a non-gloo group; gloo is all this container has).
+        # A rank outside `sub` holds torch's NON_GROUP_MEMBER for it, on
+        # which get_backend raises: it is never asked
+        D.dist.get_backend = lambda g=None: "nccl" if member and g is sub else real(g)
         res = []
-        if rank in (0, 1):
+        if member:
             try:
                 D._meta_group(sub)
                 res.append("no error")
             except RuntimeError as e:
                 res.append("prepare_meta_group" in str(e))
-        D.prepare_meta_group(sub)  # every rank of the default group
-        if rank in (0, 1):
+        else:
+            try:
+                D.prepare_meta_group(sub)  # the handle names no ranks here
+                res.append("no error")
+            except ValueError as e:
+                res.append("ranks=" in str(e))
+        # every rank of the default group, members by handle, the other by ranks
+        g1 = D.prepare_meta_group(sub) if member else D.prepare_meta_group(ranks=[0, 1])
+        g2 = D.prepare_meta_group(sub2) if rank in (1, 2) else D.prepare_meta_group(ranks=[2, 1])
+        res.append(g1 is not g2)  # two subgroups, two meta groups (on the non-member too)
+        if member:
             g = D._meta_group(sub)
-            res.append(real(g) == "gloo" and dist.get_world_size(g) == 2)
+            res.append(g is g1 and real(g) == "gloo" and dist.get_world_size(g) == 2)
             t = torch.tensor([rank + 1])
             dist.all_reduce(t, group=g)
             res.append(int(t) == 3)
@@ -566,14 +579,16 @@ def _subgroup_worker(rank, world, port, outdir):
 def test_meta_group_of_a_subgroup():
     """the host-integer group of a strict subgroup: asking for it before it
     exists raises (dist.new_group would hang: it is collective over every
-    rank), prepare_meta_group on every rank creates it"""
+    rank); prepare_meta_group on every rank creates it — members by the
+    subgroup's handle, a rank outside it by the ranks (its handle names none,
+    and asking with it raises instead of leaving the members blocked)"""
     import torch.multiprocessing as mp
     world = 3
     with tempfile.TemporaryDirectory() as d:
         mp.start_processes(_subgroup_worker, args=(world, _free_port(), d), nprocs=world, join=True,
                            start_method="spawn")
         res = [list(np.load(os.path.join(d, f"r{r}.npy"), allow_pickle=True)) for r in range(world)]
-    assert res[0] == [True, True, True] and res[1] == [True, True, True] and res[2] == []
+    assert res[0] == [True, True, True, True] and res[1] == [True, True, True, True] and res[2] == [True, True]
 
 
 @pytest.mark.gpu
