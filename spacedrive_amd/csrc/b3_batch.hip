@@ -40,7 +40,9 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
-#include <hipcub/hipcub.hpp>
+#ifdef SDCAS_ABLATIONS
+#include <hipcub/hipcub.hpp>  // the quad-layout ablation's scan only
+#endif
 #include <stdint.h>
 #include <cstdio>
 #include <cstring>
@@ -90,9 +92,6 @@ __host__ __device__ inline bool parent_in_tile(uint64_t j, uint64_t C, uint32_t 
   return j + w <= C && 2 * w < C && s >= w && (uint64_t)s + w <= kTile;
 }
 
-struct ChunkCountOp {
-  __host__ __device__ uint64_t operator()(uint64_t len) const { return chunk_count(len); }
-};
 
 template <uint32_t TILE = kTile>
 __global__ void k_tile_first(const uint64_t* __restrict__ lens, const uint64_t* __restrict__ S, uint32_t n,
@@ -1660,16 +1659,14 @@ using QuadIt = hipcub::TransformInputIterator<uint64_t, QuadSlotsOp, hipcub::Cou
 #endif
 
 size_t batch_scan_temp_bytes(uint32_t max_msgs) {
-  size_t bytes = 0, qbytes = 0;
-  hipcub::TransformInputIterator<uint64_t, ChunkCountOp, const uint64_t*> it(nullptr, ChunkCountOp());
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, it, (uint64_t*)nullptr, (int)max_msgs);
+  size_t qbytes = 0;
 #ifdef SDCAS_ABLATIONS
   QuadIt qit(hipcub::CountingInputIterator<uint32_t>(0), QuadSlotsOp{nullptr, max_msgs});
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, qbytes, qit, (uint64_t*)nullptr, (int)max_msgs);
 #endif
-  // and the slot plan's workgroup sums (k_plan_sums)
+  // the slot plan's workgroup sums (k_plan_sums)
   const size_t plan = sizeof(uint64_t) * ((size_t)max_msgs / kPlanPer + 2);
-  return std::max({bytes, qbytes, plan});
+  return std::max(qbytes, plan);
 }
 
 // Leaf/tree kernel variants, numbered as in the A/B runs of rounds 1-2

@@ -43,15 +43,14 @@ struct DistWs {
       cap = 0;
     }
   };
-  Buf<uint64_t> key_a, key_b, umin, ukey, emin;
-  Buf<uint32_t> idx_a, idx_b, scan, nvalid, starts;
-  Buf<uint32_t> hi_a, hi_b;  // top 32 key bits: the combine's sort key
+  Buf<uint32_t> idx_a, idx_b, starts;  // the combine's table, the files' slots, owner starts (and resolve's cfg)
+  Buf<uint32_t> ocnt;                  // the combine's per-owner record counts / fills
   Buf<uint64_t> tkey, tmin;  // resolve's hash table: keys, (files' min, existing min) per entry
   Buf<uint32_t> tpos;        // table entry of each received file record
-  Buf<uint8_t> valid, temp;
   Buf<uint32_t> stay_idx, nstay;  // the batch's stay-orphan rows (dd_local's plan)
-  Buf<uint32_t> stay_cnt;         // per-workgroup stays counts, then offsets (select_stays)
+  Buf<uint32_t> stay_cnt;         // per-tile stays counts (select_stays, the fused insert, the bitmap)
   Buf<uint64_t> plan, stay_sorted;
+  Buf<uint32_t> bitmap;           // dd_plan: the stays ordinals of a long gathered list
   void release();
 };
 
@@ -98,7 +97,8 @@ hipError_t dd_plan(DistWs& w, const uint64_t* stays, uint32_t n_stays, uint64_t 
 // Stage 1. keys/has_key/status/ids: [n] (has_key, status may be null = all
 // present / all ok); ids ascending (the rank's files in orphan order, or the
 // rank's existing Objects in DB order). Writes one (key, min id) record per
-// distinct key to rec[2*u..2*u+1], key-sorted (hence grouped by owner), the
+// distinct key to rec[2*u..2*u+1], grouped by owner (in no particular order
+// within an owner's range), the
 // record index of every file to slot[i] (or kSlotNoKey/kSlotDropped; slot may
 // be null), and starts[0..world] (record index where each owner's range
 // begins) to h_starts after a stream sync. Returns the record count in *h_u.

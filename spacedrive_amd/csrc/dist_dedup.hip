@@ -13,11 +13,10 @@
 // the owner RESOLVES each key against its slice of existing Objects, and the
 // answers travel back in send order for each rank to APPLY to its files.
 //
-// HBM-bound integer work: the combine is one stable radix sort of
-// (top 32 key bits | low bits + file index) entries and streaming passes; the
-// resolve is a hash table with 64-bit atomicMin per key, no sort.
+// HBM-bound integer work, no sort anywhere: the combine is a compact hash
+// table (each key's lowest file index) and an emit pass into owner ranges;
+// the resolve is a hash table with 64-bit atomicMin per key.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstdlib>
@@ -32,87 +31,6 @@ namespace {
 constexpr uint32_t TB = 256;
 constexpr int64_t kLinkDeferred = INT64_MIN + 1;  // SDCAS_LINK_DEFERRED
 inline uint32_t blocks(uint32_t n) { return (n + TB - 1) / TB; }
-
-__global__ void k_dd_prepare(const uint8_t* __restrict__ has_key, const int32_t* __restrict__ status, uint32_t n,
-                             uint32_t* __restrict__ flag, uint32_t* __restrict__ slot) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const bool ok = status == nullptr || status[i] == 0;  // mod.rs:125-141: errored files are dropped
-  const bool has = has_key == nullptr || has_key[i];    // mod.rs:83-86: empty files have no cas_id
-  flag[i] = ok && has ? 1u : 0u;
-  if (slot) slot[i] = !ok ? kSlotDropped : kSlotNoKey;
-}
-
-// The combine's sort entries: key = top 32 key bits, value = (low 32 key
-// bits, file index) — the full key travels with the entry, so no pass after
-// the sort gathers it. Present files are compacted to the front in file order
-// (pos = inclusive scan of the present flags - 1); the tail [nv, n) keeps
-// all-ones fillers, which the stable sort leaves behind every real entry
-// (a real all-ones key sorts before them: it comes earlier in the input).
-__global__ void k_dd_hi(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ scan, uint32_t n,
-                        uint32_t* __restrict__ hi, uint64_t* __restrict__ val, uint32_t* __restrict__ nv_p) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t nv = scan[n - 1];
-  if (i == 0) *nv_p = nv;
-  const uint32_t c = scan[i];
-  if (c != (i ? scan[i - 1] : 0u)) {
-    const uint64_t k = keys[i];
-    hi[c - 1] = (uint32_t)(k >> 32);
-    val[c - 1] = (k << 32) | i;
-  }
-  if (i >= nv) {
-    hi[i] = 0xFFFFFFFFu;
-    val[i] = 0xFFFFFFFF00000000ull;
-  }
-}
-
-__device__ __forceinline__ uint64_t hv_key(const uint32_t* hi, const uint64_t* val, uint32_t p) {
-  return ((uint64_t)hi[p] << 32) | (val[p] >> 32);
-}
-
-// run heads of the sorted entries by FULL key: distinct keys sharing their
-// top bits may interleave, which splits a key into several runs but never
-// merges two keys
-__global__ void k_dd_flags_hv(const uint32_t* __restrict__ hi, const uint64_t* __restrict__ val,
-                              const uint32_t* __restrict__ nv_p, uint32_t n, uint32_t* __restrict__ flag) {
-  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= n) return;
-  const uint32_t nv = *nv_p;
-  flag[p] = (p < nv && (p == 0 || hv_key(hi, val, p) != hv_key(hi, val, p - 1))) ? 1u : 0u;
-}
-
-__global__ void k_dd_emit_hv(const uint32_t* __restrict__ hi, const uint64_t* __restrict__ val,
-                             const uint32_t* __restrict__ scan, const uint32_t* __restrict__ nv_p,
-                             const uint64_t* __restrict__ ids, uint64_t* __restrict__ rec,
-                             uint32_t* __restrict__ slot) {
-  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= *nv_p) return;
-  const uint32_t u = scan[p] - 1;
-  const uint32_t i = (uint32_t)val[p];
-  if (slot) slot[i] = u;
-  const uint64_t key = hv_key(hi, val, p);
-  if (p == 0 || key != hv_key(hi, val, p - 1)) {
-    // stable sort + ascending ids: the run's first entry carries the minimum
-    rec[2 * (uint64_t)u] = key;
-    rec[2 * (uint64_t)u + 1] = ids[i];
-  }
-}
-
-__global__ void k_dd_starts(const uint64_t* __restrict__ rec, const uint32_t* __restrict__ scan,
-                            const uint32_t* __restrict__ nv_p, uint32_t world, uint32_t* __restrict__ starts) {
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r > world) return;
-  const uint32_t nv = *nv_p;
-  const uint32_t U = nv ? scan[nv - 1] : 0u;
-  uint32_t lo = 0, hi = U;  // first record whose owner is >= r
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (dd_owner(rec[2 * (uint64_t)mid], world) < r) lo = mid + 1;
-    else hi = mid;
-  }
-  starts[r] = r == world ? U : lo;
-}
 
 // ---- the steps' positions (see dist_dedup.h, "the job's steps") -------------------
 
@@ -438,70 +356,19 @@ __global__ __launch_bounds__(64) void k_plan_walk(const uint64_t* __restrict__ s
   }
 }
 
-hipError_t ensure_temp(DistWs& w, uint32_t n) {
-  size_t a = 0, b = 0, c = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                                           (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
-  size_t b2 = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b2, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                           (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)n, 0, 32);
-  b = b > b2 ? b : b2;
-  (void)hipcub::DeviceScan::InclusiveSum(nullptr, c, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
-  size_t m = a > b ? a : b;
-  m = m > c ? m : c;
-  return w.temp.ensure(m + 256);
-}
-
-hipError_t ensure_n(DistWs& w, uint32_t n) {
-  hipError_t e;
-  if ((e = w.key_a.ensure(n)) || (e = w.key_b.ensure(n)) || (e = w.scan.ensure(n)) || (e = w.nvalid.ensure(4)))
-    return e;
-  return ensure_temp(w, n);
-}
-
 }  // namespace
 
 void DistWs::release() {
-  key_a.release(); key_b.release(); umin.release(); ukey.release(); emin.release();
-  idx_a.release(); idx_b.release(); scan.release(); nvalid.release(); starts.release(); hi_a.release();
-  hi_b.release(); tkey.release(); tmin.release(); tpos.release();
-  valid.release(); temp.release();
-  stay_idx.release(); nstay.release(); stay_cnt.release(); plan.release(); stay_sorted.release();
+  idx_a.release(); idx_b.release(); starts.release(); ocnt.release(); tkey.release(); tmin.release();
+  tpos.release(); stay_idx.release(); nstay.release(); stay_cnt.release(); plan.release(); stay_sorted.release();
+  bitmap.release();
 }
 
 // the combine up to its device outputs: rec, slot, w.starts[0..world] (n > 0)
+// (defined with the bucket combine below)
 static hipError_t combine_core(DistWs& w, const uint64_t* keys, const uint8_t* has_key, const int32_t* status,
                                const uint64_t* ids, uint32_t n, uint32_t world, uint64_t* rec, uint32_t* slot,
-                               hipStream_t st) {
-  hipError_t e;
-  if ((e = w.starts.ensure(world + 1))) return e;
-  if ((e = ensure_n(w, n))) return e;
-  if ((e = w.hi_a.ensure(n)) || (e = w.hi_b.ensure(n))) return e;
-  hipLaunchKernelGGL(k_dd_prepare, dim3(blocks(n)), dim3(TB), 0, st, has_key, status, n, w.scan.p, slot);
-  size_t tmp = w.temp.cap;
-  if ((e = hipcub::DeviceScan::InclusiveSum(w.temp.p, tmp, w.scan.p, w.scan.p, (int)n, st))) return e;
-  // The combine only has to bring equal keys together and order the owners
-  // (top 12 bits): a stable sort of (top 32 key bits, file index) pairs does
-  // both in half the passes over 2/3 of the bytes of a full 64-bit sort.
-  // Distinct keys sharing their top 32 bits (~n^2 / 2^33 pairs) may
-  // interleave and split a key into several records; resolve takes the
-  // minimum over all records of a key, so the answer is unchanged.
-  // Entries (hi32 | lo32:index) go to hi_a / key_b, sorted into hi_b / key_a.
-  hipLaunchKernelGGL(k_dd_hi, dim3(blocks(n)), dim3(TB), 0, st, keys, w.scan.p, n, w.hi_a.p, w.key_b.p,
-                     w.nvalid.p);
-  tmp = w.temp.cap;
-  if ((e = hipcub::DeviceRadixSort::SortPairs(w.temp.p, tmp, w.hi_a.p, w.hi_b.p, w.key_b.p, w.key_a.p, (int)n, 0, 32,
-                                              st)))
-    return e;
-  hipLaunchKernelGGL(k_dd_flags_hv, dim3(blocks(n)), dim3(TB), 0, st, w.hi_b.p, w.key_a.p, w.nvalid.p, n, w.scan.p);
-  tmp = w.temp.cap;
-  if ((e = hipcub::DeviceScan::InclusiveSum(w.temp.p, tmp, w.scan.p, w.scan.p, (int)n, st))) return e;
-  hipLaunchKernelGGL(k_dd_emit_hv, dim3(blocks(n)), dim3(TB), 0, st, w.hi_b.p, w.key_a.p, w.scan.p, w.nvalid.p, ids,
-                     rec, slot);
-  hipLaunchKernelGGL(k_dd_starts, dim3(blocks(world + 1)), dim3(TB), 0, st, rec, w.scan.p, w.nvalid.p, world,
-                     w.starts.p);
-  return hipGetLastError();
-}
+                               hipStream_t st);
 
 hipError_t dd_combine(DistWs& w, const uint64_t* keys, const uint8_t* has_key, const int32_t* status,
                       const uint64_t* ids, uint32_t n, uint32_t world, uint64_t* rec, uint32_t* slot,
@@ -546,49 +413,6 @@ hipError_t dd_combine_dev(DistWs& w, const uint64_t* keys, const uint8_t* has_ke
 // that travels with the final counts, and the caller then reruns the exact
 // path. Record u of owner r goes to send[r * cap + (u - starts[r])].
 
-__global__ void k_dd_pack(const uint64_t* __restrict__ rec, const uint32_t* __restrict__ scan,
-                          const uint32_t* __restrict__ nv_p, const uint32_t* __restrict__ starts, uint32_t world,
-                          uint32_t cap, uint64_t* __restrict__ send, uint32_t* __restrict__ overflow) {
-  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t nv = *nv_p;
-  const uint32_t U = nv ? scan[nv - 1] : 0u;
-  if (u >= U) return;
-  const uint64_t key = rec[2 * (uint64_t)u];
-  const uint32_t r = dd_owner(key, world);
-  const uint32_t p = u - starts[r];
-  if (p >= cap) {
-    atomicOr(overflow, 1u);
-    return;
-  }
-  const uint64_t q = (uint64_t)r * cap + p;
-  send[2 * q] = key;
-  send[2 * q + 1] = rec[2 * (uint64_t)u + 1];
-}
-
-__global__ void k_dd_bucket_counts(const uint32_t* __restrict__ starts, uint32_t world, uint32_t cap,
-                                   int64_t* __restrict__ counts) {
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= world) return;
-  const uint32_t c = starts[r + 1] - starts[r];
-  counts[r] = c < cap ? c : cap;
-}
-
-// a file's record index -> its bucket position (codes of files without a
-// record are kept)
-__global__ void k_dd_slot_remap(const uint64_t* __restrict__ rec, const uint32_t* __restrict__ starts,
-                                uint32_t world, uint32_t cap, uint32_t n, uint32_t* __restrict__ slot) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t u = slot[i];
-  if (u >= kSlotDropped) return;
-  const uint32_t r = dd_owner(rec[2 * (uint64_t)u], world);
-  const uint32_t p = u - starts[r];
-  // a record past its bucket's capacity was not sent (k_dd_pack raised the
-  // overflow flag, the caller discards this pass): keep apply's reads in
-  // bounds by pointing the file nowhere
-  slot[i] = p < cap ? r * cap + p : kSlotNoKey;
-}
-
 // (defined with the world-of-one path below)
 __global__ void k_solo_insert_idx(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ ekeys, uint32_t n,
                                   const uint8_t* __restrict__ has_key, const int32_t* __restrict__ status,
@@ -596,22 +420,27 @@ __global__ void k_solo_insert_idx(const uint64_t* __restrict__ keys, const uint6
                                   uint32_t* __restrict__ tab, unsigned long long* __restrict__ emin, uint32_t mask,
                                   uint32_t shift, uint32_t* __restrict__ pos, uint32_t* __restrict__ stay_cnt);
 
-// ---- the bucket combine through a hash table (default; SDCAS_COMBINE=sort: radix sort) --
+// ---- the combine through a hash table ----------------------------------------------
 //
-// The same outputs as the sort-based combine below — one (key, min ordinal)
-// record per distinct key in its owner's bucket, each file's bucket position
-// — from the compact table of the world-of-one path: insert (the lowest file
+// One (key, min ordinal) record per distinct key in its owner's bucket (or,
+// exact layout, its owner's range), each file's record position — from the
+// compact table of the world-of-one path: insert (the lowest file
 // index per key), then each key's lowest file emits the record into its
 // owner's bucket at a position taken per workgroup (LDS counters, one global
 // atomicAdd per owner present), then every file reads its key's position. No
 // sort; the records of a bucket are in no particular order, which neither the
 // exchange nor the owner's resolve needs.
-constexpr uint32_t kEmitR = 16;          // files per thread: 4096 per workgroup
-constexpr uint32_t kEmitMaxWorld = 256;  // owners a workgroup counts in LDS (more: the sort combine)
+constexpr uint32_t kEmitR = 16;           // files per thread: 4096 per workgroup
+constexpr uint32_t kEmitMaxWorld = 1024;  // owners a workgroup counts in LDS (more: one global atomic per record)
 
+// base null: the buckets — record p of owner r at r * cap + p, p < cap (a
+// fuller owner raises *overflow); base set: the exact layout — owner r's
+// records from base[r] on, no capacity. count_only: each owner's record
+// count added to fill[], nothing written (the exact layout's first pass).
 __global__ void __launch_bounds__(TB) k_cb_emit(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ ids,
                                                 uint32_t n, const uint32_t* __restrict__ pos,
                                                 const uint32_t* __restrict__ tab, uint32_t world, uint32_t cap,
+                                                const uint32_t* __restrict__ base, uint32_t count_only,
                                                 uint32_t* __restrict__ fill, uint64_t* __restrict__ send,
                                                 uint32_t* __restrict__ bpos, uint32_t* __restrict__ overflow) {
   // positions are taken per workgroup: LDS counters per owner, then ONE
@@ -619,7 +448,8 @@ __global__ void __launch_bounds__(TB) k_cb_emit(const uint64_t* __restrict__ key
   // aggregate left ~ 8 atomics per wave on `world` addresses: 7.5 ms for
   // C5's 6.25 M files at world 8, profiles/r04_dedup_world.json)
   __shared__ uint32_t s_cnt[kEmitMaxWorld], s_base[kEmitMaxWorld];
-  for (uint32_t t = threadIdx.x; t < world; t += TB) s_cnt[t] = 0;
+  const bool lds = world <= kEmitMaxWorld;
+  for (uint32_t t = threadIdx.x; lds && t < world; t += TB) s_cnt[t] = 0;
   __syncthreads();
   const uint64_t i0 = (uint64_t)blockIdx.x * TB * kEmitR + threadIdx.x;
   uint32_t h[kEmitR], lp[kEmitR], rr[kEmitR];
@@ -639,26 +469,57 @@ __global__ void __launch_bounds__(TB) k_cb_emit(const uint64_t* __restrict__ key
     rr[k] = 0;
     if (lp[k] == ~0u) continue;
     rr[k] = dd_owner(keys[i0 + (uint64_t)k * TB], world);
-    lp[k] = atomicAdd(&s_cnt[rr[k]], 1u);
+    lp[k] = lds ? atomicAdd(&s_cnt[rr[k]], 1u) : atomicAdd(&fill[rr[k]], 1u);
   }
   __syncthreads();
-  for (uint32_t t = threadIdx.x; t < world; t += TB) s_base[t] = s_cnt[t] ? atomicAdd(&fill[t], s_cnt[t]) : 0u;
+  for (uint32_t t = threadIdx.x; lds && t < world; t += TB)
+    s_base[t] = s_cnt[t] ? atomicAdd(&fill[t], s_cnt[t]) : 0u;
+  if (count_only) return;
   __syncthreads();
 #pragma unroll
   for (uint32_t k = 0; k < kEmitR; ++k) {
     if (lp[k] == ~0u) continue;
     const uint64_t i = i0 + (uint64_t)k * TB;
-    const uint32_t p = s_base[rr[k]] + lp[k];
-    if (p >= cap) {
+    const uint32_t p = (lds ? s_base[rr[k]] : 0u) + lp[k];
+    if (!base && p >= cap) {
       atomicOr(overflow, 1u);  // the caller reruns the exact stages
       bpos[i] = kSlotNoKey;
       continue;
     }
-    const uint64_t q = (uint64_t)rr[k] * cap + p;
+    const uint64_t q = base ? (uint64_t)base[rr[k]] + p : (uint64_t)rr[k] * cap + p;
     send[2 * q] = keys[i];
     send[2 * q + 1] = ids[i];
     bpos[i] = (uint32_t)q;
   }
+}
+
+// one workgroup: starts[0..world] = the exclusive prefix of cnt[0..world)
+__global__ void __launch_bounds__(1024) k_owner_starts(const uint32_t* __restrict__ cnt, uint32_t world,
+                                                       uint32_t* __restrict__ starts) {
+  __shared__ uint32_t ws[16];
+  __shared__ uint32_t carry;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t b = 0; b < world; b += 1024) {
+    const uint32_t i = b + tid;
+    const uint32_t v = i < world ? cnt[i] : 0u;
+    uint32_t inc = v;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint32_t t = __shfl_up(inc, d);
+      if (lane >= d) inc += t;
+    }
+    if (lane == 63) ws[wave] = inc;
+    __syncthreads();
+    uint32_t before = carry;
+    for (uint32_t w = 0; w < wave; ++w) before += ws[w];
+    if (i < world) starts[i] = before + inc - v;
+    __syncthreads();
+    if (tid == 1023) carry = before + inc;
+    __syncthreads();
+  }
+  if (tid == 0) starts[world] = carry;
 }
 
 __global__ void k_cb_slot(const uint32_t* __restrict__ pos, const uint32_t* __restrict__ tab,
@@ -673,14 +534,6 @@ __global__ void k_cb_counts(const uint32_t* __restrict__ fill, uint32_t world, u
                             int64_t* __restrict__ counts) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r < world) counts[r] = fill[r] < cap ? fill[r] : cap;
-}
-
-// the default since round 4 (one rank's bucket stages, profiles/r04_dedup_world.json:
-// C5 at world 8 1.41 -> 1.08 ms, C3 0.57 -> 0.44 ms); SDCAS_COMBINE=sort: the
-// radix-sort combine (A/B)
-static bool combine_by_hash() {
-  const char* v = getenv("SDCAS_COMBINE");
-  return !(v && strcmp(v, "sort") == 0);
 }
 
 // ---- resolve: per-key minima in an open-addressing hash table -----------------
@@ -1226,25 +1079,138 @@ hipError_t dd_stays(DistWs& w, const uint8_t* has_key, const int32_t* status, co
   return hipGetLastError();
 }
 
+// ---- the gathered stays list in order (dd_plan), without a library sort -------------
+//
+// Every rank's stays ordinals arrive concatenated; the plan walk needs them
+// ascending. A list of at most kSortLds entries (the bucket protocol's
+// 256 per rank) is sorted by one workgroup in LDS (bitonic); a longer one
+// (the exact protocol with dense stays rows) becomes a bitmap over the
+// job's ordinals [0, n_total) read back in order by the stays pass's own
+// ordered compaction. Round 4 ran hipcub::DeviceRadixSort over the list.
+constexpr uint32_t kSortLds = 4096;
+
+__global__ void __launch_bounds__(1024) k_sort_small(const uint64_t* __restrict__ in, uint32_t m,
+                                                     uint64_t* __restrict__ out) {
+  __shared__ uint64_t v[kSortLds];
+  const uint32_t tid = threadIdx.x;
+  uint32_t P = 1;
+  while (P < m) P <<= 1;
+  for (uint32_t t = tid; t < P; t += 1024) v[t] = t < m ? in[t] : ~0ull;
+  __syncthreads();
+  for (uint32_t k = 2; k <= P; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t t = tid; t < P; t += 1024) {
+        const uint32_t u = t ^ j;
+        if (u > t) {
+          const uint64_t a = v[t], b = v[u];
+          if ((a > b) == ((t & k) == 0)) {
+            v[t] = b;
+            v[u] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (uint32_t t = tid; t < m; t += 1024) out[t] = v[t];
+}
+
+__global__ void k_stays_bits(const uint64_t* __restrict__ in, uint32_t m, uint64_t n_total, uint32_t* __restrict__ bm) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const uint64_t p = in[j];
+  if (p < n_total) atomicOr(&bm[p >> 5], 1u << (p & 31));
+}
+
+constexpr uint32_t kBitsR = 16, kBitsPer = TB * kBitsR;  // words per workgroup
+
+__global__ void __launch_bounds__(TB) k_bits_count(const uint32_t* __restrict__ bm, uint64_t words,
+                                                   uint32_t* __restrict__ bcnt) {
+  __shared__ uint32_t ws[TB / 64];
+  uint32_t c = 0;
+#pragma unroll
+  for (uint32_t r = 0; r < kBitsR; ++r) {
+    const uint64_t w = (uint64_t)blockIdx.x * kBitsPer + r * TB + threadIdx.x;
+    c += w < words ? (uint32_t)__popc(bm[w]) : 0u;
+  }
+#pragma unroll
+  for (uint32_t d = 32; d; d >>= 1) c += __shfl_xor(c, d);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) bcnt[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+// workgroup b's set bits, ascending, from the offset the workgroups before it
+// add up to: thread t takes words [b * kBitsPer + t * kBitsR, + kBitsR)
+__global__ void __launch_bounds__(TB) k_bits_write(const uint32_t* __restrict__ bm, uint64_t words,
+                                                   const uint32_t* __restrict__ bcnt, uint64_t* __restrict__ out) {
+  __shared__ uint32_t ws[TB / 64];
+  const uint32_t b = blockIdx.x;
+  if (bcnt[b] == 0) return;  // uniform over the workgroup
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint32_t s = 0;
+  for (uint32_t t = tid; t < b; t += TB) s += bcnt[t];
+#pragma unroll
+  for (uint32_t d = 32; d; d >>= 1) s += __shfl_xor(s, d);
+  if (lane == 0) ws[wave] = s;
+  __syncthreads();
+  uint32_t run = ws[0] + ws[1] + ws[2] + ws[3];
+  __syncthreads();
+  const uint64_t w0 = (uint64_t)b * kBitsPer + (uint64_t)tid * kBitsR;
+  uint32_t v[kBitsR], c = 0;
+#pragma unroll
+  for (uint32_t r = 0; r < kBitsR; ++r) {
+    v[r] = w0 + r < words ? bm[w0 + r] : 0u;
+    c += (uint32_t)__popc(v[r]);
+  }
+  uint32_t inc = c;  // the workgroup's exclusive prefix of c, in thread order
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t t = __shfl_up(inc, d);
+    if (lane >= d) inc += t;
+  }
+  if (lane == 63) ws[wave] = inc;
+  __syncthreads();
+  for (uint32_t w = 0; w < wave; ++w) run += ws[w];
+  uint64_t at = run + inc - c;
+#pragma unroll
+  for (uint32_t r = 0; r < kBitsR; ++r) {
+    uint32_t x = v[r];
+    while (x) {
+      const uint32_t bit = (uint32_t)__ffs(x) - 1;
+      out[at++] = ((w0 + r) << 5) + bit;
+      x &= x - 1;
+    }
+  }
+}
+
 hipError_t dd_plan(DistWs& w, const uint64_t* stays, uint32_t n_stays, uint64_t cs, const StepWindow& win,
                    uint64_t* plan, hipStream_t st) {
   hipError_t e;
   const uint64_t* sorted = stays;
-  if (n_stays > 1) {
-    // the ranks' lists concatenated: one radix sort (all-ones padding last)
+  const uint32_t* tcnt = nullptr;
+  uint32_t ntiles = 0;
+  if (n_stays > 1 && win.n_total) {
     if ((e = w.stay_sorted.ensure(n_stays))) return e;
-    size_t need = 0;
-    (void)hipcub::DeviceRadixSort::SortKeys(nullptr, need, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                                            (int)n_stays, 0, 64, st);
-    if ((e = w.temp.ensure(need + 256))) return e;
-    size_t tmp = w.temp.cap;
-    if ((e = hipcub::DeviceRadixSort::SortKeys(w.temp.p, tmp, stays, w.stay_sorted.p, (int)n_stays, 0, 64, st)))
-      return e;
+    if (n_stays <= kSortLds) {
+      hipLaunchKernelGGL(k_sort_small, dim3(1), dim3(1024), 0, st, stays, n_stays, w.stay_sorted.p);
+    } else {
+      const uint64_t words = (win.n_total + 31) / 32;
+      ntiles = (uint32_t)((words + kBitsPer - 1) / kBitsPer);
+      if ((e = w.bitmap.ensure(words)) || (e = w.stay_cnt.ensure(ntiles + 1))) return e;
+      if ((e = hipMemsetAsync(w.bitmap.p, 0, sizeof(uint32_t) * words, st))) return e;
+      hipLaunchKernelGGL(k_stays_bits, dim3(blocks(n_stays)), dim3(TB), 0, st, stays, n_stays, win.n_total,
+                         w.bitmap.p);
+      hipLaunchKernelGGL(k_bits_count, dim3(ntiles), dim3(TB), 0, st, w.bitmap.p, words, w.stay_cnt.p);
+      hipLaunchKernelGGL(k_bits_write, dim3(ntiles), dim3(TB), 0, st, w.bitmap.p, words, w.stay_cnt.p,
+                         w.stay_sorted.p);
+      tcnt = w.stay_cnt.p;
+    }
     sorted = w.stay_sorted.p;
   }
   hipLaunchKernelGGL(k_plan_walk, dim3(1), dim3(64), 0, st, sorted, (const uint32_t*)nullptr,
                      (const uint64_t*)nullptr, n_stays, (const uint32_t*)nullptr, win.n_total, cs, win.max_steps,
-                     win.more, plan);
+                     win.more, plan, tcnt, ntiles);
   return hipGetLastError();
 }
 
@@ -1323,29 +1289,48 @@ hipError_t dd_apply(const uint64_t* ids, const uint32_t* slot, uint32_t n, const
   return hipGetLastError();
 }
 
-static hipError_t combine_buckets_hash(DistWs& w, const uint64_t* keys, const uint8_t* has_key,
-                                       const int32_t* status, const uint64_t* ids, uint32_t n, uint32_t world,
-                                       uint32_t cap, uint64_t* send, uint32_t* slot, int64_t* counts,
-                                       uint32_t* overflow, hipStream_t st) {
+// The compact table of the files' keys (each key's lowest file index) in
+// w.idx_a, each file's slot in w.idx_b: the first step of both combines.
+static hipError_t combine_table(DistWs& w, const uint64_t* keys, const uint8_t* has_key, const int32_t* status,
+                                uint32_t n, uint32_t world, hipStream_t st) {
   uint64_t tcap = 1024;
   while (tcap < 2 * (uint64_t)n) tcap <<= 1;
   if (tcap > (1ull << 31)) return hipErrorInvalidValue;
   hipError_t e;
   if ((e = w.idx_a.ensure(tcap)) || (e = w.idx_b.ensure(n)) || (e = w.tpos.ensure(n)) ||
-      (e = w.starts.ensure(world + 1)))
+      (e = w.starts.ensure(world + 1)) || (e = w.ocnt.ensure(world + 1)))
     return e;
   const uint32_t mask = (uint32_t)(tcap - 1);
   const uint32_t shift = 64u - (uint32_t)__builtin_ctzll(tcap);
   if ((e = hipMemsetAsync(w.idx_a.p, 0xFF, sizeof(uint32_t) * tcap, st)) ||
-      (e = hipMemsetAsync(w.starts.p, 0, sizeof(uint32_t) * (world + 1), st)))
+      (e = hipMemsetAsync(w.ocnt.p, 0, sizeof(uint32_t) * (world + 1), st)))
     return e;
   hipLaunchKernelGGL(k_solo_insert_idx, dim3(blocks(n)), dim3(TB), 0, st, keys, (const uint64_t*)nullptr, n, has_key,
                      status, (const uint64_t*)nullptr, n, 0u, w.idx_a.p, (unsigned long long*)nullptr, mask, shift,
                      w.idx_b.p, (uint32_t*)nullptr);
-  hipLaunchKernelGGL(k_cb_emit, dim3((uint32_t)((n + TB * kEmitR - 1) / (TB * kEmitR))), dim3(TB), 0, st, keys, ids,
-                     n, w.idx_b.p, w.idx_a.p, world, cap,
-                     w.starts.p, send, w.tpos.p, overflow);
-  hipLaunchKernelGGL(k_cb_counts, dim3(blocks(world)), dim3(TB), 0, st, w.starts.p, world, cap, counts);
+  return hipGetLastError();
+}
+
+static uint32_t emit_grid(uint32_t n) { return (uint32_t)((n + TB * kEmitR - 1) / (TB * kEmitR)); }
+
+// the exact layout (dd_combine): owner r's records at [starts[r],
+// starts[r+1]) in no particular order, slot[i] = the record of file i's key.
+// Round 5: the bucket combine's table and emit, the owners' record counts
+// taken by a first emit pass, in place of round 4's stable radix sort and
+// scans (hipCUB), the library's last CUB-API dependency with the stays sort
+// (dd_plan)
+static hipError_t combine_core(DistWs& w, const uint64_t* keys, const uint8_t* has_key, const int32_t* status,
+                               const uint64_t* ids, uint32_t n, uint32_t world, uint64_t* rec, uint32_t* slot,
+                               hipStream_t st) {
+  hipError_t e;
+  if ((e = combine_table(w, keys, has_key, status, n, world, st))) return e;
+  hipLaunchKernelGGL(k_cb_emit, dim3(emit_grid(n)), dim3(TB), 0, st, keys, ids, n, w.idx_b.p, w.idx_a.p, world, ~0u,
+                     (const uint32_t*)nullptr, 1u, w.ocnt.p, (uint64_t*)nullptr, (uint32_t*)nullptr,
+                     (uint32_t*)nullptr);
+  hipLaunchKernelGGL(k_owner_starts, dim3(1), dim3(1024), 0, st, w.ocnt.p, world, w.starts.p);
+  if ((e = hipMemsetAsync(w.ocnt.p, 0, sizeof(uint32_t) * (world + 1), st))) return e;
+  hipLaunchKernelGGL(k_cb_emit, dim3(emit_grid(n)), dim3(TB), 0, st, keys, ids, n, w.idx_b.p, w.idx_a.p, world, ~0u,
+                     (const uint32_t*)w.starts.p, 0u, w.ocnt.p, rec, w.tpos.p, (uint32_t*)nullptr);
   if (slot) hipLaunchKernelGGL(k_cb_slot, dim3(blocks(n)), dim3(TB), 0, st, w.idx_b.p, w.idx_a.p, w.tpos.p, n, slot);
   return hipGetLastError();
 }
@@ -1356,15 +1341,11 @@ hipError_t dd_combine_buckets(DistWs& w, const uint64_t* keys, const uint8_t* ha
   hipError_t e;
   if ((e = hipMemsetAsync(overflow, 0, sizeof(uint32_t), st))) return e;
   if (n == 0) return hipMemsetAsync(counts, 0, sizeof(int64_t) * world, st);
-  if (combine_by_hash() && world <= kEmitMaxWorld)
-    return combine_buckets_hash(w, keys, has_key, status, ids, n, world, cap, send, slot, counts, overflow, st);
-  if ((e = w.ukey.ensure(2 * (size_t)n))) return e;
-  if ((e = combine_core(w, keys, has_key, status, ids, n, world, w.ukey.p, slot, st))) return e;
-  hipLaunchKernelGGL(k_dd_pack, dim3(blocks(n)), dim3(TB), 0, st, w.ukey.p, w.scan.p, w.nvalid.p, w.starts.p, world,
-                     cap, send, overflow);
-  hipLaunchKernelGGL(k_dd_bucket_counts, dim3(blocks(world)), dim3(TB), 0, st, w.starts.p, world, cap, counts);
-  if (slot)
-    hipLaunchKernelGGL(k_dd_slot_remap, dim3(blocks(n)), dim3(TB), 0, st, w.ukey.p, w.starts.p, world, cap, n, slot);
+  if ((e = combine_table(w, keys, has_key, status, n, world, st))) return e;
+  hipLaunchKernelGGL(k_cb_emit, dim3(emit_grid(n)), dim3(TB), 0, st, keys, ids, n, w.idx_b.p, w.idx_a.p, world, cap,
+                     (const uint32_t*)nullptr, 0u, w.ocnt.p, send, w.tpos.p, overflow);
+  hipLaunchKernelGGL(k_cb_counts, dim3(blocks(world)), dim3(TB), 0, st, w.ocnt.p, world, cap, counts);
+  if (slot) hipLaunchKernelGGL(k_cb_slot, dim3(blocks(n)), dim3(TB), 0, st, w.idx_b.p, w.idx_a.p, w.tpos.p, n, slot);
   return hipGetLastError();
 }
 

@@ -1473,7 +1473,7 @@ int sdcas_dev_dedup_combine(sdcas_ctx* c, const uint64_t* d_keys, const uint8_t*
                             const uint64_t* d_ids, size_t n, uint32_t world, uint64_t* d_rec, uint32_t* d_slot,
                             uint64_t* out_starts, void* stream) {
   if (!c || world == 0 || !out_starts || (n && (!d_keys || !d_ids || !d_rec))) return SDCAS_E_INVALID;
-  // the combine's radix sort and scans take an int count (hipcub)
+  // record indices and slot codes are 32-bit
   if (n > SDCAS_MAX_BATCH) return c->fail(SDCAS_E_CAPACITY, "dedup_combine: %zu records exceed 2^31 - 1", n);
   DevCall call(c, stream);
   if (call.rc) return call.rc;

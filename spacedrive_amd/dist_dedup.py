@@ -8,7 +8,7 @@ only needs two per-key minima — the first existing Object in DB order and the
 lowest orphan ordinal carrying the key — plus a per-file rule, so it shards:
 
   1. combine   every rank reduces its files to one (key, min ordinal) record
-               per distinct key, key-sorted, hence grouped by owner rank
+               per distinct key, grouped by owner rank
                (owner = top 12 key bits split into `world` ranges); existing
                Objects likewise to (key, min DB index)
   2. exchange  RCCL all-to-all of both record sets (16 B records)

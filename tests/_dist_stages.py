@@ -101,9 +101,10 @@ class NumpyStages:
         valid = ok & has
         slot = np.where(ok, NOKEY, DROPPED).astype(np.uint32)
         vi = np.nonzero(valid)[0]
-        # the device combine sorts stably on the top 32 key bits only (a key
-        # whose top bits another key shares may split into several records)
-        order = vi[np.argsort(k[vi] >> np.uint64(32), kind="stable")]
+        # one record per distinct key (its lowest id: ids ascend), key order;
+        # the device combine (a hash table since round 5) emits the same
+        # records grouped by owner in no particular order within an owner
+        order = vi[np.argsort(k[vi], kind="stable")]
         sk = k[order]
         head = np.ones(sk.size, bool)
         head[1:] = sk[1:] != sk[:-1]

@@ -87,6 +87,16 @@ def test_product_library_holds_only_product_kernels():
     assert sorted(pieces) == ["k_piece_l4<259, 6>", "k_piece_top<259>", "k_piece_tree<259, 6, 1, 0, 10>"], pieces
 
 
+def test_product_library_has_no_cub():
+    """round 5: the last hipCUB / rocPRIM uses left the product library — the
+    exact combine goes through the compact table (two emit passes), the
+    gathered stays list is sorted by one workgroup or read back from a
+    bitmap (dist_dedup.hip); only the ablation library's quad-layout scan
+    keeps hipCUB"""
+    out = subprocess.run(["nm", "-C", N.LIB_PATH], capture_output=True, text=True).stdout
+    assert out and not re.search(r"hipcub|rocprim|\bcub::", out)
+
+
 def test_ablation_build_is_separate():
     """the A/B library is a different file that no product module names"""
     assert N.ABLATION_LIB_PATH != N.LIB_PATH

@@ -237,18 +237,27 @@ def test_device_stages_on_callers_stream(eng, oracle, R):
 
 @pytest.mark.gpu
 def test_device_stages_match_numpy_stages(eng):
-    """stage by stage, device vs numpy restatement (records, slots, answers)"""
+    """stage by stage, device vs numpy restatement (records, slots, answers):
+    the device combine's records within an owner's range come in no
+    particular order (a hash table), so records are compared as per-owner
+    sets and slots through the records they name"""
     from spacedrive_amd.dist_dedup import DeviceStages
     keys, has, status, existing = make_corpus(5, 20000)
-    keys[:3] = np.uint64(2**64 - 1)  # the sort's filler value is a legal key
+    keys[:3] = np.uint64(2**64 - 1)  # the table's empty marker is a legal key
     (k, h, s, ids), = shard(keys, has, status, existing, 1, device="cuda")[0]
     st, ns = DeviceStages(eng), NumpyStages()
     for world in (1, 4, 7):
         rec_d, slot_d, starts_d = st.combine(k, h, s, ids, world)
         rec_n, slot_n, starts_n = ns.combine(k.cpu(), h.cpu(), s.cpu(), ids.cpu(), world)
         assert starts_d == starts_n
-        assert torch.equal(rec_d.cpu(), rec_n)
-        assert torch.equal(slot_d.cpu(), slot_n)
+        rd, rn = rec_d.cpu().numpy(), rec_n.numpy()
+        for r in range(world):
+            a, b = rd[starts_d[r]:starts_d[r + 1]], rn[starts_n[r]:starts_n[r + 1]]
+            assert np.array_equal(a[np.lexsort(a.T[::-1])], b[np.lexsort(b.T[::-1])]), r
+        sd, sn = slot_d.cpu().numpy().view(np.uint32), slot_n.numpy().view(np.uint32)
+        keyed = sn < 0xFFFFFFFE
+        assert np.array_equal(sd[~keyed], sn[~keyed])
+        assert np.array_equal(rd[sd[keyed]], rn[sn[keyed]])
     ek = torch.from_numpy(existing.view(np.int64)).cuda()
     eids = torch.arange(existing.size, dtype=torch.int64, device="cuda")
     erec_d, _, _ = st.combine(ek, None, None, eids, 1)
@@ -474,6 +483,38 @@ def test_device_stages_dense_stays_vs_oracle(eng, oracle, R, chunk_size):
     assert (c, l) == (wc, wl)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("m", [1, 2, 300, 4096, 4097, 50_000])
+def test_device_plan_sorts_gathered_stays(eng, oracle, m):
+    """sdcas_dev_dedup_plan over every rank's stays ordinals concatenated in
+    no order, padded with all-ones entries: up to 4096 entries one
+    workgroup's bitonic sort, more a bitmap over the job's ordinals read back
+    in order (round 5; round 4: hipCUB's radix sort) — the plan equals the
+    one from the sorted list, and the oracle's for a job whose stays rows
+    are exactly those ordinals"""
+    from spacedrive_amd import _native as N
+    from spacedrive_amd.dist_dedup import DeviceStages
+    rng = np.random.default_rng(m)
+    n_total = max(2 * m, 1000) + 17
+    stays = np.sort(rng.choice(n_total, m, replace=False)).astype(np.int64)
+    shuffled = np.concatenate([rng.permutation(stays), np.full(m // 7 + 3, -1, np.int64)])
+    rng.shuffle(shuffled)
+    st = DeviceStages(eng)
+    for cs, max_steps, more in ((100, 0, False), (7, 0, True), (100, 3, False), (1, 0, False)):
+        got = st.plan(torch.from_numpy(shuffled).cuda(), n_total, cs, max_steps, more).cpu().numpy()
+        ref = st.plan(torch.from_numpy(np.concatenate([stays, np.full(4, -1, np.int64)])).cuda(), n_total, cs,
+                      max_steps, more).cpu().numpy()
+        h = N.SDCAS_PLAN_HEADER_WORDS
+        nr = int(got[1])
+        assert np.array_equal(got[:h], ref[:h]) and np.array_equal(got[h:h + nr], ref[h:h + nr]), (cs, max_steps)
+        # the oracle: rows without a cas_id at exactly those ordinals
+        has = np.ones(n_total, np.uint8)
+        has[stays] = 0
+        keys = rng.integers(0, 2**64, n_total, dtype=np.uint64)
+        _, _, _, ww = oracle.identifier_job(keys, has, None, cs, np.zeros(0, np.uint64), max_steps, more)
+        assert (int(got[2]), int(got[3]), int(got[8])) == (ww["steps"], ww["rows"], ww["rereads"]), (cs, max_steps)
+
+
 # ---- the piece split of big-file checksums (spacedrive_amd/dist_checksum.py) ----
 
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
@@ -592,20 +633,18 @@ def test_meta_group_of_a_subgroup():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("combine", ["sort", "hash", "hash-split"])
+@pytest.mark.parametrize("combine", ["hash", "hash-split"])
 @pytest.mark.parametrize("R,chunk_size", [(2, 100), (8, 100), (5, 7)])
 def test_device_bucket_protocol_vs_oracle(eng, oracle, R, chunk_size, combine, monkeypatch):
     """the bucket protocol's device stages (combine_buckets -> equal-split
     exchange -> resolve_buckets -> apply) over R virtual ranks with existing
-    Objects, every combine and resolve: the hash-table combine (the
-    default), the radix-sort one (SDCAS_COMBINE=sort); the owner's resolve
+    Objects, the hash-table combine and every resolve: the owner's resolve
     in a table sized on the device from the valid counts (the default) and
     round 4's sized from the buckets' capacity (SDCAS_RESOLVE=split); then
     buckets one record too small, which must raise the overflow flag (the
     caller then reruns the exact stages)"""
     from spacedrive_amd.dist_dedup import DeviceStages
     from tests._dist_stages import dedup_virtual_buckets
-    monkeypatch.setenv("SDCAS_COMBINE", combine.split("-")[0])
     if combine == "hash-split":
         monkeypatch.setenv("SDCAS_RESOLVE", "split")
     keys, has, status, existing = make_corpus(700 + R, 24000, pool=5000, p_none=0.05, p_err=0.05)

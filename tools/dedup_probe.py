@@ -39,7 +39,6 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--existing", type=int, default=0, help="existing Objects (cas keys of the first K files)")
     ap.add_argument("--tables", default="", help="A/B: comma-separated SDCAS_DEDUP_TABLE values, interleaved per rep")
-    ap.add_argument("--combines", default="hash", help="--world > 1: comma-separated SDCAS_COMBINE values (A/B)")
     ap.add_argument("--ab", default="",
                     help="A/B of settings, interleaved per rep: 'NAME=v1,v2' or 'N1=a+N2=b,N1=c+N2=d' (environment "
                          "values each library call reads), e.g. SDCAS_DEDUP_TABLE=tile,idx")
@@ -90,7 +89,7 @@ def main():
     if a.world > 1:
         W = a.world
         cap = int(n / W * 1.125) + 256
-        combines = settings(a.ab) if a.ab else [{"SDCAS_COMBINE": c} for c in a.combines.split(",") if c]
+        combines = settings(a.ab) if a.ab else [{}]
         combines = {label(c): c for c in combines}
         tm = {c: {"combine_buckets": [], "resolve_buckets": [], "apply": []} for c in combines}
         links = {}
