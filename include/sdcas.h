@@ -125,8 +125,9 @@ typedef struct sdcas_options {
 
 /* "sdcas-mi355x <major>.<minor>.<patch> (gfx950)"; the C ABI of this header is
  * SDCAS_ABI_VERSION (changes: 2 added sdcas_options.progress/cancel; 3 the
- * struct_size field, sdcas_dedup_window and the dedup step plan) */
-#define SDCAS_ABI_VERSION 3
+ * struct_size field, sdcas_dedup_window and the dedup step plan; 4
+ * sdcas_dev_bind_stream) */
+#define SDCAS_ABI_VERSION 4
 int sdcas_abi_version(void);
 const char *sdcas_version(void);
 
@@ -193,6 +194,20 @@ int sdcas_dev_hash_messages(sdcas_ctx *ctx, const uint8_t *d_blob, const uint64_
                             const uint64_t *d_lens, size_t n, uint8_t *d_out32, uint64_t *d_out_keys,
                             void *stream);
 int sdcas_dev_sync(sdcas_ctx *ctx, void *stream);
+/* Name a stream's identity. The device calls of a context share its scratch
+ * workspace, so each call makes its stream wait for the previous call's use
+ * of it (an event wait: a barrier that idles the GPU ~15 us) unless both ran
+ * on the same stream, whose order covers it. A handle alone cannot tell
+ * "the same stream" (a destroyed stream's handle can come back for a new
+ * one); a token can: consecutive calls on a stream bound with one nonzero
+ * token skip the wait. The caller never hands the same token to another
+ * stream while the context lives, and binds again (a new token, or 0 to
+ * unbind) before destroying a bound stream or reusing its handle for a new
+ * one. The end-of-call event a bound stream owes is recorded only when
+ * another stream or a host wait needs it (a recorded event idles the GPU
+ * ~6-8 us between calls). At most 64 streams per context are bound at once
+ * (SDCAS_E_CAPACITY beyond). */
+int sdcas_dev_bind_stream(sdcas_ctx *ctx, void *stream, uint64_t token);
 
 /* ---- device-resident big messages, streamed in pieces ------------------
  *

@@ -26,7 +26,7 @@ SDCAS_STATUS_UNEXPECTED_EOF = 100001
 SDCAS_STATUS_CANCELLED = 125
 SDCAS_MAX_BATCH = 0x7FFFFFFF
 SDCAS_OPT_DIRECT_IO = 1
-SDCAS_ABI_VERSION = 3
+SDCAS_ABI_VERSION = 4
 SDCAS_LINK_DROPPED = -(1 << 63)
 SDCAS_LINK_DEFERRED = SDCAS_LINK_DROPPED + 1
 SDCAS_PLAN_HEADER_WORDS = 12
@@ -35,7 +35,7 @@ SDCAS_PLAN_HEADER_WORDS = 12
 ABI_SYMBOLS = [
     "sdcas_version", "sdcas_abi_version", "sdcas_init", "sdcas_destroy", "sdcas_last_error", "sdcas_cas_ids",
     "sdcas_checksums", "sdcas_hash_messages", "sdcas_cas_ids_from_messages", "sdcas_dev_reserve",
-    "sdcas_dev_hash_messages", "sdcas_dev_sync", "sdcas_dedup", "sdcas_dedup_window", "sdcas_job_plan",
+    "sdcas_dev_hash_messages", "sdcas_dev_sync", "sdcas_dev_bind_stream", "sdcas_dedup", "sdcas_dedup_window", "sdcas_job_plan",
     "sdcas_key_to_hex",
     "sdcas_digest_to_hex", "sdcas_cas_message_len", "sdcas_dev_dedup_combine", "sdcas_dev_dedup_combine_async",
     "sdcas_dev_dedup_resolve",
@@ -138,6 +138,7 @@ def load():
     L.sdcas_dev_reserve.argtypes = [_vp, _sz, _u64]
     L.sdcas_dev_hash_messages.argtypes = [_vp, _vp, _vp, _vp, _sz, _vp, _vp, _vp]
     L.sdcas_dev_sync.argtypes = [_vp, _vp]
+    L.sdcas_dev_bind_stream.argtypes = [_vp, _vp, ctypes.c_uint64]
     L.sdcas_dedup.argtypes = [_vp, _vp, _vp, _vp, _sz, _sz, _vp, _sz, _vp, _vp, _vp]
     L.sdcas_job_plan.argtypes = [_vp, _vp, _sz, _sz, ctypes.POINTER(JobWindow), _vp, _vp]
     L.sdcas_dedup_window.argtypes = [_vp, _vp, _vp, _vp, _sz, _sz, _vp, _sz, ctypes.POINTER(JobWindow), _vp, _vp,

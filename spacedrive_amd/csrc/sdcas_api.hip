@@ -203,6 +203,15 @@ struct sdcas_ctx {
   hipEvent_t scratch_ev = nullptr;
   hipStream_t scratch_st = nullptr;
   bool scratch_pending = false;
+  // sdcas_dev_bind_stream: streams whose identity the caller named
+  std::vector<std::pair<hipStream_t, uint64_t>> bound;
+  uint64_t scratch_token = 0;  // the token of the stream the last call used (0: none)
+  bool scratch_recorded = true;  // scratch_ev marks the last call's end (else: record it first)
+  uint64_t token_of(hipStream_t st) const {
+    for (const auto& b : bound)
+      if (b.first == st) return b.second;
+    return 0;
+  }
   uint32_t upload_parts = 4;  // sdcas_cas_ids: a lone slot's reads and upload overlapped in this many parts (0/1: off)
   bool plan_small = true;      // small batches planned on the host (SDCAS_PLAN_SMALL=0: on the device)
 
@@ -229,21 +238,41 @@ struct sdcas_ctx {
     return fail(e == hipErrorOutOfMemory ? SDCAS_E_OOM : SDCAS_E_HIP, "%s: %s", what, hipGetErrorString(e));
   }
   // before enqueuing on st: wait for the previous call's use of the scratch
-  // (also on the same stream handle: a handle value may have been reused by a
-  // new stream after the caller destroyed the old one; a same-stream wait is
-  // nearly free)
+  // — unless it ran on this same stream, which only a bound token can tell
+  // (a handle value may have been reused by a new stream after the caller
+  // destroyed the old one)
   hipError_t fence_in(hipStream_t st) {
     if (!scratch_pending) return hipSuccess;
-    return hipStreamWaitEvent(st, scratch_ev, 0);
+    if (st == scratch_st && scratch_token && token_of(st) == scratch_token) return hipSuccess;
+    hipError_t e = scratch_event();
+    return e ? e : hipStreamWaitEvent(st, scratch_ev, 0);
   }
-  // after enqueuing on st
+  // after enqueuing on st. On a bound stream the event is recorded only when
+  // something needs it — a call on another stream, a host wait for the
+  // scratch — and then on that stream, behind everything enqueued on it so
+  // far: a recorded event is a barrier packet that idled the GPU ~6-8 us
+  // between two calls on the step's stream (the C5 step's kernel trace)
   hipError_t fence_out(hipStream_t st) {
+    scratch_st = st;
+    scratch_token = token_of(st);
+    scratch_pending = true;
+    scratch_recorded = false;
+    return scratch_token ? hipSuccess : scratch_event();
+  }
+  // the scratch event, recorded on the last call's stream if it was not yet
+  hipError_t scratch_event() {
+    if (scratch_recorded) return hipSuccess;
     hipError_t e = hipSuccess;
     if (!scratch_ev && (e = hipEventCreateWithFlags(&scratch_ev, hipEventDisableTiming))) return e;
-    if ((e = hipEventRecord(scratch_ev, st))) return e;
-    scratch_st = st;
-    scratch_pending = true;
+    if ((e = hipEventRecord(scratch_ev, scratch_st))) return e;
+    scratch_recorded = true;
     return hipSuccess;
+  }
+  // the host waits until no enqueued call still uses the scratch
+  hipError_t scratch_sync() {
+    if (!scratch_pending) return hipSuccess;
+    hipError_t e = scratch_event();
+    return e ? e : hipEventSynchronize(scratch_ev);
   }
   bool cancelled() const { return cancel && __atomic_load_n(cancel, __ATOMIC_ACQUIRE) != 0; }
   void report(uint64_t done, uint64_t total) {
@@ -693,7 +722,10 @@ void sdcas_destroy(sdcas_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
-  if (c->scratch_ev) (void)hipEventSynchronize(c->scratch_ev);
+  // a bound stream's last call may not have recorded its event, and the
+  // caller's stream may be gone by now: wait for the whole device instead
+  if (!c->scratch_recorded) (void)hipDeviceSynchronize();
+  else (void)c->scratch_sync();
   for (auto* b : {&c->ws_S, &c->ws_total, &c->ws_soffs, &c->ws_slens, &c->dd_keys, &c->dd_ekeys, &c->dd_ids})
     b->release();
   for (auto* b : {&c->ws_tile_first, &c->ws_nodes, &c->ws_perm, &c->ws_sort_keys, &c->d_file_nodes, &c->piece_ctr, &c->piece_l4})
@@ -834,10 +866,7 @@ int sdcas_dev_reserve(sdcas_ctx* c, size_t max_msgs, uint64_t max_chunks) {
   std::lock_guard<std::mutex> g(c->mu);
   (void)hipSetDevice(c->device);
   // the workspace is reallocated: no earlier call may still be using it
-  if (c->scratch_pending) {
-    hipError_t e = hipEventSynchronize(c->scratch_ev);
-    if (e) return c->hip_fail(e, "sync");
-  }
+  if (hipError_t e = c->scratch_sync()) return c->hip_fail(e, "sync");
   return reserve_ws(c, max_msgs, max_chunks);
 }
 
@@ -850,6 +879,26 @@ int sdcas_dev_hash_messages(sdcas_ctx* c, const uint8_t* d_blob, const uint64_t*
   if (n > c->ws.cap_msgs || !c->ws.S)
     return c->fail(SDCAS_E_CAPACITY, "dev_hash_messages: %zu messages > reserved %u", n, c->ws.cap_msgs);
   return launch_batch(c, d_blob, d_offsets, d_lens, (uint32_t)n, d_out32, d_out_keys, call.st);
+}
+
+int sdcas_dev_bind_stream(sdcas_ctx* c, void* stream, uint64_t token) {
+  if (!c) return SDCAS_E_INVALID;
+  std::lock_guard<std::mutex> g(c->mu);
+  const hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  // the last call's event, owed by this stream, is recorded while the
+  // stream surely lives (a caller unbinds before destroying it)
+  if (c->scratch_pending && st == c->scratch_st)
+    if (hipError_t e = c->scratch_event()) return c->hip_fail(e, "dev_bind_stream");
+  for (size_t i = 0; i < c->bound.size(); ++i) {
+    if (c->bound[i].first != st) continue;
+    if (token) c->bound[i].second = token;
+    else c->bound.erase(c->bound.begin() + (long)i);
+    return SDCAS_OK;
+  }
+  if (!token) return SDCAS_OK;
+  if (c->bound.size() >= 64) return c->fail(SDCAS_E_CAPACITY, "dev_bind_stream: 64 streams bound");
+  c->bound.push_back({st, token});
+  return SDCAS_OK;
 }
 
 int sdcas_dev_sync(sdcas_ctx* c, void* stream) {
@@ -1603,7 +1652,7 @@ static hipError_t grow(sdcas_ctx* c, DevBuf<T>& b, size_t n, hipStream_t st = nu
   if (n <= b.cap) return hipSuccess;
   hipError_t e;
   if (st && (e = hipStreamSynchronize(st))) return e;
-  if (c->scratch_pending && (e = hipEventSynchronize(c->scratch_ev))) return e;
+  if ((e = c->scratch_sync())) return e;
   return b.ensure(n);
 }
 extern "C" {

@@ -18,6 +18,7 @@ The batch forms (``generate_cas_ids``, ``file_checksums``,
 chunk instead of per file. Everything runs on the GPU; there is no CPU path.
 """
 import ctypes
+import itertools
 import os
 import sys
 
@@ -25,6 +26,9 @@ import numpy as np
 
 from . import _native as N
 
+
+
+_STREAM_TOKENS = itertools.count(1)  # sdcas_dev_bind_stream tokens: unique per process
 
 def _cpaths(paths):
     """(buffer, pointers) for a `const char* const*` argument: the paths
@@ -241,6 +245,15 @@ class Engine:
 
     def dev_sync(self, stream=0):
         self._check(self.L.sdcas_dev_sync(self.ctx, stream or None), "dev_sync")
+
+    def dev_bind_stream(self, stream, token=None):
+        """name `stream`'s identity (sdcas_dev_bind_stream): consecutive
+        device calls on it skip the scratch fence's event wait. token None:
+        a fresh one (never reused in this process); 0: unbind"""
+        if token is None:
+            token = next(_STREAM_TOKENS)
+        self._check(self.L.sdcas_dev_bind_stream(self.ctx, stream or None, int(token)), "dev_bind_stream")
+        return token
 
     def dev_synth_cas_messages(self, keys, sizes, offs, n, blob, stream=0):
         self._check(self.L.sdcas_dev_synth_cas_messages(self.ctx, keys, sizes, offs, int(n), blob,

@@ -99,17 +99,25 @@ def test_two_process_device_dedup(oracle, existing_mode):
     assert [str(p["proto1"]) for p in parts] == ["buckets"] * world
 
 
-def test_two_streams_share_one_context(oracle):
+@pytest.mark.parametrize("bind", ["unbound", "bound", "rebound"])
+def test_two_streams_share_one_context(oracle, bind):
     """dedup_local on two raw streams of one context, enqueued back to back
     with no ordering between the streams on the caller's side: the second
     call clears the shared resolve table while the first may still run, so
-    the library must order them (sdcas_ctx::fence_in). Both results exact."""
+    the library must order them (sdcas_ctx::fence_in). Both results exact —
+    also with both streams bound to tokens (sdcas_dev_bind_stream: the wait
+    is skipped only between calls on one bound stream), and with one stream's
+    handle bound to a token, then rebound to another (as after the caller
+    re-created a stream whose handle came back)"""
     from spacedrive_amd import Engine
     eng = Engine()
     try:
         corpora = [make_corpus(s, 400_000, pool=50_000) for s in (1, 2)]
         dev = torch.device("cuda", 0)
         s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        if bind != "unbound":
+            eng.dev_bind_stream(s1.cuda_stream)
+            eng.dev_bind_stream(s2.cuda_stream)
         bufs = []
         for keys, has, status, existing in corpora:
             t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
@@ -124,6 +132,8 @@ def test_two_streams_share_one_context(oracle):
             for b in bufs:
                 b["cnt"].zero_()
             torch.cuda.synchronize()
+            if bind == "rebound":
+                eng.dev_bind_stream(s1.cuda_stream)  # a fresh token: the next call on s1 waits again
             for b, s in zip(bufs, (s1, s2)):
                 rc = eng.L.sdcas_dev_dedup_local(eng.ctx, b["k"].data_ptr(), b["h"].data_ptr(), b["s"].data_ptr(),
                                                  b["ids"].data_ptr(), b["k"].numel(), b["ek"].data_ptr(),
