@@ -973,6 +973,7 @@ struct PathCall {
     // the readers start with the context's first path call (a context used
     // only for device-resident batches never creates them)
     if (!c->pool) c->pool.reset(new sdcas_io::WorkerPool(c->io_threads));
+    sdcas_io::new_path_epoch();
     hipError_t e = c->fence_in(c->stream);
     if (e) rc = c->hip_fail(e, "stream wait");
   }

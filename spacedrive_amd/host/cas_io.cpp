@@ -12,6 +12,7 @@
 #include <cerrno>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 
 namespace sdcas_io {
 
@@ -49,17 +50,67 @@ int pread_direct(int fd, uint8_t* dst, uint64_t n, uint64_t off) {
   return got >= n ? 0 : kUnexpectedEof;
 }
 
+namespace {
+// Files are opened relative to their directory, whose descriptor a reader
+// thread keeps while consecutive files share it (a batch lists a location's
+// files directory by directory): openat(dir, name) walks one component
+// where open(path) walks them all — on the GPU box's container filesystem
+// the walk is most of an open (profiles/r05_job_read_side.json). A path call
+// starts a new epoch, so no descriptor outlives the call that opened it (a
+// directory replaced between calls is looked up again). SDCAS_DIRFD=0:
+// open(path) (A/B).
+std::atomic<uint64_t> g_epoch{1};
+bool dirfd_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("SDCAS_DIRFD");
+    return !(v && strcmp(v, "0") == 0);
+  }();
+  return on;
+}
+struct DirCache {
+  uint64_t epoch = 0;
+  std::string dir;
+  int fd = -1;
+  ~DirCache() {
+    if (fd >= 0) close(fd);
+  }
+};
+// the descriptor to open `path` against, and the name to open there
+int dir_of(const char* path, const char** name) {
+  *name = path;
+  const char* slash = strrchr(path, '/');
+  // a name without a directory, a file in "/", a trailing slash: the plain open
+  if (!slash || slash == path || !slash[1] || !dirfd_enabled()) return AT_FDCWD;
+  thread_local DirCache c;
+  const uint64_t e = g_epoch.load(std::memory_order_relaxed);
+  const size_t dl = (size_t)(slash - path);
+  if (c.epoch != e || c.fd < 0 || c.dir.size() != dl || memcmp(c.dir.data(), path, dl) != 0) {
+    if (c.fd >= 0) close(c.fd);
+    c.dir.assign(path, dl);
+    c.fd = open(c.dir.c_str(), O_PATH | O_DIRECTORY | O_CLOEXEC);
+    c.epoch = e;
+    if (c.fd < 0) return AT_FDCWD;  // the full path then reports its own error
+  }
+  *name = slash + 1;
+  return c.fd;
+}
+}  // namespace
+
+void new_path_epoch() { g_epoch.fetch_add(1, std::memory_order_relaxed); }
+
 int open_for_read(const char* path, bool direct, bool* is_direct) {
   *is_direct = false;
+  const char* name = path;
+  const int dir = dir_of(path, &name);
   if (direct) {
-    int fd = open(path, O_RDONLY | O_CLOEXEC | O_DIRECT);
+    int fd = openat(dir, name, O_RDONLY | O_CLOEXEC | O_DIRECT);
     if (fd >= 0) {
       *is_direct = true;
       return fd;
     }
     if (errno != EINVAL) return -errno;
   }
-  int fd = open(path, O_RDONLY | O_CLOEXEC);
+  int fd = openat(dir, name, O_RDONLY | O_CLOEXEC);
   return fd >= 0 ? fd : -errno;
 }
 

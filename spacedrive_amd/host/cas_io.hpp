@@ -42,6 +42,9 @@ int pread_direct(int fd, uint8_t* dst, uint64_t n, uint64_t off);
 // accepts it (tmpfs and some overlays refuse it: then the page cache is
 // used); *is_direct says which. Returns the fd or -errno.
 int open_for_read(const char* path, bool direct, bool* is_direct);
+// a path call begins: the reader threads' cached directory descriptors
+// (open_for_read) are not reused past it
+void new_path_epoch();
 
 // Whole file into dst (capacity cap > expect, the size the indexer or a stat
 // just saw); returns status, *len = bytes read; sets *overflow when the file

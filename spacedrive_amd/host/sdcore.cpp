@@ -3,6 +3,8 @@
 #include "sdcore.hpp"
 
 #include <dirent.h>
+#include <fcntl.h>
+#include <unistd.h>
 #include <sys/stat.h>
 
 #include <algorithm>
@@ -346,6 +348,15 @@ void MemoryLibrary::set_integrity_checksum(int32_t id, const std::string& checks
 
 // ---- file_identifier ----------------------------------------------------------------
 
+// SDCORE_DIRFD=0: the stat pass by full path (A/B)
+static bool stat_dirfd() {
+  static const bool on = [] {
+    const char* v = getenv("SDCORE_DIRFD");
+    return !(v && strcmp(v, "0") == 0);
+  }();
+  return on;
+}
+
 std::vector<Result<FileMetadata>> file_metadata_batch(Engine& engine,
                                                       const std::vector<std::pair<std::string, ObjectKind>>& files) {
   const size_t n = files.size();
@@ -354,10 +365,30 @@ std::vector<Result<FileMetadata>> file_metadata_batch(Engine& engine,
   std::vector<uint8_t> is_dir(n, 0);
   // fs::metadata and the kind per file (mod.rs:63-76), on up to 16 threads for
   // a big batch (the reference's join_all runs them concurrently too)
+  // each file is stat'ed relative to its directory, whose descriptor a
+  // thread keeps while consecutive files share it (one path component walked
+  // instead of all; the library's readers open the same way, cas_io.cpp)
   auto stat_range = [&](size_t lo, size_t hi) {
+    std::string dir;
+    int dfd = -1;
     for (size_t i = lo; i < hi; ++i) {
       struct stat sb;
-      if (::stat(files[i].first.c_str(), &sb) != 0) {  // fs::metadata (mod.rs:63-65)
+      const std::string& p = files[i].first;
+      const size_t slash = p.rfind('/');
+      int at = AT_FDCWD;
+      const char* name = p.c_str();
+      if (stat_dirfd() && slash != std::string::npos && slash > 0 && slash + 1 < p.size()) {
+        if (dfd < 0 || dir.size() != slash || p.compare(0, slash, dir) != 0) {
+          if (dfd >= 0) ::close(dfd);
+          dir.assign(p, 0, slash);
+          dfd = ::open(dir.c_str(), O_PATH | O_DIRECTORY | O_CLOEXEC);
+        }
+        if (dfd >= 0) {
+          at = dfd;
+          name = p.c_str() + slash + 1;
+        }
+      }
+      if (::fstatat(at, name, &sb, 0) != 0) {  // fs::metadata (mod.rs:63-65)
         err[i] = IoError{errno, files[i].first};
         continue;
       }
@@ -368,6 +399,7 @@ std::vector<Result<FileMetadata>> file_metadata_batch(Engine& engine,
       md[i].kind = files[i].second >= 0 ? files[i].second : object_kind_of(files[i].first);  // mod.rs:72-76
       md[i].len = (uint64_t)sb.st_size;
     }
+    if (dfd >= 0) ::close(dfd);
   };
   static const bool trace = [] {
     const char* v = getenv("SDCORE_TRACE_JOB");

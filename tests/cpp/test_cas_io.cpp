@@ -213,6 +213,37 @@ int main() {
     CHECK(sdcas_io::open_for_read(path("nope").c_str(), true, &d) == -ENOENT, "missing file");
   }
 
+  // files opened relative to a cached directory descriptor (open_for_read):
+  // within a path call the descriptor serves consecutive files of one
+  // directory; a directory replaced between two calls (a new epoch) is looked
+  // up again, so its new file is found; the error of a missing directory is
+  // the full path's; a trailing slash and a bare name take the plain open
+  {
+    const std::string sub = path("sub"), moved = path("sub_old");
+    CHECK(mkdir(sub.c_str(), 0755) == 0, "mkdir");
+    write_file(sub + "/a", 10, rng);
+    sdcas_io::new_path_epoch();
+    bool d = false;
+    int fd = sdcas_io::open_for_read((sub + "/a").c_str(), false, &d);
+    CHECK(fd >= 0, "open in sub: %d", fd);
+    if (fd >= 0) close(fd);
+    CHECK(std::rename(sub.c_str(), moved.c_str()) == 0, "rename");
+    CHECK(mkdir(sub.c_str(), 0755) == 0, "mkdir again");
+    write_file(sub + "/b", 20, rng);
+    sdcas_io::new_path_epoch();  // the next call
+    fd = sdcas_io::open_for_read((sub + "/b").c_str(), false, &d);
+    CHECK(fd >= 0, "the replaced directory's new file: %d", fd);
+    struct stat sb;
+    CHECK(fd >= 0 && fstat(fd, &sb) == 0 && sb.st_size == 20, "the new directory's file");
+    if (fd >= 0) close(fd);
+    CHECK(sdcas_io::open_for_read((sub + "/a").c_str(), false, &d) == -ENOENT, "the old file is gone from sub");
+    CHECK(sdcas_io::open_for_read(path("no_dir/x").c_str(), false, &d) == -ENOENT, "missing directory");
+    fd = sdcas_io::open_for_read((sub + "/").c_str(), false, &d);
+    CHECK(fd >= 0, "trailing slash opens the directory");
+    if (fd >= 0) close(fd);
+    CHECK(sdcas_io::open_for_read("no_such_relative_file", false, &d) == -ENOENT, "bare name");
+  }
+
   // plan_batch: items in order, line-aligned ascending offsets, within the
   // slot (the first item of a batch always taken), at most cap_n per batch
   std::vector<uint64_t> need(5000);
