@@ -549,8 +549,14 @@ __device__ __forceinline__ void leaf_order(uint32_t tid, const uint32_t (&bin)[T
 // chunk and each tree node by compress_quad; the quad's lead lane alone
 // writes shared state (task lists, chaining values, digests). Needs ORD 0 and
 // CA 0.
+// XT (round 5), bit 1: a tree level of at most 32 tasks — levels 5-10 in C2's
+// tiles (30, 14, 7 ... tasks), each one wave of mostly idle lanes — runs its
+// parents by quads of lanes (parent_quad: ~310 instructions per lane for a
+// task, against 680 for a lone lane; two waves at most). Bit 2: phase 1 marks
+// in a bit per slot which nodes of tile-crossing messages go to HBM, so that
+// phase 4 reads one bit per slot instead of recomputing the message's shape.
 template <int WG, int PF, int TR = 1, int ORD = 0, int DYN = 0, int CA = 0, int MINW = 0, uint32_t TL = kTile,
-          int QD = 0>
+          int QD = 0, int XT = 0>
 __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ offs,
                                                    const uint64_t* __restrict__ lens, uint32_t n,
                                                    const uint64_t* __restrict__ S,
@@ -564,6 +570,7 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
   __shared__ uint32_t task[kTaskCap<TL>];  // tree tasks by level (enc_task)
   __shared__ uint32_t ntask[12];
   __shared__ uint16_t order[ORD ? TL : 1];  // leaf loop position -> slot
+  __shared__ uint32_t sexp[(XT & 2) ? TL / 32 : 1];  // XT 2: slots whose node goes to HBM (phase 4)
   __shared__ uint64_t next_tile;
 
   const uint64_t total = *total_p;
@@ -589,6 +596,8 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
     const uint32_t cnt = m1 - m0 + 1;  // <= TL + 1
     for (uint32_t i = tid; i < cnt; i += WG) sS[i] = S[m0 + i];
     if (tid < 12) ntask[tid] = 0;
+    if constexpr ((XT & 2) != 0)
+      for (uint32_t i = tid; i < TL / 32; i += WG) sexp[i] = 0;
     if (DYN == 1 && tid == 0) next_tile = gridDim.x + atomicAdd(tile_ctr, 1ull);
     __syncthreads();
 
@@ -641,6 +650,13 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
       const uint32_t K = node_level_t<TL>(j, C, s);
       for (uint32_t k = 1; k <= K; ++k)
         task[task_base<TL>(k) + atomicAdd(&ntask[k], 1u)] = enc_task(s, s + (1u << (k - 1)), 0, false);
+      if constexpr ((XT & 2) != 0) {
+        // phase 4's test, here where the message's shape is at hand: a node
+        // of a message crossing the tile whose parent is not in the tile
+        const uint64_t S0 = g - j;
+        if ((S0 < tbase || S0 + C > tbase + TL) && !parent_in_tile_t<TL>(j, C, s, K))
+          atomicOr(&sexp[s >> 5], 1u << (s & 31));
+      }
     }
 #pragma unroll 1
     for (uint32_t i = sid; TR && lead && i < cnt; i += SW) {
@@ -747,6 +763,35 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
     for (uint32_t k = 1; TR && (1u << k) <= TL && k <= (TR == 3 ? 4u : 10u); ++k) {
       const uint32_t T = ntask[k];
       if (T == 0) continue;
+      if constexpr ((XT & 1) != 0 && !QD) {
+        if (T <= 32) {
+          // a few tasks: one quad of lanes per task (all four lanes of a
+          // task's quad run it together, as parent_quad's DPP needs)
+#pragma unroll 1
+          for (uint32_t t = tid >> 2; t < T; t += WG / 4) {
+            const uint32_t e = task[task_base<TL>(k) + t];
+            const uint32_t l = e & 1023u, r = (e >> 10) & 1023u;
+            const bool root = e >> 31;
+            uint32_t a[8], b[8], o[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+              a[q] = cvs[l][q];
+              b[q] = cvs[r][q];
+            }
+            parent_quad(a, b, root, o);
+            if (tid & 3u) continue;
+            if (root) {
+              const uint32_t mm = m0 + ((e >> 20) & 2047u);
+              store_digest(perm ? perm[mm] : mm, o, out32, out_keys);
+            } else {
+#pragma unroll
+              for (int q = 0; q < 8; ++q) cvs[l][q] = o[q];
+            }
+          }
+          __syncthreads();
+          continue;
+        }
+      }
       // TR 2 (diagnostic, still bit-exact): every lane of a wave that holds
       // tasks computes one — lanes past the level's last task repeat it and
       // do not store — to price masked lanes against active ones
@@ -780,6 +825,13 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
     // HBM at their first slot, for k_finish
 #pragma unroll 1
     for (uint32_t s = sid; TR && lead && s < TL; s += SW) {
+      if constexpr ((XT & 2) != 0) {
+        if (!((sexp[s >> 5] >> (s & 31)) & 1u)) continue;
+        uint4* o = reinterpret_cast<uint4*>(nodes + 8ull * (tbase + s));
+        o[0] = make_uint4(cvs[s][0], cvs[s][1], cvs[s][2], cvs[s][3]);
+        o[1] = make_uint4(cvs[s][4], cvs[s][5], cvs[s][6], cvs[s][7]);
+        continue;
+      }
       const uint32_t mi = smsg[s];
       if (mi == kNoMsg) continue;
       const uint64_t S0 = sS[mi];
@@ -1783,6 +1835,9 @@ static const LeafVariant kLeafVariants[] = {
     // order, 512 threads for the 128 slots
     PRODS(4 * kSmallTile, k_leaf_tree<4 * kSmallTile, 79, 1, 0, 2, 0, 0, kSmallTile, 1>),
     ABL1(512, k_leaf_tree<512, 299, 1, 1, 2, 2>),  // 74: 67 with the split line-pair loop (hash_chunk_split)
+    ABL1(512, k_leaf_tree<512, 279, 1, 1, 2, 2, 0, kTile, 0, 3>),  // 75: 67 with quad tree levels and phase-4 bits (XT 3)
+    ABL1(512, k_leaf_tree<512, 279, 1, 1, 2, 2, 0, kTile, 0, 1>),  // 76: 67 with quad tree levels (XT 1)
+    ABL1(512, k_leaf_tree<512, 279, 1, 1, 2, 2, 0, kTile, 0, 2>),  // 77: 67 with phase-4 bits (XT 2)
 };
 #undef PROD
 #undef PROD1
