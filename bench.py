@@ -42,6 +42,7 @@ per rank against the oracle, summed over the ranks.
 import argparse
 import ctypes
 import json
+import math
 import os
 import sys
 import time
@@ -872,6 +873,10 @@ def main():
                     help="c2/c3/c5: byte alignment of each message in HBM")
     ap.add_argument("--e2e-files", type=int, default=200_000, help="c2: files in the end-to-end / faithful leg")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--sustain-s", type=float, default=6.0,
+                    help="after the timed steps, the same steps back to back for this long (untimed by the "
+                         "contract; reported as `sustained`): the rate the card holds at its power limit, and "
+                         "a window long enough for a GPU-busy sampler to see (0: skip)")
     ap.add_argument("--no-bind-stream", action="store_true",
                     help="A/B: leave the step's stream unbound (every device call then waits on the previous "
                          "call's event even on the same stream, sdcas_dev_bind_stream)")
@@ -988,6 +993,25 @@ def main():
     eng.dev_sync(sp)
     if distributed:
         dt, leaf_ms, seq_ms = max_over_ranks(torch, dist, dev, [dt, leaf_ms, seq_ms])
+    sustained = None
+    if args.sustain_s > 0:
+        # the same steps for a few seconds more, outside the timed region: the
+        # steady-state rate (clock and power settled); the count follows from
+        # the timed steps' max-over-ranks time, so every rank runs as many
+        k = max(16, int(math.ceil(args.sustain_s / (dt / args.steps))))
+        if distributed:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(k):
+            step()
+        torch.cuda.synchronize()
+        st = time.perf_counter() - t1
+        if distributed:
+            st = max_over_ranks(torch, dist, dev, [st])[0]
+        sustained = {"steps": k, "seconds": st, "value": n * world * k / st, "ms_per_step": st / k * 1e3,
+                     "note": "the timed steps' workload repeated back to back after them, untimed by the "
+                             "contract (not part of `value`)"}
     if dd is not None:
         # the dedup's share of a step: the same calls on the same resident
         # inputs, `steps` of them back to back between one pair of HIP events
@@ -1053,7 +1077,7 @@ def main():
                    "chunks_per_gpu": chunks,
                    "parallelism": f"files sharded over {world} GPU(s)" +
                                   (", dedup: one RCCL all-to-all exchange" if W["dedup"] else ", no collective")},
-        "blake3_gbps": gbps, "roofline": roof,
+        "blake3_gbps": gbps, "roofline": roof, "sustained": sustained,
     }
     if dd is not None:
         ms = med = float(dd["ms"])

@@ -272,7 +272,7 @@ def test_bench_two_ranks(workload, launcher):
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     args = ["bench.py", "--gpus", "2", "--workload", workload, "--files", "20000", "--steps", "2", "--warmup", "1",
-            "--c4-total-gib", "4"]
+            "--sustain-s", "0.5", "--c4-total-gib", "4"]
     if launcher == "torchrun":
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + args
@@ -286,6 +286,8 @@ def test_bench_two_ranks(workload, launcher):
     line = lines[-1]
     d = json.loads(line[line.index('{"metric"'):])  # torchrun may prefix a rank tag
     assert d["n_gpus"] == 2 and d["value"] > 0
+    if workload != "c4":  # the untimed sustained phase, as many steps on every rank
+        assert d["sustained"]["steps"] >= 16 and d["sustained"]["value"] > 0
     assert d["parity"]["ranks"] == 2 and d["parity"]["checked_files"] >= (2 if workload == "c4" else 2000)
     assert d["parity"]["mismatches"] == 0
     if workload == "c5":
