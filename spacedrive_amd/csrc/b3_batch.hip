@@ -555,6 +555,8 @@ __device__ __forceinline__ void leaf_order(uint32_t tid, const uint32_t (&bin)[T
 // task, against 680 for a lone lane; two waves at most). Bit 2: phase 1 marks
 // in a bit per slot which nodes of tile-crossing messages go to HBM, so that
 // phase 4 reads one bit per slot instead of recomputing the message's shape.
+// Bit 4: phase 1 appends a wave's tree tasks level by level with one LDS
+// atomic per wave (a ballot and a lane count place each task).
 template <int WG, int PF, int TR = 1, int ORD = 0, int DYN = 0, int CA = 0, int MINW = 0, uint32_t TL = kTile,
           int QD = 0, int XT = 0>
 __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ offs,
@@ -622,40 +624,60 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
 #pragma unroll kPhase1Unroll
     for (uint32_t s = sid; s < TL; s += SW) {
       const uint64_t g = tbase + s;
+      uint32_t K = 0;  // levels of the tree tasks this slot starts (0: none)
       if (g >= total) {
         smsg[s] = kNoMsg;
-        continue;
+      } else {
+        uint32_t lo = 0, hi = cnt - 1;  // last message with S <= g
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi + 1) >> 1;
+          if (sS[mid] <= g) lo = mid;
+          else hi = mid - 1;
+        }
+        smsg[s] = (uint16_t)lo;
+        if (TR || CA) {
+          const uint64_t j = g - sS[lo];
+          const uint64_t len = lens[m0 + lo];
+          const uint64_t C = chunk_count(len);
+          if (CA && (CA == 1 || s == tid)) {
+            const uint32_t r = (s - tid) / WG;
+            c_ok[r] = true;
+            c_m[r] = m0 + lo;
+            c_j[r] = j;
+            c_clen[r] = len == 0 ? 0u : (uint32_t)min<uint64_t>(CHUNK_LEN, len - j * CHUNK_LEN);
+            c_root[r] = C == 1;
+            c_p[r] = blob + offs[m0 + lo] + j * CHUNK_LEN;
+          }
+          if (TR && C != 1 && lead) {
+            K = node_level_t<TL>(j, C, s);
+            if constexpr ((XT & 4) == 0)
+              for (uint32_t k = 1; k <= K; ++k)
+                task[task_base<TL>(k) + atomicAdd(&ntask[k], 1u)] = enc_task(s, s + (1u << (k - 1)), 0, false);
+            if constexpr ((XT & 2) != 0) {
+              // phase 4's test, here where the message's shape is at hand: a
+              // node of a message crossing the tile whose parent is not in it
+              const uint64_t S0 = g - j;
+              if ((S0 < tbase || S0 + C > tbase + TL) && !parent_in_tile_t<TL>(j, C, s, K))
+                atomicOr(&sexp[s >> 5], 1u << (s & 31));
+            }
+          }
+        }
       }
-      uint32_t lo = 0, hi = cnt - 1;  // last message with S <= g
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi + 1) >> 1;
-        if (sS[mid] <= g) lo = mid;
-        else hi = mid - 1;
-      }
-      smsg[s] = (uint16_t)lo;
-      if (!TR && !CA) continue;
-      const uint64_t j = g - sS[lo];
-      const uint64_t len = lens[m0 + lo];
-      const uint64_t C = chunk_count(len);
-      if (CA && (CA == 1 || s == tid)) {
-        const uint32_t r = (s - tid) / WG;
-        c_ok[r] = true;
-        c_m[r] = m0 + lo;
-        c_j[r] = j;
-        c_clen[r] = len == 0 ? 0u : (uint32_t)min<uint64_t>(CHUNK_LEN, len - j * CHUNK_LEN);
-        c_root[r] = C == 1;
-        c_p[r] = blob + offs[m0 + lo] + j * CHUNK_LEN;
-      }
-      if (!TR || C == 1 || !lead) continue;
-      const uint32_t K = node_level_t<TL>(j, C, s);
-      for (uint32_t k = 1; k <= K; ++k)
-        task[task_base<TL>(k) + atomicAdd(&ntask[k], 1u)] = enc_task(s, s + (1u << (k - 1)), 0, false);
-      if constexpr ((XT & 2) != 0) {
-        // phase 4's test, here where the message's shape is at hand: a node
-        // of a message crossing the tile whose parent is not in the tile
-        const uint64_t S0 = g - j;
-        if ((S0 < tbase || S0 + C > tbase + TL) && !parent_in_tile_t<TL>(j, C, s, K))
-          atomicOr(&sexp[s >> 5], 1u << (s & 31));
+      if constexpr ((XT & 4) != 0) {
+        // the wave's tasks appended level by level with one LDS atomic per
+        // wave and level (64 lanes adding to one counter serialise in LDS)
+        for (uint32_t k = 1;; ++k) {
+          const bool want = K >= k;
+          const uint64_t bal = __ballot(want);
+          if (!bal) break;
+          const uint32_t first = (uint32_t)__ffsll((long long)bal) - 1;
+          uint32_t base = 0;
+          if (__lane_id() == first) base = atomicAdd(&ntask[k], (uint32_t)__popcll(bal));
+          base = __shfl(base, (int)first);
+          const uint32_t below =
+              __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+          if (want) task[task_base<TL>(k) + base + below] = enc_task(s, s + (1u << (k - 1)), 0, false);
+        }
       }
     }
 #pragma unroll 1
@@ -1838,6 +1860,7 @@ static const LeafVariant kLeafVariants[] = {
     ABL1(512, k_leaf_tree<512, 279, 1, 1, 2, 2, 0, kTile, 0, 3>),  // 75: 67 with quad tree levels and phase-4 bits (XT 3)
     ABL1(512, k_leaf_tree<512, 279, 1, 1, 2, 2, 0, kTile, 0, 1>),  // 76: 67 with quad tree levels (XT 1)
     ABL1(512, k_leaf_tree<512, 279, 1, 1, 2, 2, 0, kTile, 0, 2>),  // 77: 67 with phase-4 bits (XT 2)
+    ABL1(512, k_leaf_tree<512, 279, 1, 1, 2, 2, 0, kTile, 0, 7>),  // 78: 75 with the tree tasks appended per wave (XT 7)
 };
 #undef PROD
 #undef PROD1
