@@ -1027,6 +1027,17 @@ static DedupTable dedup_table() {
   return kTableIdx;
 }
 
+// a world of one's table: a power of two of at least `load` slots per item
+// (SDCAS_DEDUP_LOAD, default 2: at most half full when every key differs)
+static uint64_t local_cap(uint64_t items) {
+  const char* v = getenv("SDCAS_DEDUP_LOAD");  // read per call (A/B in one process)
+  const double x = v ? atof(v) : 2.0;
+  const double load = x >= 1.05 && x <= 8.0 ? x : 2.0;
+  uint64_t cap = 1024;
+  while ((double)cap < load * (double)items) cap <<= 1;
+  return cap;
+}
+
 static hipError_t local_fused(DistWs& w, const uint64_t* keys, const uint8_t* has_key, const int32_t* status,
                               const uint64_t* ids, uint32_t n, const uint64_t* ekeys, const uint64_t* eids,
                               uint32_t ne, uint64_t cs, const StepWindow& win, int64_t* link,
@@ -1224,8 +1235,7 @@ hipError_t dd_local(DistWs& w, const uint64_t* keys, const uint8_t* has_key, con
   if ((e = w.nstay.ensure(1)) || (e = w.plan.ensure(kPlanHeader + (uint64_t)n + 1))) return e;
   const DedupTable table = dedup_table();
   if (n && table == kTableIdx) {
-    uint64_t cap = 1024;
-    while (cap < 2 * ((uint64_t)n + ne)) cap <<= 1;
+    const uint64_t cap = local_cap((uint64_t)n + ne);
     if (cap > (1ull << 31)) return hipErrorInvalidValue;
     return local_fused(w, keys, has_key, status, ids, n, ekeys, eids, ne, chunk_size, win, link, counts, cap, st);
   }
@@ -1237,8 +1247,7 @@ hipError_t dd_local(DistWs& w, const uint64_t* keys, const uint8_t* has_key, con
   hipLaunchKernelGGL(k_plan_walk, dim3(1), dim3(64), 0, st, (const uint64_t*)nullptr, w.stay_idx.p, ids, n,
                      w.nstay.p, win.n_total ? win.n_total : (uint64_t)n, chunk_size, win.max_steps, win.more, w.plan.p);
   if (n == 0) return hipGetLastError();
-  uint64_t cap = 1024;
-  while (cap < 2 * ((uint64_t)n + ne)) cap <<= 1;
+  const uint64_t cap = local_cap((uint64_t)n + ne);
   if (cap > (1ull << 31)) return hipErrorInvalidValue;
   if (table == kTableIdx4) {
     const uint32_t mask = (uint32_t)(cap - 1);
