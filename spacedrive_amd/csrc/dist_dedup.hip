@@ -961,17 +961,88 @@ __global__ void k_solo_apply_idx(const uint64_t* __restrict__ ids, const uint32_
 // a key's lowest file per tile touches the table (C5's 4096-file tiles hold
 // 71 % distinct keys) — every shape was slower on C5, 0.43-0.67 ms against
 // 0.40, the barrier a tile needs holding its workgroup until its slowest
-// probe chain ends.
+// probe chain ends; and, without tiles, the files' insert taking 2 or 4
+// files per thread with each probe phase issued for all of them (C5 insert
+// 210 -> 467 us at 4, profiles/r05_ab_dedup_apply.json).
 constexpr uint32_t kStayTile = 1024;  // rows per stays count (a multiple of the wave)
 
+constexpr uint32_t kCountShards = 64;  // the apply's count pairs (a workgroup adds to blockIdx % 64)
+
 __global__ void k_local_clear(uint4* __restrict__ tab, uint64_t tab_q, uint4* __restrict__ em, uint64_t em_q,
-                              uint32_t* __restrict__ cnt, uint32_t nt) {
+                              uint32_t* __restrict__ cnt, uint32_t nt, unsigned long long* __restrict__ shard) {
   const uint4 ones = make_uint4(~0u, ~0u, ~0u, ~0u);
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   for (uint64_t q = t0; q < tab_q; q += stride) tab[q] = ones;
   for (uint64_t q = t0; q < em_q; q += stride) em[q] = ones;
   for (uint64_t q = t0; q < nt; q += stride) cnt[q] = 0;
+  if (shard && t0 < 2 * kCountShards) shard[t0] = 0;
+}
+
+// The apply with R files per thread, each phase's loads issued for all R
+// before the next phase (slot, then the table's lowest index and the existing
+// minimum, then the winner's ordinal) and a grid of one workgroup per TB * R
+// files: full occupancy instead of 1024 workgroups walking their files one
+// dependent chain at a time. The counts go to kCountShards pairs (workgroup
+// b adds to pair b % kCountShards), folded into the caller's by
+// k_counts_fold — thousands of workgroups adding to one address serialise.
+template <uint32_t R>
+__global__ void __launch_bounds__(TB) k_solo_apply_r(const uint64_t* __restrict__ ids,
+                                                     const uint32_t* __restrict__ pos, uint32_t n,
+                                                     const uint32_t* __restrict__ tab,
+                                                     const uint64_t* __restrict__ emin, uint64_t cs,
+                                                     const uint64_t* __restrict__ plan, int64_t* __restrict__ link,
+                                                     unsigned long long* __restrict__ shard) {
+  __shared__ unsigned long long sc[2];
+  if (threadIdx.x < 2) sc[threadIdx.x] = 0;
+  __syncthreads();
+  const PlanView pv = plan_view(plan);
+  const uint64_t i0 = (uint64_t)blockIdx.x * TB * R + threadIdx.x;
+  uint32_t h[R], f[R];
+  uint64_t e[R], r[R], me[R];
+#pragma unroll
+  for (uint32_t k = 0; k < R; ++k) {
+    const uint64_t i = i0 + (uint64_t)k * TB;
+    h[k] = i < n ? pos[i] : kSlotDropped;
+    me[k] = i < n ? ids[i] : 0;
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < R; ++k) {
+    const bool keyed = h[k] < kSlotDropped && h[k] != kSlotNoKey;
+    f[k] = keyed ? tab[h[k]] : 0u;
+    e[k] = keyed && emin ? emin[h[k]] : ~0ull;
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < R; ++k) {
+    const uint64_t i = i0 + (uint64_t)k * TB;
+    const bool keyed = h[k] < kSlotDropped && h[k] != kSlotNoKey;
+    // mod.rs:202-238: the first existing Object; else (mod.rs:246-254) the
+    // key's first file — a file, as this one carries the key
+    r[k] = !keyed || e[k] != ~0ull || f[k] == (uint32_t)i ? me[k] : ids[f[k]];
+  }
+  unsigned long long c = 0, l = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < R; ++k) {
+    const uint64_t i = i0 + (uint64_t)k * TB;
+    if (i >= n) continue;
+    const int kind = h[k] == kSlotDropped ? kFileDropped : h[k] == kSlotNoKey ? kFileNoKey : kFileKeyed;
+    const int64_t rk = kind != kFileKeyed ? 0 : e[k] != ~0ull ? -(int64_t)e[k] - 1 : (int64_t)r[k];
+    link[i] = step_link(kind, (int64_t)me[k], rk, cs, pv, c, l);
+  }
+  add_counts(c, l, sc, shard ? shard + 2 * (blockIdx.x % kCountShards) : nullptr);
+}
+
+// the shards' sums added to the caller's counts (one wave)
+__global__ void k_counts_fold(const unsigned long long* __restrict__ shard, unsigned long long* __restrict__ counts) {
+  unsigned long long c = shard[2 * threadIdx.x], l = shard[2 * threadIdx.x + 1];
+  for (int off = 32; off > 0; off >>= 1) {
+    c += __shfl_down(c, off);
+    l += __shfl_down(l, off);
+  }
+  if (threadIdx.x == 0) {
+    atomicAdd(&counts[0], c);
+    atomicAdd(&counts[1], l);
+  }
 }
 
 // the stays rows of tile blockIdx.x (PER rows) in order, at the offset the
@@ -1027,6 +1098,15 @@ static DedupTable dedup_table() {
   return kTableIdx;
 }
 
+// SDCAS_APPLY_R: files per thread of the fused path's apply (1, 2, 4, 8;
+// 0 = round 5's grid-stride apply over at most 1024 workgroups), read per
+// call (A/B in one process)
+static uint32_t apply_files_per_thread() {
+  const char* v = getenv("SDCAS_APPLY_R");
+  const int x = v ? atoi(v) : 4;
+  return x == 0 || x == 1 || x == 2 || x == 4 || x == 8 ? (uint32_t)x : 4u;
+}
+
 // a world of one's table: a power of two of at least `load` slots per item
 // (SDCAS_DEDUP_LOAD, default 2: at most half full when every key differs)
 static uint64_t local_cap(uint64_t items) {
@@ -1049,15 +1129,19 @@ static hipError_t local_fused(DistWs& w, const uint64_t* keys, const uint8_t* ha
   const uint32_t shift = 64u - (uint32_t)__builtin_ctzll(cap);
   // the u32 table borrows tmin's storage (cap u32 = cap / 4 of its u64);
   // the existing Objects' minima live in tkey (cap u64), when there are any
+  const uint32_t ar = apply_files_per_thread();
+  const bool sharded = ar && counts;
   if ((e = w.tmin.ensure(cap / 2 + 1)) || (e = w.tpos.ensure(n)) || (ne && (e = w.tkey.ensure(cap + 1))) ||
-      (e = w.stay_cnt.ensure(nt + 1)) || (stays && (e = w.stay_idx.ensure(n))))
+      (e = w.stay_cnt.ensure(nt + 1)) || (stays && (e = w.stay_idx.ensure(n))) ||
+      (sharded && (e = w.shard.ensure(2 * kCountShards))))
     return e;
   auto* tab = reinterpret_cast<uint32_t*>(w.tmin.p);
   auto* em = ne ? reinterpret_cast<unsigned long long*>(w.tkey.p) : nullptr;
   const uint64_t tab_q = cap / 4, em_q = ne ? cap / 2 : 0;  // uint4 stores (cap >= 1024)
   const uint32_t cg = (uint32_t)std::min<uint64_t>((tab_q + em_q + TB - 1) / TB, 2048);
   hipLaunchKernelGGL(k_local_clear, dim3(cg), dim3(TB), 0, st, reinterpret_cast<uint4*>(tab), tab_q,
-                     reinterpret_cast<uint4*>(em), em_q, w.stay_cnt.p, stays ? nt : 0u);
+                     reinterpret_cast<uint4*>(em), em_q, w.stay_cnt.p, stays ? nt : 0u,
+                     sharded ? w.shard.p : nullptr);
   if (ne)
     hipLaunchKernelGGL(k_solo_insert_idx, dim3(blocks(ne)), dim3(TB), 0, st, keys, ekeys, n, (const uint8_t*)nullptr,
                        (const int32_t*)nullptr, eids, ne, n, tab, em, mask, shift, (uint32_t*)nullptr,
@@ -1071,8 +1155,22 @@ static hipError_t local_fused(DistWs& w, const uint64_t* keys, const uint8_t* ha
   hipLaunchKernelGGL(k_plan_walk, dim3(1), dim3(64), 0, st, (const uint64_t*)nullptr, w.stay_idx.p, ids,
                      stays ? n : 0u, (const uint32_t*)nullptr, win.n_total ? win.n_total : (uint64_t)n, cs,
                      win.max_steps, win.more, w.plan.p, stays ? w.stay_cnt.p : (const uint32_t*)nullptr, nt);
-  hipLaunchKernelGGL(k_solo_apply_idx, dim3(blocks(n) < 1024 ? blocks(n) : 1024), dim3(TB), 0, st, ids, w.tpos.p, n,
-                     tab, ne ? w.tkey.p : nullptr, cs, w.plan.p, link, counts);
+  const uint64_t* emp = ne ? w.tkey.p : nullptr;
+  auto apply = [&](auto kern, uint32_t r) {
+    const uint32_t g = (uint32_t)(((uint64_t)n + (uint64_t)TB * r - 1) / ((uint64_t)TB * r));
+    if (g) hipLaunchKernelGGL(kern, dim3(g), dim3(TB), 0, st, ids, w.tpos.p, n, tab, emp, cs, w.plan.p, link,
+                              sharded ? w.shard.p : nullptr);
+  };
+  switch (ar) {
+    case 1: apply(k_solo_apply_r<1>, 1); break;
+    case 2: apply(k_solo_apply_r<2>, 2); break;
+    case 4: apply(k_solo_apply_r<4>, 4); break;
+    case 8: apply(k_solo_apply_r<8>, 8); break;
+    default:
+      hipLaunchKernelGGL(k_solo_apply_idx, dim3(blocks(n) < 1024 ? blocks(n) : 1024), dim3(TB), 0, st, ids, w.tpos.p,
+                         n, tab, emp, cs, w.plan.p, link, counts);
+  }
+  if (sharded) hipLaunchKernelGGL(k_counts_fold, dim3(1), dim3(kCountShards), 0, st, w.shard.p, counts);
   return hipGetLastError();
 }
 

@@ -77,9 +77,10 @@ def test_product_library_holds_only_product_kernels():
     wrong digests and live only in libsdcas_ablate.so)"""
     stubs = _kernel_stubs(N.LIB_PATH)
     leaf = [s for s in stubs if s.startswith("k_leaf")]
-    assert leaf == ["k_leaf_tree<128, 79, 1, 1, 2, 2, 0, 128u, 0>", "k_leaf_tree<512, 209, 1, 1, 2, 2, 0, 1024u, 0>",
-                    "k_leaf_tree<512, 279, 1, 1, 2, 2, 0, 1024u, 0>",
-                    "k_leaf_tree<512, 79, 1, 0, 2, 0, 0, 128u, 1>"], leaf
+    assert leaf == ["k_leaf_tree<128, 79, 1, 1, 2, 2, 0, 128u, 0, 0>",
+                    "k_leaf_tree<512, 209, 1, 1, 2, 2, 0, 1024u, 0, 0>",
+                    "k_leaf_tree<512, 279, 1, 1, 2, 2, 0, 1024u, 0, 0>",
+                    "k_leaf_tree<512, 79, 1, 0, 2, 0, 0, 128u, 1, 0>"], leaf
     finish = [s for s in stubs if s.startswith("k_finish")]
     assert finish == ["k_finish_q<1024u>", "k_finish_q<128u>", "k_finish_t<1024u>", "k_finish_t<128u>"], finish
     assert not [s for s in stubs if "slim" in s or "quad" in s]

@@ -362,7 +362,7 @@ def test_rccl_world1(eng, oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("table", ["idx", "idx4", "kv"])
+@pytest.mark.parametrize("table", ["idx", "idx-r0", "idx-r1", "idx-r8", "idx4", "kv"])
 @pytest.mark.parametrize("corpus,chunk_size", [("default", 100), ("default", 7), ("default", 1),
                                                ("collisions", 100), ("clustered", 100)])
 def test_device_local_vs_oracle(eng, oracle, corpus, chunk_size, table, monkeypatch):
@@ -371,12 +371,16 @@ def test_device_local_vs_oracle(eng, oracle, corpus, chunk_size, table, monkeypa
     every table: the compact u32 table (the default; since round 5 the
     insert also counts the stays rows per 1024-row tile, five launches),
     the same table behind round 4's eight launches, round 3's 16-byte kv
-    table; and the
+    table; the default table's apply with 0 (the grid-stride form), 1 and 8
+    files per thread beside the default 4 (`idx-rN`, SDCAS_APPLY_R); and the
     existing Objects passed in DB order and shuffled (their DB indices then
     not ascending: the first Object is the lowest DB index, not the first
     entry)"""
     from spacedrive_amd.dist_dedup import DeviceStages
+    table, _, knob = table.partition("-")
     monkeypatch.setenv("SDCAS_DEDUP_TABLE", table)
+    if knob:
+        monkeypatch.setenv("SDCAS_APPLY_R", knob[1:])
     if corpus == "default":
         keys, has, status, existing = make_corpus(91, 40000, pool=6000)
         keys[:2] = np.uint64(2**64 - 1)  # the table's empty marker is a legal key
