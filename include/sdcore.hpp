@@ -244,6 +244,16 @@ class Library {
     set_cas_id(file_path_id, cas_id);
     connect(file_path_id, object_id);
   }
+  // set_cas_id_and_connect of many rows, one write per row, each row at most
+  // once (the default writes them one by one)
+  struct CasLink {
+    int32_t file_path_id;
+    std::optional<std::string> cas_id;
+    int32_t object_id;
+  };
+  virtual void set_cas_ids_and_connect(const std::vector<CasLink>& rows) {
+    for (const auto& r : rows) set_cas_id_and_connect(r.file_path_id, r.cas_id, r.object_id);
+  }
   // mod.rs:290-327: object::create_unchecked(kind, date_created) -> object id
   virtual int32_t create_object(ObjectKind kind, int64_t date_created) = 0;
   // object::create_many (mod.rs:314-327): Objects created in this order, ids
@@ -361,6 +371,10 @@ class SqliteLibrary : public Library {
   std::vector<std::pair<std::string, int32_t>> first_objects(const std::vector<std::string>& cas_ids) override;
   void set_cas_id_and_connect(int32_t file_path_id, const std::optional<std::string>& cas_id,
                               int32_t object_id) override;
+  // UPDATE ... FROM (VALUES ...) of up to 64 rows per statement (bulk
+  // identify: of rows without an Object, a row found with one takes the
+  // general path)
+  void set_cas_ids_and_connect(const std::vector<CasLink>& rows) override;
   int32_t create_object(ObjectKind kind, int64_t date_created) override;
   // multi-row INSERTs of up to 64 Objects each
   std::vector<int32_t> create_objects(const std::vector<std::pair<ObjectKind, int64_t>>& kinds_dates) override;

@@ -605,15 +605,9 @@ static std::pair<size_t, size_t> step_db(Library& db, const std::vector<FilePath
                    [](const std::pair<uint64_t, size_t>& a, const std::pair<uint64_t, size_t>& b) {
                      return a.first < b.first;
                    });
-  std::vector<int32_t> created_object(n, 0);
-  auto link_row = [&](size_t i, int32_t oid) {
-    if (cas_pending[i]) {
-      db.set_cas_id_and_connect(file_paths[i].id, md[i].value().cas_id, oid);
-      cas_pending[i] = 0;
-    } else {
-      db.connect(file_paths[i].id, oid);
-    }
-  };
+  // each row's last link: a row several steps read links to the Object of
+  // the last (creates are in step order); 0 = not linked
+  std::vector<int32_t> created_object(n, 0), link_to(n, 0);
   db.begin_batch();
   {
     // object::create_many (mod.rs:314-327), then the links of :331-342
@@ -624,18 +618,32 @@ static std::pair<size_t, size_t> step_db(Library& db, const std::vector<FilePath
     if (oids.size() != creates.size()) throw std::logic_error("identifier_step_db: create_objects returned a wrong count");
     for (size_t k = 0; k < creates.size(); ++k) {
       const size_t i = creates[k].second;
-      created_object[i] = oids[k];
-      link_row(i, created_object[i]);
+      created_object[i] = link_to[i] = oids[k];
     }
   }
   // links to the first Object carrying the cas_id (mod.rs:202-238)
   for (size_t i = 0; i < n; ++i) {
     const int64_t l = d.link[i];
     if (l == SDCAS_LINK_DROPPED || l == SDCAS_LINK_DEFERRED || l == (int64_t)i) continue;
-    link_row(i, l >= 0 ? created_object[(size_t)l] : eobj[(size_t)(-(l + 1))]);
+    link_to[i] = l >= 0 ? created_object[(size_t)l] : eobj[(size_t)(-(l + 1))];
   }
-  for (size_t i = 0; i < n; ++i)  // read but not linked (none such today)
-    if (cas_pending[i]) db.set_cas_id(file_paths[i].id, md[i].value().cas_id);
+  // one write per row, in row order: a row without an Object takes its
+  // cas_id and its link together (set_cas_ids_and_connect), a row with one
+  // its link (connect); a row read but not linked its cas_id (none such today)
+  std::vector<Library::CasLink> writes;
+  writes.reserve(n);
+  for (size_t i = 0; i < n; ++i) {
+    if (link_to[i] && cas_pending[i]) writes.push_back({file_paths[i].id, md[i].value().cas_id, link_to[i]});
+    else if (link_to[i]) db.connect(file_paths[i].id, link_to[i]);
+    else if (cas_pending[i]) db.set_cas_id(file_paths[i].id, md[i].value().cas_id);
+  }
+  // SDCORE_LINKS=each: the rows one statement each (A/B)
+  static const bool each = [] {
+    const char* v = getenv("SDCORE_LINKS");
+    return v && !strcmp(v, "each");
+  }();
+  if (each) db.Library::set_cas_ids_and_connect(writes);
+  else db.set_cas_ids_and_connect(writes);
   db.end_batch();
   trace_lap(JobTrace::kObjects);
   if (window) *window = win;

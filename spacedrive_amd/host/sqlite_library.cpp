@@ -53,6 +53,8 @@ struct SqliteLibrary::Impl {
   Stmt row_state, set_cas_connect_free, count_cas, load_first;
   static constexpr int kManyObjects = 64;
   Stmt new_objects;  // kManyObjects rows of (id, pub_id, kind, date_created)
+  static constexpr int kManyLinks = 64;
+  Stmt links, links_free;  // kManyLinks rows of (id, cas_id, object_id); _free: rows without an Object
   // the job's read-ahead connection (concurrent_orphan_reads): read-only, one
   // statement, used by one thread at a time
   std::string path;
@@ -277,6 +279,13 @@ std::unique_ptr<SqliteLibrary> SqliteLibrary::open(const std::string& path, bool
     std::string q = "INSERT INTO object (id, pub_id, kind, date_created) VALUES ";
     for (int k = 0; k < Impl::kManyObjects; ++k) q += k ? ", (?, ?, ?, ?)" : "(?, ?, ?, ?)";
     x.prepare(x.new_objects, q.c_str());
+  }
+  for (int free = 0; free < 2; ++free) {
+    std::string q = "UPDATE file_path SET cas_id = v.column2, object_id = v.column3 FROM (VALUES ";
+    for (int k = 0; k < Impl::kManyLinks; ++k) q += k ? ", (?, ?, ?)" : "(?, ?, ?)";
+    q += ") AS v WHERE file_path.id = v.column1";
+    if (free) q += " AND file_path.object_id IS NULL";
+    x.prepare(free ? x.links_free : x.links, q.c_str());
   }
   x.prepare(x.connect, "UPDATE file_path SET object_id = ?1 WHERE id = ?2");
   x.prepare(x.set_cas_connect, "UPDATE file_path SET cas_id = ?1, object_id = ?2 WHERE id = ?3");
@@ -548,6 +557,40 @@ void SqliteLibrary::set_cas_id_and_connect(int32_t file_path_id, const std::opti
   sqlite3_bind_int64(x.set_cas_connect.s, 2, object_id);
   sqlite3_bind_int64(x.set_cas_connect.s, 3, file_path_id);
   x.done(x.set_cas_connect);
+}
+
+void SqliteLibrary::set_cas_ids_and_connect(const std::vector<CasLink>& rows) {
+  Impl& x = *d_;
+  size_t k = 0;
+  begin_batch();
+  for (; k + Impl::kManyLinks <= rows.size(); k += Impl::kManyLinks) {
+    Stmt& st = x.bulk ? x.links_free : x.links;
+    for (int r = 0; r < Impl::kManyLinks; ++r) {
+      const CasLink& w = rows[k + r];
+      sqlite3_bind_int64(st.s, 3 * r + 1, w.file_path_id);
+      x.opt_text(st, 3 * r + 2, w.cas_id);
+      sqlite3_bind_int64(st.s, 3 * r + 3, w.object_id);
+    }
+    x.done(st);
+    if (!x.bulk) continue;
+    const bool all = sqlite3_changes(x.db) == Impl::kManyLinks;
+    for (int r = 0; r < Impl::kManyLinks; ++r) {
+      const CasLink& w = rows[k + r];
+      if (!all) {
+        // a row that had an Object kept it (or is gone): the general path,
+        // as set_cas_id_and_connect takes for it
+        auto [cas, oid] = x.state(w.file_path_id);
+        if (!(oid && *oid == w.object_id && cas == w.cas_id)) {
+          set_cas_id(w.file_path_id, w.cas_id);
+          connect(w.file_path_id, w.object_id);
+          continue;
+        }
+      }
+      if (w.cas_id) x.first_min(*w.cas_id, w.object_id);
+    }
+  }
+  for (; k < rows.size(); ++k) set_cas_id_and_connect(rows[k].file_path_id, rows[k].cas_id, rows[k].object_id);
+  end_batch();
 }
 
 void SqliteLibrary::connect(int32_t file_path_id, int32_t object_id) {

@@ -823,6 +823,65 @@ static void test_library_edges() {
   for (const char* suf : {"", "-wal", "-shm"}) std::remove((std::string(fpath) + suf).c_str());
 }
 
+// set_cas_ids_and_connect (64 rows per UPDATE ... FROM (VALUES ...)) against
+// the same writes one by one: with and without bulk identify, a chunk holding
+// rows that already have an Object (bulk: the statement skips them, they take
+// the general path) and a remainder shorter than a chunk
+static void test_cas_links() {
+  for (bool bulk : {false, true}) {
+    auto many = SqliteLibrary::open(":memory:", true);
+    auto one = SqliteLibrary::open(":memory:", true);
+    for (auto* db : {many.get(), one.get()}) {
+      std::vector<FilePathRow> rows(150);
+      for (size_t i = 0; i < rows.size(); ++i) {
+        rows[i].location_id = 1;
+        rows[i].materialized_path = "/";
+        rows[i].name = "f" + std::to_string(i);
+        rows[i].size_in_bytes = 1 + i;
+      }
+      db->add_file_paths(rows);
+      for (int i = 0; i < 40; ++i) db->create_object(ObjectKindImage, i);
+      // rows 10 and 70 have an Object (and 10 a cas_id) before the job
+      db->set_cas_id_and_connect(10, std::string("00000000000000aa"), 3);
+      db->connect(70, 4);
+      if (bulk) CHECK(db->begin_bulk_identify(150), "bulk identify (%d)", (int)bulk);
+    }
+    std::vector<Library::CasLink> w;
+    for (int32_t id = 1; id <= 150; ++id) {
+      std::optional<std::string> cas;
+      if (id % 11) {
+        char b[17];
+        std::snprintf(b, sizeof b, "%016x", (unsigned)(id % 37));
+        cas = std::string(b);
+      }
+      w.push_back({id, cas, 1 + (id * 7) % 40});
+    }
+    many->set_cas_ids_and_connect(w);
+    for (const auto& x : w) one->set_cas_id_and_connect(x.file_path_id, x.cas_id, x.object_id);
+    std::vector<std::string> want;
+    for (int k = 0; k < 37; ++k) {
+      char b[17];
+      std::snprintf(b, sizeof b, "%016x", (unsigned)k);
+      want.push_back(b);
+    }
+    want.push_back("00000000000000aa");
+    auto sorted = [](std::vector<std::pair<std::string, int32_t>> v) {
+      std::sort(v.begin(), v.end());
+      return v;
+    };
+    CHECK(sorted(many->first_objects(want)) == sorted(one->first_objects(want)), "first objects (bulk %d)", (int)bulk);
+    if (bulk) {
+      many->end_bulk_identify();
+      one->end_bulk_identify();
+      CHECK(sorted(many->first_objects(want)) == sorted(one->first_objects(want)), "first objects after the rebuild");
+    }
+    for (int32_t id = 1; id <= 150; ++id) {
+      const auto a = many->file_path(id), b = one->file_path(id);
+      CHECK(a && b && a->cas_id == b->cas_id && a->object_id == b->object_id, "row %d (bulk %d)", id, (int)bulk);
+    }
+  }
+}
+
 int main(int argc, char** argv) {
   if (argc > 2 && std::strcmp(argv[1], "--bench") == 0) return bench((size_t)std::atoll(argv[2]));
   test_parity(true);
@@ -837,6 +896,7 @@ int main(int argc, char** argv) {
   test_walk();
   test_kind();
   test_library_edges();
+  test_cas_links();
   std::printf("%s (%d failures)\n", failures ? "FAILED" : "ALL OK", failures);
   return failures ? 1 : 0;
 }
