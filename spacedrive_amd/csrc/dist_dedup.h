@@ -49,7 +49,7 @@ struct DistWs {
   Buf<uint32_t> tpos;        // table entry of each received file record
   Buf<uint32_t> stay_idx, nstay;  // the batch's stay-orphan rows (dd_local's plan)
   Buf<uint32_t> stay_cnt;         // per-tile stays counts (select_stays, the fused insert, the bitmap)
-  Buf<unsigned long long> shard;  // the fused apply's (created, linked) counts, kCountShards pairs
+  Buf<unsigned long long> shard;  // the applies' (created, linked) counts, kCountShards pairs (kept zeroed)
   Buf<uint64_t> plan, stay_sorted;
   Buf<uint32_t> bitmap;           // dd_plan: the stays ordinals of a long gathered list
   void release();
@@ -148,7 +148,7 @@ hipError_t dd_resolve(DistWs& w, const uint64_t* frec, uint32_t nf, const uint64
 // chunks are the steps' positions, a file past the plan's limit is
 // SDCAS_LINK_DEFERRED, and a re-read file without cas_id creates a second
 // Object when its second read is inside the limit.
-hipError_t dd_apply(const uint64_t* ids, const uint32_t* slot, uint32_t n, const int64_t* result,
+hipError_t dd_apply(DistWs& w, const uint64_t* ids, const uint32_t* slot, uint32_t n, const int64_t* result,
                     uint64_t chunk_size, const uint64_t* plan, int64_t* link, unsigned long long* counts,
                     hipStream_t st);
 

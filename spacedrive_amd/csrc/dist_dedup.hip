@@ -31,6 +31,7 @@ namespace {
 constexpr uint32_t TB = 256;
 constexpr int64_t kLinkDeferred = INT64_MIN + 1;  // SDCAS_LINK_DEFERRED
 inline uint32_t blocks(uint32_t n) { return (n + TB - 1) / TB; }
+constexpr uint32_t kCountShards = 64;  // the apply's count pairs (a workgroup adds to blockIdx % 64)
 
 // ---- the steps' positions (see dist_dedup.h, "the job's steps") -------------------
 
@@ -130,6 +131,40 @@ __global__ void k_dd_apply(const uint64_t* __restrict__ ids, const uint32_t* __r
     link[i] = step_link(kind, (int64_t)ids[i], kind == kFileKeyed ? result[s] : 0, cs, pv, c, l);
   }
   add_counts(c, l, sc, counts);
+}
+
+// k_dd_apply with R files per thread over a full grid, the counts into
+// kCountShards pairs (as k_solo_apply_r; folded by k_counts_fold)
+template <uint32_t R>
+__global__ void __launch_bounds__(TB) k_dd_apply_r(const uint64_t* __restrict__ ids,
+                                                   const uint32_t* __restrict__ slot, uint32_t n,
+                                                   const int64_t* __restrict__ result, uint64_t cs,
+                                                   const uint64_t* __restrict__ plan, int64_t* __restrict__ link,
+                                                   unsigned long long* __restrict__ shard) {
+  __shared__ unsigned long long sc[2];
+  if (threadIdx.x < 2) sc[threadIdx.x] = 0;
+  __syncthreads();
+  const PlanView pv = plan_view(plan);
+  const uint64_t i0 = (uint64_t)blockIdx.x * TB * R + threadIdx.x;
+  uint32_t s[R];
+  int64_t me[R], r[R];
+#pragma unroll
+  for (uint32_t k = 0; k < R; ++k) {
+    const uint64_t i = i0 + (uint64_t)k * TB;
+    s[k] = i < n ? slot[i] : kSlotDropped;
+    me[k] = i < n ? (int64_t)ids[i] : 0;
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < R; ++k) r[k] = s[k] < kSlotDropped && s[k] != kSlotNoKey ? result[s[k]] : 0;
+  unsigned long long c = 0, l = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < R; ++k) {
+    const uint64_t i = i0 + (uint64_t)k * TB;
+    if (i >= n) continue;
+    const int kind = s[k] == kSlotDropped ? kFileDropped : s[k] == kSlotNoKey ? kFileNoKey : kFileKeyed;
+    link[i] = step_link(kind, me[k], r[k], cs, pv, c, l);
+  }
+  add_counts(c, l, sc, shard ? shard + 2 * (blockIdx.x % kCountShards) : nullptr);
 }
 
 // Stays rows — their step leaves them orphans (file_identifier_job.rs:258-264)
@@ -966,17 +1001,15 @@ __global__ void k_solo_apply_idx(const uint64_t* __restrict__ ids, const uint32_
 // 210 -> 467 us at 4, profiles/r05_ab_dedup_apply.json).
 constexpr uint32_t kStayTile = 1024;  // rows per stays count (a multiple of the wave)
 
-constexpr uint32_t kCountShards = 64;  // the apply's count pairs (a workgroup adds to blockIdx % 64)
 
 __global__ void k_local_clear(uint4* __restrict__ tab, uint64_t tab_q, uint4* __restrict__ em, uint64_t em_q,
-                              uint32_t* __restrict__ cnt, uint32_t nt, unsigned long long* __restrict__ shard) {
+                              uint32_t* __restrict__ cnt, uint32_t nt) {
   const uint4 ones = make_uint4(~0u, ~0u, ~0u, ~0u);
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   for (uint64_t q = t0; q < tab_q; q += stride) tab[q] = ones;
   for (uint64_t q = t0; q < em_q; q += stride) em[q] = ones;
   for (uint64_t q = t0; q < nt; q += stride) cnt[q] = 0;
-  if (shard && t0 < 2 * kCountShards) shard[t0] = 0;
 }
 
 // The apply with R files per thread, each phase's loads issued for all R
@@ -1032,9 +1065,12 @@ __global__ void __launch_bounds__(TB) k_solo_apply_r(const uint64_t* __restrict_
   add_counts(c, l, sc, shard ? shard + 2 * (blockIdx.x % kCountShards) : nullptr);
 }
 
-// the shards' sums added to the caller's counts (one wave)
-__global__ void k_counts_fold(const unsigned long long* __restrict__ shard, unsigned long long* __restrict__ counts) {
+// the shards' sums added to the caller's counts (one wave); the shards are
+// left zeroed for the next call (and zeroed when allocated: shard_counts)
+__global__ void k_counts_fold(unsigned long long* __restrict__ shard, unsigned long long* __restrict__ counts) {
   unsigned long long c = shard[2 * threadIdx.x], l = shard[2 * threadIdx.x + 1];
+  shard[2 * threadIdx.x] = 0;
+  shard[2 * threadIdx.x + 1] = 0;
   for (int off = 32; off > 0; off >>= 1) {
     c += __shfl_down(c, off);
     l += __shfl_down(l, off);
@@ -1107,6 +1143,14 @@ static uint32_t apply_files_per_thread() {
   return x == 0 || x == 1 || x == 2 || x == 4 || x == 8 ? (uint32_t)x : 4u;
 }
 
+// the applies' count shards: zeroed when allocated, and by k_counts_fold
+// after every use
+static hipError_t shard_counts(DistWs& w, hipStream_t st) {
+  if (w.shard.cap >= 2 * kCountShards) return hipSuccess;
+  hipError_t e = w.shard.ensure(2 * kCountShards);
+  return e ? e : hipMemsetAsync(w.shard.p, 0, 2 * kCountShards * sizeof(unsigned long long), st);
+}
+
 // a world of one's table: a power of two of at least `load` slots per item
 // (SDCAS_DEDUP_LOAD, default 2: at most half full when every key differs)
 static uint64_t local_cap(uint64_t items) {
@@ -1132,16 +1176,14 @@ static hipError_t local_fused(DistWs& w, const uint64_t* keys, const uint8_t* ha
   const uint32_t ar = apply_files_per_thread();
   const bool sharded = ar && counts;
   if ((e = w.tmin.ensure(cap / 2 + 1)) || (e = w.tpos.ensure(n)) || (ne && (e = w.tkey.ensure(cap + 1))) ||
-      (e = w.stay_cnt.ensure(nt + 1)) || (stays && (e = w.stay_idx.ensure(n))) ||
-      (sharded && (e = w.shard.ensure(2 * kCountShards))))
+      (e = w.stay_cnt.ensure(nt + 1)) || (stays && (e = w.stay_idx.ensure(n))) || (sharded && (e = shard_counts(w, st))))
     return e;
   auto* tab = reinterpret_cast<uint32_t*>(w.tmin.p);
   auto* em = ne ? reinterpret_cast<unsigned long long*>(w.tkey.p) : nullptr;
   const uint64_t tab_q = cap / 4, em_q = ne ? cap / 2 : 0;  // uint4 stores (cap >= 1024)
   const uint32_t cg = (uint32_t)std::min<uint64_t>((tab_q + em_q + TB - 1) / TB, 2048);
   hipLaunchKernelGGL(k_local_clear, dim3(cg), dim3(TB), 0, st, reinterpret_cast<uint4*>(tab), tab_q,
-                     reinterpret_cast<uint4*>(em), em_q, w.stay_cnt.p, stays ? nt : 0u,
-                     sharded ? w.shard.p : nullptr);
+                     reinterpret_cast<uint4*>(em), em_q, w.stay_cnt.p, stays ? nt : 0u);
   if (ne)
     hipLaunchKernelGGL(k_solo_insert_idx, dim3(blocks(ne)), dim3(TB), 0, st, keys, ekeys, n, (const uint8_t*)nullptr,
                        (const int32_t*)nullptr, eids, ne, n, tab, em, mask, shift, (uint32_t*)nullptr,
@@ -1388,11 +1430,29 @@ hipError_t dd_local(DistWs& w, const uint64_t* keys, const uint8_t* has_key, con
   return hipGetLastError();
 }
 
-hipError_t dd_apply(const uint64_t* ids, const uint32_t* slot, uint32_t n, const int64_t* result, uint64_t chunk_size,
-                    const uint64_t* plan, int64_t* link, unsigned long long* counts, hipStream_t st) {
+hipError_t dd_apply(DistWs& w, const uint64_t* ids, const uint32_t* slot, uint32_t n, const int64_t* result,
+                    uint64_t chunk_size, const uint64_t* plan, int64_t* link, unsigned long long* counts,
+                    hipStream_t st) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_dd_apply, dim3(blocks(n) < 1024 ? blocks(n) : 1024), dim3(TB), 0, st, ids, slot, n, result,
-                     chunk_size ? chunk_size : 100, plan, link, counts);
+  const uint64_t cs = chunk_size ? chunk_size : 100;
+  const uint32_t ar = apply_files_per_thread();
+  hipError_t e;
+  if (ar && counts && (e = shard_counts(w, st))) return e;
+  unsigned long long* sh = ar && counts ? w.shard.p : nullptr;
+  auto apply = [&](auto kern, uint32_t r) {
+    const uint32_t g = (uint32_t)(((uint64_t)n + (uint64_t)TB * r - 1) / ((uint64_t)TB * r));
+    hipLaunchKernelGGL(kern, dim3(g), dim3(TB), 0, st, ids, slot, n, result, cs, plan, link, sh);
+  };
+  switch (ar) {
+    case 1: apply(k_dd_apply_r<1>, 1); break;
+    case 2: apply(k_dd_apply_r<2>, 2); break;
+    case 4: apply(k_dd_apply_r<4>, 4); break;
+    case 8: apply(k_dd_apply_r<8>, 8); break;
+    default:
+      hipLaunchKernelGGL(k_dd_apply, dim3(blocks(n) < 1024 ? blocks(n) : 1024), dim3(TB), 0, st, ids, slot, n, result,
+                         cs, plan, link, counts);
+  }
+  if (sh) hipLaunchKernelGGL(k_counts_fold, dim3(1), dim3(kCountShards), 0, st, sh, counts);
   return hipGetLastError();
 }
 

@@ -1637,7 +1637,7 @@ int sdcas_dev_dedup_apply(sdcas_ctx* c, const uint64_t* d_ids, const uint32_t* d
   if (n > SDCAS_MAX_BATCH) return c->fail(SDCAS_E_CAPACITY, "dedup_apply: %zu files exceed 2^31 - 1", n);
   DevCall call(c, stream);
   if (call.rc) return call.rc;
-  hipError_t e = dd_apply(d_ids, d_slot, (uint32_t)n, d_result, chunk_size ? chunk_size : SDCAS_IDENTIFIER_CHUNK_SIZE,
+  hipError_t e = dd_apply(c->dist, d_ids, d_slot, (uint32_t)n, d_result, chunk_size ? chunk_size : SDCAS_IDENTIFIER_CHUNK_SIZE,
                           d_plan, d_link, (unsigned long long*)d_counts, call.st);
   return e ? c->hip_fail(e, "dedup_apply") : SDCAS_OK;
 }

@@ -1,7 +1,9 @@
 #!/bin/bash
 # round 5 (j): the GPU suite and smoke at HEAD, then the job's row writes
 # batched (set_cas_ids_and_connect: 64 rows per UPDATE ... FROM (VALUES ...))
-# against one statement per row (SDCORE_LINKS=each), alternating processes
+# against one statement per row (SDCORE_LINKS=each), alternating processes;
+# the world-8 stages with the bucket apply at 4 files per thread against
+# round 5's grid-stride apply (SDCAS_APPLY_R=0), same process
 set -o pipefail
 cd "$(dirname "$0")/.."
 OUT=${1:-gpurun_out/r05j}
@@ -16,5 +18,9 @@ for rep in 1 2 3; do
       > $OUT/job_${mode}_$rep.json 2> $OUT/job_${mode}_$rep.err || exit 1
     echo "job $mode rep $rep ok"
   done
+done
+for w in c5 c3; do
+  timeout -k 10 300 python -u tools/dedup_probe.py --workload $w --world 8 --reps 20 \
+    --ab "SDCAS_APPLY_R=0,SDCAS_APPLY_R=4" > $OUT/probe_${w}_w8_apply.json 2> $OUT/probe_${w}_w8_apply.err || exit 1
 done
 echo done
