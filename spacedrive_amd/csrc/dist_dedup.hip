@@ -31,6 +31,7 @@ namespace {
 constexpr uint32_t TB = 256;
 constexpr int64_t kLinkDeferred = INT64_MIN + 1;  // SDCAS_LINK_DEFERRED
 inline uint32_t blocks(uint32_t n) { return (n + TB - 1) / TB; }
+constexpr uint32_t kIdxEmpty = 0xFFFFFFFFu;
 constexpr uint32_t kCountShards = 64;  // the apply's count pairs (a workgroup adds to blockIdx % 64)
 
 // ---- the steps' positions (see dist_dedup.h, "the job's steps") -------------------
@@ -766,11 +767,113 @@ __global__ void k_rb_answer(const uint32_t* __restrict__ pos, uint32_t total, co
   result[q] = e != ~0ull ? -(int64_t)e - 1 : (int64_t)tab[2 * (uint64_t)h + 1];
 }
 
-// SDCAS_RESOLVE=split: round 4's resolve (key array + minima pairs sized from
-// the buckets' capacity; A/B)
-static bool resolve_split() {
+// The owner's table in its compact form (the default): one u32 per slot, the
+// index of the record that claimed the key (file records 0..nf, existing
+// records nf + j), the key read back through it; the claim is the key's only
+// atomic, and every other record of the key folds its value into a side
+// minimum (vmin for files, emin for existing Objects) — one atomic per record
+// instead of the claim's CAS plus its atomicMin, which put the 16-byte table
+// at the chip's atomic rate (C5 at world 8: 6.1 M atomics, 269 us). The
+// claimer's own value is its record's, read back by the others through the
+// table (a claimer marks its slot in tpos and reads only the minimum). A
+// plain store of the claimer's value beside the minima cost the insert more
+// than it saved the answer (C5 at world 8: +50 / -4 us). Existing records
+// are inserted first, so a key with any existing Object has one as its
+// claimer.
+// a file record's slot in tpos carries this bit when the record claimed it
+// (slots stay below 2^31: the table takes at most 2^30 + 1 entries here)
+constexpr uint32_t kPosClaimed = 1u << 31;
+
+__device__ __forceinline__ const uint64_t* rb_rec(const uint64_t* frec, const uint64_t* erec, uint32_t nf,
+                                                  uint32_t x) {
+  return x < nf ? frec + 2 * (uint64_t)x : erec + 2 * (uint64_t)(x - nf);
+}
+
+__global__ void k_rb_insert_idx(const uint64_t* __restrict__ frec, const uint64_t* __restrict__ erec, uint32_t nf,
+                                uint32_t bcap, const int64_t* __restrict__ counts, uint32_t total, uint32_t base,
+                                uint32_t* __restrict__ tab, unsigned long long* __restrict__ vmin,
+                                const uint32_t* __restrict__ cfg, uint32_t* __restrict__ pos_out) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= total) return;
+  const uint32_t r = q / bcap, p = q - r * bcap;
+  if ((int64_t)p >= counts[r]) {
+    if (pos_out) pos_out[q] = kNoEntry;
+    return;
+  }
+  const uint32_t mask = cfg[0], shift = cfg[1];
+  const uint32_t x = base + q;
+  const uint64_t* me = rb_rec(frec, erec, nf, x);
+  const uint64_t key = me[0];
+  uint32_t h = mask + 1;  // the all-ones key's own entry
+  bool claimed = false;
+  if (key != kEmptyKey) {
+    h = (uint32_t)((key << kOwnerBits) >> shift) & mask;  // below the owner bits (ht_find)
+    for (;;) {
+      uint32_t cur = __hip_atomic_load(&tab[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cur == kIdxEmpty) {
+        cur = atomicCAS(&tab[h], kIdxEmpty, x);
+        if (cur == kIdxEmpty) {
+          claimed = true;
+          break;
+        }
+      }
+      if (rb_rec(frec, erec, nf, cur)[0] == key) break;
+      h = (h + 1) & mask;
+    }
+  } else {
+    claimed = atomicCAS(&tab[h], kIdxEmpty, x) == kIdxEmpty;
+  }
+  if (!claimed) {
+    const unsigned long long v = me[1];
+    unsigned long long* m = &vmin[h];
+    if (__hip_atomic_load(m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > v) atomicMin(m, v);
+  }
+  if (pos_out) pos_out[q] = h | (claimed ? kPosClaimed : 0u);
+}
+
+__global__ void k_rb_answer_idx(const uint32_t* __restrict__ pos, uint32_t nf, const uint64_t* __restrict__ frec,
+                                const uint64_t* __restrict__ erec, const uint32_t* __restrict__ tab,
+                                const uint64_t* __restrict__ vmin, const uint64_t* __restrict__ emin,
+                                int64_t* __restrict__ result) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nf) return;
+  const uint32_t hp = pos[q];
+  if (hp == kNoEntry) return;  // padding: nobody reads its answer
+  const uint32_t h = hp & ~kPosClaimed;
+  // the claimer knows its own value (a file claimer: no existing Object has
+  // the key); another record reads the claimer's through the table
+  const uint32_t c = (hp & kPosClaimed) ? q : tab[h];
+  const uint64_t own = rb_rec(frec, erec, nf, c)[1];
+  // mod.rs:202-238: the first existing Object carrying the key (a key with
+  // one has an existing record as its claimer); else the key's first file
+  // (mod.rs:246-254)
+  if (c >= nf) {
+    const uint64_t e = emin[h] < own ? emin[h] : own;
+    result[q] = -(int64_t)e - 1;
+  } else {
+    result[q] = (int64_t)(vmin[h] < own ? vmin[h] : own);
+  }
+}
+
+__global__ void k_rb_clear_idx(uint32_t* __restrict__ tab, unsigned long long* __restrict__ vmin,
+                               unsigned long long* __restrict__ emin, const uint32_t* __restrict__ cfg) {
+  const uint64_t m = (uint64_t)cfg[0] + 2;
+  for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < m; q += (uint64_t)gridDim.x * blockDim.x) {
+    tab[q] = kIdxEmpty;
+    vmin[q] = ~0ull;
+    if (emin) emin[q] = ~0ull;
+  }
+}
+
+// SDCAS_RESOLVE: "idx" (the default, above), "kv" = round 5's 16-byte (key,
+// files' minimum) entries sized on the device, "split" = round 4's key array
+// + minima pairs sized from the buckets' capacity (A/B)
+enum ResolveTable { kResolveIdx = 0, kResolveKv = 1, kResolveSplit = 2 };
+static ResolveTable resolve_table() {
   const char* v = getenv("SDCAS_RESOLVE");
-  return v && strcmp(v, "split") == 0;
+  if (v && strcmp(v, "split") == 0) return kResolveSplit;
+  if (v && strcmp(v, "kv") == 0) return kResolveKv;
+  return kResolveIdx;
 }
 
 hipError_t dd_resolve_buckets(DistWs& w, const uint64_t* frec, uint32_t fcap, const int64_t* fcounts,
@@ -782,7 +885,31 @@ hipError_t dd_resolve_buckets(DistWs& w, const uint64_t* frec, uint32_t fcap, co
   uint64_t cap = 1024;
   while (cap < 2 * ((uint64_t)nf + ne)) cap <<= 1;
   if (cap > (1ull << 31)) return hipErrorInvalidValue;
-  if (!resolve_split()) {
+  ResolveTable rt = resolve_table();
+  if (rt == kResolveIdx && cap > (1ull << 30)) rt = kResolveKv;  // tpos' claimed bit needs slots below 2^31
+  if (rt == kResolveIdx) {
+    // tmin holds the u32 table (cap + 1 u32 in its first cap + 1 u64) and
+    // the existing minima; tkey the files' minima
+    if ((e = w.tmin.ensure(2 * (cap + 1))) || (e = w.tkey.ensure(cap + 1)) || (e = w.tpos.ensure(nf)) ||
+        (e = w.starts.ensure(2)))
+      return e;
+    auto* tab = reinterpret_cast<uint32_t*>(w.tmin.p);
+    auto* vm = reinterpret_cast<unsigned long long*>(w.tkey.p);
+    auto* em = ne ? reinterpret_cast<unsigned long long*>(w.tmin.p + (cap + 1)) : nullptr;
+    hipLaunchKernelGGL(k_rb_size, dim3(1), dim3(64), 0, st, fcounts, ne ? ecounts : nullptr, world, w.starts.p);
+    const uint64_t slots = cap + 1;
+    const uint32_t cg = (uint32_t)std::min<uint64_t>((slots + TB - 1) / TB, 2048);
+    hipLaunchKernelGGL(k_rb_clear_idx, dim3(cg), dim3(TB), 0, st, tab, vm, em, w.starts.p);
+    if (ne)
+      hipLaunchKernelGGL(k_rb_insert_idx, dim3(blocks(ne)), dim3(TB), 0, st, frec, erec, nf, ecap, ecounts, ne, nf,
+                         tab, em, w.starts.p, (uint32_t*)nullptr);
+    hipLaunchKernelGGL(k_rb_insert_idx, dim3(blocks(nf)), dim3(TB), 0, st, frec, erec, nf, fcap, fcounts, nf, 0u, tab,
+                       vm, w.starts.p, w.tpos.p);
+    hipLaunchKernelGGL(k_rb_answer_idx, dim3(blocks(nf)), dim3(TB), 0, st, w.tpos.p, nf, frec, erec, tab, w.tkey.p,
+                       (const uint64_t*)em, result);
+    return hipGetLastError();
+  }
+  if (rt == kResolveKv) {
     // cap bounds the table the valid counts ask for; allocate that, clear what they ask
     if ((e = w.tmin.ensure(2 * (cap + 1))) || (ne && (e = w.tkey.ensure(cap + 1))) || (e = w.tpos.ensure(nf)) ||
         (e = w.starts.ensure(2)))
@@ -901,7 +1028,6 @@ __global__ void k_solo_apply(const uint64_t* __restrict__ ids, const uint32_t* _
 // are ascending, so the lowest file index has the lowest ordinal). Existing
 // Objects fold their DB index into a u64 side array (emin) by slot, which
 // exists only when there are existing Objects.
-constexpr uint32_t kIdxEmpty = 0xFFFFFFFFu;
 
 __device__ __forceinline__ uint64_t idx_key(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ ekeys,
                                             uint32_t n, uint32_t x) {

@@ -637,22 +637,24 @@ def test_meta_group_of_a_subgroup():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("combine", ["hash", "hash-split", "hash-r0", "hash-r1"])
+@pytest.mark.parametrize("combine", ["hash", "hash-kv", "hash-split", "hash-r0", "hash-r1"])
 @pytest.mark.parametrize("R,chunk_size", [(2, 100), (8, 100), (5, 7)])
 def test_device_bucket_protocol_vs_oracle(eng, oracle, R, chunk_size, combine, monkeypatch):
     """the bucket protocol's device stages (combine_buckets -> equal-split
     exchange -> resolve_buckets -> apply) over R virtual ranks with existing
     Objects, the hash-table combine and every resolve: the owner's resolve
-    in a table sized on the device from the valid counts (the default) and
-    round 4's sized from the buckets' capacity (SDCAS_RESOLVE=split); the
+    in a u32 table of claiming record indices sized on the device from the
+    valid counts (the default), round 5's 16-byte (key, minimum) entries
+    (SDCAS_RESOLVE=kv) and round 4's tables sized from the buckets' capacity
+    (SDCAS_RESOLVE=split); the
     apply with 4 files per thread (the default), round 5's grid-stride apply
     (SDCAS_APPLY_R=0) and one file per thread (1); then buckets one record too
     small, which must raise the overflow flag (the caller then reruns the
     exact stages)"""
     from spacedrive_amd.dist_dedup import DeviceStages
     from tests._dist_stages import dedup_virtual_buckets
-    if combine == "hash-split":
-        monkeypatch.setenv("SDCAS_RESOLVE", "split")
+    if combine in ("hash-split", "hash-kv"):
+        monkeypatch.setenv("SDCAS_RESOLVE", combine[len("hash-"):])
     elif combine.startswith("hash-r"):
         monkeypatch.setenv("SDCAS_APPLY_R", combine[len("hash-r"):])
     keys, has, status, existing = make_corpus(700 + R, 24000, pool=5000, p_none=0.05, p_err=0.05)
