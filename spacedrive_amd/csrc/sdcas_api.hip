@@ -706,6 +706,8 @@ int sdcas_init(const sdcas_options* opts, sdcas_ctx** out) {
   if (const char* e = getenv("SDCAS_SMALL_VARIANT")) c->ws.small_variant = atoi(e);
   if (const char* e = getenv("SDCAS_UPLOAD_PARTS")) c->upload_parts = (uint32_t)std::min(atoi(e) > 0 ? atoi(e) : 0, 16);
   if (const char* e = getenv("SDCAS_PLAN_SMALL")) c->plan_small = atoi(e) != 0;
+  // pinned staging per slot in MiB, over the caller's choice (A/B runs)
+  if (const char* e = getenv("SDCAS_STAGING_MB"); e && atoi(e) > 0) c->staging_bytes = (uint64_t)atoi(e) << 20;
   c->device = dev;
   if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess) {
