@@ -14,7 +14,7 @@ import os
 import re
 import sys
 
-HASH = ("k_leaf_tree", "k_finish_t", "k_tile_first", "k_shape_", "k_synth_cas_messages")
+HASH = ("k_leaf_tree", "k_finish_t", "k_finish_q", "k_tile_first", "k_plan_", "k_shape_", "k_synth_cas_messages")
 
 
 def short(name):
@@ -35,7 +35,11 @@ def after_hash(rs):
     """the dispatches after the hash's last kernel, up to the last dedup
     apply (the probe's read-back copies after it are not the dedup's)"""
     rs = sorted(rs, key=lambda r: int(r["Dispatch_Id"]))
-    last = max((int(r["Dispatch_Id"]) for r in rs if any(h in r["Kernel_Name"] for h in HASH)), default=-1)
+    # the hash's kernels before the first dedup insert (a later hash, e.g. a
+    # parity check after the calls, is not the boundary)
+    first = min((int(r["Dispatch_Id"]) for r in rs if "insert" in r["Kernel_Name"]), default=1 << 62)
+    last = max((int(r["Dispatch_Id"]) for r in rs
+                if any(h in r["Kernel_Name"] for h in HASH) and int(r["Dispatch_Id"]) < first), default=-1)
     end = max((int(r["Dispatch_Id"]) for r in rs if "apply" in r["Kernel_Name"]), default=1 << 62)
     return [r for r in rs if last < int(r["Dispatch_Id"]) <= end]
 
