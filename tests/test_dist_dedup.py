@@ -658,6 +658,11 @@ def test_device_bucket_protocol_vs_oracle(eng, oracle, R, chunk_size, combine, m
     elif combine.startswith("hash-r"):
         monkeypatch.setenv("SDCAS_APPLY_R", combine[len("hash-r"):])
     keys, has, status, existing = make_corpus(700 + R, 24000, pool=5000, p_none=0.05, p_err=0.05)
+    # the all-ones key (the tables' empty marker, a legal cas key) on several
+    # files and ranks, once with an existing Object
+    keys[[5, 4000, 17000]] = np.uint64(2**64 - 1)
+    if chunk_size == 100:
+        existing = np.concatenate([existing, np.array([2**64 - 1], np.uint64)])
     want, wc, wl = oracle.identifier_dedup(keys, has, status, chunk_size, existing)
     shards, ex = shard(keys, has, status, existing, R, device="cuda")
     st = DeviceStages(eng)
