@@ -49,6 +49,7 @@ struct DistWs {
   Buf<uint32_t> tpos;        // table entry of each received file record
   Buf<uint32_t> stay_idx, nstay;  // the batch's stay-orphan rows (dd_local's plan)
   Buf<uint32_t> stay_cnt;         // per-tile stays counts (select_stays, the fused insert, the bitmap)
+  Buf<uint32_t> flag;              // the fused insert's non-contiguous-ordinals flag
   Buf<unsigned long long> shard;  // the applies' (created, linked) counts, kCountShards pairs (kept zeroed)
   Buf<uint64_t> plan, stay_sorted;
   Buf<uint32_t> bitmap;           // dd_plan: the stays ordinals of a long gathered list

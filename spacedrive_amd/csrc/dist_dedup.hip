@@ -454,7 +454,8 @@ __global__ void k_solo_insert_idx(const uint64_t* __restrict__ keys, const uint6
                                   const uint8_t* __restrict__ has_key, const int32_t* __restrict__ status,
                                   const uint64_t* __restrict__ eids, uint32_t count, uint32_t base,
                                   uint32_t* __restrict__ tab, unsigned long long* __restrict__ emin, uint32_t mask,
-                                  uint32_t shift, uint32_t* __restrict__ pos, uint32_t* __restrict__ stay_cnt);
+                                  uint32_t shift, uint32_t* __restrict__ pos, uint32_t* __restrict__ stay_cnt,
+                                  uint32_t* __restrict__ noncontig);
 
 // ---- the combine through a hash table ----------------------------------------------
 //
@@ -1038,15 +1039,24 @@ __device__ __forceinline__ uint64_t idx_key(const uint64_t* __restrict__ keys, c
 // one; existing Objects (emin set, base n): min-fold eids[j] into emin[slot]
 // stay_cnt (files, may be null): += the rows of each 1024-row tile that stay
 // orphans, one atomicAdd per wave holding one
+// noncontig (files, may be null; eids = the files' ordinals then): set when
+// some file's ordinal is not eids[0] + its index (one atomicOr per wave
+// that finds one), so that the apply can take a key's first ordinal from its
+// index instead of reading it
 __global__ void k_solo_insert_idx(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ ekeys, uint32_t n,
                                   const uint8_t* __restrict__ has_key, const int32_t* __restrict__ status,
                                   const uint64_t* __restrict__ eids, uint32_t count, uint32_t base,
                                   uint32_t* __restrict__ tab, unsigned long long* __restrict__ emin, uint32_t mask,
-                                  uint32_t shift, uint32_t* __restrict__ pos, uint32_t* __restrict__ stay_cnt) {
+                                  uint32_t shift, uint32_t* __restrict__ pos, uint32_t* __restrict__ stay_cnt,
+                                  uint32_t* __restrict__ noncontig) {
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= count) return;
   const uint32_t x = base + q;
   if (!emin) {
+    if (noncontig) {
+      const uint64_t bad = __ballot(eids[q] != eids[0] + q);
+      if (bad && (threadIdx.x & 63) == (uint32_t)(__ffsll((long long)bad) - 1)) atomicOr(noncontig, 1u);
+    }
     const bool ok = status == nullptr || status[q] == 0;  // mod.rs:125-141
     const bool has = has_key == nullptr || has_key[q];    // mod.rs:83-86
     if (stay_cnt) {
@@ -1129,13 +1139,14 @@ constexpr uint32_t kStayTile = 1024;  // rows per stays count (a multiple of the
 
 
 __global__ void k_local_clear(uint4* __restrict__ tab, uint64_t tab_q, uint4* __restrict__ em, uint64_t em_q,
-                              uint32_t* __restrict__ cnt, uint32_t nt) {
+                              uint32_t* __restrict__ cnt, uint32_t nt, uint32_t* __restrict__ flag) {
   const uint4 ones = make_uint4(~0u, ~0u, ~0u, ~0u);
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   for (uint64_t q = t0; q < tab_q; q += stride) tab[q] = ones;
   for (uint64_t q = t0; q < em_q; q += stride) em[q] = ones;
   for (uint64_t q = t0; q < nt; q += stride) cnt[q] = 0;
+  if (flag && t0 == 0) *flag = 0;
 }
 
 // The apply with R files per thread, each phase's loads issued for all R
@@ -1151,11 +1162,15 @@ __global__ void __launch_bounds__(TB) k_solo_apply_r(const uint64_t* __restrict_
                                                      const uint32_t* __restrict__ tab,
                                                      const uint64_t* __restrict__ emin, uint64_t cs,
                                                      const uint64_t* __restrict__ plan, int64_t* __restrict__ link,
-                                                     unsigned long long* __restrict__ shard) {
+                                                     unsigned long long* __restrict__ shard,
+                                                     const uint32_t* __restrict__ noncontig) {
   __shared__ unsigned long long sc[2];
   if (threadIdx.x < 2) sc[threadIdx.x] = 0;
   __syncthreads();
   const PlanView pv = plan_view(plan);
+  // ordinals eids[0] + index (the insert found no other): a key's first
+  // ordinal follows from its first file's index, no read
+  const bool contig = noncontig && *noncontig == 0;
   const uint64_t i0 = (uint64_t)blockIdx.x * TB * R + threadIdx.x;
   uint32_t h[R], f[R];
   uint64_t e[R], r[R], me[R];
@@ -1177,7 +1192,9 @@ __global__ void __launch_bounds__(TB) k_solo_apply_r(const uint64_t* __restrict_
     const bool keyed = h[k] < kSlotDropped && h[k] != kSlotNoKey;
     // mod.rs:202-238: the first existing Object; else (mod.rs:246-254) the
     // key's first file — a file, as this one carries the key
-    r[k] = !keyed || e[k] != ~0ull || f[k] == (uint32_t)i ? me[k] : ids[f[k]];
+    r[k] = !keyed || e[k] != ~0ull || f[k] == (uint32_t)i ? me[k]
+           : contig                                           ? me[k] - i + f[k]
+                                                              : ids[f[k]];
   }
   unsigned long long c = 0, l = 0;
 #pragma unroll
@@ -1269,6 +1286,12 @@ static uint32_t apply_files_per_thread() {
   return x == 0 || x == 1 || x == 2 || x == 4 || x == 8 ? (uint32_t)x : 4u;
 }
 
+// SDCAS_CONTIG=0: the world-of-one apply reads every first ordinal (A/B)
+static bool contig_ordinals() {
+  const char* v = getenv("SDCAS_CONTIG");
+  return !(v && strcmp(v, "0") == 0);
+}
+
 // the applies' count shards: zeroed when allocated, and by k_counts_fold
 // after every use
 static hipError_t shard_counts(DistWs& w, hipStream_t st) {
@@ -1301,22 +1324,25 @@ static hipError_t local_fused(DistWs& w, const uint64_t* keys, const uint8_t* ha
   // the existing Objects' minima live in tkey (cap u64), when there are any
   const uint32_t ar = apply_files_per_thread();
   const bool sharded = ar && counts;
+  const bool contig = ar && contig_ordinals() && n > 0;
   if ((e = w.tmin.ensure(cap / 2 + 1)) || (e = w.tpos.ensure(n)) || (ne && (e = w.tkey.ensure(cap + 1))) ||
-      (e = w.stay_cnt.ensure(nt + 1)) || (stays && (e = w.stay_idx.ensure(n))) || (sharded && (e = shard_counts(w, st))))
+      (e = w.stay_cnt.ensure(nt + 1)) || (stays && (e = w.stay_idx.ensure(n))) || (sharded && (e = shard_counts(w, st))) ||
+      (contig && (e = w.flag.ensure(1))))
     return e;
   auto* tab = reinterpret_cast<uint32_t*>(w.tmin.p);
   auto* em = ne ? reinterpret_cast<unsigned long long*>(w.tkey.p) : nullptr;
   const uint64_t tab_q = cap / 4, em_q = ne ? cap / 2 : 0;  // uint4 stores (cap >= 1024)
   const uint32_t cg = (uint32_t)std::min<uint64_t>((tab_q + em_q + TB - 1) / TB, 2048);
   hipLaunchKernelGGL(k_local_clear, dim3(cg), dim3(TB), 0, st, reinterpret_cast<uint4*>(tab), tab_q,
-                     reinterpret_cast<uint4*>(em), em_q, w.stay_cnt.p, stays ? nt : 0u);
+                     reinterpret_cast<uint4*>(em), em_q, w.stay_cnt.p, stays ? nt : 0u,
+                     contig ? w.flag.p : (uint32_t*)nullptr);
   if (ne)
     hipLaunchKernelGGL(k_solo_insert_idx, dim3(blocks(ne)), dim3(TB), 0, st, keys, ekeys, n, (const uint8_t*)nullptr,
                        (const int32_t*)nullptr, eids, ne, n, tab, em, mask, shift, (uint32_t*)nullptr,
-                       (uint32_t*)nullptr);
+                       (uint32_t*)nullptr, (uint32_t*)nullptr);
   hipLaunchKernelGGL(k_solo_insert_idx, dim3(blocks(n)), dim3(TB), 0, st, keys, ekeys, n, has_key, status,
-                     (const uint64_t*)nullptr, n, 0u, tab, (unsigned long long*)nullptr, mask, shift, w.tpos.p,
-                     stays ? w.stay_cnt.p : (uint32_t*)nullptr);
+                     contig ? ids : (const uint64_t*)nullptr, n, 0u, tab, (unsigned long long*)nullptr, mask, shift,
+                     w.tpos.p, stays ? w.stay_cnt.p : (uint32_t*)nullptr, contig ? w.flag.p : (uint32_t*)nullptr);
   if (stays)
     hipLaunchKernelGGL(k_stays_write_t<kStayTile>, dim3(nt), dim3(TB), 0, st, has_key, status, n, w.stay_cnt.p,
                        w.stay_idx.p);
@@ -1327,7 +1353,7 @@ static hipError_t local_fused(DistWs& w, const uint64_t* keys, const uint8_t* ha
   auto apply = [&](auto kern, uint32_t r) {
     const uint32_t g = (uint32_t)(((uint64_t)n + (uint64_t)TB * r - 1) / ((uint64_t)TB * r));
     if (g) hipLaunchKernelGGL(kern, dim3(g), dim3(TB), 0, st, ids, w.tpos.p, n, tab, emp, cs, w.plan.p, link,
-                              sharded ? w.shard.p : nullptr);
+                              sharded ? w.shard.p : nullptr, contig ? (const uint32_t*)w.flag.p : nullptr);
   };
   switch (ar) {
     case 1: apply(k_solo_apply_r<1>, 1); break;
@@ -1529,10 +1555,10 @@ hipError_t dd_local(DistWs& w, const uint64_t* keys, const uint8_t* has_key, con
     if (ne)
       hipLaunchKernelGGL(k_solo_insert_idx, dim3(blocks(ne)), dim3(TB), 0, st, keys, ekeys, n,
                          (const uint8_t*)nullptr, (const int32_t*)nullptr, eids, ne, n, tab, em, mask, shift,
-                         (uint32_t*)nullptr, (uint32_t*)nullptr);
+                         (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr);
     hipLaunchKernelGGL(k_solo_insert_idx, dim3(blocks(n)), dim3(TB), 0, st, keys, ekeys, n, has_key, status,
                        (const uint64_t*)nullptr, n, 0u, tab, (unsigned long long*)nullptr, mask, shift, w.tpos.p,
-                       (uint32_t*)nullptr);
+                       (uint32_t*)nullptr, (uint32_t*)nullptr);
     hipLaunchKernelGGL(k_solo_apply_idx, dim3(blocks(n) < 1024 ? blocks(n) : 1024), dim3(TB), 0, st, ids, w.tpos.p, n,
                        tab, ne ? w.tkey.p : nullptr, chunk_size, w.plan.p, link, counts);
     return hipGetLastError();
@@ -1600,7 +1626,7 @@ static hipError_t combine_table(DistWs& w, const uint64_t* keys, const uint8_t* 
     return e;
   hipLaunchKernelGGL(k_solo_insert_idx, dim3(blocks(n)), dim3(TB), 0, st, keys, (const uint64_t*)nullptr, n, has_key,
                      status, (const uint64_t*)nullptr, n, 0u, w.idx_a.p, (unsigned long long*)nullptr, mask, shift,
-                     w.idx_b.p, (uint32_t*)nullptr);
+                     w.idx_b.p, (uint32_t*)nullptr, (uint32_t*)nullptr);
   return hipGetLastError();
 }
 

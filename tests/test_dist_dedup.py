@@ -362,7 +362,7 @@ def test_rccl_world1(eng, oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("table", ["idx", "idx-r0", "idx-r1", "idx-r8", "idx4", "kv"])
+@pytest.mark.parametrize("table", ["idx", "idx-r0", "idx-r1", "idx-r8", "idx-c0", "idx4", "kv"])
 @pytest.mark.parametrize("corpus,chunk_size", [("default", 100), ("default", 7), ("default", 1),
                                                ("collisions", 100), ("clustered", 100)])
 def test_device_local_vs_oracle(eng, oracle, corpus, chunk_size, table, monkeypatch):
@@ -372,7 +372,8 @@ def test_device_local_vs_oracle(eng, oracle, corpus, chunk_size, table, monkeypa
     insert also counts the stays rows per 1024-row tile, five launches),
     the same table behind round 4's eight launches, round 3's 16-byte kv
     table; the default table's apply with 0 (the grid-stride form), 1 and 8
-    files per thread beside the default 4 (`idx-rN`, SDCAS_APPLY_R); and the
+    files per thread beside the default 4 (`idx-rN`, SDCAS_APPLY_R), every
+    first ordinal read instead of taken from the index (`idx-c0`); and the
     existing Objects passed in DB order and shuffled (their DB indices then
     not ascending: the first Object is the lowest DB index, not the first
     entry)"""
@@ -380,7 +381,7 @@ def test_device_local_vs_oracle(eng, oracle, corpus, chunk_size, table, monkeypa
     table, _, knob = table.partition("-")
     monkeypatch.setenv("SDCAS_DEDUP_TABLE", table)
     if knob:
-        monkeypatch.setenv("SDCAS_APPLY_R", knob[1:])
+        monkeypatch.setenv({"r": "SDCAS_APPLY_R", "c": "SDCAS_CONTIG"}[knob[0]], knob[1:])
     if corpus == "default":
         keys, has, status, existing = make_corpus(91, 40000, pool=6000)
         keys[:2] = np.uint64(2**64 - 1)  # the table's empty marker is a legal key
@@ -446,6 +447,34 @@ def _plan_cases(count, seed0=0):
                                 (int(rng.integers(1, 2 * n + 2)), True), (0, True)):
             yield keys, has, status, existing, cs, max_steps, more
 
+
+
+@pytest.mark.gpu
+def test_device_local_ordinals_not_contiguous(eng, oracle, monkeypatch):
+    """the fused apply takes a key's first ordinal from its first file's index
+    only when every ordinal is ids[0] + index: offset ordinals (a rank's
+    share) take the shortcut, one moved ordinal must send the apply back to
+    reading them (checked against the reading path, SDCAS_CONTIG=0)"""
+    from spacedrive_amd.dist_dedup import DeviceStages
+    keys, has, status, existing = make_corpus(17, 30000, pool=3000)
+    (k, h, s, ids), = shard(keys, has, status, existing, 1, device="cuda")[0]
+    st = DeviceStages(eng)
+    # a first file of a duplicated key: its ordinal is what its key's other files link to
+    _, first, counts = np.unique(keys, return_index=True, return_counts=True)
+    f = int(first[np.argmax(counts)])
+    for name, d_ids in (("offset", ids + 1000), ("moved", ids.clone())):
+        if name == "moved":
+            d_ids[f] += 5
+        monkeypatch.setenv("SDCAS_CONTIG", "1")
+        got, gc = st.local(k, h, s, d_ids, 100)
+        got = got.cpu().numpy().copy()
+        monkeypatch.setenv("SDCAS_CONTIG", "0")
+        ref, rc = st.local(k, h, s, d_ids, 100)
+        assert np.array_equal(got, ref.cpu().numpy()), name
+        assert gc.tolist() == rc.tolist(), name
+    want, _, _ = oracle.identifier_dedup(keys, has, status, 100, np.zeros(0, np.uint64))
+    got, _ = st.local(k, h, s, ids, 100)
+    assert np.array_equal(got.cpu().numpy(), want)
 
 @pytest.mark.gpu
 def test_device_step_plan_matches_literal_step_loop(eng, oracle):
