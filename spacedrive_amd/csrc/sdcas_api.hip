@@ -9,6 +9,7 @@
 // path: every digest this library returns comes from the HIP kernels.
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -80,6 +81,7 @@ struct DevBuf {
 struct Slot {
   uint8_t* h = nullptr;   // pinned message bytes
   size_t h_cap = 0;
+  bool h_mapped = false;  // h is an mmap'd, hipHostRegister'ed range (SDCAS_STAGING_THP)
   uint64_t* hm = nullptr;  // pinned: offs[cap_n] | lens[cap_n] | results (32 B per message)
   size_t cap_n = 0;
   DevBuf<uint8_t> d_blob;
@@ -360,14 +362,56 @@ int launch_batch(sdcas_ctx* c, const uint8_t* blob, const uint64_t* offs, const 
 // kernels and D2H are enqueued on the context stream and fenced by the slot's
 // event, which is waited for only when the slot is about to be refilled.
 
+// The message slots are anonymous mappings advised to transparent huge
+// pages and then pinned (hipHostRegister): the readers' page-cache copies
+// into a slot walk 2 MiB pages instead of hipHostMalloc's 4 KiB ones
+// (profiles/r05_staging_thp_ab.json). A mapping or registration that fails
+// falls back to hipHostMalloc; SDCAS_STAGING_THP=0 always takes it (A/B).
+static bool staging_thp() {
+  static const bool on = [] {
+    const char* v = getenv("SDCAS_STAGING_THP");
+    return !(v && strcmp(v, "0") == 0);
+  }();
+  return on;
+}
+
+static void free_staging(Slot& s) {
+  if (!s.h) return;
+  if (s.h_mapped) {
+    (void)hipHostUnregister(s.h);
+    munmap(s.h, s.h_cap);
+  } else {
+    (void)hipHostFree(s.h);
+  }
+  s.h = nullptr;
+  s.h_cap = 0;
+  s.h_mapped = false;
+}
+
 int slot_prepare(sdcas_ctx* c, Slot& s, uint64_t bytes, size_t n) {
   hipError_t e;
   if (bytes + kSlack > s.h_cap) {
-    if (s.h) (void)hipHostFree(s.h);
-    s.h = nullptr;
-    s.h_cap = 0;
-    if ((e = hipHostMalloc(&s.h, bytes + kSlack, hipHostMallocDefault))) return c->hip_fail(e, "pinned staging");
-    s.h_cap = bytes + kSlack;
+    free_staging(s);
+    const size_t want = bytes + kSlack;
+    if (staging_thp()) {
+      const size_t huge = 2u << 20, len = (want + huge - 1) / huge * huge;
+      void* p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+      if (p != MAP_FAILED) {
+        (void)madvise(p, len, MADV_HUGEPAGE);
+        if (hipHostRegister(p, len, hipHostRegisterDefault) == hipSuccess) {
+          s.h = static_cast<uint8_t*>(p);
+          s.h_cap = len;
+          s.h_mapped = true;
+        } else {
+          (void)hipGetLastError();  // the fallback below; not this call's error
+          munmap(p, len);
+        }
+      }
+    }
+    if (!s.h) {
+      if ((e = hipHostMalloc(&s.h, want, hipHostMallocDefault))) return c->hip_fail(e, "pinned staging");
+      s.h_cap = want;
+    }
   }
   if (n > s.cap_n) {
     if (s.hm) (void)hipHostFree(s.hm);
@@ -386,11 +430,10 @@ int slot_prepare(sdcas_ctx* c, Slot& s, uint64_t bytes, size_t n) {
 }
 
 void slot_release(Slot& s) {
-  if (s.h) (void)hipHostFree(s.h);
+  free_staging(s);
   if (s.hm) (void)hipHostFree(s.hm);
-  s.h = nullptr;
   s.hm = nullptr;
-  s.h_cap = s.cap_n = 0;
+  s.cap_n = 0;
   s.d_blob.release();
   s.d_meta.release();
   s.d_res.release();
@@ -1126,6 +1169,14 @@ int sdcas_cas_ids_from_messages(sdcas_ctx* c, const uint8_t* blob, const uint64_
 
 // SDCAS_TRACE_IO=1: per-call wall time of sdcas_cas_ids' phases on stderr
 // (measurement aid for the page-cache path; no effect otherwise)
+static bool last_parts() {
+  static const bool on = [] {
+    const char* v = getenv("SDCAS_LAST_PARTS");
+    return v && strcmp(v, "1") == 0;
+  }();
+  return on;
+}
+
 struct IoTrace {
   bool on = getenv("SDCAS_TRACE_IO") != nullptr;
   double t[5] = {0, 0, 0, 0, 0};  // drain, plan, read, bookkeeping, submit
@@ -1214,8 +1265,10 @@ int sdcas_cas_ids(sdcas_ctx* c, const char* const* paths, const uint64_t* sizes,
       // the flag is set only once every part is enqueued: a failed part
       // returns with it clear, so no later submit of this slot skips an upload
       s.blob_uploaded = false;
-      const bool in_parts = parts > 1 && !other.busy && p == 0 && q == todo.size() && round == 0 &&
-                            used >= kUploadSplitMin && m >= parts;
+      // (and, SDCAS_LAST_PARTS=1, the last slot of a longer call: its upload
+      // is the call's tail, the reads being over when it starts)
+      const bool in_parts = parts > 1 && (!other.busy || last_parts()) && (p == 0 || last_parts()) &&
+                            q == todo.size() && round == 0 && used >= kUploadSplitMin && m >= parts;
       if (in_parts) {
         size_t k0 = 0;
         for (uint32_t part = 1; part <= parts && k0 < m; ++part) {
