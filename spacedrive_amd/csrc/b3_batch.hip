@@ -575,6 +575,10 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
   __shared__ uint32_t sexp[(XT & 2) ? TL / 32 : 1];  // XT 2: slots whose node goes to HBM (phase 4)
   __shared__ uint64_t next_tile;
 
+  // XT bits 3-5 (ablation): that many s_nop at the entry, shifting the
+  // kernel's code by 4-byte steps (code placement A/B, cdna_hip_programming.md
+  // rule 27)
+  if constexpr (((XT >> 3) & 7) != 0) asm volatile(".rept %c0\n s_nop 0\n .endr" ::"i"((XT >> 3) & 7));
   const uint64_t total = *total_p;
   if (total > cap_chunks) return;  // reported by sdcas_dev_sync
   const uint64_t ntiles = (total + TL - 1) / TL;
@@ -1861,6 +1865,10 @@ static const LeafVariant kLeafVariants[] = {
     ABL1(512, k_leaf_tree<512, 279, 1, 1, 2, 2, 0, kTile, 0, 1>),  // 76: 67 with quad tree levels (XT 1)
     ABL1(512, k_leaf_tree<512, 279, 1, 1, 2, 2, 0, kTile, 0, 2>),  // 77: 67 with phase-4 bits (XT 2)
     ABL1(512, k_leaf_tree<512, 279, 1, 1, 2, 2, 0, kTile, 0, 7>),  // 78: 75 with the tree tasks appended per wave (XT 7)
+    ABL1(512, k_leaf_tree<512, 279, 1, 1, 2, 2, 0, kTile, 0, 8>),   // 79-82: 67 with its code shifted by 4, 8, 12, 16 bytes
+    ABL1(512, k_leaf_tree<512, 279, 1, 1, 2, 2, 0, kTile, 0, 16>),  //   (s_nop at the entry: code placement A/B)
+    ABL1(512, k_leaf_tree<512, 279, 1, 1, 2, 2, 0, kTile, 0, 24>),
+    ABL1(512, k_leaf_tree<512, 279, 1, 1, 2, 2, 0, kTile, 0, 32>),
 };
 #undef PROD
 #undef PROD1
