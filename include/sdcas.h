@@ -126,8 +126,10 @@ typedef struct sdcas_options {
 /* "sdcas-mi355x <major>.<minor>.<patch> (gfx950)"; the C ABI of this header is
  * SDCAS_ABI_VERSION (changes: 2 added sdcas_options.progress/cancel; 3 the
  * struct_size field, sdcas_dedup_window and the dedup step plan; 4
- * sdcas_dev_bind_stream) */
-#define SDCAS_ABI_VERSION 4
+ * sdcas_dev_bind_stream; 5 the combine's output contract: one record per
+ * distinct key, any order within an owner's range — same signatures, but a
+ * caller that relied on ABI 4's documented key order must change) */
+#define SDCAS_ABI_VERSION 5
 int sdcas_abi_version(void);
 const char *sdcas_version(void);
 
@@ -326,14 +328,15 @@ int sdcas_dedup(sdcas_ctx *ctx, const uint64_t *keys, const uint8_t *has_key, co
  *   SDCAS_PLAN_WORDS(n_stays)): word 2 the steps run, 3 rows and 8 rereads
  *   (as in sdcas_job_window); the rest is the plan's own (dist_dedup.h).
  * combine: d_ids[n] ascending; d_has_key / d_status may be NULL (all
- *   present / all ok). Writes d_rec[2*u], d_rec[2*u+1] = (cas key, min id)
- *   per key (a key whose top 32 bits another key shares may take more
- *   than one record: resolve's minimum covers all of them; capacity 2*n
- *   u64), records grouped by owner in ascending key order of their top 32
- *   bits, d_slot[i] = record of file i
- *   (0xFFFFFFFF no cas_id, 0xFFFFFFFE dropped; may be NULL), and
- *   out_starts[0..world] (host) = first record of each owner; out_starts[world]
- *   is the record count.
+ *   present / all ok). Writes exactly one record d_rec[2*u], d_rec[2*u+1] =
+ *   (cas key, min id over the files carrying it) per distinct key (capacity
+ *   2*n u64), grouped by owner: owner r's records are d_rec's records
+ *   [out_starts[r], out_starts[r+1]), in NO particular order inside that
+ *   range (ABI 5; ABI 4 and earlier documented ascending top-32-bit order and
+ *   possibly several records per key — do not binary-search or merge the
+ *   ranges); d_slot[i] = record of file i (0xFFFFFFFF no cas_id, 0xFFFFFFFE
+ *   dropped; may be NULL), and out_starts[0..world] (host) = first record of
+ *   each owner; out_starts[world] is the record count.
  * resolve: d_result[p] for received file record p = -(db+1) if existing
  *   Object db carries the key (the first in DB order), else the lowest orphan
  *   ordinal carrying it on any rank.

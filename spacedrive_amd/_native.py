@@ -26,7 +26,7 @@ SDCAS_STATUS_UNEXPECTED_EOF = 100001
 SDCAS_STATUS_CANCELLED = 125
 SDCAS_MAX_BATCH = 0x7FFFFFFF
 SDCAS_OPT_DIRECT_IO = 1
-SDCAS_ABI_VERSION = 4
+SDCAS_ABI_VERSION = 5
 SDCAS_LINK_DROPPED = -(1 << 63)
 SDCAS_LINK_DEFERRED = SDCAS_LINK_DROPPED + 1
 SDCAS_PLAN_HEADER_WORDS = 12

@@ -51,6 +51,7 @@ struct DistWs {
   Buf<uint32_t> stay_cnt;         // per-tile stays counts (select_stays, the fused insert, the bitmap)
   Buf<uint32_t> flag;              // the fused insert's non-contiguous-ordinals flag
   Buf<unsigned long long> shard;  // the applies' (created, linked) counts, kCountShards pairs (kept zeroed)
+  bool shard_dirty = false;       // a failed call may have left partial sums in `shard`: zero before use
   Buf<uint64_t> plan, stay_sorted;
   Buf<uint32_t> bitmap;           // dd_plan: the stays ordinals of a long gathered list
   void release();

@@ -397,7 +397,8 @@ __global__ __launch_bounds__(64) void k_plan_walk(const uint64_t* __restrict__ s
 void DistWs::release() {
   idx_a.release(); idx_b.release(); starts.release(); ocnt.release(); tkey.release(); tmin.release();
   tpos.release(); stay_idx.release(); nstay.release(); stay_cnt.release(); plan.release(); stay_sorted.release();
-  bitmap.release();
+  bitmap.release(); flag.release(); shard.release();
+  shard_dirty = false;
 }
 
 // the combine up to its device outputs: rec, slot, w.starts[0..world] (n > 0)
@@ -1035,10 +1036,27 @@ __device__ __forceinline__ uint64_t idx_key(const uint64_t* __restrict__ keys, c
   return x < n ? keys[x] : ekeys[x - n];
 }
 
+// Rows per stays count of the world-of-one path: the files' insert counts each
+// tile's stays rows (below), the clear zeroes, the stays writer sums and the
+// plan walk reads exactly these tiles, so all four must take this one constant.
+// Round 5's tile-shape experiment changed it to 2048 / 4096 while the insert
+// still counted per literal 1024 rows (gpurun_out/r05dbg/seq_tile_*.log): the
+// counts were allocated and zeroed for ceil(n / 2048) tiles while the insert
+// filled ceil(n / 1024) (past the allocation), the writer placed tile b's rows
+// after the counts of 1024-row tiles 0..b-1 (about half the rows before it, so
+// tiles overwrote each other's entries), and the walk summed only the first
+// ceil(n / 2048) counts; the stays list it walked held misplaced, unordered
+// ordinals, so the plan took re-reads the job never makes and the batch's last
+// rows fell past task_count's limit (file 29994 of 30000 came back
+// SDCAS_LINK_DEFERRED instead of linked to 14).
+constexpr uint32_t kStayTile = 1024;
+static_assert(kStayTile % 64 == 0, "the insert's per-wave ballot add needs a wave's 64 rows in one tile");
+static_assert(kStayTile % TB == 0, "k_stays_write_t walks a tile in whole workgroups");
+
 // files (emin null, base 0): pos[i] = slot, or the code of a file without
 // one; existing Objects (emin set, base n): min-fold eids[j] into emin[slot]
-// stay_cnt (files, may be null): += the rows of each 1024-row tile that stay
-// orphans, one atomicAdd per wave holding one
+// stay_cnt (files, may be null): += the rows of each kStayTile-row tile that
+// stay orphans, one atomicAdd per wave holding one
 // noncontig (files, may be null; eids = the files' ordinals then): set when
 // some file's ordinal is not eids[0] + its index (one atomicOr per wave
 // that finds one), so that the apply can take a key's first ordinal from its
@@ -1062,7 +1080,7 @@ __global__ void k_solo_insert_idx(const uint64_t* __restrict__ keys, const uint6
     if (stay_cnt) {
       const uint64_t bal = __ballot(!(ok && has));
       if (bal && (threadIdx.x & 63) == (uint32_t)(__ffsll((long long)bal) - 1))
-        atomicAdd(&stay_cnt[q / 1024], (uint32_t)__popcll(bal));  // a wave's 64 rows share a tile
+        atomicAdd(&stay_cnt[q / kStayTile], (uint32_t)__popcll(bal));  // a wave's 64 rows share a tile
     }
     if (!(ok && has)) {
       pos[q] = !ok ? kSlotDropped : kSlotNoKey;
@@ -1134,8 +1152,8 @@ __global__ void k_solo_apply_idx(const uint64_t* __restrict__ ids, const uint32_
 // 0.40, the barrier a tile needs holding its workgroup until its slowest
 // probe chain ends; and, without tiles, the files' insert taking 2 or 4
 // files per thread with each probe phase issued for all of them (C5 insert
-// 210 -> 467 us at 4, profiles/r05_ab_dedup_apply.json).
-constexpr uint32_t kStayTile = 1024;  // rows per stays count (a multiple of the wave)
+// 210 -> 467 us at 4, profiles/r05_ab_dedup_apply.json). The tile is
+// kStayTile (defined above the insert, which counts per tile).
 
 
 __global__ void k_local_clear(uint4* __restrict__ tab, uint64_t tab_q, uint4* __restrict__ em, uint64_t em_q,
@@ -1293,11 +1311,21 @@ static bool contig_ordinals() {
 }
 
 // the applies' count shards: zeroed when allocated, and by k_counts_fold
-// after every use
+// after every use; a call whose launches failed between the apply and the
+// fold marks them dirty (sharded_done), and the next call zeroes them first
 static hipError_t shard_counts(DistWs& w, hipStream_t st) {
-  if (w.shard.cap >= 2 * kCountShards) return hipSuccess;
+  if (w.shard.cap >= 2 * kCountShards && !w.shard_dirty) return hipSuccess;
   hipError_t e = w.shard.ensure(2 * kCountShards);
-  return e ? e : hipMemsetAsync(w.shard.p, 0, 2 * kCountShards * sizeof(unsigned long long), st);
+  if (!e) e = hipMemsetAsync(w.shard.p, 0, 2 * kCountShards * sizeof(unsigned long long), st);
+  if (!e) w.shard_dirty = false;
+  return e;
+}
+
+// the end of a call that used the shards: any launch error leaves them dirty
+static hipError_t sharded_done(DistWs& w, bool sharded) {
+  const hipError_t e = hipGetLastError();
+  if (e && sharded) w.shard_dirty = true;
+  return e;
 }
 
 // a world of one's table: a power of two of at least `load` slots per item
@@ -1365,7 +1393,7 @@ static hipError_t local_fused(DistWs& w, const uint64_t* keys, const uint8_t* ha
                          n, tab, emp, cs, w.plan.p, link, counts);
   }
   if (sharded) hipLaunchKernelGGL(k_counts_fold, dim3(1), dim3(kCountShards), 0, st, w.shard.p, counts);
-  return hipGetLastError();
+  return sharded_done(w, sharded);
 }
 
 hipError_t dd_stays(DistWs& w, const uint8_t* has_key, const int32_t* status, const uint64_t* ids, uint32_t n,
@@ -1605,7 +1633,7 @@ hipError_t dd_apply(DistWs& w, const uint64_t* ids, const uint32_t* slot, uint32
                          cs, plan, link, counts);
   }
   if (sh) hipLaunchKernelGGL(k_counts_fold, dim3(1), dim3(kCountShards), 0, st, sh, counts);
-  return hipGetLastError();
+  return sharded_done(w, sh != nullptr);
 }
 
 // The compact table of the files' keys (each key's lowest file index) in

@@ -1022,7 +1022,10 @@ struct PathCall {
     hipError_t e = c->fence_in(c->stream);
     if (e) rc = c->hip_fail(e, "stream wait");
   }
-  ~PathCall() { (void)c->fence_out(c->stream); }
+  ~PathCall() {
+    (void)c->fence_out(c->stream);
+    sdcas_io::drop_dir_cache();  // the caller's thread (big-file opens) keeps no directory open
+  }
 };
 
 // Staging bytes per slot for one path call. The two slots alternate: the I/O

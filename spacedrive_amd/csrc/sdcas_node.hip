@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -139,6 +140,7 @@ struct sdcas_node {
   std::mutex prog_mu;   // the ranks' progress reports, merged
   sdcas_progress_fn progress = nullptr;
   void* progress_user = nullptr;
+  std::chrono::steady_clock::time_point t_call;  // the running node call's start (SDCAS_NODE_TRACE)
   int fail(int code, const char* fmt, ...) {
     char buf[512];
     va_list ap;
@@ -242,13 +244,25 @@ void trace_wait(const sdcas_node* n, const char* phase) {
   if (node_trace()) fprintf(stderr, "sdcas_node: host wait [%s] over %zu ranks\n", phase, n->ranks.size());
 }
 
+double ms_since(std::chrono::steady_clock::time_point t) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+}
+
+// after a traced wait: how long the host waited, and the call's time so far
+void trace_waited(const sdcas_node* n, const char* phase, std::chrono::steady_clock::time_point t_wait) {
+  if (node_trace())
+    fprintf(stderr, "sdcas_node: waited [%s] %.3f ms, call at %.3f ms\n", phase, ms_since(t_wait), ms_since(n->t_call));
+}
+
 int sync_all(sdcas_node* n, const char* what) {
   trace_wait(n, what);
+  const auto t0 = std::chrono::steady_clock::now();
   for (Rank& k : n->ranks) {
     (void)hipSetDevice(k.dev);
     hipError_t e = hipStreamSynchronize(k.st);
     if (e) return n->hip_fail(e, what);
   }
+  trace_waited(n, what, t0);
   return SDCAS_OK;
 }
 
@@ -443,6 +457,7 @@ int sdcas_node_dedup_window(sdcas_node* n, const uint64_t* keys, const uint8_t* 
   if ((uint64_t)nf + n_existing > (1ull << 30))
     return n->fail(SDCAS_E_CAPACITY, "node dedup of %zu files + %zu Objects exceeds 2^30", nf, n_existing);
   std::lock_guard<std::mutex> g(n->mu);
+  n->t_call = std::chrono::steady_clock::now();
   const size_t R = n->ranks.size();
   const uint32_t world = (uint32_t)R;
   if (chunk_size == 0) chunk_size = SDCAS_IDENTIFIER_CHUNK_SIZE;
@@ -533,6 +548,7 @@ int sdcas_node_dedup_window(sdcas_node* n, const uint64_t* keys, const uint8_t* 
       return n->hip_fail(e, "node dedup owner ranges");
   }
   trace_wait(n, "owner ranges");
+  const auto t_ranges = std::chrono::steady_clock::now();
   for (size_t r = 0; r < R; ++r) {
     Rank& k = n->ranks[r];
     (void)hipSetDevice(k.dev);
@@ -544,6 +560,7 @@ int sdcas_node_dedup_window(sdcas_node* n, const uint64_t* keys, const uint8_t* 
       ecnt[r][d] = k.estarts[d + 1] - k.estarts[d];
     }
   }
+  trace_waited(n, "owner ranges", t_ranges);
   // records to their owners
   std::vector<size_t> nf_recv(R, 0), ne_recv(R, 0);
   for (size_t d = 0; d < R; ++d)

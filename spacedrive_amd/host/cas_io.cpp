@@ -56,8 +56,10 @@ namespace {
 // files directory by directory): openat(dir, name) walks one component
 // where open(path) walks them all — on the GPU box's container filesystem
 // the walk is most of an open (profiles/r05_job_read_side.json). A path call
-// starts a new epoch, so no descriptor outlives the call that opened it (a
-// directory replaced between calls is looked up again). SDCAS_DIRFD=0:
+// starts a new epoch (a directory replaced between calls is looked up
+// again), and every thread drops its descriptor when its share of a pool run
+// ends and when the path call ends (drop_dir_cache): an idle engine holds no
+// directory open, so a volume it just indexed can be unmounted. SDCAS_DIRFD=0:
 // open(path) (A/B).
 std::atomic<uint64_t> g_epoch{1};
 bool dirfd_enabled() {
@@ -71,17 +73,20 @@ struct DirCache {
   uint64_t epoch = 0;
   std::string dir;
   int fd = -1;
-  ~DirCache() {
+  void drop() {
     if (fd >= 0) close(fd);
+    fd = -1;
   }
+  ~DirCache() { drop(); }
 };
+thread_local DirCache t_dir;
 // the descriptor to open `path` against, and the name to open there
 int dir_of(const char* path, const char** name) {
   *name = path;
   const char* slash = strrchr(path, '/');
   // a name without a directory, a file in "/", a trailing slash: the plain open
   if (!slash || slash == path || !slash[1] || !dirfd_enabled()) return AT_FDCWD;
-  thread_local DirCache c;
+  DirCache& c = t_dir;
   const uint64_t e = g_epoch.load(std::memory_order_relaxed);
   const size_t dl = (size_t)(slash - path);
   if (c.epoch != e || c.fd < 0 || c.dir.size() != dl || memcmp(c.dir.data(), path, dl) != 0) {
@@ -97,6 +102,7 @@ int dir_of(const char* path, const char** name) {
 }  // namespace
 
 void new_path_epoch() { g_epoch.fetch_add(1, std::memory_order_relaxed); }
+void drop_dir_cache() { t_dir.drop(); }
 
 int open_for_read(const char* path, bool direct, bool* is_direct) {
   *is_direct = false;
@@ -291,6 +297,7 @@ void WorkerPool::dispatch(size_t n, const std::function<void(size_t)>* fn) {
   }
   go_.notify_all();
   drain();  // the calling thread is one of the workers
+  drop_dir_cache();
   std::unique_lock<std::mutex> g(m_);
   done_.wait(g, [this] { return active_ == 0; });
   fn_ = nullptr;
@@ -305,6 +312,7 @@ void WorkerPool::loop() {
     seen = gen_;
     g.unlock();
     drain();
+    drop_dir_cache();  // no directory descriptor held while the pool idles
     g.lock();
     if (--active_ == 0) done_.notify_one();
   }

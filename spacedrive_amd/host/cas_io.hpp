@@ -45,6 +45,8 @@ int open_for_read(const char* path, bool direct, bool* is_direct);
 // a path call begins: the reader threads' cached directory descriptors
 // (open_for_read) are not reused past it
 void new_path_epoch();
+// close the calling thread's cached directory descriptor (if any)
+void drop_dir_cache();
 
 // Whole file into dst (capacity cap > expect, the size the indexer or a stat
 // just saw); returns status, *len = bytes read; sets *overflow when the file

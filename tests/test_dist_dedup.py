@@ -266,6 +266,104 @@ def test_device_stages_match_numpy_stages(eng):
     assert torch.equal(ans_d.cpu(), ans_n)
 
 
+def _owner_np(keys, world):
+    return ((keys >> np.uint64(52)).astype(np.uint64) * np.uint64(world)) >> np.uint64(12)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("corpus", ["default", "collisions"])
+def test_combine_contract_one_record_per_key(eng, corpus):
+    """sdcas.h's combine contract (ABI 5), checked against numpy directly
+    rather than against the numpy stages: owner r's range
+    [starts[r], starts[r+1]) holds, as a multiset, exactly one (key, lowest
+    id) record per distinct key of a keyed, unerrored file whose owner is r
+    (no duplicate, no order assumed), and every such file's slot names its
+    key's record; the same through sdcas_dev_dedup_combine_async with the
+    starts left on the device"""
+    import ctypes
+
+    from spacedrive_amd.dist_dedup import DeviceStages
+    if corpus == "default":
+        keys, has, status, _ = make_corpus(23, 25000)
+        keys[:3] = np.uint64(2**64 - 1)
+    else:
+        keys, has, status, _ = collision_corpus()
+    (k, h, s, ids), = shard(keys, has, status, keys[:0], 1, device="cuda")[0]
+    ok = (has != 0) & (status == 0)
+    st = DeviceStages(eng)
+    for world in (1, 3, 8):
+        rec, slot, starts = st.combine(k, h, s, ids, world)
+        n = keys.size
+        rec2 = torch.empty((n, 2), dtype=torch.int64, device="cuda")
+        slot2 = torch.empty(n, dtype=torch.int32, device="cuda")
+        d_starts = torch.empty(world + 1, dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        rc = eng.L.sdcas_dev_dedup_combine_async(eng.ctx, k.data_ptr(), h.data_ptr(), s.data_ptr(), ids.data_ptr(),
+                                                 n, world, rec2.data_ptr(), slot2.data_ptr(), d_starts.data_ptr(),
+                                                 None)
+        eng._check(rc, "sdcas_dev_dedup_combine_async")
+        eng._check(eng.L.sdcas_dev_sync(eng.ctx, None), "sdcas_dev_sync")
+        starts2 = d_starts.cpu().numpy().view(np.uint32).astype(np.int64).tolist()
+        uk, first = np.unique(keys[ok], return_index=True)
+        want_id = np.flatnonzero(ok)[first]
+        own = _owner_np(uk, world)
+        for got_rec, got_slot, got_starts in ((rec, slot, starts), (rec2, slot2, starts2)):
+            rd = got_rec[: got_starts[world]].cpu().numpy()
+            assert got_starts[world] == uk.size, world
+            for r in range(world):
+                a = rd[got_starts[r]:got_starts[r + 1]]
+                sel = own == r
+                assert a.shape[0] == int(sel.sum()), (world, r)
+                ak = a[:, 0].view(np.uint64)
+                o = np.argsort(ak, kind="stable")
+                assert np.array_equal(ak[o], uk[sel]), (world, r)  # each key once
+                assert np.array_equal(a[o, 1], want_id[sel]), (world, r)
+            sl = got_slot[:n].cpu().numpy().view(np.uint32)
+            assert np.all(sl[~ok & (status != 0)] == 0xFFFFFFFE)
+            assert np.all(sl[(status == 0) & (has == 0)] == 0xFFFFFFFF)
+            assert np.array_equal(rd[sl[ok], 0].view(np.uint64), keys[ok]), world
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1024 * 7 + 1, 1024 * 7 + 63, 1024 * 7 + 65, 1024 * 29 + 1000])
+@pytest.mark.parametrize("chunk_size", [100, 7])
+def test_device_local_stays_in_partial_last_tile(eng, oracle, n, chunk_size):
+    """stays rows (no cas_id, and errored) in the last, partial stays tile
+    (kStayTile = 1024 rows, dist_dedup.hip): the insert counts them per tile,
+    the writer places them after the tiles before, the plan walk sums every
+    tile — the round-5 hazard was those three disagreeing on the tile. The
+    last rows are stays rows at step ends, so a miscounted tile shows as
+    DEFERRED or missing re-reads; every link, both counts and the plan's
+    steps / rows / rereads against the oracle's literal step loop"""
+    from spacedrive_amd.dist_dedup import DeviceStages
+    keys, has, status, existing = make_corpus(1000 + n, n, pool=max(50, n // 5), p_none=0.05, p_err=0.05)
+    tail = n - (n // 1024) * 1024
+    lo = n - tail
+    has[lo:] = 1
+    status[lo:] = 0
+    # in the partial tile: rows without cas_id and errored rows, among them the
+    # very last row and rows at step ends
+    pick = np.unique(np.concatenate([[n - 1, n - 2, lo], np.arange(lo + chunk_size - 1, n, chunk_size),
+                                     lo + np.random.default_rng(n).integers(0, tail, max(1, tail // 8))]))
+    pick = pick[(pick >= lo) & (pick < n)]
+    has[pick[::2]] = 0
+    status[pick[1::2]] = 5
+    st = DeviceStages(eng)
+    header = torch.zeros(12, dtype=torch.int64, device="cuda")
+    (k, h, s, ids), = shard(keys, has, status, existing, 1, device="cuda")[0]
+    ek = torch.from_numpy(existing.view(np.int64)).cuda()
+    eids = torch.arange(existing.size, dtype=torch.int64, device="cuda")
+    want, wc, wl, ww = oracle.identifier_job(keys, has, status, chunk_size, existing)
+    for _ in range(2):  # the second call over a dirty workspace
+        link, cnt = st.local(k, h, s, ids, chunk_size, ek, eids, header=header)
+        assert np.array_equal(link.cpu().numpy(), want)
+        assert tuple(cnt.tolist()) == (wc, wl)
+        hd = header.cpu().numpy()
+        assert (int(hd[2]), int(hd[3]), int(hd[8])) == (ww["steps"], ww["rows"], ww["rereads"])
+    got, gc, gl, gw = eng.identifier_dedup_window(keys, has, status, chunk_size, existing, 0, False)
+    assert np.array_equal(got, want) and (gc, gl) == (wc, wl) and gw == ww
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("R", [1, 3])
 def test_device_stages_top32_collisions(eng, oracle, R):

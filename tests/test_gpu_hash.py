@@ -92,6 +92,43 @@ def test_generate_cas_id_files_direct_io(tmp_path):
     assert (d_direct == d_plain).all()
 
 
+def _fds_on(path):
+    """this process's descriptors open on `path` (the directory itself)"""
+    out = []
+    for fd in os.listdir("/proc/self/fd"):
+        try:
+            if os.readlink(f"/proc/self/fd/{fd}") == str(path):
+                out.append(fd)
+        except OSError:
+            pass
+    return out
+
+
+def test_no_directory_descriptor_outlives_a_path_call(tmp_path):
+    """the readers open files relative to a cached directory descriptor
+    (cas_io.cpp dir_of); once a path call returns, neither the pool threads nor
+    the calling thread (big-file checksums open on it) may keep one — an idle
+    engine must not hold a volume it just indexed busy"""
+    from spacedrive_amd import Engine
+    d = tmp_path / "vol"
+    d.mkdir()
+    small = []
+    for i in range(200):
+        p = d / f"s{i}"
+        p.write_bytes(os.urandom(1000 + 517 * i))
+        small.append(str(p))
+    big = d / "big"
+    big.write_bytes(os.urandom((3 << 20) + 5))
+    with Engine(io_threads=8, staging_bytes=8 << 20) as e:
+        keys, st = e.generate_cas_ids(small, [os.path.getsize(p) for p in small])
+        assert not st.any()
+        assert _fds_on(d) == []
+        out, st = e.file_checksums(small[:50] + [str(big)])
+        assert not st.any()
+        assert _fds_on(d) == []
+    assert _fds_on(d) == []
+
+
 def eng_plain_checksums(paths):
     from spacedrive_amd import Engine
     with Engine() as e:

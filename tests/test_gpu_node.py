@@ -1,8 +1,10 @@
 """A node: one process driving several GPU contexts (sdcas_node_*,
 spacedrive_amd.Node) — sd-core is one process (apps/server/src/main.rs:40,
 job/manager.rs:32), so the multi-GPU paths must be reachable without a
-process per GPU. On this one-GPU box the node is [0, 0]: two contexts on one
-device, the exchange as device-to-device copies — the default between
+process per GPU. On this one-GPU box the node is [0, 0] (up to eight
+contexts, [0] * 8: the layout sd-core's one process would drive on an
+8-GPU node, include/sdcas.h:395-427) on one device, the exchange as
+device-to-device copies — the default between
 distinct devices too (over xGMI); RCCL (ncclCommInitAll) is opt-in with
 SDCAS_NODE_EXCHANGE=rccl and unmeasured here.
 Everything against the oracle."""
@@ -16,7 +18,7 @@ pytestmark = pytest.mark.gpu
 MiB = 1 << 20
 
 
-@pytest.fixture(scope="module", params=[(0,), (0, 0), (0, 0, 0)], ids=["node1", "node2", "node3"])
+@pytest.fixture(scope="module", params=[(0,), (0, 0), (0, 0, 0), (0,) * 8], ids=["node1", "node2", "node3", "node8"])
 def node(request):
     from spacedrive_amd import Node
     n = Node(devices=request.param, staging_bytes=16 * MiB)
@@ -89,3 +91,42 @@ def test_node_cas_ids_and_checksums(node, oracle, tmp_path):
     assert st[-1] == 2 and not st[:-1].any()
     for i, p in enumerate(big):
         assert bytes(out[i]).hex() == oracle.file_checksum(p), p
+
+
+def c5_share_keys(oracle, n, world=8):
+    """real cas keys (upstream BLAKE3 C) of an even sample of the C5 corpus
+    (bench.c5_share: the Zipf head and ~60 % duplicates at any size)"""
+    import bench
+    sizes, ckeys, _ = bench.files_of("c5", 0, n, world)
+    keys, _ = oracle.synth_cas_keys(ckeys, sizes, threads=16)
+    return keys, sizes
+
+
+def test_node_dedup_c5_share_waits_per_phase(node, oracle, monkeypatch, capfd):
+    """sdcas_node_dedup_window over a C5 share with the Zipf head (one
+    content carries ~7 % of the files, so one owner context receives far more
+    records than the others), existing Objects present: links and counts
+    against the oracle, two host waits, and the per-phase wait times the
+    trace reports (printed: gpurun logs keep them)"""
+    keys, sizes = c5_share_keys(oracle, 160_000)
+    rng = np.random.default_rng(41)
+    has = (sizes != 0).astype(np.uint8)
+    status = np.where(rng.random(keys.size) < 0.003, 5, 0).astype(np.int32)
+    existing = np.concatenate([keys[rng.choice(keys.size, 2000, replace=False)],
+                               rng.integers(0, 2**64, 400, dtype=np.uint64)])
+    assert 1 - np.unique(keys).size / keys.size > 0.4  # the share duplicates as the corpus does
+    want, wc, wl, ww = oracle.identifier_job(keys, has, status, 100, existing)
+    for rep in range(2):  # the second call on warm buffers
+        capfd.readouterr()
+        monkeypatch.setenv("SDCAS_NODE_TRACE", "1")
+        got, gc, gl, gw = node.identifier_dedup_window(keys, has, status, 100, existing)
+        monkeypatch.delenv("SDCAS_NODE_TRACE")
+        err = capfd.readouterr().err
+        assert np.array_equal(got, want), rep
+        assert (gc, gl) == (wc, wl) and gw == ww, rep
+        waits = [ln for ln in err.splitlines() if ln.startswith("sdcas_node: host wait")]
+        assert len(waits) == 2, err
+        waited = [ln for ln in err.splitlines() if ln.startswith("sdcas_node: waited")]
+        assert len(waited) == 2, err
+        with capfd.disabled():
+            print(f"\n[node{node.size} c5 share {keys.size} files, call {rep}] " + " | ".join(waited))
