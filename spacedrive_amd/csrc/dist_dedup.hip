@@ -91,7 +91,11 @@ __device__ __forceinline__ int64_t step_link(int kind, int64_t me, int64_t r, ui
   // created in the key's first step: a file of that step creates its own
   // Object (mod.rs:246-254), files of later steps link to the first one
   const uint64_t rpos = pv.rr ? (uint64_t)r + rr_below(pv, (uint64_t)r) : (uint64_t)r;
-  if (pos / cs == rpos / cs) {
+  // the same step? (32-bit division when everything fits: a 64-bit one is a
+  // long software sequence, paid by every keyed file)
+  const bool same = ((pos | rpos | cs) >> 32) == 0 ? (uint32_t)pos / (uint32_t)cs == (uint32_t)rpos / (uint32_t)cs
+                                                   : pos / cs == rpos / cs;
+  if (same) {
     c += 1;
     return me;
   }
@@ -312,30 +316,52 @@ __global__ __launch_bounds__(64) void k_plan_walk(const uint64_t* __restrict__ s
   uint64_t* rr = plan + kPlanHeader;
   uint64_t r = 0;
   uint64_t first = ~0ull, last_stay = ~0ull;  // smallest / largest valid stays ordinal
-  for (uint32_t base = 0; base < m; base += 64) {
-    const uint32_t j = base + (uint32_t)lane;
-    uint64_t p = ~0ull;
-    if (j < m) p = idx ? ids[idx[j]] : stays[j];
-    const bool in = p < n_total;
-    const unsigned long long inm = __ballot(in);
-    if (inm) {
-      const int lo = __ffsll((long long)inm) - 1, hi = 63 - __clzll((long long)inm);
-      const uint64_t plo = __shfl(p, lo), phi = __shfl(p, hi);
-      if (first == ~0ull) first = plo;
-      last_stay = phi;
+  // kWalkU batches of 64 ordinals are loaded together (a batch's ordinal is
+  // two dependent loads, ids[idx[j]]: one memory round trip per 64 * kWalkU
+  // ordinals) and their residues p % cs computed together; then each batch
+  // is walked in order. Between two re-reads r is constant, so the next
+  // re-read is the first candidate whose residue is the target
+  // (cs - 1 - r) mod cs: a batch without it costs one compare and one
+  // ballot, and each re-read moves the target down by one.
+  constexpr uint32_t kWalkU = 8;
+  const bool small = cs < (1ull << 32);
+  uint64_t target = cs - 1;  // (cs - 1 - r) mod cs
+  bool done = false;
+  for (uint32_t base = 0; base < m && !done; base += 64 * kWalkU) {
+    uint64_t pv[kWalkU], pm[kWalkU];
+#pragma unroll
+    for (uint32_t u = 0; u < kWalkU; ++u) {
+      const uint32_t j = base + 64 * u + (uint32_t)lane;
+      pv[u] = j < m ? (idx ? ids[idx[j]] : stays[j]) : ~0ull;
     }
-    const bool cand = cs > 1 && in && p + 1 < n_total;
-    int last = -1;
-    for (;;) {
-      const bool hit = cand && lane > last && (p + r) % cs == cs - 1;
-      const unsigned long long mask = __ballot(hit);
-      if (!mask) break;
-      const int f = __ffsll((long long)mask) - 1;
-      if (lane == f) rr[r] = p;
-      ++r;
-      last = f;
+    uint32_t pad = 0;  // batches holding a padding entry (sorted: padding from there on)
+#pragma unroll
+    for (uint32_t u = 0; u < kWalkU; ++u) {
+      const uint32_t j = base + 64 * u + (uint32_t)lane;
+      const uint64_t p = pv[u];
+      const bool cand = cs > 1 && n_total && p < n_total - 1;  // the job's last orphan is never re-read
+      pm[u] = !cand ? ~0ull : small && p < (1ull << 32) ? (uint64_t)((uint32_t)p % (uint32_t)cs) : p % cs;
+      if (__ballot(j < m && p >= n_total)) pad |= 1u << u;
     }
-    if (__ballot(j < m && !in)) break;  // sorted: padding from here on
+    // the valid range: the first entry of all, the last before padding or m
+    const uint64_t p00 = __shfl(pv[0], 0);
+    if (base == 0 && m && p00 < n_total) first = p00;
+#pragma unroll
+    for (uint32_t u = 0; u < kWalkU; ++u) {
+      if (done) break;
+      const uint32_t j = base + 64 * u + (uint32_t)lane;
+      const unsigned long long inm = __ballot(j < m && pv[u] < n_total);
+      if (inm) last_stay = __shfl(pv[u], 63 - __clzll((long long)inm));
+      unsigned long long mask = __ballot(pm[u] == target);
+      while (mask) {
+        const int f = __ffsll((long long)mask) - 1;
+        if (lane == f) rr[r] = pv[u];
+        ++r;
+        target = target == 0 ? cs - 1 : target - 1;
+        mask = __ballot(pm[u] == target && lane > f);
+      }
+      if ((pad >> u) & 1u || base + 64 * (u + 1) >= m) done = true;
+    }
   }
   if (lane == 0) {
     const uint64_t T = max_steps ? max_steps : (n_total + cs - 1) / cs;
@@ -456,7 +482,7 @@ __global__ void k_solo_insert_idx(const uint64_t* __restrict__ keys, const uint6
                                   const uint64_t* __restrict__ eids, uint32_t count, uint32_t base,
                                   uint32_t* __restrict__ tab, unsigned long long* __restrict__ emin, uint32_t mask,
                                   uint32_t shift, uint32_t* __restrict__ pos, uint32_t* __restrict__ stay_cnt,
-                                  uint32_t* __restrict__ noncontig);
+                                  uint32_t* __restrict__ noncontig, uint32_t sticky);
 
 // ---- the combine through a hash table ----------------------------------------------
 //
@@ -1052,9 +1078,14 @@ __device__ __forceinline__ uint64_t idx_key(const uint64_t* __restrict__ keys, c
 constexpr uint32_t kStayTile = 1024;
 static_assert(kStayTile % 64 == 0, "the insert's per-wave ballot add needs a wave's 64 rows in one tile");
 static_assert(kStayTile % TB == 0, "k_stays_write_t walks a tile in whole workgroups");
+constexpr uint32_t kStayScanTiles = 64;  // more tiles: k_tile_scan instead of per-writer sums
 
 // files (emin null, base 0): pos[i] = slot, or the code of a file without
 // one; existing Objects (emin set, base n): min-fold eids[j] into emin[slot]
+// (sticky = kIdxEmpty: slot mode) or into emin[j'] for the key's claiming
+// Object j' (sticky = n: entry mode — the existing Objects' pass runs first,
+// their claims stay, and a file finding one leaves it: the apply reads the
+// minimum through the claim, from an array of ne entries instead of cap)
 // stay_cnt (files, may be null): += the rows of each kStayTile-row tile that
 // stay orphans, one atomicAdd per wave holding one
 // noncontig (files, may be null; eids = the files' ordinals then): set when
@@ -1066,7 +1097,7 @@ __global__ void k_solo_insert_idx(const uint64_t* __restrict__ keys, const uint6
                                   const uint64_t* __restrict__ eids, uint32_t count, uint32_t base,
                                   uint32_t* __restrict__ tab, unsigned long long* __restrict__ emin, uint32_t mask,
                                   uint32_t shift, uint32_t* __restrict__ pos, uint32_t* __restrict__ stay_cnt,
-                                  uint32_t* __restrict__ noncontig) {
+                                  uint32_t* __restrict__ noncontig, uint32_t sticky) {
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= count) return;
   const uint32_t x = base + q;
@@ -1089,6 +1120,7 @@ __global__ void k_solo_insert_idx(const uint64_t* __restrict__ keys, const uint6
   }
   const uint64_t key = idx_key(keys, ekeys, n, x);
   uint32_t h = (uint32_t)(key >> shift) & mask;
+  uint32_t x_claim = x;
   for (;;) {
     uint32_t cur = __hip_atomic_load(&tab[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (cur == kIdxEmpty) {
@@ -1097,14 +1129,20 @@ __global__ void k_solo_insert_idx(const uint64_t* __restrict__ keys, const uint6
       cur = prev;
     }
     if (idx_key(keys, ekeys, n, cur) == key) {
-      if (cur > x) atomicMin(&tab[h], x);
+      // an existing Object's claim is sticky (entry mode): files leave it
+      if (cur > x && cur < sticky && !(emin && sticky != kIdxEmpty)) atomicMin(&tab[h], x);
+      if (emin && sticky != kIdxEmpty) x_claim = cur;
       break;
     }
     h = (h + 1) & mask;
   }
   if (emin) {
+    // slot mode: the DB index min-folds into emin[slot] (cap entries);
+    // entry mode: into emin[claimer - n] (ne entries, the claimer fixed by
+    // its CAS: existing Objects never lower a claim)
+    unsigned long long* m = sticky != kIdxEmpty ? &emin[x_claim - n] : &emin[h];
     const unsigned long long v = eids[q];
-    if (__hip_atomic_load(&emin[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > v) atomicMin(&emin[h], v);
+    if (__hip_atomic_load(m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > v) atomicMin(m, v);
   } else {
     pos[q] = h;
   }
@@ -1113,7 +1151,7 @@ __global__ void k_solo_insert_idx(const uint64_t* __restrict__ keys, const uint6
 __global__ void k_solo_apply_idx(const uint64_t* __restrict__ ids, const uint32_t* __restrict__ pos, uint32_t n,
                                  const uint32_t* __restrict__ tab, const uint64_t* __restrict__ emin, uint64_t cs,
                                  const uint64_t* __restrict__ plan, int64_t* __restrict__ link,
-                                 unsigned long long* __restrict__ counts) {
+                                 unsigned long long* __restrict__ counts, uint32_t ebase) {
   __shared__ unsigned long long sc[2];
   if (threadIdx.x < 2) sc[threadIdx.x] = 0;
   __syncthreads();
@@ -1126,8 +1164,9 @@ __global__ void k_solo_apply_idx(const uint64_t* __restrict__ ids, const uint32_
     if (kind == kFileKeyed) {
       // mod.rs:202-238: the first existing Object; else (mod.rs:246-254) the
       // key's first file — a file, as this one carries the key
-      const uint64_t e = emin ? emin[h] : ~0ull;
       const uint32_t f = tab[h];
+      // entry mode (ebase = n): a claim by existing Object f - n holds its minimum
+      const uint64_t e = ebase != kIdxEmpty ? (f >= ebase ? emin[f - ebase] : ~0ull) : emin ? emin[h] : ~0ull;
       r = e != ~0ull ? -(int64_t)e - 1 : (int64_t)(f == i ? ids[i] : ids[f]);
     }
     link[i] = step_link(kind, (int64_t)ids[i], r, cs, pv, c, l);
@@ -1181,7 +1220,7 @@ __global__ void __launch_bounds__(TB) k_solo_apply_r(const uint64_t* __restrict_
                                                      const uint64_t* __restrict__ emin, uint64_t cs,
                                                      const uint64_t* __restrict__ plan, int64_t* __restrict__ link,
                                                      unsigned long long* __restrict__ shard,
-                                                     const uint32_t* __restrict__ noncontig) {
+                                                     const uint32_t* __restrict__ noncontig, uint32_t ebase) {
   __shared__ unsigned long long sc[2];
   if (threadIdx.x < 2) sc[threadIdx.x] = 0;
   __syncthreads();
@@ -1198,11 +1237,19 @@ __global__ void __launch_bounds__(TB) k_solo_apply_r(const uint64_t* __restrict_
     h[k] = i < n ? pos[i] : kSlotDropped;
     me[k] = i < n ? ids[i] : 0;
   }
+  const bool entry = ebase != kIdxEmpty;  // existing minima by claiming Object (ne entries), not by slot
 #pragma unroll
   for (uint32_t k = 0; k < R; ++k) {
     const bool keyed = h[k] < kSlotDropped && h[k] != kSlotNoKey;
     f[k] = keyed ? tab[h[k]] : 0u;
-    e[k] = keyed && emin ? emin[h[k]] : ~0ull;
+    e[k] = keyed && emin && !entry ? emin[h[k]] : ~0ull;
+  }
+  if (entry) {
+#pragma unroll
+    for (uint32_t k = 0; k < R; ++k) {
+      const bool keyed = h[k] < kSlotDropped && h[k] != kSlotNoKey;
+      if (keyed && f[k] >= ebase) e[k] = emin[f[k] - ebase];
+    }
   }
 #pragma unroll
   for (uint32_t k = 0; k < R; ++k) {
@@ -1243,25 +1290,35 @@ __global__ void k_counts_fold(unsigned long long* __restrict__ shard, unsigned l
 }
 
 // the stays rows of tile blockIdx.x (PER rows) in order, at the offset the
-// tiles before it add up to (only tiles holding one do any work)
+// tiles before it add up to (only tiles holding one do any work). cnt holds
+// the tiles' counts (each writer sums the counts before its own: for a few
+// tiles) or, with `offs`, their exclusive offsets from k_tile_scan and the
+// total in *total (many tiles: summing would cost tiles^2 reads — 50 M files
+// with stays in every tile, 48 828 tiles: 433 us)
 template <uint32_t PER>
 __global__ void __launch_bounds__(TB) k_stays_write_t(const uint8_t* __restrict__ has_key,
                                                       const int32_t* __restrict__ status, uint32_t n,
-                                                      const uint32_t* __restrict__ cnt, uint32_t* __restrict__ out) {
+                                                      const uint32_t* __restrict__ cnt, uint32_t* __restrict__ out,
+                                                      const uint32_t* __restrict__ total) {
   __shared__ uint32_t ws[TB / 64];
   const uint32_t b = blockIdx.x;
-  if (cnt[b] == 0) return;  // uniform over the workgroup
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  uint32_t s = 0;
-  for (uint32_t t = tid; t < b; t += TB) s += cnt[t];
-#pragma unroll
-  for (uint32_t d = 32; d; d >>= 1) s += __shfl_xor(s, d);
-  if (lane == 0) ws[wave] = s;
-  __syncthreads();
   uint32_t run = 0;
+  if (total) {
+    run = cnt[b];
+    if ((b + 1 < gridDim.x ? cnt[b + 1] : *total) == run) return;  // uniform over the workgroup
+  } else {
+    if (cnt[b] == 0) return;  // uniform over the workgroup
+    uint32_t s = 0;
+    for (uint32_t t = tid; t < b; t += TB) s += cnt[t];
 #pragma unroll
-  for (uint32_t w = 0; w < TB / 64; ++w) run += ws[w];
-  __syncthreads();
+    for (uint32_t d = 32; d; d >>= 1) s += __shfl_xor(s, d);
+    if (lane == 0) ws[wave] = s;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t w = 0; w < TB / 64; ++w) run += ws[w];
+    __syncthreads();
+  }
   const uint64_t lo = (uint64_t)b * PER;
 #pragma unroll 1
   for (uint32_t r = 0; r < PER / TB; ++r) {
@@ -1281,6 +1338,47 @@ __global__ void __launch_bounds__(TB) k_stays_write_t(const uint8_t* __restrict_
     if (f) out[before + below] = (uint32_t)i;
     run += all;
   }
+}
+
+// one workgroup: cnt[0..nt) <- exclusive prefix sums in place, *total <- the
+// sum; 16 counts per thread per pass (a pass covers 16 K tiles)
+constexpr uint32_t kScanR = 16;
+__global__ void __launch_bounds__(1024) k_tile_scan(uint32_t* __restrict__ cnt, uint32_t nt,
+                                                    uint32_t* __restrict__ total) {
+  __shared__ uint32_t ws[16];
+  __shared__ uint32_t carry;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t base = 0; base < nt; base += 1024 * kScanR) {
+    const uint32_t i0 = base + tid * kScanR;
+    uint32_t v[kScanR], sum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanR; ++k) {
+      v[k] = i0 + k < nt ? cnt[i0 + k] : 0u;
+      sum += v[k];
+    }
+    uint32_t inc = sum;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint32_t t = __shfl_up(inc, d);
+      if (lane >= d) inc += t;
+    }
+    if (lane == 63) ws[wave] = inc;
+    __syncthreads();
+    uint32_t run = carry;
+    for (uint32_t w = 0; w < wave; ++w) run += ws[w];
+    run += inc - sum;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanR; ++k) {
+      if (i0 + k < nt) cnt[i0 + k] = run;
+      run += v[k];
+    }
+    __syncthreads();
+    if (tid == 1023) carry = run;
+    __syncthreads();
+  }
+  if (tid == 0) *total = carry;
 }
 
 // SDCAS_DEDUP_TABLE: "idx" (the default) = the compact u32 table, the
@@ -1339,6 +1437,14 @@ static uint64_t local_cap(uint64_t items) {
   return cap;
 }
 
+// SDCAS_EXIST_MIN=slot: the existing Objects' minima by table slot (cap u64,
+// round 5) instead of by claiming Object (ne u64; the default), read per call
+// (A/B in one process)
+static bool exist_min_by_entry() {
+  const char* v = getenv("SDCAS_EXIST_MIN");
+  return !(v && strcmp(v, "slot") == 0);
+}
+
 static hipError_t local_fused(DistWs& w, const uint64_t* keys, const uint8_t* has_key, const int32_t* status,
                               const uint64_t* ids, uint32_t n, const uint64_t* ekeys, const uint64_t* eids,
                               uint32_t ne, uint64_t cs, const StepWindow& win, int64_t* link,
@@ -1353,13 +1459,16 @@ static hipError_t local_fused(DistWs& w, const uint64_t* keys, const uint8_t* ha
   const uint32_t ar = apply_files_per_thread();
   const bool sharded = ar && counts;
   const bool contig = ar && contig_ordinals() && n > 0;
-  if ((e = w.tmin.ensure(cap / 2 + 1)) || (e = w.tpos.ensure(n)) || (ne && (e = w.tkey.ensure(cap + 1))) ||
+  const bool entry = ne && exist_min_by_entry();
+  const uint32_t sticky = entry ? n : kIdxEmpty;  // k_solo_insert_idx / the applies: entry mode from index n
+  if ((e = w.tmin.ensure(cap / 2 + 1)) || (e = w.tpos.ensure(n)) || (e = w.nstay.ensure(1)) ||
+      (ne && (e = w.tkey.ensure(entry ? (uint64_t)ne + 2 : cap + 1))) ||
       (e = w.stay_cnt.ensure(nt + 1)) || (stays && (e = w.stay_idx.ensure(n))) || (sharded && (e = shard_counts(w, st))) ||
       (contig && (e = w.flag.ensure(1))))
     return e;
   auto* tab = reinterpret_cast<uint32_t*>(w.tmin.p);
   auto* em = ne ? reinterpret_cast<unsigned long long*>(w.tkey.p) : nullptr;
-  const uint64_t tab_q = cap / 4, em_q = ne ? cap / 2 : 0;  // uint4 stores (cap >= 1024)
+  const uint64_t tab_q = cap / 4, em_q = !ne ? 0 : entry ? ((uint64_t)ne + 1) / 2 : cap / 2;  // uint4 stores
   const uint32_t cg = (uint32_t)std::min<uint64_t>((tab_q + em_q + TB - 1) / TB, 2048);
   hipLaunchKernelGGL(k_local_clear, dim3(cg), dim3(TB), 0, st, reinterpret_cast<uint4*>(tab), tab_q,
                      reinterpret_cast<uint4*>(em), em_q, w.stay_cnt.p, stays ? nt : 0u,
@@ -1367,21 +1476,28 @@ static hipError_t local_fused(DistWs& w, const uint64_t* keys, const uint8_t* ha
   if (ne)
     hipLaunchKernelGGL(k_solo_insert_idx, dim3(blocks(ne)), dim3(TB), 0, st, keys, ekeys, n, (const uint8_t*)nullptr,
                        (const int32_t*)nullptr, eids, ne, n, tab, em, mask, shift, (uint32_t*)nullptr,
-                       (uint32_t*)nullptr, (uint32_t*)nullptr);
+                       (uint32_t*)nullptr, (uint32_t*)nullptr, sticky);
   hipLaunchKernelGGL(k_solo_insert_idx, dim3(blocks(n)), dim3(TB), 0, st, keys, ekeys, n, has_key, status,
                      contig ? ids : (const uint64_t*)nullptr, n, 0u, tab, (unsigned long long*)nullptr, mask, shift,
-                     w.tpos.p, stays ? w.stay_cnt.p : (uint32_t*)nullptr, contig ? w.flag.p : (uint32_t*)nullptr);
+                     w.tpos.p, stays ? w.stay_cnt.p : (uint32_t*)nullptr, contig ? w.flag.p : (uint32_t*)nullptr,
+                     sticky);
+  // many tiles: one scan turns the counts into offsets (the writers then
+  // read their own, the walk the total) instead of each writer summing the
+  // tiles before it
+  const bool scan = stays && nt > kStayScanTiles;
+  if (scan) hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, st, w.stay_cnt.p, nt, w.nstay.p);
   if (stays)
     hipLaunchKernelGGL(k_stays_write_t<kStayTile>, dim3(nt), dim3(TB), 0, st, has_key, status, n, w.stay_cnt.p,
-                       w.stay_idx.p);
+                       w.stay_idx.p, scan ? (const uint32_t*)w.nstay.p : (const uint32_t*)nullptr);
   hipLaunchKernelGGL(k_plan_walk, dim3(1), dim3(64), 0, st, (const uint64_t*)nullptr, w.stay_idx.p, ids,
-                     stays ? n : 0u, (const uint32_t*)nullptr, win.n_total ? win.n_total : (uint64_t)n, cs,
-                     win.max_steps, win.more, w.plan.p, stays ? w.stay_cnt.p : (const uint32_t*)nullptr, nt);
+                     stays ? n : 0u, scan ? (const uint32_t*)w.nstay.p : (const uint32_t*)nullptr,
+                     win.n_total ? win.n_total : (uint64_t)n, cs, win.max_steps, win.more, w.plan.p,
+                     stays && !scan ? w.stay_cnt.p : (const uint32_t*)nullptr, nt);
   const uint64_t* emp = ne ? w.tkey.p : nullptr;
   auto apply = [&](auto kern, uint32_t r) {
     const uint32_t g = (uint32_t)(((uint64_t)n + (uint64_t)TB * r - 1) / ((uint64_t)TB * r));
     if (g) hipLaunchKernelGGL(kern, dim3(g), dim3(TB), 0, st, ids, w.tpos.p, n, tab, emp, cs, w.plan.p, link,
-                              sharded ? w.shard.p : nullptr, contig ? (const uint32_t*)w.flag.p : nullptr);
+                              sharded ? w.shard.p : nullptr, contig ? (const uint32_t*)w.flag.p : nullptr, sticky);
   };
   switch (ar) {
     case 1: apply(k_solo_apply_r<1>, 1); break;
@@ -1390,7 +1506,7 @@ static hipError_t local_fused(DistWs& w, const uint64_t* keys, const uint8_t* ha
     case 8: apply(k_solo_apply_r<8>, 8); break;
     default:
       hipLaunchKernelGGL(k_solo_apply_idx, dim3(blocks(n) < 1024 ? blocks(n) : 1024), dim3(TB), 0, st, ids, w.tpos.p,
-                         n, tab, emp, cs, w.plan.p, link, counts);
+                         n, tab, emp, cs, w.plan.p, link, counts, sticky);
   }
   if (sharded) hipLaunchKernelGGL(k_counts_fold, dim3(1), dim3(kCountShards), 0, st, w.shard.p, counts);
   return sharded_done(w, sharded);
@@ -1583,12 +1699,12 @@ hipError_t dd_local(DistWs& w, const uint64_t* keys, const uint8_t* has_key, con
     if (ne)
       hipLaunchKernelGGL(k_solo_insert_idx, dim3(blocks(ne)), dim3(TB), 0, st, keys, ekeys, n,
                          (const uint8_t*)nullptr, (const int32_t*)nullptr, eids, ne, n, tab, em, mask, shift,
-                         (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr);
+                         (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr, kIdxEmpty);
     hipLaunchKernelGGL(k_solo_insert_idx, dim3(blocks(n)), dim3(TB), 0, st, keys, ekeys, n, has_key, status,
                        (const uint64_t*)nullptr, n, 0u, tab, (unsigned long long*)nullptr, mask, shift, w.tpos.p,
-                       (uint32_t*)nullptr, (uint32_t*)nullptr);
+                       (uint32_t*)nullptr, (uint32_t*)nullptr, kIdxEmpty);
     hipLaunchKernelGGL(k_solo_apply_idx, dim3(blocks(n) < 1024 ? blocks(n) : 1024), dim3(TB), 0, st, ids, w.tpos.p, n,
-                       tab, ne ? w.tkey.p : nullptr, chunk_size, w.plan.p, link, counts);
+                       tab, ne ? w.tkey.p : nullptr, chunk_size, w.plan.p, link, counts, kIdxEmpty);
     return hipGetLastError();
   }
   // (key, file minimum) pairs in tmin, existing minima in tkey (when ne > 0)
@@ -1654,7 +1770,7 @@ static hipError_t combine_table(DistWs& w, const uint64_t* keys, const uint8_t* 
     return e;
   hipLaunchKernelGGL(k_solo_insert_idx, dim3(blocks(n)), dim3(TB), 0, st, keys, (const uint64_t*)nullptr, n, has_key,
                      status, (const uint64_t*)nullptr, n, 0u, w.idx_a.p, (unsigned long long*)nullptr, mask, shift,
-                     w.idx_b.p, (uint32_t*)nullptr, (uint32_t*)nullptr);
+                     w.idx_b.p, (uint32_t*)nullptr, (uint32_t*)nullptr, kIdxEmpty);
   return hipGetLastError();
 }
 

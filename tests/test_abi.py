@@ -33,6 +33,15 @@ def test_library_exports_every_declared_symbol():
     assert declared_symbols() <= exported
 
 
+def test_library_has_no_undefined_own_symbols():
+    """a kernel declared with one signature and defined with another links as
+    two overloads, the declared one undefined: the library then fails to load
+    on the GPU box (round 6, k_solo_insert_idx) — catch it here"""
+    out = subprocess.run(["nm", "-u", "-C", N.LIB_PATH], capture_output=True, text=True).stdout
+    own = [ln for ln in out.splitlines() if "sdcas" in ln]
+    assert own == [], own
+
+
 def test_library_is_gfx950():
     out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-n", N.LIB_PATH], capture_output=True,
                          text=True)

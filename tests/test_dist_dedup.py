@@ -325,13 +325,15 @@ def test_combine_contract_one_record_per_key(eng, corpus):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [1024 * 7 + 1, 1024 * 7 + 63, 1024 * 7 + 65, 1024 * 29 + 1000])
+@pytest.mark.parametrize("n", [1024 * 7 + 1, 1024 * 7 + 63, 1024 * 7 + 65, 1024 * 29 + 1000, 1024 * 300 + 17])
 @pytest.mark.parametrize("chunk_size", [100, 7])
 def test_device_local_stays_in_partial_last_tile(eng, oracle, n, chunk_size):
     """stays rows (no cas_id, and errored) in the last, partial stays tile
     (kStayTile = 1024 rows, dist_dedup.hip): the insert counts them per tile,
     the writer places them after the tiles before, the plan walk sums every
-    tile — the round-5 hazard was those three disagreeing on the tile. The
+    tile — the round-5 hazard was those three disagreeing on the tile (past
+    64 tiles the counts go through k_tile_scan and the writers read offsets:
+    n = 300 K). The
     last rows are stays rows at step ends, so a miscounted tile shows as
     DEFERRED or missing re-reads; every link, both counts and the plan's
     steps / rows / rereads against the oracle's literal step loop"""
@@ -460,7 +462,7 @@ def test_rccl_world1(eng, oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("table", ["idx", "idx-r0", "idx-r1", "idx-r8", "idx-c0", "idx4", "kv"])
+@pytest.mark.parametrize("table", ["idx", "idx-r0", "idx-r1", "idx-r8", "idx-c0", "idx-xslot", "idx4", "kv"])
 @pytest.mark.parametrize("corpus,chunk_size", [("default", 100), ("default", 7), ("default", 1),
                                                ("collisions", 100), ("clustered", 100)])
 def test_device_local_vs_oracle(eng, oracle, corpus, chunk_size, table, monkeypatch):
@@ -471,7 +473,9 @@ def test_device_local_vs_oracle(eng, oracle, corpus, chunk_size, table, monkeypa
     the same table behind round 4's eight launches, round 3's 16-byte kv
     table; the default table's apply with 0 (the grid-stride form), 1 and 8
     files per thread beside the default 4 (`idx-rN`, SDCAS_APPLY_R), every
-    first ordinal read instead of taken from the index (`idx-c0`); and the
+    first ordinal read instead of taken from the index (`idx-c0`), the
+    existing Objects' minima by table slot instead of by claiming Object
+    (`idx-xslot`, round 5's form); and the
     existing Objects passed in DB order and shuffled (their DB indices then
     not ascending: the first Object is the lowest DB index, not the first
     entry)"""
@@ -479,7 +483,7 @@ def test_device_local_vs_oracle(eng, oracle, corpus, chunk_size, table, monkeypa
     table, _, knob = table.partition("-")
     monkeypatch.setenv("SDCAS_DEDUP_TABLE", table)
     if knob:
-        monkeypatch.setenv({"r": "SDCAS_APPLY_R", "c": "SDCAS_CONTIG"}[knob[0]], knob[1:])
+        monkeypatch.setenv({"r": "SDCAS_APPLY_R", "c": "SDCAS_CONTIG", "x": "SDCAS_EXIST_MIN"}[knob[0]], knob[1:])
     if corpus == "default":
         keys, has, status, existing = make_corpus(91, 40000, pool=6000)
         keys[:2] = np.uint64(2**64 - 1)  # the table's empty marker is a legal key

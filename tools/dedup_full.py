@@ -15,8 +15,9 @@ oracle). Then:
     chunked dedup (oracle/cas_ref.c), for the device call AND for the host
     C ABI sd-core binds (sdcas_dedup: host keys in, links out), the latter
     timed too.
-Run under rocprofv3 --pmc with --no-parity --reps 3 for the HBM bytes (every
-dispatch after the last hash kernel is the dedup's).
+Run under rocprofv3 --pmc with --no-parity (tools/pmc_dedup.sh W REPS full;
+tools/pmc_dedup_summary.py with CALLS = REPS + 1) for the HBM bytes: every
+dispatch after the last hash kernel is the dedup's.
 
 usage: dedup_full.py [--workload c5] [--files N] [--reps 5] [--existing K] [--errors F]"""
 import argparse
@@ -70,7 +71,7 @@ def device_keys(eng, torch, dev, sizes, ckeys, chunk, stream=0):
 
 
 def run(workload="c5", files=0, reps=5, existing=0, errors=0.0, parity=True, host_abi=True, sample=20000,
-        chunk=0, seed=17, log=print):
+        chunk=0, seed=17, ab="", log=print):
     import torch
 
     import bench
@@ -85,15 +86,17 @@ def run(workload="c5", files=0, reps=5, existing=0, errors=0.0, parity=True, hos
     eng = Engine(device=0)
     res = {"workload": workload.upper(), "files": n}
     try:
-        t0 = time.perf_counter()
-        d_keys = device_keys(eng, torch, dev, sizes, ckeys, chunk or CHUNK[workload])
-        res["keys_s"] = time.perf_counter() - t0
+        # every device input but the keys exists before the hash, so that under
+        # rocprofv3 every dispatch after the hash's last kernel is the dedup's
         rng = np.random.default_rng(seed)
         has = (sizes != 0).astype(np.uint8)  # mod.rs:78-86: an empty file has no cas_id
         status = np.where(rng.random(n) < errors, 5, 0).astype(np.int32) if errors else None
         d_has = torch.from_numpy(has).to(dev)
         d_status = torch.from_numpy(status).to(dev) if status is not None else None
         d_ids = torch.arange(n, dtype=torch.int64, device=dev)
+        t0 = time.perf_counter()
+        d_keys = device_keys(eng, torch, dev, sizes, ckeys, chunk or CHUNK[workload])
+        res["keys_s"] = time.perf_counter() - t0
         keys = d_keys.cpu().numpy().view(np.uint64) if (parity or existing) else None
         ex = np.zeros(0, np.uint64)
         if existing:  # existing Objects: keys of random files and keys nobody carries, in DB order
@@ -104,18 +107,35 @@ def run(workload="c5", files=0, reps=5, existing=0, errors=0.0, parity=True, hos
         log(f"[dedup_full] keys on the device in {res['keys_s']:.1f} s")
         stream = torch.cuda.Stream(dev)
         st = DeviceStages(eng, 0, same_stream=True)
-        ms = []
+        # A/B: settings (environment values the library reads per call)
+        # interleaved per rep; the last setting is the one reported
+        settings = [dict(kv.split("=") for kv in part.split("+")) for part in ab.replace("/", ",").split(",")] \
+            if ab else [{}]
+        per = {i: [] for i in range(len(settings))}
+        outs = {}
         link = counts = None
         with torch.cuda.stream(stream):
             for r in range(reps + 1):
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
-                link, counts = st.local(d_keys, d_has, d_status, d_ids, 100, d_ek, d_ei)
-                e1.record(stream)
-                e1.synchronize()
-                if r:  # the first call sizes the workspace
-                    ms.append(e0.elapsed_time(e1))
+                for i, env in enumerate(settings):
+                    os.environ.update(env)
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(stream)
+                    link, counts = st.local(d_keys, d_has, d_status, d_ids, 100, d_ek, d_ei)
+                    e1.record(stream)
+                    e1.synchronize()
+                    if r:  # the first call sizes the workspace
+                        per[i].append(e0.elapsed_time(e1))
+                    if r == reps and len(settings) > 1:
+                        outs[i] = (link.clone(), counts.clone())
         torch.cuda.synchronize()
+        ms = per[len(settings) - 1]
+        if len(settings) > 1:
+            res["ab"] = {"+".join(f"{k}={v}" for k, v in env.items()): {"ms_median": float(np.median(per[i])),
+                                                                      "ms_min": float(np.min(per[i]))}
+                         for i, env in enumerate(settings)}
+            l0, c0 = outs[0]
+            res["ab_equal"] = all(torch.equal(l0, l) and torch.equal(c0, c) for l, c in outs.values())
+            log(f"[dedup_full] A/B {res['ab']} equal {res['ab_equal']}")
         med = float(np.median(ms)) if ms else float("nan")
         algo = bench.dedup_bytes(n, ex.size)
         res.update({"existing": int(ex.size), "errors_frac": errors, "reps": reps, "ms_median": med,
@@ -165,10 +185,11 @@ def main():
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-host-abi", action="store_true")
     ap.add_argument("--chunk", type=int, default=0)
+    ap.add_argument("--ab", default="", help="A/B: 'N1=a+N2=b,N1=c' (or '/' for ',') settings interleaved per rep")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     res = run(a.workload, a.files, a.reps, a.existing, a.errors, not a.no_parity, not a.no_host_abi,
-              chunk=a.chunk, log=lambda s: print(s, file=sys.stderr, flush=True))
+              chunk=a.chunk, ab=a.ab, log=lambda s: print(s, file=sys.stderr, flush=True))
     line = json.dumps(res)
     print(line, flush=True)
     if a.out:

@@ -13,6 +13,7 @@
 #   pmcdedup=W[:ARGS]     tools/pmc_dedup.sh over tools/dedup_full.py or dedup_probe.py (ARGS: 'full' or probe flags)
 #   probe=ARGS            tools/dedup_probe.py ARGS (',' for ' '), OUT/probe_N.json
 #   jobbench[=ARGS]       tests/cpp/build/job_bench ARGS (',' for ' '; default 100000 files), OUT/job_bench.json
+#   trace=PY[,ARGS]       rocprofv3 --kernel-trace --stats -- python3 PY ARGS (',' for ' '), OUT/trace_N/
 #   cmd=TEXT              any command (',' for ' '), OUT/cmd_N.log, 600 s
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -61,6 +62,10 @@ step() {
       local a=${arg//,/ }
       timeout -k 10 600 tests/cpp/build/job_bench ${a:-100000} > "$OUT/job_bench_$n.json" 2> "$OUT/job_bench_$n.err"
       local rc=$?; tail -c 800 "$OUT/job_bench_$n.json"; return $rc ;;
+    trace)
+      (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/$OUT/trace_$n" -o trace \
+        --output-format csv -- python3 "$R"/${arg//,/ } > "$R/$OUT/trace_$n.log" 2>&1)
+      local rc=$?; tail -2 "$OUT/trace_$n.log" | cut -c1-300; return $rc ;;
     cmd)
       timeout -k 10 600 bash -c "${arg//,/ }" > "$OUT/cmd_$n.log" 2>&1
       local rc=$?; tail -5 "$OUT/cmd_$n.log"; return $rc ;;
