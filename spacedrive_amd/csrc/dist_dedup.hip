@@ -323,7 +323,7 @@ __global__ __launch_bounds__(64) void k_plan_walk(const uint64_t* __restrict__ s
   // re-read is the first candidate whose residue is the target
   // (cs - 1 - r) mod cs: a batch without it costs one compare and one
   // ballot, and each re-read moves the target down by one.
-  constexpr uint32_t kWalkU = 8;
+  constexpr uint32_t kWalkU = 16;
   const bool small = cs < (1ull << 32);
   uint64_t target = cs - 1;  // (cs - 1 - r) mod cs
   bool done = false;
@@ -346,12 +346,20 @@ __global__ __launch_bounds__(64) void k_plan_walk(const uint64_t* __restrict__ s
     // the valid range: the first entry of all, the last before padding or m
     const uint64_t p00 = __shfl(pv[0], 0);
     if (base == 0 && m && p00 < n_total) first = p00;
+    // every batch of the group is walked (no early exit: the register
+    // arrays must stay fully unrolled); batches past the end or past padding
+    // hold no candidate and move nothing
+    const uint32_t nu = min(kWalkU, (m - base + 63) / 64);
+    const uint32_t upad = pad ? (uint32_t)__builtin_ctz(pad) : kWalkU;  // first batch with padding
+    const uint32_t ulast = min(nu - 1, upad);                          // the last batch holding valid entries
 #pragma unroll
     for (uint32_t u = 0; u < kWalkU; ++u) {
-      if (done) break;
-      const uint32_t j = base + 64 * u + (uint32_t)lane;
-      const unsigned long long inm = __ballot(j < m && pv[u] < n_total);
-      if (inm) last_stay = __shfl(pv[u], 63 - __clzll((long long)inm));
+      if (u == ulast) {
+        const uint32_t j = base + 64 * u + (uint32_t)lane;
+        const unsigned long long inm = __ballot(j < m && pv[u] < n_total);
+        if (inm) last_stay = __shfl(pv[u], 63 - __clzll((long long)inm));
+        else if (u) last_stay = __shfl(pv[u - 1], 63);
+      }
       unsigned long long mask = __ballot(pm[u] == target);
       while (mask) {
         const int f = __ffsll((long long)mask) - 1;
@@ -360,8 +368,8 @@ __global__ __launch_bounds__(64) void k_plan_walk(const uint64_t* __restrict__ s
         target = target == 0 ? cs - 1 : target - 1;
         mask = __ballot(pm[u] == target && lane > f);
       }
-      if ((pad >> u) & 1u || base + 64 * (u + 1) >= m) done = true;
     }
+    if (pad || base + 64 * kWalkU >= m) done = true;
   }
   if (lane == 0) {
     const uint64_t T = max_steps ? max_steps : (n_total + cs - 1) / cs;
@@ -1078,7 +1086,13 @@ __device__ __forceinline__ uint64_t idx_key(const uint64_t* __restrict__ keys, c
 constexpr uint32_t kStayTile = 1024;
 static_assert(kStayTile % 64 == 0, "the insert's per-wave ballot add needs a wave's 64 rows in one tile");
 static_assert(kStayTile % TB == 0, "k_stays_write_t walks a tile in whole workgroups");
-constexpr uint32_t kStayScanTiles = 64;  // more tiles: k_tile_scan instead of per-writer sums
+// the tiles' counts are kept at two levels: per tile, and per group of
+// kStayGroup tiles (after the tile counts), so that a writer's offset is at
+// most nt / kStayGroup + kStayGroup - 1 counts (a plain sum over the tiles
+// before it cost tiles^2 reads: 50 M files with stays in every tile, 48 828
+// tiles: 433 us) and a batch without stays rows pays nothing
+constexpr uint32_t kStayGroup = 64;
+__host__ __device__ constexpr uint32_t stay_groups(uint32_t nt) { return (nt + kStayGroup - 1) / kStayGroup; }
 
 // files (emin null, base 0): pos[i] = slot, or the code of a file without
 // one; existing Objects (emin set, base n): min-fold eids[j] into emin[slot]
@@ -1110,8 +1124,13 @@ __global__ void k_solo_insert_idx(const uint64_t* __restrict__ keys, const uint6
     const bool has = has_key == nullptr || has_key[q];    // mod.rs:83-86
     if (stay_cnt) {
       const uint64_t bal = __ballot(!(ok && has));
-      if (bal && (threadIdx.x & 63) == (uint32_t)(__ffsll((long long)bal) - 1))
-        atomicAdd(&stay_cnt[q / kStayTile], (uint32_t)__popcll(bal));  // a wave's 64 rows share a tile
+      if (bal && (threadIdx.x & 63) == (uint32_t)(__ffsll((long long)bal) - 1)) {
+        // a wave's 64 rows share a tile; the tile's count, then its group's
+        // (kStayGroup tiles, after the nt tile counts)
+        const uint32_t nt = (count + kStayTile - 1) / kStayTile;
+        atomicAdd(&stay_cnt[q / kStayTile], (uint32_t)__popcll(bal));
+        atomicAdd(&stay_cnt[nt + q / (kStayTile * kStayGroup)], (uint32_t)__popcll(bal));
+      }
     }
     if (!(ok && has)) {
       pos[q] = !ok ? kSlotDropped : kSlotNoKey;
@@ -1290,35 +1309,35 @@ __global__ void k_counts_fold(unsigned long long* __restrict__ shard, unsigned l
 }
 
 // the stays rows of tile blockIdx.x (PER rows) in order, at the offset the
-// tiles before it add up to (only tiles holding one do any work). cnt holds
-// the tiles' counts (each writer sums the counts before its own: for a few
-// tiles) or, with `offs`, their exclusive offsets from k_tile_scan and the
-// total in *total (many tiles: summing would cost tiles^2 reads — 50 M files
-// with stays in every tile, 48 828 tiles: 433 us)
+// tiles before it add up to (only tiles holding one do any work): cnt holds
+// the gridDim.x tile counts and, after them, the counts of their groups of
+// kStayGroup tiles (the insert fills both), so the offset is the groups
+// before this tile's group plus the tiles before it in its group.
+// out32: the rows' indices; or, with ids (out64), their ordinals ids[i]
+// (the plan walk then reads a dense list, not ids[idx[j]])
 template <uint32_t PER>
 __global__ void __launch_bounds__(TB) k_stays_write_t(const uint8_t* __restrict__ has_key,
                                                       const int32_t* __restrict__ status, uint32_t n,
                                                       const uint32_t* __restrict__ cnt, uint32_t* __restrict__ out,
-                                                      const uint32_t* __restrict__ total) {
+                                                      const uint64_t* __restrict__ ids = nullptr,
+                                                      uint64_t* __restrict__ out64 = nullptr) {
   __shared__ uint32_t ws[TB / 64];
   const uint32_t b = blockIdx.x;
+  if (cnt[b] == 0) return;  // uniform over the workgroup
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t g = b / kStayGroup;
+  const uint32_t* gcnt = cnt + gridDim.x;
+  uint32_t s = 0;
+  for (uint32_t t = tid; t < g; t += TB) s += gcnt[t];
+  for (uint32_t t = g * kStayGroup + tid; t < b; t += TB) s += cnt[t];
+#pragma unroll
+  for (uint32_t d = 32; d; d >>= 1) s += __shfl_xor(s, d);
+  if (lane == 0) ws[wave] = s;
+  __syncthreads();
   uint32_t run = 0;
-  if (total) {
-    run = cnt[b];
-    if ((b + 1 < gridDim.x ? cnt[b + 1] : *total) == run) return;  // uniform over the workgroup
-  } else {
-    if (cnt[b] == 0) return;  // uniform over the workgroup
-    uint32_t s = 0;
-    for (uint32_t t = tid; t < b; t += TB) s += cnt[t];
 #pragma unroll
-    for (uint32_t d = 32; d; d >>= 1) s += __shfl_xor(s, d);
-    if (lane == 0) ws[wave] = s;
-    __syncthreads();
-#pragma unroll
-    for (uint32_t w = 0; w < TB / 64; ++w) run += ws[w];
-    __syncthreads();
-  }
+  for (uint32_t w = 0; w < TB / 64; ++w) run += ws[w];
+  __syncthreads();
   const uint64_t lo = (uint64_t)b * PER;
 #pragma unroll 1
   for (uint32_t r = 0; r < PER / TB; ++r) {
@@ -1335,50 +1354,12 @@ __global__ void __launch_bounds__(TB) k_stays_write_t(const uint8_t* __restrict_
       all += ws[w];
     }
     __syncthreads();
-    if (f) out[before + below] = (uint32_t)i;
+    if (f) {
+      if (out64) out64[before + below] = ids[i];
+      else out[before + below] = (uint32_t)i;
+    }
     run += all;
   }
-}
-
-// one workgroup: cnt[0..nt) <- exclusive prefix sums in place, *total <- the
-// sum; 16 counts per thread per pass (a pass covers 16 K tiles)
-constexpr uint32_t kScanR = 16;
-__global__ void __launch_bounds__(1024) k_tile_scan(uint32_t* __restrict__ cnt, uint32_t nt,
-                                                    uint32_t* __restrict__ total) {
-  __shared__ uint32_t ws[16];
-  __shared__ uint32_t carry;
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid == 0) carry = 0;
-  __syncthreads();
-  for (uint32_t base = 0; base < nt; base += 1024 * kScanR) {
-    const uint32_t i0 = base + tid * kScanR;
-    uint32_t v[kScanR], sum = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < kScanR; ++k) {
-      v[k] = i0 + k < nt ? cnt[i0 + k] : 0u;
-      sum += v[k];
-    }
-    uint32_t inc = sum;
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-      const uint32_t t = __shfl_up(inc, d);
-      if (lane >= d) inc += t;
-    }
-    if (lane == 63) ws[wave] = inc;
-    __syncthreads();
-    uint32_t run = carry;
-    for (uint32_t w = 0; w < wave; ++w) run += ws[w];
-    run += inc - sum;
-#pragma unroll
-    for (uint32_t k = 0; k < kScanR; ++k) {
-      if (i0 + k < nt) cnt[i0 + k] = run;
-      run += v[k];
-    }
-    __syncthreads();
-    if (tid == 1023) carry = run;
-    __syncthreads();
-  }
-  if (tid == 0) *total = carry;
 }
 
 // SDCAS_DEDUP_TABLE: "idx" (the default) = the compact u32 table, the
@@ -1461,9 +1442,10 @@ static hipError_t local_fused(DistWs& w, const uint64_t* keys, const uint8_t* ha
   const bool contig = ar && contig_ordinals() && n > 0;
   const bool entry = ne && exist_min_by_entry();
   const uint32_t sticky = entry ? n : kIdxEmpty;  // k_solo_insert_idx / the applies: entry mode from index n
-  if ((e = w.tmin.ensure(cap / 2 + 1)) || (e = w.tpos.ensure(n)) || (e = w.nstay.ensure(1)) ||
+  if ((e = w.tmin.ensure(cap / 2 + 1)) || (e = w.tpos.ensure(n)) ||
       (ne && (e = w.tkey.ensure(entry ? (uint64_t)ne + 2 : cap + 1))) ||
-      (e = w.stay_cnt.ensure(nt + 1)) || (stays && (e = w.stay_idx.ensure(n))) || (sharded && (e = shard_counts(w, st))) ||
+      (e = w.stay_cnt.ensure(nt + stay_groups(nt) + 1)) || (stays && (e = w.stay_sorted.ensure(n))) ||
+      (sharded && (e = shard_counts(w, st))) ||
       (contig && (e = w.flag.ensure(1))))
     return e;
   auto* tab = reinterpret_cast<uint32_t*>(w.tmin.p);
@@ -1471,7 +1453,7 @@ static hipError_t local_fused(DistWs& w, const uint64_t* keys, const uint8_t* ha
   const uint64_t tab_q = cap / 4, em_q = !ne ? 0 : entry ? ((uint64_t)ne + 1) / 2 : cap / 2;  // uint4 stores
   const uint32_t cg = (uint32_t)std::min<uint64_t>((tab_q + em_q + TB - 1) / TB, 2048);
   hipLaunchKernelGGL(k_local_clear, dim3(cg), dim3(TB), 0, st, reinterpret_cast<uint4*>(tab), tab_q,
-                     reinterpret_cast<uint4*>(em), em_q, w.stay_cnt.p, stays ? nt : 0u,
+                     reinterpret_cast<uint4*>(em), em_q, w.stay_cnt.p, stays ? nt + stay_groups(nt) : 0u,
                      contig ? w.flag.p : (uint32_t*)nullptr);
   if (ne)
     hipLaunchKernelGGL(k_solo_insert_idx, dim3(blocks(ne)), dim3(TB), 0, st, keys, ekeys, n, (const uint8_t*)nullptr,
@@ -1481,18 +1463,15 @@ static hipError_t local_fused(DistWs& w, const uint64_t* keys, const uint8_t* ha
                      contig ? ids : (const uint64_t*)nullptr, n, 0u, tab, (unsigned long long*)nullptr, mask, shift,
                      w.tpos.p, stays ? w.stay_cnt.p : (uint32_t*)nullptr, contig ? w.flag.p : (uint32_t*)nullptr,
                      sticky);
-  // many tiles: one scan turns the counts into offsets (the writers then
-  // read their own, the walk the total) instead of each writer summing the
-  // tiles before it
-  const bool scan = stays && nt > kStayScanTiles;
-  if (scan) hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, st, w.stay_cnt.p, nt, w.nstay.p);
+  // the stays rows' ordinals, dense, for the walk (stay_sorted: dd_plan's
+  // buffer, free in a world of one); the walk's count is the groups' sum
   if (stays)
     hipLaunchKernelGGL(k_stays_write_t<kStayTile>, dim3(nt), dim3(TB), 0, st, has_key, status, n, w.stay_cnt.p,
-                       w.stay_idx.p, scan ? (const uint32_t*)w.nstay.p : (const uint32_t*)nullptr);
-  hipLaunchKernelGGL(k_plan_walk, dim3(1), dim3(64), 0, st, (const uint64_t*)nullptr, w.stay_idx.p, ids,
-                     stays ? n : 0u, scan ? (const uint32_t*)w.nstay.p : (const uint32_t*)nullptr,
-                     win.n_total ? win.n_total : (uint64_t)n, cs, win.max_steps, win.more, w.plan.p,
-                     stays && !scan ? w.stay_cnt.p : (const uint32_t*)nullptr, nt);
+                       w.stay_idx.p, ids, w.stay_sorted.p);
+  hipLaunchKernelGGL(k_plan_walk, dim3(1), dim3(64), 0, st, (const uint64_t*)w.stay_sorted.p, (const uint32_t*)nullptr,
+                     ids, stays ? n : 0u, (const uint32_t*)nullptr, win.n_total ? win.n_total : (uint64_t)n, cs,
+                     win.max_steps, win.more, w.plan.p, stays ? w.stay_cnt.p + nt : (const uint32_t*)nullptr,
+                     stay_groups(nt));
   const uint64_t* emp = ne ? w.tkey.p : nullptr;
   auto apply = [&](auto kern, uint32_t r) {
     const uint32_t g = (uint32_t)(((uint64_t)n + (uint64_t)TB * r - 1) / ((uint64_t)TB * r));

@@ -331,9 +331,9 @@ def test_device_local_stays_in_partial_last_tile(eng, oracle, n, chunk_size):
     """stays rows (no cas_id, and errored) in the last, partial stays tile
     (kStayTile = 1024 rows, dist_dedup.hip): the insert counts them per tile,
     the writer places them after the tiles before, the plan walk sums every
-    tile — the round-5 hazard was those three disagreeing on the tile (past
-    64 tiles the counts go through k_tile_scan and the writers read offsets:
-    n = 300 K). The
+    tile — the round-5 hazard was those three disagreeing on the tile (the
+    counts are kept per tile and per group of 64 tiles: n = 300 K spans five
+    groups). The
     last rows are stays rows at step ends, so a miscounted tile shows as
     DEFERRED or missing re-reads; every link, both counts and the plan's
     steps / rows / rereads against the oracle's literal step loop"""
