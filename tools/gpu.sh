@@ -9,7 +9,7 @@
 #   smoke                 __graft_entry__.smoke()
 #   bench=W[:STEPS:WARM]  bench.py --workload W (c2 c3 c4 c5), OUT/bench_W.json
 #   stats=W               rocprofv3 --kernel-trace --stats of a short bench.py W run, OUT/stats_W/
-#   dedupfull=W[:ARGS]    tools/dedup_full.py --workload W (ARGS: extra flags, ',' for ' '), OUT/dedup_full_W.json
+#   dedupfull=W[:ARGS]    tools/dedup_full.py --workload W (ARGS: extra flags, ',' for ' '), OUT/dedup_full_W_N.json
 #   pmcdedup=W[:ARGS]     tools/pmc_dedup.sh over tools/dedup_full.py or dedup_probe.py (ARGS: 'full' or probe flags)
 #   probe=ARGS            tools/dedup_probe.py ARGS (',' for ' '), OUT/probe_N.json
 #   jobbench[=ARGS]       tests/cpp/build/job_bench ARGS (',' for ' '; default 100000 files), OUT/job_bench.json
@@ -49,9 +49,9 @@ step() {
         > "$R/$OUT/stats_$arg.json" 2> "$R/$OUT/stats_$arg.err") ;;
     dedupfull)
       IFS=: read -r w rest <<< "$arg"
-      timeout -k 10 900 python -u tools/dedup_full.py --workload "$w" ${rest//,/ } --out "$OUT/dedup_full_$w.json" \
-        > "$OUT/dedup_full_$w.log" 2>&1
-      local rc=$?; tail -3 "$OUT/dedup_full_$w.log" | cut -c1-400; return $rc ;;
+      timeout -k 10 900 python -u tools/dedup_full.py --workload "$w" ${rest//,/ } --out "$OUT/dedup_full_${w}_$n.json" \
+        > "$OUT/dedup_full_${w}_$n.log" 2>&1
+      local rc=$?; tail -3 "$OUT/dedup_full_${w}_$n.log" | cut -c1-400; return $rc ;;
     pmcdedup)
       IFS=: read -r w rest <<< "$arg"
       bash tools/pmc_dedup.sh "$OUT/pmc_dedup_$w" "$w" 3 ${rest//,/ } ;;
