@@ -371,10 +371,15 @@ int sdcas_dev_dedup_apply(sdcas_ctx *ctx, const uint64_t *d_ids, const uint32_t 
  * int64) = its valid records, d_slot[i] = the bucket position r * cap + p of
  * file i, and sets *d_overflow (device u32) to 1 when some owner has
  * more than cap records (the buckets are then unusable: rerun the exact
- * stages). resolve_buckets answers the received buckets (world x fcap file
- * records, world x ecap existing records, the first d_fcounts[r] /
- * d_ecounts[r] of bucket r valid) into d_result[world * fcap], bucket layout;
- * apply then reads the answers returned in the same layout. */
+ * stages). The bucket combine may send several records of one key (one per
+ * key per 2048-file tile of the rank, each with the tile's lowest ordinal);
+ * the owner's minimum covers them. resolve_buckets answers the received
+ * buckets (world x fcap file records, world x ecap existing records, the
+ * first d_fcounts[r] / d_ecounts[r] of bucket r valid) into
+ * d_result[world * fcap], bucket layout, and uses the received buckets as
+ * scratch: the value word of valid records may be overwritten (each key's
+ * claiming record takes the key's minimum). apply then reads the answers
+ * returned in the same layout. */
 int sdcas_dev_dedup_combine_buckets(sdcas_ctx *ctx, const uint64_t *d_keys, const uint8_t *d_has_key,
                                     const int32_t *d_status, const uint64_t *d_ids, size_t n, uint32_t world,
                                     size_t cap, uint64_t *d_send, uint32_t *d_slot, int64_t *d_counts,

@@ -565,6 +565,128 @@ __global__ void __launch_bounds__(TB) k_cb_emit(const uint64_t* __restrict__ key
   }
 }
 
+// ---- round 6: the bucket combine without a rank-side hash table -------------------
+//
+// The bucket protocol's owner resolve takes the minimum over every record of
+// a key (records of one key from several ranks, and now from several tiles
+// of one rank), so the rank side need not reduce to one record per key: each
+// workgroup pre-aggregates its own tile of kTileN files in LDS (the Zipf
+// head's copies in a tile collapse to one record) and sends one (key, lowest
+// ordinal in the tile) record per distinct key of the tile to its owner's
+// bucket. One pass over the files, all of its probing in LDS, instead of the
+// global table's clear, insert, emit and slot passes (C5 at world 8: 0.50 ms
+// of one rank's 0.89 ms), for more records in the exchange and at the owner.
+constexpr uint32_t kTileR = 8, kTileN = TB * kTileR;  // 2048 files per workgroup
+constexpr uint32_t kTileSlots = 2 * kTileN;            // the LDS table's slots (local indices)
+
+__device__ __forceinline__ uint32_t tile_hash(uint64_t key) {
+  return ((uint32_t)(key ^ (key >> 32)) * 0x9E3779B1u) >> (32 - 12);  // 12 bits: kTileSlots
+}
+static_assert(kTileSlots == 1u << 12, "tile_hash takes 12 bits");
+
+// fill[0..world] and the overflow flag zeroed in one launch (two memsets
+// were two). The owners' valid counts come from k_cb_counts after the tiles:
+// a last-workgroup-writes-them pattern measured 113 -> 540 us for the tile
+// kernel on C5 at world 8 — every workgroup's device-scope release fence
+// writes back its XCD's L2 (profiles/r06_dedup_world.json)
+__global__ void k_cb_prep(uint32_t* __restrict__ fill, uint32_t world, uint32_t* __restrict__ overflow) {
+  for (uint32_t t = threadIdx.x; t <= world; t += blockDim.x) fill[t] = 0;
+  if (threadIdx.x == 0) *overflow = 0;
+}
+
+__global__ void __launch_bounds__(TB) k_cb_tile(const uint64_t* __restrict__ keys, const uint8_t* __restrict__ has_key,
+                                                const int32_t* __restrict__ status, const uint64_t* __restrict__ ids,
+                                                uint32_t n, uint32_t world, uint32_t cap, uint32_t* __restrict__ fill,
+                                                uint64_t* __restrict__ send, uint32_t* __restrict__ slot,
+                                                uint32_t* __restrict__ overflow) {
+  __shared__ uint64_t skey[kTileN];
+  __shared__ uint32_t tab[kTileSlots];
+  __shared__ uint32_t spos[kTileN];
+  __shared__ uint32_t s_cnt[kEmitMaxWorld], s_base[kEmitMaxWorld];
+  const uint32_t tid = threadIdx.x;
+  const bool lds = world <= kEmitMaxWorld;
+  for (uint32_t t = tid; lds && t < world; t += TB) s_cnt[t] = 0;
+  for (uint32_t t = tid; t < kTileSlots; t += TB) tab[t] = kIdxEmpty;
+  const uint64_t tile0 = (uint64_t)blockIdx.x * kTileN;
+  // code: the file's LDS slot (keyed), or its slot code (no key / dropped)
+  uint32_t code[kTileR];
+#pragma unroll
+  for (uint32_t k = 0; k < kTileR; ++k) {
+    const uint32_t t = k * TB + tid;
+    const uint64_t i = tile0 + t;
+    code[k] = kSlotDropped;
+    if (i < n) {
+      const bool ok = status == nullptr || status[i] == 0;  // mod.rs:125-141
+      const bool has = has_key == nullptr || has_key[i];    // mod.rs:83-86
+      skey[t] = keys[i];
+      code[k] = !ok ? kSlotDropped : !has ? kSlotNoKey : 0u;
+    }
+  }
+  __syncthreads();
+  // the tile's table: each key's slot holds its lowest local index (local
+  // order is ordinal order), the key read back from skey
+#pragma unroll
+  for (uint32_t k = 0; k < kTileR; ++k) {
+    if (code[k] != 0u) continue;
+    const uint32_t t = k * TB + tid;
+    const uint64_t key = skey[t];
+    uint32_t h = tile_hash(key);
+    for (;;) {
+      uint32_t cur = tab[h];
+      if (cur == kIdxEmpty) {
+        const uint32_t prev = atomicCAS(&tab[h], kIdxEmpty, t);
+        if (prev == kIdxEmpty) break;
+        cur = prev;
+      }
+      if (skey[cur] == key) {
+        if (cur > t) atomicMin(&tab[h], t);
+        break;
+      }
+      h = (h + 1) & (kTileSlots - 1);
+    }
+    code[k] = h;
+  }
+  __syncthreads();
+  // each key's lowest file of the tile carries the record: a position in its
+  // owner's bucket per workgroup (LDS counters, one global atomic per owner)
+  uint32_t lp[kTileR], own[kTileR];
+#pragma unroll
+  for (uint32_t k = 0; k < kTileR; ++k) {
+    const uint32_t t = k * TB + tid;
+    lp[k] = ~0u;
+    own[k] = 0;
+    if (code[k] < kTileSlots && tab[code[k]] == t) {
+      own[k] = dd_owner(skey[t], world);
+      lp[k] = lds ? atomicAdd(&s_cnt[own[k]], 1u) : atomicAdd(&fill[own[k]], 1u);
+    }
+  }
+  __syncthreads();
+  for (uint32_t t = tid; lds && t < world; t += TB) s_base[t] = s_cnt[t] ? atomicAdd(&fill[t], s_cnt[t]) : 0u;
+  __syncthreads();
+#pragma unroll
+  for (uint32_t k = 0; k < kTileR; ++k) {
+    if (lp[k] == ~0u) continue;
+    const uint32_t t = k * TB + tid;
+    const uint32_t p = (lds ? s_base[own[k]] : 0u) + lp[k];
+    if (p >= cap) {
+      atomicOr(overflow, 1u);  // the caller reruns the exact stages
+      spos[t] = kSlotNoKey;
+      continue;
+    }
+    const uint64_t q = (uint64_t)own[k] * cap + p;
+    send[2 * q] = skey[t];
+    send[2 * q + 1] = ids[tile0 + t];
+    spos[t] = (uint32_t)q;
+  }
+  if (!slot) return;
+  __syncthreads();
+#pragma unroll
+  for (uint32_t k = 0; k < kTileR; ++k) {
+    const uint64_t i = tile0 + k * TB + tid;
+    if (i < n) slot[i] = code[k] < kTileSlots ? spos[tab[code[k]]] : code[k];
+  }
+}
+
 // one workgroup: starts[0..world] = the exclusive prefix of cnt[0..world)
 __global__ void __launch_bounds__(1024) k_owner_starts(const uint32_t* __restrict__ cnt, uint32_t world,
                                                        uint32_t* __restrict__ starts) {
@@ -867,6 +989,98 @@ __global__ void k_rb_insert_idx(const uint64_t* __restrict__ frec, const uint64_
   if (pos_out) pos_out[q] = h | (claimed ? kPosClaimed : 0u);
 }
 
+// Round 6 ("rec", the default): the other records of a key fold their value
+// into the CLAIMING record's own value field (the received buckets are the
+// protocol's scratch) instead of a side minimum per table slot, so there is
+// no minima array to clear (C5 at world 8: cap u64 = 128 MiB per call) and the
+// answer reads one record. A file record whose claimer is an existing Object
+// folds nothing (the key's answer is the existing minimum); existing records
+// are inserted first and fold into their existing claimer.
+__global__ void k_rb_insert_rec(uint64_t* __restrict__ frec, uint64_t* __restrict__ erec, uint32_t nf, uint32_t bcap,
+                                const int64_t* __restrict__ counts, uint32_t total, uint32_t base,
+                                uint32_t* __restrict__ tab, const uint32_t* __restrict__ cfg,
+                                uint32_t* __restrict__ pos_out) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= total) return;
+  const uint32_t r = q / bcap, p = q - r * bcap;
+  if ((int64_t)p >= counts[r]) {
+    if (pos_out) pos_out[q] = kNoEntry;
+    return;
+  }
+  const uint32_t mask = cfg[0], shift = cfg[1];
+  const uint32_t x = base + q;
+  const uint64_t* me = rb_rec(frec, erec, nf, x);
+  const uint64_t key = me[0];
+  uint32_t h = mask + 1;  // the all-ones key's own entry
+  uint32_t cur = kIdxEmpty;
+  if (key != kEmptyKey) {
+    h = (uint32_t)((key << kOwnerBits) >> shift) & mask;  // below the owner bits (ht_find)
+    for (;;) {
+      cur = __hip_atomic_load(&tab[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cur == kIdxEmpty) {
+        cur = atomicCAS(&tab[h], kIdxEmpty, x);
+        if (cur == kIdxEmpty) break;  // claimed
+      }
+      if (rb_rec(frec, erec, nf, cur)[0] == key) break;
+      h = (h + 1) & mask;
+    }
+  } else {
+    cur = atomicCAS(&tab[h], kIdxEmpty, x);
+  }
+  const bool claimed = cur == kIdxEmpty;
+  // fold into the claimer's value (same domain only: files into a file
+  // claimer, existing Objects into an existing claimer)
+  if (!claimed && (cur >= nf) == (x >= nf)) {
+    unsigned long long* m = reinterpret_cast<unsigned long long*>(
+        const_cast<uint64_t*>(rb_rec(frec, erec, nf, cur)) + 1);
+    const unsigned long long v = me[1];
+    if (__hip_atomic_load(m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > v) atomicMin(m, v);
+  }
+  if (pos_out) pos_out[q] = h | (claimed ? kPosClaimed : 0u);
+}
+
+__global__ void k_rb_answer_rec(const uint32_t* __restrict__ pos, uint32_t nf, const uint64_t* __restrict__ frec,
+                                const uint64_t* __restrict__ erec, const uint32_t* __restrict__ tab,
+                                int64_t* __restrict__ result) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nf) return;
+  const uint32_t hp = pos[q];
+  if (hp == kNoEntry) return;  // padding: nobody reads its answer
+  const uint32_t c = (hp & kPosClaimed) ? q : tab[hp & ~kPosClaimed];
+  const uint64_t v = rb_rec(frec, erec, nf, c)[1];  // the claimer's value: the key's minimum
+  // mod.rs:202-238: the first existing Object (an existing claimer); else
+  // the key's first file (mod.rs:246-254)
+  result[q] = c >= nf ? -(int64_t)v - 1 : (int64_t)v;
+}
+
+// the table's size from the valid counts (as k_rb_size, computed by every
+// workgroup; workgroup 0 stores it in cfg for the inserts), then its clear:
+// one launch
+__global__ void k_rb_clear_tab(uint32_t* __restrict__ tab, const int64_t* __restrict__ fcounts,
+                               const int64_t* __restrict__ ecounts, uint32_t world, uint32_t* __restrict__ cfg) {
+  __shared__ uint64_t s_cap;
+  if (threadIdx.x < 64) {
+    uint64_t s = 0;
+    for (uint32_t r = threadIdx.x; r < world; r += 64)
+      s += (uint64_t)fcounts[r] + (ecounts ? (uint64_t)ecounts[r] : 0ull);
+#pragma unroll
+    for (int d = 32; d; d >>= 1) s += __shfl_xor(s, d);
+    if (threadIdx.x == 0) {
+      uint64_t cap = 1024;
+      while (cap < 2 * s) cap <<= 1;
+      s_cap = cap;
+      if (blockIdx.x == 0) {
+        cfg[0] = (uint32_t)(cap - 1);
+        cfg[1] = 64u - (uint32_t)__builtin_ctzll(cap);
+      }
+    }
+  }
+  __syncthreads();
+  const uint64_t m = s_cap + 1;
+  for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < m; q += (uint64_t)gridDim.x * blockDim.x)
+    tab[q] = kIdxEmpty;
+}
+
 __global__ void k_rb_answer_idx(const uint32_t* __restrict__ pos, uint32_t nf, const uint64_t* __restrict__ frec,
                                 const uint64_t* __restrict__ erec, const uint32_t* __restrict__ tab,
                                 const uint64_t* __restrict__ vmin, const uint64_t* __restrict__ emin,
@@ -904,12 +1118,13 @@ __global__ void k_rb_clear_idx(uint32_t* __restrict__ tab, unsigned long long* _
 // SDCAS_RESOLVE: "idx" (the default, above), "kv" = round 5's 16-byte (key,
 // files' minimum) entries sized on the device, "split" = round 4's key array
 // + minima pairs sized from the buckets' capacity (A/B)
-enum ResolveTable { kResolveIdx = 0, kResolveKv = 1, kResolveSplit = 2 };
+enum ResolveTable { kResolveIdx = 0, kResolveKv = 1, kResolveSplit = 2, kResolveRec = 3 };
 static ResolveTable resolve_table() {
   const char* v = getenv("SDCAS_RESOLVE");
   if (v && strcmp(v, "split") == 0) return kResolveSplit;
   if (v && strcmp(v, "kv") == 0) return kResolveKv;
-  return kResolveIdx;
+  if (v && strcmp(v, "idx") == 0) return kResolveIdx;
+  return kResolveRec;
 }
 
 hipError_t dd_resolve_buckets(DistWs& w, const uint64_t* frec, uint32_t fcap, const int64_t* fcounts,
@@ -922,7 +1137,24 @@ hipError_t dd_resolve_buckets(DistWs& w, const uint64_t* frec, uint32_t fcap, co
   while (cap < 2 * ((uint64_t)nf + ne)) cap <<= 1;
   if (cap > (1ull << 31)) return hipErrorInvalidValue;
   ResolveTable rt = resolve_table();
-  if (rt == kResolveIdx && cap > (1ull << 30)) rt = kResolveKv;  // tpos' claimed bit needs slots below 2^31
+  if ((rt == kResolveIdx || rt == kResolveRec) && cap > (1ull << 30)) rt = kResolveKv;  // tpos' claimed bit: slots < 2^31
+  if (rt == kResolveRec) {
+    // the received buckets' value fields take the minima (sdcas.h: resolve_buckets)
+    if ((e = w.tmin.ensure(cap / 2 + 1)) || (e = w.tpos.ensure(nf)) || (e = w.starts.ensure(2))) return e;
+    auto* tab = reinterpret_cast<uint32_t*>(w.tmin.p);
+    auto* fr = const_cast<uint64_t*>(frec);
+    auto* er = const_cast<uint64_t*>(erec);
+    const uint32_t cg = (uint32_t)std::min<uint64_t>((cap + 1 + TB - 1) / TB, 2048);
+    hipLaunchKernelGGL(k_rb_clear_tab, dim3(cg), dim3(TB), 0, st, tab, fcounts, ne ? ecounts : nullptr, world,
+                       w.starts.p);
+    if (ne)
+      hipLaunchKernelGGL(k_rb_insert_rec, dim3(blocks(ne)), dim3(TB), 0, st, fr, er, nf, ecap, ecounts, ne, nf, tab,
+                         w.starts.p, (uint32_t*)nullptr);
+    hipLaunchKernelGGL(k_rb_insert_rec, dim3(blocks(nf)), dim3(TB), 0, st, fr, er, nf, fcap, fcounts, nf, 0u, tab,
+                       w.starts.p, w.tpos.p);
+    hipLaunchKernelGGL(k_rb_answer_rec, dim3(blocks(nf)), dim3(TB), 0, st, w.tpos.p, nf, frec, erec, tab, result);
+    return hipGetLastError();
+  }
   if (rt == kResolveIdx) {
     // tmin holds the u32 table (cap + 1 u32 in its first cap + 1 u64) and
     // the existing minima; tkey the files' minima
@@ -1777,12 +2009,31 @@ static hipError_t combine_core(DistWs& w, const uint64_t* keys, const uint8_t* h
   return hipGetLastError();
 }
 
+// SDCAS_COMBINE=hash: the bucket combine through the rank's global table
+// (round 5: one record per key) instead of the per-tile LDS pre-aggregation
+// (the default), read per call (A/B in one process)
+static bool combine_by_tile() {
+  const char* v = getenv("SDCAS_COMBINE");
+  return !(v && strcmp(v, "hash") == 0);
+}
+
 hipError_t dd_combine_buckets(DistWs& w, const uint64_t* keys, const uint8_t* has_key, const int32_t* status,
                               const uint64_t* ids, uint32_t n, uint32_t world, uint32_t cap, uint64_t* send,
                               uint32_t* slot, int64_t* counts, uint32_t* overflow, hipStream_t st) {
   hipError_t e;
+  if (n == 0) {
+    if ((e = hipMemsetAsync(overflow, 0, sizeof(uint32_t), st))) return e;
+    return hipMemsetAsync(counts, 0, sizeof(int64_t) * world, st);
+  }
+  if (combine_by_tile()) {
+    if ((e = w.ocnt.ensure(world + 1))) return e;
+    hipLaunchKernelGGL(k_cb_prep, dim3(1), dim3(TB), 0, st, w.ocnt.p, world, overflow);
+    hipLaunchKernelGGL(k_cb_tile, dim3((n + kTileN - 1) / kTileN), dim3(TB), 0, st, keys, has_key, status, ids, n,
+                       world, cap, w.ocnt.p, send, slot, overflow);
+    hipLaunchKernelGGL(k_cb_counts, dim3(blocks(world)), dim3(TB), 0, st, w.ocnt.p, world, cap, counts);
+    return hipGetLastError();
+  }
   if ((e = hipMemsetAsync(overflow, 0, sizeof(uint32_t), st))) return e;
-  if (n == 0) return hipMemsetAsync(counts, 0, sizeof(int64_t) * world, st);
   if ((e = combine_table(w, keys, has_key, status, n, world, st))) return e;
   hipLaunchKernelGGL(k_cb_emit, dim3(emit_grid(n)), dim3(TB), 0, st, keys, ids, n, w.idx_b.p, w.idx_a.p, world, cap,
                      (const uint32_t*)nullptr, 0u, w.ocnt.p, send, w.tpos.p, overflow);

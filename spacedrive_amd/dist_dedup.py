@@ -158,6 +158,14 @@ class DeviceStages:
         self.eng._check(rc, "sdcas_dev_dedup_plan")
         return plan
 
+    @property
+    def combine_tiles(self):
+        """the bucket combine pre-aggregates per 2048-file tile (the default;
+        SDCAS_COMBINE=hash: one record per key through the rank's table): its
+        buckets hold up to one record per key per tile, more than the exact
+        combine's one per key"""
+        return os.environ.get("SDCAS_COMBINE", "") != "hash"
+
     def combine_buckets(self, keys, has_key, status, ids, world, cap, need_slot=True):
         """-> (send int64[world * cap, 2], slot int32[n] or None, counts int64[world],
         overflow int32[1]), all on the device, no host synchronisation"""
@@ -422,7 +430,12 @@ def _dedup_exact(stages, world, keys, has_key, status, ids, chunk_size, existing
     dist.all_reduce(fills, op=dist.ReduceOp.MAX, group=group)
     c, f = cnt.tolist(), fills.tolist()
     if hasattr(stages, "combine_buckets"):
-        _learn(stages, win, f[0], f[1], f[2])
+        # the exact combine's fills are one record per key; a bucket combine
+        # that pre-aggregates per tile sends up to one per key per tile: learn
+        # at least the first call's even split of the files then
+        tiles = getattr(stages, "combine_tiles", False)
+        _learn(stages, win, max(f[0], win["max_n"] // world) if tiles else f[0],
+               max(f[1], win["max_ne"] // world) if tiles else f[1], f[2])
     return link, int(c[0]), int(c[1])
 
 

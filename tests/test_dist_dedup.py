@@ -768,14 +768,18 @@ def test_meta_group_of_a_subgroup():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("combine", ["hash", "hash-kv", "hash-split", "hash-r0", "hash-r1"])
+@pytest.mark.parametrize("combine", ["tile", "tile-idx", "tile-kv", "tile-split", "tile-r0", "tile-r1", "hash",
+                                     "hash-idx"])
 @pytest.mark.parametrize("R,chunk_size", [(2, 100), (8, 100), (5, 7)])
 def test_device_bucket_protocol_vs_oracle(eng, oracle, R, chunk_size, combine, monkeypatch):
     """the bucket protocol's device stages (combine_buckets -> equal-split
     exchange -> resolve_buckets -> apply) over R virtual ranks with existing
-    Objects, the hash-table combine and every resolve: the owner's resolve
-    in a u32 table of claiming record indices sized on the device from the
-    valid counts (the default), round 5's 16-byte (key, minimum) entries
+    Objects, both combines — round 6's per-tile LDS pre-aggregation (the
+    default: a key may take one record per 2048-file tile) and round 5's
+    global hash table (SDCAS_COMBINE=hash, one record per key) — and every
+    resolve: the owner's u32 claim table folding the other records' values
+    into the claiming record (the default), the same table with per-slot side
+    minima (SDCAS_RESOLVE=idx), round 5's 16-byte (key, minimum) entries
     (SDCAS_RESOLVE=kv) and round 4's tables sized from the buckets' capacity
     (SDCAS_RESOLVE=split); the
     apply with 4 files per thread (the default), round 5's grid-stride apply
@@ -784,10 +788,12 @@ def test_device_bucket_protocol_vs_oracle(eng, oracle, R, chunk_size, combine, m
     exact stages)"""
     from spacedrive_amd.dist_dedup import DeviceStages
     from tests._dist_stages import dedup_virtual_buckets
-    if combine in ("hash-split", "hash-kv"):
-        monkeypatch.setenv("SDCAS_RESOLVE", combine[len("hash-"):])
-    elif combine.startswith("hash-r"):
-        monkeypatch.setenv("SDCAS_APPLY_R", combine[len("hash-r"):])
+    comb, _, knob = combine.partition("-")
+    monkeypatch.setenv("SDCAS_COMBINE", comb)
+    if knob in ("split", "kv", "idx"):
+        monkeypatch.setenv("SDCAS_RESOLVE", knob)
+    elif knob.startswith("r"):
+        monkeypatch.setenv("SDCAS_APPLY_R", knob[1:])
     keys, has, status, existing = make_corpus(700 + R, 24000, pool=5000, p_none=0.05, p_err=0.05)
     # the all-ones key (the tables' empty marker, a legal cas key) on several
     # files and ranks, once with an existing Object

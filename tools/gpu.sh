@@ -9,12 +9,12 @@
 #   smoke                 __graft_entry__.smoke()
 #   bench=W[:STEPS:WARM]  bench.py --workload W (c2 c3 c4 c5), OUT/bench_W.json
 #   stats=W               rocprofv3 --kernel-trace --stats of a short bench.py W run, OUT/stats_W/
-#   dedupfull=W[:ARGS]    tools/dedup_full.py --workload W (ARGS: extra flags, ',' for ' '), OUT/dedup_full_W_N.json
+#   dedupfull=W[:ARGS]    tools/dedup_full.py --workload W (ARGS: extra flags, '~' for ' '), OUT/dedup_full_W_N.json
 #   pmcdedup=W[:ARGS]     tools/pmc_dedup.sh over tools/dedup_full.py or dedup_probe.py (ARGS: 'full' or probe flags)
-#   probe=ARGS            tools/dedup_probe.py ARGS (',' for ' '), OUT/probe_N.json
-#   jobbench[=ARGS]       tests/cpp/build/job_bench ARGS (',' for ' '; default 100000 files), OUT/job_bench.json
-#   trace=PY[,ARGS]       rocprofv3 --kernel-trace --stats -- python3 PY ARGS (',' for ' '), OUT/trace_N/
-#   cmd=TEXT              any command (',' for ' '), OUT/cmd_N.log, 600 s
+#   probe=ARGS            tools/dedup_probe.py ARGS ('~' for ' '), OUT/probe_N.json
+#   jobbench[=ARGS]       tests/cpp/build/job_bench ARGS ('~' for ' '; default 100000 files), OUT/job_bench.json
+#   trace=PY[~ARGS]       rocprofv3 --kernel-trace --stats -- python3 PY ARGS ('~' for ' '), OUT/trace_N/
+#   cmd=TEXT              any command ('~' for ' '), OUT/cmd_N.log, 600 s
 set -o pipefail
 cd "$(dirname "$0")/.."
 OUT=$1
@@ -49,25 +49,25 @@ step() {
         > "$R/$OUT/stats_$arg.json" 2> "$R/$OUT/stats_$arg.err") ;;
     dedupfull)
       IFS=: read -r w rest <<< "$arg"
-      timeout -k 10 900 python -u tools/dedup_full.py --workload "$w" ${rest//,/ } --out "$OUT/dedup_full_${w}_$n.json" \
+      timeout -k 10 900 python -u tools/dedup_full.py --workload "$w" ${rest//\~/ } --out "$OUT/dedup_full_${w}_$n.json" \
         > "$OUT/dedup_full_${w}_$n.log" 2>&1
       local rc=$?; tail -3 "$OUT/dedup_full_${w}_$n.log" | cut -c1-400; return $rc ;;
     pmcdedup)
       IFS=: read -r w rest <<< "$arg"
-      bash tools/pmc_dedup.sh "$OUT/pmc_dedup_$w" "$w" 3 ${rest//,/ } ;;
+      bash tools/pmc_dedup.sh "$OUT/pmc_dedup_$w" "$w" 3 ${rest//\~/ } ;;
     probe)
-      timeout -k 10 600 python -u tools/dedup_probe.py ${arg//,/ } > "$OUT/probe_$n.json" 2> "$OUT/probe_$n.err"
+      timeout -k 10 600 python -u tools/dedup_probe.py ${arg//\~/ } > "$OUT/probe_$n.json" 2> "$OUT/probe_$n.err"
       local rc=$?; cut -c1-600 "$OUT/probe_$n.json"; return $rc ;;
     jobbench)
-      local a=${arg//,/ }
+      local a=${arg//\~/ }
       timeout -k 10 600 tests/cpp/build/job_bench ${a:-100000} > "$OUT/job_bench_$n.json" 2> "$OUT/job_bench_$n.err"
       local rc=$?; tail -c 800 "$OUT/job_bench_$n.json"; return $rc ;;
     trace)
       (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/$OUT/trace_$n" -o trace \
-        --output-format csv -- python3 "$R"/${arg//,/ } > "$R/$OUT/trace_$n.log" 2>&1)
+        --output-format csv -- python3 "$R"/${arg//\~/ } > "$R/$OUT/trace_$n.log" 2>&1)
       local rc=$?; tail -2 "$OUT/trace_$n.log" | cut -c1-300; return $rc ;;
     cmd)
-      timeout -k 10 600 bash -c "${arg//,/ }" > "$OUT/cmd_$n.log" 2>&1
+      timeout -k 10 600 bash -c "${arg//\~/ }" > "$OUT/cmd_$n.log" 2>&1
       local rc=$?; tail -5 "$OUT/cmd_$n.log"; return $rc ;;
     *) echo "unknown step $s"; return 2 ;;
   esac
