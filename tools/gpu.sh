@@ -8,7 +8,9 @@
 #   tests[=EXPR]          pytest -m gpu (EXPR: a -k expression), OUT/pytest_gpu[_EXPR].log
 #   smoke                 __graft_entry__.smoke()
 #   bench=W[:STEPS:WARM]  bench.py --workload W (c2 c3 c4 c5), OUT/bench_W.json
-#   stats=W               rocprofv3 --kernel-trace --stats of a short bench.py W run, OUT/stats_W/
+#   stats=W               rocprofv3 --kernel-trace --stats of a bench.py W run (20 steps, no baselines), OUT/stats_W/
+#   n8=W                  bench.py --gpus 8 --workload W at 100 000 files per rank, gloo on the one GPU (the driver's
+#                         N = 8 launch rehearsed; every rank's links against the oracle), OUT/n8_gloo_W.json
 #   dedupfull=W[:ARGS]    tools/dedup_full.py --workload W (ARGS: extra flags, '~' for ' '), OUT/dedup_full_W_N.json
 #   pmcdedup=W[:ARGS]     tools/pmc_dedup.sh over tools/dedup_full.py or dedup_probe.py (ARGS: 'full' or probe flags)
 #   probe=ARGS            tools/dedup_probe.py ARGS ('~' for ' '), OUT/probe_N.json
@@ -44,9 +46,16 @@ step() {
       timeout -k 10 700 python -u bench.py --workload "$w" "${extra[@]}" > "$OUT/bench_$w.json" 2> "$OUT/bench_$w.err"
       local rc=$?; cut -c1-300 "$OUT/bench_$w.json"; return $rc ;;
     stats)
+      local st=20
+      [ "$arg" = c4 ] && st=3
       (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/$OUT/stats_$arg" -o "$arg" \
-        --output-format csv -- python3 "$R/bench.py" --workload "$arg" --steps 10 --warmup 3 \
-        > "$R/$OUT/stats_$arg.json" 2> "$R/$OUT/stats_$arg.err") ;;
+        --output-format csv -- python3 "$R/bench.py" --workload "$arg" --steps $st --warmup 1 --no-cpu-baseline \
+        --no-e2e --sustain-s 0 > "$R/$OUT/stats_$arg.json" 2> "$R/$OUT/stats_$arg.err")
+      local rc=$?; find "$OUT/stats_$arg" -name '*kernel_trace.csv' -delete; return $rc ;;
+    n8)
+      SDCAS_BENCH_BACKEND=gloo OMP_NUM_THREADS=2 timeout -k 10 500 python3 -u bench.py --gpus 8 --workload "$arg" \
+        --files 100000 --steps 3 --warmup 1 --sustain-s 0 > "$OUT/n8_gloo_$arg.json" 2> "$OUT/n8_gloo_$arg.err"
+      local rc=$?; cut -c1-300 "$OUT/n8_gloo_$arg.json"; return $rc ;;
     dedupfull)
       IFS=: read -r w rest <<< "$arg"
       timeout -k 10 900 python -u tools/dedup_full.py --workload "$w" ${rest//\~/ } --out "$OUT/dedup_full_${w}_$n.json" \
