@@ -13,7 +13,11 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
+#include <deque>
+#include <exception>
 #include <future>
+#include <mutex>
 #include <set>
 #include <thread>
 #include <unordered_map>
@@ -677,8 +681,193 @@ struct StepLoop {
 };
 using Fetch = std::function<std::vector<FilePathRow>(int32_t cursor, size_t take)>;
 
+// Round 6: the orphans read ahead in chunks on the read-ahead connection by a
+// thread of their own, `batch` rows past the last row read so far, up to two
+// chunks ahead. Rows past the job's cursor are never written by the batch
+// that fetched them (its steps write only the rows they read, all at or
+// before the cursor), so a chunk fetched before a batch's writes is what a
+// fetch after them would return.
+class ChunkFetcher {
+ public:
+  struct Chunk {
+    std::vector<FilePathRow> rows;
+    bool full = false;  // `take` rows: more may follow
+    std::exception_ptr err;
+  };
+  ChunkFetcher(const Fetch& fetch, int32_t after, size_t take) : fetch_(fetch), after_(after), take_(take) {
+    th_ = std::thread([this] { loop(); });
+  }
+  ~ChunkFetcher() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    th_.join();
+  }
+  // the next chunk (empty rows: none left), in id order
+  Chunk next() {
+    std::unique_lock<std::mutex> g(m_);
+    cv_.wait(g, [this] { return !q_.empty(); });
+    Chunk c = std::move(q_.front());
+    q_.pop_front();
+    cv_.notify_all();
+    return c;
+  }
+
+ private:
+  static constexpr size_t kDepth = 2;
+  void loop() {
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [this] { return stop_ || q_.size() < kDepth; });
+        if (stop_) return;
+      }
+      Chunk c;
+      try {
+        c.rows = fetch_(after_ + 1, take_);  // id >= after + 1 ORDER BY id
+        c.full = c.rows.size() == take_;
+        if (!c.rows.empty()) after_ = c.rows.back().id;
+      } catch (...) {
+        c.err = std::current_exception();
+      }
+      const bool last = c.err || !c.full;
+      {
+        std::lock_guard<std::mutex> g(m_);
+        q_.push_back(std::move(c));
+      }
+      cv_.notify_all();
+      if (last) return;
+    }
+  }
+  const Fetch& fetch_;
+  int32_t after_;
+  const size_t take_;
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::deque<Chunk> q_;
+  bool stop_ = false;
+  std::thread th_;
+};
+
+// SDCORE_PIPELINE=0: round 5's loop (the next batch fetched after the plan,
+// on the same thread as its FileMetadata) (A/B)
+static bool pipeline_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("SDCORE_PIPELINE");
+    return !(v && strcmp(v, "0") == 0);
+  }();
+  return on;
+}
+
+// The step loop with the chunk fetcher: each batch is the cursor row when it
+// stays an orphan (fetched again after the writes: its Object may be new),
+// then the rows the batch fetched but its steps did not read, then the next
+// chunk, whose FileMetadata runs beside this batch's writes (as round 5's
+// read-ahead) but no longer waits for its own fetch.
+StepLoop run_steps_chunked(Library& db, uint64_t task_count, int32_t cursor, size_t batch_rows, const Fetch& fetch,
+                           const MetadataFn& metadata, const GroupBy& group_by, const Fetch& fetch_ahead) {
+  StepLoop L;
+  L.cursor = cursor;
+  const size_t cs = SDCAS_IDENTIFIER_CHUNK_SIZE;
+  const size_t batch = std::max(cs, batch_rows);
+  uint64_t steps_left = task_count;
+  trace_mark();
+  std::vector<FilePathRow> rows = fetch(L.cursor, batch);  // id >= cursor ORDER BY id (file_identifier_job.rs:296-319)
+  trace_lap(JobTrace::kFetch);
+  bool more = rows.size() == batch;
+  std::unique_ptr<ChunkFetcher> fetcher;
+  if (more) fetcher = std::make_unique<ChunkFetcher>(fetch_ahead, rows.back().id, batch);
+  trace_mark();
+  std::vector<Result<FileMetadata>> md = metadata(rows);
+  trace_lap(JobTrace::kMetadata);
+  struct Ahead {
+    ChunkFetcher::Chunk chunk;
+    std::vector<Result<FileMetadata>> md;
+  };
+  while (steps_left) {
+    if (rows.empty()) {
+      L.ran_dry = true;
+      break;
+    }
+    if (L.batches && rows[0].id == L.cursor) ++L.rereads;  // the cursor row is still an orphan
+    sdcas_job_window w{};
+    w.max_steps = steps_left;
+    w.more = more;
+    // a row to re-identify must sit in the batch's first step (identifier_step_db)
+    {
+      sdcas_job_window probe = w;
+      const StepPlan plan = plan_steps(md, cs, probe);
+      uint64_t cut = UINT64_MAX;
+      for (size_t i = 0; i < rows.size(); ++i)
+        if (plan.step[i] != UINT64_MAX && plan.step[i] > 0 && reidentified(rows[i], md[i]))
+          cut = std::min(cut, plan.step[i]);
+      if (cut != UINT64_MAX) w.max_steps = cut;
+    }
+    std::future<Ahead> next_md;
+    const OnGrouped start_next = [&](const sdcas_job_window& done) {
+      if (done.steps == 0 || done.steps >= steps_left || !fetcher) return;
+      ChunkFetcher* f = fetcher.get();
+      next_md = std::async(std::launch::async, [f, &metadata] {
+        Ahead a;
+        a.chunk = f->next();
+        if (!a.chunk.err && !a.chunk.rows.empty()) a.md = metadata(a.chunk.rows);
+        return a;
+      });
+    };
+    auto [created, linked] = step_db(db, rows, md, group_by, &w, cs, &start_next);
+    if (w.steps == 0) break;  // cannot happen: a batch of >= cs rows holds a whole step
+    L.created += created;
+    L.linked += linked;
+    L.steps += w.steps;
+    L.rereads += w.rereads;
+    ++L.batches;
+    steps_left -= std::min<uint64_t>(steps_left, w.steps);
+    const size_t last = w.rows - 1;
+    L.cursor = rows[last].id;
+    if (!steps_left) break;
+    // the next batch: the cursor row again if it stays an orphan, the rows
+    // past it, the next chunk
+    std::vector<FilePathRow> nrows;
+    std::vector<Result<FileMetadata>> nmd;
+    trace_mark();
+    if (!md[last].ok() || !md[last].value().cas_id) {
+      std::vector<FilePathRow> cur = fetch(L.cursor, 1);
+      if (cur.size() == 1 && cur[0].id == L.cursor) {
+        nrows.push_back(std::move(cur[0]));
+        nmd.push_back(md[last]);  // the same file: its FileMetadata as this batch read it
+      }
+    }
+    trace_lap(JobTrace::kFetch);
+    for (size_t i = w.rows; i < rows.size(); ++i) {
+      nrows.push_back(std::move(rows[i]));
+      nmd.push_back(std::move(md[i]));
+    }
+    if (next_md.valid()) {
+      trace_mark();
+      Ahead a = next_md.get();
+      trace_lap(JobTrace::kWaitAhead);
+      if (a.chunk.err) std::rethrow_exception(a.chunk.err);
+      more = a.chunk.full;
+      if (!more) fetcher.reset();  // the fetcher has ended
+      for (size_t i = 0; i < a.chunk.rows.size(); ++i) {
+        nrows.push_back(std::move(a.chunk.rows[i]));
+        nmd.push_back(std::move(a.md[i]));
+      }
+    } else if (!fetcher) {
+      more = false;
+    }
+    rows = std::move(nrows);
+    md = std::move(nmd);
+  }
+  return L;
+}
+
 StepLoop run_steps(Library& db, uint64_t task_count, int32_t cursor, size_t batch_rows, const Fetch& fetch,
                    const MetadataFn& metadata, const GroupBy& group_by, const Fetch* fetch_ahead = nullptr) {
+  if (fetch_ahead && pipeline_enabled())
+    return run_steps_chunked(db, task_count, cursor, batch_rows, fetch, metadata, group_by, *fetch_ahead);
   StepLoop L;
   L.cursor = cursor;
   const size_t cs = SDCAS_IDENTIFIER_CHUNK_SIZE;
