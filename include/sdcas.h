@@ -128,8 +128,10 @@ typedef struct sdcas_options {
  * struct_size field, sdcas_dedup_window and the dedup step plan; 4
  * sdcas_dev_bind_stream; 5 the combine's output contract: one record per
  * distinct key, any order within an owner's range — same signatures, but a
- * caller that relied on ABI 4's documented key order must change) */
-#define SDCAS_ABI_VERSION 5
+ * caller that relied on ABI 4's documented key order must change; 6
+ * sdcas_file_metadata, and resolve_buckets may overwrite the received
+ * records' value words) */
+#define SDCAS_ABI_VERSION 6
 int sdcas_abi_version(void);
 const char *sdcas_version(void);
 
@@ -155,6 +157,23 @@ int sdcas_set_progress(sdcas_ctx *ctx, sdcas_progress_fn progress, void *user, c
  * writer either way; the caller may retry the file later). */
 int sdcas_cas_ids(sdcas_ctx *ctx, const char *const *paths, const uint64_t *sizes, size_t n,
                   uint64_t *out_keys, int32_t *out_status);
+
+/* FileMetadata::new (file_identifier/mod.rs:48-96) of n files: fs::metadata,
+ * then generate_cas_id(path, len) when the file is not empty (mod.rs:78-86) —
+ * the length taken by fstat of the descriptor the cas_id reads use (one path
+ * lookup per file instead of two; the same statuses). Per file:
+ * out_sizes[i] the metadata's len, out_flags[i] SDCAS_META_HAS_CAS_ID when
+ * out_keys[i] holds the cas key (a non-empty file read without error),
+ * SDCAS_META_DIR for a directory (the reference refuses those, mod.rs:67-70;
+ * no cas_id), out_status[i] 0 or the errno of the metadata or of the reads
+ * (SDCAS_STATUS_UNEXPECTED_EOF as sdcas_cas_ids). A call holds up to n
+ * descriptors open at once: it raises the process's soft RLIMIT_NOFILE
+ * toward the hard limit when it needs more, and otherwise works in windows
+ * of what the limit allows. ABI 6. */
+#define SDCAS_META_HAS_CAS_ID 1u
+#define SDCAS_META_DIR 2u
+int sdcas_file_metadata(sdcas_ctx *ctx, const char *const *paths, size_t n, uint64_t *out_sizes,
+                        uint64_t *out_keys, int32_t *out_status, uint8_t *out_flags);
 
 /* file_checksum of n files (hash.rs:11-25): BLAKE3 of the whole content.
  * out32 receives 32*n bytes. The content hashed is the file's first L bytes,

@@ -97,6 +97,15 @@ class Engine {
   std::vector<Result<std::string>> generate_cas_ids(const std::vector<std::pair<std::string, uint64_t>>& files);
   // hash.rs:11-25 over a batch: path -> 64 lowercase hex
   std::vector<Result<std::string>> file_checksums(const std::vector<std::string>& paths);
+  // fs::metadata + generate_cas_id of FileMetadata::new (mod.rs:48-96) in one
+  // call (sdcas_file_metadata: the length from fstat of the descriptor the
+  // reads use)
+  struct RawMetadata {
+    std::vector<uint64_t> size, key;
+    std::vector<int32_t> status;
+    std::vector<uint8_t> flags;  // SDCAS_META_*
+  };
+  RawMetadata file_metadata(const std::vector<const char*>& paths);
 
   // the canonical group-by of mod.rs:149-254 over the job's steps
   // (sdcas_dedup_window; sdcas_dedup encoding of out_link). window may be

@@ -26,7 +26,9 @@ SDCAS_STATUS_UNEXPECTED_EOF = 100001
 SDCAS_STATUS_CANCELLED = 125
 SDCAS_MAX_BATCH = 0x7FFFFFFF
 SDCAS_OPT_DIRECT_IO = 1
-SDCAS_ABI_VERSION = 5
+SDCAS_ABI_VERSION = 6
+SDCAS_META_HAS_CAS_ID = 1
+SDCAS_META_DIR = 2
 SDCAS_LINK_DROPPED = -(1 << 63)
 SDCAS_LINK_DEFERRED = SDCAS_LINK_DROPPED + 1
 SDCAS_PLAN_HEADER_WORDS = 12
@@ -34,6 +36,7 @@ SDCAS_PLAN_HEADER_WORDS = 12
 # every entry point include/sdcas.h and include/sdcas_bench.h declare
 ABI_SYMBOLS = [
     "sdcas_version", "sdcas_abi_version", "sdcas_init", "sdcas_destroy", "sdcas_last_error", "sdcas_cas_ids",
+    "sdcas_file_metadata",
     "sdcas_checksums", "sdcas_hash_messages", "sdcas_cas_ids_from_messages", "sdcas_dev_reserve",
     "sdcas_dev_hash_messages", "sdcas_dev_sync", "sdcas_dev_bind_stream", "sdcas_dedup", "sdcas_dedup_window", "sdcas_job_plan",
     "sdcas_key_to_hex",
@@ -132,6 +135,7 @@ def load():
     L.sdcas_last_error.argtypes = [_vp]
     L.sdcas_last_error.restype = ctypes.c_char_p
     L.sdcas_cas_ids.argtypes = [_vp, _vp, _vp, _sz, _vp, _vp]
+    L.sdcas_file_metadata.argtypes = [_vp, _vp, _sz, _vp, _vp, _vp, _vp]
     L.sdcas_checksums.argtypes = [_vp, _vp, _sz, _vp, _vp]
     L.sdcas_hash_messages.argtypes = [_vp, _vp, _vp, _vp, _sz, _vp]
     L.sdcas_cas_ids_from_messages.argtypes = [_vp, _vp, _vp, _vp, _sz, _vp]

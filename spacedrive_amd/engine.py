@@ -157,6 +157,22 @@ class Engine:
         del buf
         return keys, st
 
+    def file_metadata(self, paths):
+        """FileMetadata::new's fs::metadata + generate_cas_id (mod.rs:48-96) for
+        many files, the length from fstat of the read descriptor
+        (sdcas_file_metadata) -> (sizes uint64[n], keys uint64[n], status
+        int32[n], flags uint8[n]: SDCAS_META_HAS_CAS_ID | SDCAS_META_DIR)"""
+        n = len(paths)
+        buf, parr = _cpaths(paths)
+        sizes = np.zeros(n, np.uint64)
+        keys = np.zeros(n, np.uint64)
+        st = np.zeros(n, np.int32)
+        fl = np.zeros(n, np.uint8)
+        self._check(self.L.sdcas_file_metadata(self.ctx, _ptr(parr), n, _ptr(sizes), _ptr(keys), _ptr(st), _ptr(fl)),
+                    "sdcas_file_metadata", (sizes, keys, st, fl))
+        del buf
+        return sizes, keys, st, fl
+
     def file_checksums(self, paths):
         """hash.rs:11-25 for many files -> (digests uint8[n, 32], status int32[n])"""
         n = len(paths)

@@ -68,6 +68,21 @@ uint64_t hex_to_key(const std::string& cas_id) {
   return std::stoull(cas_id, nullptr, 16);
 }
 
+Engine::RawMetadata Engine::file_metadata(const std::vector<const char*>& paths) {
+  const size_t n = paths.size();
+  RawMetadata m;
+  m.size.resize(n);
+  m.key.resize(n);
+  m.status.resize(n);
+  m.flags.resize(n);
+  if (n) {
+    const int rc = sdcas_file_metadata(ctx_, paths.data(), n, m.size.data(), m.key.data(), m.status.data(),
+                                       m.flags.data());
+    if (rc != SDCAS_OK) fail(rc, "sdcas_file_metadata");
+  }
+  return m;
+}
+
 std::vector<Result<std::string>> Engine::generate_cas_ids(
     const std::vector<std::pair<std::string, uint64_t>>& files) {
   const size_t n = files.size();
@@ -361,9 +376,50 @@ static bool stat_dirfd() {
   return on;
 }
 
+// SDCORE_FOLD_STAT=0: fs::metadata as its own fstatat pass before the cas_id
+// reads (round 5) instead of inside them (sdcas_file_metadata) (A/B)
+static bool fold_stat() {
+  static const bool on = [] {
+    const char* v = getenv("SDCORE_FOLD_STAT");
+    return !(v && strcmp(v, "0") == 0);
+  }();
+  return on;
+}
+
 std::vector<Result<FileMetadata>> file_metadata_batch(Engine& engine,
                                                       const std::vector<std::pair<std::string, ObjectKind>>& files) {
   const size_t n = files.size();
+  if (fold_stat()) {
+    // fs::metadata, the kind and generate_cas_id (mod.rs:63-86) in one library
+    // call: the metadata is the fstat of the descriptor the reads use
+    std::vector<const char*> paths(n);
+    for (size_t i = 0; i < n; ++i) paths[i] = files[i].first.c_str();
+    const auto t0 = std::chrono::steady_clock::now();
+    const Engine::RawMetadata raw = engine.file_metadata(paths);
+    static const bool trace = [] {
+      const char* v = getenv("SDCORE_TRACE_JOB");
+      return v && *v && strcmp(v, "0") != 0;
+    }();
+    if (trace)
+      fprintf(stderr, "sdcore file_metadata_batch: %zu files, sdcas_file_metadata %.2f ms\n", n,
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    std::vector<Result<FileMetadata>> out;
+    out.reserve(n);
+    for (size_t i = 0; i < n; ++i) {
+      if (raw.flags[i] & SDCAS_META_DIR)
+        throw std::logic_error("We can't generate cas_id for directories");  // mod.rs:67-70
+      if (raw.status[i]) {
+        out.emplace_back(IoError{raw.status[i], files[i].first});
+        continue;
+      }
+      FileMetadata m;
+      m.kind = files[i].second >= 0 ? files[i].second : object_kind_of(files[i].first);  // mod.rs:72-76
+      m.len = raw.size[i];
+      if (raw.flags[i] & SDCAS_META_HAS_CAS_ID) m.cas_id = key_to_hex(raw.key[i]);
+      out.emplace_back(std::move(m));
+    }
+    return out;
+  }
   std::vector<std::optional<IoError>> err(n);
   std::vector<FileMetadata> md(n);
   std::vector<uint8_t> is_dir(n, 0);
@@ -522,7 +578,8 @@ using OnGrouped = std::function<void(const sdcas_job_window& done)>;
 
 static std::pair<size_t, size_t> step_db(Library& db, const std::vector<FilePathRow>& file_paths,
                                          const std::vector<Result<FileMetadata>>& md, const GroupBy& group_by,
-                                         sdcas_job_window* window, size_t chunk_size, const OnGrouped* on_grouped);
+                                         sdcas_job_window* window, size_t chunk_size, const OnGrouped* on_grouped,
+                                         const OnGrouped* after_group_by = nullptr);
 
 std::pair<size_t, size_t> identifier_step_db(Library& db, const std::vector<FilePathRow>& file_paths,
                                              const std::vector<Result<FileMetadata>>& md, const GroupBy& group_by,
@@ -532,7 +589,8 @@ std::pair<size_t, size_t> identifier_step_db(Library& db, const std::vector<File
 
 static std::pair<size_t, size_t> step_db(Library& db, const std::vector<FilePathRow>& file_paths,
                                          const std::vector<Result<FileMetadata>>& md, const GroupBy& group_by,
-                                         sdcas_job_window* window, size_t chunk_size, const OnGrouped* on_grouped) {
+                                         sdcas_job_window* window, size_t chunk_size, const OnGrouped* on_grouped,
+                                         const OnGrouped* after_group_by) {
   const size_t n = file_paths.size();
   if (md.size() != n) throw std::invalid_argument("identifier_step_db: one metadata per file_path");
   sdcas_job_window win{};
@@ -594,6 +652,9 @@ static std::pair<size_t, size_t> step_db(Library& db, const std::vector<FilePath
   gw.more = win.more;
   auto d = group_by(keys, has_key, status, ekeys, gw);
   trace_lap(JobTrace::kGroupBy);
+  // (the chunked loop's read-ahead starts here: its FileMetadata call would
+  // otherwise hold the engine while this batch's group-by waits for it)
+  if (after_group_by) (*after_group_by)(win);
   if (d.link.size() != n) throw std::logic_error("identifier_step_db: group-by returned a wrong link count");
   if (gw.steps != win.steps || gw.rows != win.rows)
     throw std::logic_error("identifier_step_db: the group-by ran other steps than the plan");
@@ -761,6 +822,16 @@ static bool pipeline_enabled() {
   return on;
 }
 
+// SDCORE_AHEAD_AT=plan: the chunked loop's read-ahead FileMetadata starts
+// at the batch's plan (as round 5's) instead of after its group-by (A/B)
+static bool ahead_at_plan() {
+  static const bool on = [] {
+    const char* v = getenv("SDCORE_AHEAD_AT");
+    return v && strcmp(v, "plan") == 0;
+  }();
+  return on;
+}
+
 // The step loop with the chunk fetcher: each batch is the cursor row when it
 // stays an orphan (fetched again after the writes: its Object may be new),
 // then the rows the batch fetched but its steps did not read, then the next
@@ -816,7 +887,8 @@ StepLoop run_steps_chunked(Library& db, uint64_t task_count, int32_t cursor, siz
         return a;
       });
     };
-    auto [created, linked] = step_db(db, rows, md, group_by, &w, cs, &start_next);
+    auto [created, linked] = ahead_at_plan() ? step_db(db, rows, md, group_by, &w, cs, &start_next)
+                                             : step_db(db, rows, md, group_by, &w, cs, nullptr, &start_next);
     if (w.steps == 0) break;  // cannot happen: a batch of >= cs rows holds a whole step
     L.created += created;
     L.linked += linked;

@@ -129,6 +129,72 @@ def test_no_directory_descriptor_outlives_a_path_call(tmp_path):
     assert _fds_on(d) == []
 
 
+def test_file_metadata_matches_stat_then_cas_ids(eng, oracle, tmp_path):
+    """sdcas_file_metadata (fs::metadata folded into the cas_id reads,
+    mod.rs:48-96) against the two-step form — os.stat, then sdcas_cas_ids for
+    the non-empty files — and the oracle: whole-file and sampled sizes, an
+    empty file (no cas_id, no error), a missing path (ENOENT), a directory
+    (flagged, no cas_id), every key exact"""
+    import errno
+    rng = np.random.default_rng(23)
+    paths = []
+    for i, size in enumerate([0, 1, 1000, 65536, 102400, 102401, 300_000, 5 << 20]
+                             + [int(x) for x in rng.integers(1, 200_000, 300)]):
+        p = tmp_path / f"m{i}"
+        write_sparse_file(str(p), "synth", 1000 + i, size, cas_windows(size))
+        paths.append(str(p))
+    d = tmp_path / "adir"
+    d.mkdir()
+    paths += [str(tmp_path / "missing"), str(d)]
+    sizes, keys, st, fl = eng.file_metadata(paths)
+    assert st[-2] == errno.ENOENT and fl[-2] == 0
+    assert st[-1] == 0 and fl[-1] == 2  # SDCAS_META_DIR
+    real = paths[:-2]
+    want_sz = [os.path.getsize(p) for p in real]
+    assert sizes[:-2].tolist() == want_sz and not st[:-2].any()
+    nonempty = [i for i, z in enumerate(want_sz) if z]
+    assert all(fl[i] == 1 for i in nonempty) and all(fl[i] == 0 for i, z in enumerate(want_sz) if not z)
+    k2, s2 = eng.generate_cas_ids([real[i] for i in nonempty], [want_sz[i] for i in nonempty])
+    assert not s2.any() and np.array_equal(keys[nonempty], k2)
+    for i in nonempty[::17]:
+        assert f"{int(keys[i]):016x}" == oracle.generate_cas_id(real[i], want_sz[i]), i
+
+
+def test_file_metadata_in_descriptor_windows(tmp_path):
+    """a process whose descriptor limit is below the call's file count: the
+    call works in windows of what the limit allows (a child process with a
+    hard RLIMIT_NOFILE of 300, so it cannot be raised), keys equal to the
+    unlimited call's"""
+    import subprocess
+    import sys
+    paths = []
+    for i in range(700):
+        p = tmp_path / f"w{i}"
+        p.write_bytes(os.urandom(1 + (i * 7919) % 150_000))
+        paths.append(str(p))
+    listing = tmp_path / "list.txt"
+    listing.write_text("\n".join(paths))
+    code = (
+        "import resource, sys, numpy as np\n"
+        "resource.setrlimit(resource.RLIMIT_NOFILE, (300, 300))\n"
+        "from spacedrive_amd import Engine\n"
+        "paths = open(sys.argv[1]).read().split('\\n')\n"
+        "with Engine(staging_bytes=8 << 20) as e:\n"
+        "    sz, k, st, fl = e.file_metadata(paths)\n"
+        "np.save(sys.argv[2], np.stack([sz.astype(np.int64), k.view(np.int64), st.astype(np.int64), fl.astype(np.int64)]))\n")
+    out = tmp_path / "r.npy"
+    r = subprocess.run([sys.executable, "-c", code, str(listing), str(out)], capture_output=True, text=True,
+                       timeout=120, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = np.load(out)
+    from spacedrive_amd import Engine
+    with Engine(staging_bytes=8 << 20) as e:
+        sz, k, st, fl = e.file_metadata(paths)
+    assert not st.any() and (fl == 1).all()
+    assert np.array_equal(got[0], sz.astype(np.int64)) and np.array_equal(got[1], k.view(np.int64))
+    assert not got[2].any() and (got[3] == 1).all()
+
+
 def eng_plain_checksums(paths):
     from spacedrive_amd import Engine
     with Engine() as e:
