@@ -160,20 +160,20 @@ int sdcas_cas_ids(sdcas_ctx *ctx, const char *const *paths, const uint64_t *size
 
 /* FileMetadata::new (file_identifier/mod.rs:48-96) of n files: fs::metadata,
  * then generate_cas_id(path, len) when the file is not empty (mod.rs:78-86) —
- * the length taken by fstat of the descriptor the cas_id reads use (one path
- * lookup per file instead of two; the same statuses). Per file:
- * out_sizes[i] the metadata's len, out_flags[i] SDCAS_META_HAS_CAS_ID when
- * out_keys[i] holds the cas key (a non-empty file read without error),
- * SDCAS_META_DIR for a directory (the reference refuses those, mod.rs:67-70;
- * no cas_id), out_status[i] 0 or the errno of the metadata or of the reads
- * (SDCAS_STATUS_UNEXPECTED_EOF as sdcas_cas_ids). A call holds up to n
- * descriptors open at once: it raises the process's soft RLIMIT_NOFILE
- * toward the hard limit when it needs more, and otherwise works in windows
- * of what the limit allows. ABI 6. */
+ * the metadata being fstat of the descriptor the cas_id reads use (one path
+ * lookup per file; the same statuses). size_hints (may be NULL: one stat
+ * pass first) only plan the staging — the indexer's sizes (file_path
+ * size_in_bytes); a file of another size now is read again with room for
+ * it. Per file: out_sizes[i] the metadata's len, out_flags[i]
+ * SDCAS_META_HAS_CAS_ID when out_keys[i] holds the cas key (a non-empty
+ * file read without error), SDCAS_META_DIR for a directory (the reference
+ * refuses those, mod.rs:67-70; no cas_id), out_status[i] 0 or the errno of
+ * the metadata or of the reads (SDCAS_STATUS_UNEXPECTED_EOF as
+ * sdcas_cas_ids). ABI 6. */
 #define SDCAS_META_HAS_CAS_ID 1u
 #define SDCAS_META_DIR 2u
-int sdcas_file_metadata(sdcas_ctx *ctx, const char *const *paths, size_t n, uint64_t *out_sizes,
-                        uint64_t *out_keys, int32_t *out_status, uint8_t *out_flags);
+int sdcas_file_metadata(sdcas_ctx *ctx, const char *const *paths, const uint64_t *size_hints, size_t n,
+                        uint64_t *out_sizes, uint64_t *out_keys, int32_t *out_status, uint8_t *out_flags);
 
 /* file_checksum of n files (hash.rs:11-25): BLAKE3 of the whole content.
  * out32 receives 32*n bytes. The content hashed is the file's first L bytes,

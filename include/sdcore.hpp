@@ -105,7 +105,7 @@ class Engine {
     std::vector<int32_t> status;
     std::vector<uint8_t> flags;  // SDCAS_META_*
   };
-  RawMetadata file_metadata(const std::vector<const char*>& paths);
+  RawMetadata file_metadata(const std::vector<const char*>& paths, const uint64_t* size_hints = nullptr);
 
   // the canonical group-by of mod.rs:149-254 over the job's steps
   // (sdcas_dedup_window; sdcas_dedup encoding of out_link). window may be
@@ -427,9 +427,13 @@ struct FileMetadata {
 // is_dir assertion (mod.rs:67-70, std::logic_error here), the kind from the
 // path (object_kind_of) unless the pair carries one (>= 0), cas_id only for
 // len != 0, one generate_cas_ids call for the batch (the join_all of
-// mod.rs:105-147). Errors carry the path (FileIOError).
+// mod.rs:105-147). Errors carry the path (FileIOError). size_hints (may be
+// null; one per file): the indexer's sizes (file_path size_in_bytes), which
+// only plan the reads' staging (sdcas_file_metadata: the metadata is fstat of
+// each read's descriptor).
 std::vector<Result<FileMetadata>> file_metadata_batch(Engine& engine,
-                                                      const std::vector<std::pair<std::string, ObjectKind>>& files);
+                                                      const std::vector<std::pair<std::string, ObjectKind>>& files,
+                                                      const std::vector<uint64_t>* size_hints = nullptr);
 
 // The DB half of the job's steps over a batch of its orphans (mod.rs:157-342
 // per step): write the cas_id of every row the steps read, look up the

@@ -135,7 +135,7 @@ def load():
     L.sdcas_last_error.argtypes = [_vp]
     L.sdcas_last_error.restype = ctypes.c_char_p
     L.sdcas_cas_ids.argtypes = [_vp, _vp, _vp, _sz, _vp, _vp]
-    L.sdcas_file_metadata.argtypes = [_vp, _vp, _sz, _vp, _vp, _vp, _vp]
+    L.sdcas_file_metadata.argtypes = [_vp, _vp, _vp, _sz, _vp, _vp, _vp, _vp]
     L.sdcas_checksums.argtypes = [_vp, _vp, _sz, _vp, _vp]
     L.sdcas_hash_messages.argtypes = [_vp, _vp, _vp, _vp, _sz, _vp]
     L.sdcas_cas_ids_from_messages.argtypes = [_vp, _vp, _vp, _vp, _sz, _vp]

@@ -10,7 +10,6 @@
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <sys/mman.h>
-#include <sys/resource.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -1202,8 +1201,16 @@ struct IoTrace {
 // null): a file already open (fds[i] >= 0, `aligned[i]` = opened with
 // O_DIRECT; sdcas_file_metadata) is read through its descriptor; any other
 // is opened by path.
+// meta (sdcas_file_metadata): `sizes` only plan the staging; each read takes
+// the file's metadata from fstat of its descriptor (meta->sizes, meta->flags)
+struct Meta {
+  uint64_t* sizes;
+  uint8_t* flags;
+};
+
 static int cas_ids_core(sdcas_ctx* c, const char* const* paths, const int* fds, const uint8_t* aligned,
-                        const uint64_t* sizes, size_t n, uint64_t* out_keys, int32_t* out_status) {
+                        const uint64_t* sizes, size_t n, uint64_t* out_keys, int32_t* out_status,
+                        const Meta* meta = nullptr) {
   const uint64_t cap = c->staging_bytes;
   const size_t cap_n = (size_t)(cap / 128) + 1;
   int rc;
@@ -1253,10 +1260,18 @@ static int cas_ids_core(sdcas_ctx* c, const char* const* paths, const int* fds, 
       auto read_files = [&](size_t k0, size_t k1) {
         c->pool->run(k1 - k0, [&](size_t kk) {
           const size_t k = k0 + kk, i = todo[p + k];
-          st[k] = fds && fds[i] >= 0 ? sdcas_io::read_cas_message_fd(fds[i], aligned[i] != 0, sizes[i], s.h + slot_off[k],
-                                                      align16(want[i]), &mlen[k], &retry_len[k])
-                      : read_cas_message(paths[i], sizes[i], s.h + slot_off[k], align16(want[i]), &mlen[k],
-                                         &retry_len[k], c->direct_io);
+          if (meta) {
+            bool dir = false;
+            st[k] = sdcas_io::read_file_metadata(paths[i], c->direct_io, s.h + slot_off[k], align16(want[i]),
+                                                  &mlen[k], &retry_len[k], &meta->sizes[i], &dir);
+            meta->flags[i] = dir ? SDCAS_META_DIR : 0;
+            return;
+          }
+          st[k] = fds && fds[i] >= 0 ? sdcas_io::read_cas_message_fd(fds[i], aligned[i] != 0, sizes[i],
+                                                                     s.h + slot_off[k], align16(want[i]), &mlen[k],
+                                                                     &retry_len[k])
+                                     : read_cas_message(paths[i], sizes[i], s.h + slot_off[k], align16(want[i]),
+                                                        &mlen[k], &retry_len[k], c->direct_io);
         });
       };
       // A call that fits one slot is latency-bound: read -> upload -> hash in
@@ -1304,6 +1319,8 @@ static int cas_ids_core(sdcas_ctx* c, const char* const* paths, const int* fds, 
         out_status[i] = st[k];
         s.content += sdcas_cas_message_len(sizes[i]) - 8;
         if (st[k]) continue;
+        if (meta && mlen[k] == 0) continue;  // a directory or an empty file: no cas_id
+        if (meta) meta->flags[i] = SDCAS_META_HAS_CAS_ID;
         s.offs()[s.n] = slot_off[k];
         s.lens()[s.n] = mlen[k];
         s.idx.push_back(i);
@@ -1333,115 +1350,29 @@ int sdcas_cas_ids(sdcas_ctx* c, const char* const* paths, const uint64_t* sizes,
   return cas_ids_core(c, paths, nullptr, nullptr, sizes, n, out_keys, out_status);
 }
 
-// descriptors one sdcas_file_metadata window may hold open: the soft
-// RLIMIT_NOFILE, raised toward the hard limit when a call needs more (the
-// process keeps the raised soft limit), less 256 for everything else
-static size_t fd_window(size_t want) {
-  struct rlimit rl;
-  if (getrlimit(RLIMIT_NOFILE, &rl) != 0) return 256;
-  const rlim_t need = (rlim_t)want + 1024;
-  if (rl.rlim_cur != RLIM_INFINITY && rl.rlim_cur < need) {
-    struct rlimit up = rl;
-    up.rlim_cur = rl.rlim_max == RLIM_INFINITY ? need : std::min<rlim_t>(need, rl.rlim_max);
-    if (up.rlim_cur > rl.rlim_cur && setrlimit(RLIMIT_NOFILE, &up) == 0) rl = up;
-  }
-  if (rl.rlim_cur == RLIM_INFINITY) return want;
-  const size_t lim = (size_t)rl.rlim_cur;
-  return std::max<size_t>(1, std::min(want, lim > 512 ? lim - 256 : lim / 2));
-}
-
-int sdcas_file_metadata(sdcas_ctx* c, const char* const* paths, size_t n, uint64_t* out_sizes, uint64_t* out_keys,
-                        int32_t* out_status, uint8_t* out_flags) {
+int sdcas_file_metadata(sdcas_ctx* c, const char* const* paths, const uint64_t* size_hints, size_t n,
+                        uint64_t* out_sizes, uint64_t* out_keys, int32_t* out_status, uint8_t* out_flags) {
   if (!c || (n && (!paths || !out_sizes || !out_keys || !out_status || !out_flags))) return SDCAS_E_INVALID;
   if (n > SDCAS_MAX_BATCH) return c->fail(SDCAS_E_CAPACITY, "batch of %zu files exceeds 2^31 - 1", n);
   PathCall call(c);
   if (call.rc) return call.rc;
-  const size_t win = n ? fd_window(n) : 1;
-  for (size_t lo = 0; lo < n; lo += win) {
-    const size_t m = std::min(win, n - lo);
-    std::vector<int> fds(m, -1);
-    std::vector<uint8_t> aligned(m, 0), by_path(m, 0);
-    // fs::metadata (mod.rs:63-65) as fstat of the file generate_cas_id opens
-    // anyway: one path lookup per file instead of two
-    c->pool->run(m, [&](size_t k) {
-      const size_t i = lo + k;
-      out_flags[i] = 0;
-      out_sizes[i] = 0;
-      out_keys[i] = 0;
-      out_status[i] = 0;
-      bool is_direct = false;
-      const int fd = sdcas_io::open_for_read(paths[i], c->direct_io, &is_direct);
+  std::fill(out_sizes, out_sizes + n, 0);
+  std::fill(out_keys, out_keys + n, 0);
+  std::fill(out_flags, out_flags + n, 0);
+  // the staging plan: the caller's sizes (the indexer's), else one fstatat
+  // pass; either way each read takes the metadata from fstat of its own
+  // descriptor and a file of another size is read again with room for it
+  std::vector<uint64_t> plan(n);
+  if (size_hints) {
+    std::copy(size_hints, size_hints + n, plan.begin());
+  } else {
+    c->pool->run(n, [&](size_t i) {
       struct stat sb;
-      if (fd == -EMFILE || fd == -ENFILE) {
-        // out of descriptors (another thread of the process holds many): the
-        // metadata by path, the reads by path later
-        if (stat(paths[i], &sb) != 0) {
-          out_status[i] = errno;
-          return;
-        }
-        out_sizes[i] = (uint64_t)sb.st_size;
-        if (S_ISDIR(sb.st_mode)) out_flags[i] = SDCAS_META_DIR;
-        else if (sb.st_size != 0) by_path[k] = 1;
-        return;
-      }
-      if (fd < 0) {
-        // metadata may still succeed where the open is refused (a file
-        // without read permission): an empty one then has no cas_id and no
-        // error, as in the reference, which never opens it
-        if (stat(paths[i], &sb) != 0) {
-          out_status[i] = errno;
-          return;
-        }
-        out_sizes[i] = (uint64_t)sb.st_size;
-        if (S_ISDIR(sb.st_mode)) out_flags[i] = SDCAS_META_DIR;
-        else if (sb.st_size != 0) out_status[i] = -fd;  // generate_cas_id's open fails (mod.rs:78-82)
-        return;
-      }
-      if (fstat(fd, &sb) != 0) {
-        out_status[i] = errno;
-        close(fd);
-        return;
-      }
-      out_sizes[i] = (uint64_t)sb.st_size;
-      if (S_ISDIR(sb.st_mode) || sb.st_size == 0) {  // mod.rs:67-70, 78-86: no cas_id
-        if (S_ISDIR(sb.st_mode)) out_flags[i] = SDCAS_META_DIR;
-        close(fd);
-        return;
-      }
-      fds[k] = fd;
-      aligned[k] = is_direct ? 1 : 0;
+      plan[i] = stat(paths[i], &sb) == 0 && S_ISREG(sb.st_mode) ? (uint64_t)sb.st_size : 0;
     });
-    // the files to hash, their descriptors handed to the reads
-    std::vector<size_t> idx;
-    std::vector<const char*> p;
-    std::vector<int> f;
-    std::vector<uint8_t> al;
-    std::vector<uint64_t> sz;
-    for (size_t k = 0; k < m; ++k)
-      if (fds[k] >= 0 || by_path[k]) {
-        idx.push_back(lo + k);
-        p.push_back(paths[lo + k]);
-        f.push_back(fds[k]);
-        al.push_back(aligned[k]);
-        sz.push_back(out_sizes[lo + k]);
-      }
-    std::vector<uint64_t> keys(idx.size());
-    std::vector<int32_t> st(idx.size());
-    const int rc = cas_ids_core(c, p.data(), f.data(), al.data(), sz.data(), idx.size(), keys.data(), st.data());
-    for (int fd : f)
-      if (fd >= 0) close(fd);
-    for (size_t k = 0; k < idx.size(); ++k) {
-      out_status[idx[k]] = st[k];
-      out_keys[idx[k]] = keys[k];
-      if (!st[k]) out_flags[idx[k]] = SDCAS_META_HAS_CAS_ID;
-    }
-    if (rc) {
-      if (rc == SDCAS_E_CANCELLED)
-        for (size_t i = lo + m; i < n; ++i) out_status[i] = SDCAS_STATUS_CANCELLED;
-      return rc;
-    }
   }
-  return SDCAS_OK;
+  Meta meta{out_sizes, out_flags};
+  return cas_ids_core(c, paths, nullptr, nullptr, plan.data(), n, out_keys, out_status, &meta);
 }
 
 int sdcas_checksums(sdcas_ctx* c, const char* const* paths, size_t n, uint8_t* out32, int32_t* out_status) {

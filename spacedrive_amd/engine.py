@@ -157,18 +157,21 @@ class Engine:
         del buf
         return keys, st
 
-    def file_metadata(self, paths):
+    def file_metadata(self, paths, size_hints=None):
         """FileMetadata::new's fs::metadata + generate_cas_id (mod.rs:48-96) for
         many files, the length from fstat of the read descriptor
-        (sdcas_file_metadata) -> (sizes uint64[n], keys uint64[n], status
-        int32[n], flags uint8[n]: SDCAS_META_HAS_CAS_ID | SDCAS_META_DIR)"""
+        (sdcas_file_metadata; size_hints: the indexer's sizes, which only plan
+        the staging) -> (sizes uint64[n], keys uint64[n], status int32[n],
+        flags uint8[n]: SDCAS_META_HAS_CAS_ID | SDCAS_META_DIR)"""
         n = len(paths)
         buf, parr = _cpaths(paths)
+        hints = _arr(size_hints, np.uint64) if size_hints is not None else None
         sizes = np.zeros(n, np.uint64)
         keys = np.zeros(n, np.uint64)
         st = np.zeros(n, np.int32)
         fl = np.zeros(n, np.uint8)
-        self._check(self.L.sdcas_file_metadata(self.ctx, _ptr(parr), n, _ptr(sizes), _ptr(keys), _ptr(st), _ptr(fl)),
+        self._check(self.L.sdcas_file_metadata(self.ctx, _ptr(parr), _ptr(hints) if hints is not None else None, n,
+                                               _ptr(sizes), _ptr(keys), _ptr(st), _ptr(fl)),
                     "sdcas_file_metadata", (sizes, keys, st, fl))
         del buf
         return sizes, keys, st, fl

@@ -253,6 +253,38 @@ int read_cas_message(const char* path, uint64_t size, uint8_t* dst, uint64_t cap
   return st;
 }
 
+int read_file_metadata(const char* path, bool direct, uint8_t* dst, uint64_t cap, uint64_t* len,
+                       uint64_t* retry_len, uint64_t* size, bool* is_dir) {
+  *len = 0;
+  *retry_len = 0;
+  *size = 0;
+  *is_dir = false;
+  bool aligned = false;
+  const int fd = open_for_read(path, direct, &aligned);
+  struct stat sb;
+  if (fd < 0) {
+    if (stat(path, &sb) != 0) return errno;  // fs::metadata fails (mod.rs:63-65)
+    *size = (uint64_t)sb.st_size;
+    *is_dir = S_ISDIR(sb.st_mode);
+    return *is_dir || sb.st_size == 0 ? 0 : -fd;  // generate_cas_id's open fails (mod.rs:78-82)
+  }
+  if (fstat(fd, &sb) != 0) {
+    const int e = errno;
+    close(fd);
+    return e;
+  }
+  *size = (uint64_t)sb.st_size;
+  *is_dir = S_ISDIR(sb.st_mode);
+  int st = 0;
+  if (!*is_dir && *size) {  // mod.rs:67-70, 78-86: no cas_id for a directory or an empty file
+    const uint64_t need = (*size <= kMin ? 8 + *size + 1 : kSampledLen);
+    if (need > cap) *retry_len = need;
+    else st = read_cas_message_fd(fd, aligned, *size, dst, cap, len, retry_len);
+  }
+  close(fd);
+  return st;
+}
+
 size_t plan_batch(const uint64_t* need, const size_t* order, size_t p, size_t end, uint64_t cap, size_t cap_n,
                   std::vector<uint64_t>& offs, uint64_t* used) {
   offs.clear();

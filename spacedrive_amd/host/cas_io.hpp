@@ -75,6 +75,16 @@ int read_cas_message(const char* path, uint64_t size, uint8_t* dst, uint64_t cap
 // the same read pattern on an open descriptor (`aligned`: O_DIRECT reads)
 int read_cas_message_fd(int fd, bool aligned, uint64_t size, uint8_t* dst, uint64_t cap, uint64_t* len,
                         uint64_t* retry_len);
+// FileMetadata::new (file_identifier/mod.rs:48-96) of one file: open, the
+// metadata as fstat of that descriptor (*size, *is_dir), then — unless a
+// directory or empty (no cas_id: *len = 0) — its cas.rs message of that
+// length into dst (capacity cap). *retry_len != 0: the message needs a slot
+// of that capacity (the file is not the size the slot was planned for). An
+// open refused where the metadata succeeds (no read permission) reports the
+// metadata and, for a non-empty file, the open's errno; the reference never
+// opens an empty file.
+int read_file_metadata(const char* path, bool direct, uint8_t* dst, uint64_t cap, uint64_t* len,
+                       uint64_t* retry_len, uint64_t* size, bool* is_dir);
 
 // The next staging batch: items order[p], order[p+1], ... of `need` bytes
 // each (line-aligned here) go to offsets in one slot of `cap` bytes and at

@@ -68,7 +68,7 @@ uint64_t hex_to_key(const std::string& cas_id) {
   return std::stoull(cas_id, nullptr, 16);
 }
 
-Engine::RawMetadata Engine::file_metadata(const std::vector<const char*>& paths) {
+Engine::RawMetadata Engine::file_metadata(const std::vector<const char*>& paths, const uint64_t* size_hints) {
   const size_t n = paths.size();
   RawMetadata m;
   m.size.resize(n);
@@ -76,8 +76,8 @@ Engine::RawMetadata Engine::file_metadata(const std::vector<const char*>& paths)
   m.status.resize(n);
   m.flags.resize(n);
   if (n) {
-    const int rc = sdcas_file_metadata(ctx_, paths.data(), n, m.size.data(), m.key.data(), m.status.data(),
-                                       m.flags.data());
+    const int rc = sdcas_file_metadata(ctx_, paths.data(), size_hints, n, m.size.data(), m.key.data(),
+                                       m.status.data(), m.flags.data());
     if (rc != SDCAS_OK) fail(rc, "sdcas_file_metadata");
   }
   return m;
@@ -387,15 +387,17 @@ static bool fold_stat() {
 }
 
 std::vector<Result<FileMetadata>> file_metadata_batch(Engine& engine,
-                                                      const std::vector<std::pair<std::string, ObjectKind>>& files) {
+                                                      const std::vector<std::pair<std::string, ObjectKind>>& files,
+                                                      const std::vector<uint64_t>* size_hints) {
   const size_t n = files.size();
+  if (size_hints && size_hints->size() != n) throw std::invalid_argument("file_metadata_batch: one size hint per file");
   if (fold_stat()) {
     // fs::metadata, the kind and generate_cas_id (mod.rs:63-86) in one library
     // call: the metadata is the fstat of the descriptor the reads use
     std::vector<const char*> paths(n);
     for (size_t i = 0; i < n; ++i) paths[i] = files[i].first.c_str();
     const auto t0 = std::chrono::steady_clock::now();
-    const Engine::RawMetadata raw = engine.file_metadata(paths);
+    const Engine::RawMetadata raw = engine.file_metadata(paths, size_hints ? size_hints->data() : nullptr);
     static const bool trace = [] {
       const char* v = getenv("SDCORE_TRACE_JOB");
       return v && *v && strcmp(v, "0") != 0;
@@ -719,10 +721,14 @@ std::pair<size_t, size_t> identifier_job_step(Engine& engine, Library& db, const
                                               sdcas_job_window* window) {
   const size_t n = file_paths.size();
   std::vector<std::pair<std::string, ObjectKind>> files(n);
-  for (size_t i = 0; i < n; ++i) files[i] = {full_path(location, file_paths[i]), file_paths[i].kind};
+  std::vector<uint64_t> hints(n);
+  for (size_t i = 0; i < n; ++i) {
+    files[i] = {full_path(location, file_paths[i]), file_paths[i].kind};
+    hints[i] = file_paths[i].size_in_bytes;
+  }
   // FileMetadata::new for every row (mod.rs:105-147): failing files are
   // logged and left out of the rest of the step (mod.rs:125-141)
-  auto md = file_metadata_batch(engine, files);
+  auto md = file_metadata_batch(engine, files, &hints);
   return identifier_step_db(
       db, file_paths, md,
       [&](const std::vector<uint64_t>& k, const std::vector<uint8_t>& h, const std::vector<int32_t>& st,
@@ -1129,8 +1135,12 @@ ShallowIdentifierReport shallow_file_identifier_with(Library& db, const Location
 static std::vector<Result<FileMetadata>> metadata_of(Engine& engine, const Location& location,
                                                      const std::vector<FilePathRow>& rows) {
   std::vector<std::pair<std::string, ObjectKind>> files(rows.size());
-  for (size_t i = 0; i < rows.size(); ++i) files[i] = {full_path(location, rows[i]), rows[i].kind};
-  return file_metadata_batch(engine, files);
+  std::vector<uint64_t> hints(rows.size());
+  for (size_t i = 0; i < rows.size(); ++i) {
+    files[i] = {full_path(location, rows[i]), rows[i].kind};
+    hints[i] = rows[i].size_in_bytes;
+  }
+  return file_metadata_batch(engine, files, &hints);
 }
 
 static GroupBy gpu_group_by(Engine& engine) {

@@ -231,8 +231,12 @@ int main(int argc, char** argv) {
         md = [&](const std::vector<FilePathRow>& r) {
           const double a = now();
           std::vector<std::pair<std::string, ObjectKind>> f(r.size());
-          for (size_t i = 0; i < r.size(); ++i) f[i] = {full_path(loc, r[i]), r[i].kind};
-          auto out = file_metadata_batch(*engine, f);
+          std::vector<uint64_t> hints(r.size());
+          for (size_t i = 0; i < r.size(); ++i) {
+            f[i] = {full_path(loc, r[i]), r[i].kind};
+            hints[i] = r[i].size_in_bytes;  // the indexer's sizes (walk_location)
+          }
+          auto out = file_metadata_batch(*engine, f, &hints);
           L.metadata_s += now() - a;
           L.rows += r.size();
           return out;

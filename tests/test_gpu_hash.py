@@ -147,6 +147,11 @@ def test_file_metadata_matches_stat_then_cas_ids(eng, oracle, tmp_path):
     d.mkdir()
     paths += [str(tmp_path / "missing"), str(d)]
     sizes, keys, st, fl = eng.file_metadata(paths)
+    # the same with the indexer's sizes as hints (the directory's and the
+    # missing path's hints are 0)
+    hinted = eng.file_metadata(paths, [os.path.getsize(p) if os.path.isfile(p) else 0 for p in paths])
+    for a, b in zip((sizes, keys, st, fl), hinted):
+        assert np.array_equal(a, b)
     assert st[-2] == errno.ENOENT and fl[-2] == 0
     assert st[-1] == 0 and fl[-1] == 2  # SDCAS_META_DIR
     real = paths[:-2]
@@ -160,39 +165,29 @@ def test_file_metadata_matches_stat_then_cas_ids(eng, oracle, tmp_path):
         assert f"{int(keys[i]):016x}" == oracle.generate_cas_id(real[i], want_sz[i]), i
 
 
-def test_file_metadata_in_descriptor_windows(tmp_path):
-    """a process whose descriptor limit is below the call's file count: the
-    call works in windows of what the limit allows (a child process with a
-    hard RLIMIT_NOFILE of 300, so it cannot be raised), keys equal to the
-    unlimited call's"""
-    import subprocess
-    import sys
-    paths = []
-    for i in range(700):
-        p = tmp_path / f"w{i}"
-        p.write_bytes(os.urandom(1 + (i * 7919) % 150_000))
+def test_file_metadata_with_stale_size_hints(eng, oracle, tmp_path):
+    """sdcas_file_metadata planned from the indexer's sizes when those are
+    stale: files that grew or shrank since (across the 100 KiB branch of
+    cas.rs too) are read again with room for their size now; every size,
+    flag and key equals the hint-free call's and the oracle's"""
+    rng = np.random.default_rng(31)
+    paths, hints = [], []
+    for i in range(400):
+        size = int(rng.choice([0, 1, 5000, 99_000, 102_400, 102_401, 150_000, 3 << 20]))
+        hint = int(rng.choice([size, 0, size + 1, max(0, size - 1), 50_000, 102_400, 102_401, 1 << 22]))
+        p = tmp_path / f"h{i}"
+        write_sparse_file(str(p), "synth", 5000 + i, size, cas_windows(size))
         paths.append(str(p))
-    listing = tmp_path / "list.txt"
-    listing.write_text("\n".join(paths))
-    code = (
-        "import resource, sys, numpy as np\n"
-        "resource.setrlimit(resource.RLIMIT_NOFILE, (300, 300))\n"
-        "from spacedrive_amd import Engine\n"
-        "paths = open(sys.argv[1]).read().split('\\n')\n"
-        "with Engine(staging_bytes=8 << 20) as e:\n"
-        "    sz, k, st, fl = e.file_metadata(paths)\n"
-        "np.save(sys.argv[2], np.stack([sz.astype(np.int64), k.view(np.int64), st.astype(np.int64), fl.astype(np.int64)]))\n")
-    out = tmp_path / "r.npy"
-    r = subprocess.run([sys.executable, "-c", code, str(listing), str(out)], capture_output=True, text=True,
-                       timeout=120, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    assert r.returncode == 0, r.stderr[-2000:]
-    got = np.load(out)
-    from spacedrive_amd import Engine
-    with Engine(staging_bytes=8 << 20) as e:
-        sz, k, st, fl = e.file_metadata(paths)
-    assert not st.any() and (fl == 1).all()
-    assert np.array_equal(got[0], sz.astype(np.int64)) and np.array_equal(got[1], k.view(np.int64))
-    assert not got[2].any() and (got[3] == 1).all()
+        hints.append(hint)
+    s0, k0, st0, f0 = eng.file_metadata(paths)
+    s1, k1, st1, f1 = eng.file_metadata(paths, hints)
+    assert not st0.any() and not st1.any()
+    assert np.array_equal(s0, s1) and np.array_equal(f0, f1) and np.array_equal(k0, k1)
+    for i in range(0, 400, 13):
+        size = os.path.getsize(paths[i])
+        assert s1[i] == size and f1[i] == (1 if size else 0)
+        if size:
+            assert f"{int(k1[i]):016x}" == oracle.generate_cas_id(paths[i], size), i
 
 
 def eng_plain_checksums(paths):
