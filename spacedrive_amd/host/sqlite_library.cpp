@@ -4,6 +4,7 @@
 // (file_identifier_job.rs:251-319, mod.rs:157-342, validator_job.rs:107-172)
 // as prepared statements. See include/sdcore.hpp.
 #include <cstdlib>
+#include <chrono>
 #include <cstring>
 #include <mutex>
 #include <stdexcept>
@@ -95,20 +96,39 @@ struct SqliteLibrary::Impl {
     if (!bulk) return;
     if (batch_depth) exec("COMMIT");  // CREATE INDEX in its own transaction
     try {
+      static const bool trace = [] {
+        const char* v = getenv("SDCORE_TRACE_JOB");
+        return v && *v && strcmp(v, "0") != 0;
+      }();
+      // SDCORE_INDEX_SORT=file: the sorter's spill in SQLite's default temp
+      // store instead of memory (A/B)
+      static const bool mem_sort = [] {
+        const char* v = getenv("SDCORE_INDEX_SORT");
+        return !(v && strcmp(v, "file") == 0);
+      }();
+      const auto t0 = std::chrono::steady_clock::now();
       // the sorter may use helper threads for the one big sort (PRAGMA threads)
       exec("PRAGMA threads = 4");
+      if (mem_sort) exec("PRAGMA temp_store = MEMORY");
       if (const char* f = getenv("SDCORE_FAULT"); f && !strcmp(f, "index_restore"))  // tests: a failing rebuild
         exec("CREATE INDEX file_path_cas_id_idx_fault ON no_such_table (x)");
       exec("CREATE INDEX IF NOT EXISTS file_path_cas_id_idx ON file_path (cas_id)");
       exec("PRAGMA threads = 0");
+      if (mem_sort) exec("PRAGMA temp_store = DEFAULT");
+      const auto t1 = std::chrono::steady_clock::now();
       // the WAL checkpoints the job deferred, once (begin_bulk_identify)
       exec("PRAGMA wal_checkpoint(PASSIVE)");
       exec("PRAGMA wal_autocheckpoint = 1000");
+      if (trace)
+        fprintf(stderr, "sqlite index_restore ms: create index %.2f wal checkpoint %.2f\n",
+                std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count());
     } catch (...) {
       // leave the caller's batch open as it was (its end_batch commits it)
       // and stay in bulk mode, so that a later restore (end_bulk_identify)
       // rebuilds the index
       sqlite3_exec(db, "PRAGMA threads = 0", nullptr, nullptr, nullptr);
+      sqlite3_exec(db, "PRAGMA temp_store = DEFAULT", nullptr, nullptr, nullptr);
       if (batch_depth) sqlite3_exec(db, "BEGIN IMMEDIATE", nullptr, nullptr, nullptr);
       throw;
     }
