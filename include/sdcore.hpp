@@ -27,6 +27,7 @@
 #include <functional>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <optional>
 #include <stdexcept>
 #include <string>
@@ -121,9 +122,17 @@ class Engine {
   sdcas_ctx* raw() { return ctx_; }
 
  private:
-  explicit Engine(sdcas_ctx* c) : ctx_(c) {}
+  explicit Engine(sdcas_ctx* c, int device) : ctx_(c), device_(device) {}
   [[noreturn]] void fail(int rc, const char* what) const;
+  [[noreturn]] void fail_on(sdcas_ctx* c, int rc, const char* what) const;
+  sdcas_ctx* dedup_ctx();
   sdcas_ctx* ctx_;
+  // the group-by's own context (created with the first dedup): a job's
+  // read-ahead holds ctx_ through its path calls, which the group-by of the
+  // batch being written would otherwise wait for (SDCORE_DEDUP_CTX=same: ctx_)
+  int device_ = -1;
+  sdcas_ctx* dedup_ctx_ = nullptr;
+  std::mutex dedup_mu_;
 };
 
 // single-file forms with the reference signatures (cas.rs:23, hash.rs:11)

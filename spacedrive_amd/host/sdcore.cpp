@@ -32,8 +32,30 @@ std::string IoError::message() const {
 
 // ---- Engine -------------------------------------------------------------------
 
-void Engine::fail(int rc, const char* what) const {
-  throw LibraryError(rc, std::string(what) + ": " + sdcas_last_error(ctx_));
+void Engine::fail(int rc, const char* what) const { fail_on(ctx_, rc, what); }
+
+void Engine::fail_on(sdcas_ctx* c, int rc, const char* what) const {
+  throw LibraryError(rc, std::string(what) + ": " + sdcas_last_error(c));
+}
+
+sdcas_ctx* Engine::dedup_ctx() {
+  static const bool same = [] {
+    const char* v = getenv("SDCORE_DEDUP_CTX");
+    return v && strcmp(v, "same") == 0;
+  }();
+  if (same) return ctx_;
+  std::lock_guard<std::mutex> g(dedup_mu_);
+  if (!dedup_ctx_) {
+    sdcas_options opts = SDCAS_OPTIONS_INIT;
+    opts.device = device_;
+    sdcas_ctx* c = nullptr;
+    if (sdcas_init(&opts, &c) != SDCAS_OK) {  // no second context: share the first
+      if (c) sdcas_destroy(c);
+      return ctx_;
+    }
+    dedup_ctx_ = c;
+  }
+  return dedup_ctx_;
 }
 
 std::unique_ptr<Engine> Engine::open(const Options& o) {
@@ -52,10 +74,13 @@ std::unique_ptr<Engine> Engine::open(const Options& o) {
     if (c) sdcas_destroy(c);
     throw LibraryError(rc, msg);
   }
-  return std::unique_ptr<Engine>(new Engine(c));
+  return std::unique_ptr<Engine>(new Engine(c, o.device));
 }
 
-Engine::~Engine() { sdcas_destroy(ctx_); }
+Engine::~Engine() {
+  if (dedup_ctx_) sdcas_destroy(dedup_ctx_);
+  sdcas_destroy(ctx_);
+}
 
 std::string key_to_hex(uint64_t key) {
   char b[17];
@@ -142,10 +167,11 @@ Engine::Dedup Engine::dedup(const std::vector<uint64_t>& keys, const std::vector
     if (window) window->steps = window->rows = window->rereads = 0;
     return r;
   }
-  const int rc = sdcas_dedup_window(ctx_, keys.data(), has_key.data(), status.empty() ? nullptr : status.data(), n,
+  sdcas_ctx* dc = dedup_ctx();
+  const int rc = sdcas_dedup_window(dc, keys.data(), has_key.data(), status.empty() ? nullptr : status.data(), n,
                                     chunk_size, existing_keys.empty() ? nullptr : existing_keys.data(),
                                     existing_keys.size(), window, r.link.data(), &r.created, &r.linked);
-  if (rc != SDCAS_OK) fail(rc, "sdcas_dedup_window");
+  if (rc != SDCAS_OK) fail_on(dc, rc, "sdcas_dedup_window");
   return r;
 }
 
@@ -828,12 +854,14 @@ static bool pipeline_enabled() {
   return on;
 }
 
-// SDCORE_AHEAD_AT=plan: the chunked loop's read-ahead FileMetadata starts
-// at the batch's plan (as round 5's) instead of after its group-by (A/B)
+// SDCORE_AHEAD_AT=groupby: the chunked loop's read-ahead FileMetadata starts
+// after the batch's group-by instead of at its plan (the default: the
+// group-by runs on its own context, Engine::dedup_ctx, so the read-ahead's
+// path call does not hold it up) (A/B)
 static bool ahead_at_plan() {
   static const bool on = [] {
     const char* v = getenv("SDCORE_AHEAD_AT");
-    return v && strcmp(v, "plan") == 0;
+    return !(v && strcmp(v, "groupby") == 0);
   }();
   return on;
 }
@@ -851,9 +879,12 @@ StepLoop run_steps_chunked(Library& db, uint64_t task_count, int32_t cursor, siz
   const size_t batch = std::max(cs, batch_rows);
   uint64_t steps_left = task_count;
   trace_mark();
-  std::vector<FilePathRow> rows = fetch(L.cursor, batch);  // id >= cursor ORDER BY id (file_identifier_job.rs:296-319)
+  // a short first batch: the pipeline's fill is its FileMetadata alone (the
+  // next chunk's runs while it is written)
+  const size_t first_take = batch >= 8 * cs ? std::max(cs, batch / 8) : batch;
+  std::vector<FilePathRow> rows = fetch(L.cursor, first_take);  // id >= cursor ORDER BY id (file_identifier_job.rs:296-319)
   trace_lap(JobTrace::kFetch);
-  bool more = rows.size() == batch;
+  bool more = rows.size() == first_take;
   std::unique_ptr<ChunkFetcher> fetcher;
   if (more) fetcher = std::make_unique<ChunkFetcher>(fetch_ahead, rows.back().id, batch);
   trace_mark();

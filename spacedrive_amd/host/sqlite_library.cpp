@@ -7,6 +7,7 @@
 #include <chrono>
 #include <cstring>
 #include <mutex>
+#include <thread>
 #include <stdexcept>
 #include <unordered_map>
 
@@ -71,6 +72,13 @@ struct SqliteLibrary::Impl {
   // rows with both
   bool bulk = false;
   std::unordered_map<std::string, int32_t> first;
+  // the WAL checkpoint a bulk job deferred, run after it on a connection of
+  // its own (joined by the next bulk job and at close)
+  std::thread checkpointer;
+  void join_checkpoint() {
+    if (checkpointer.joinable()) checkpointer.join();
+  }
+  ~Impl() { join_checkpoint(); }
 
   void first_min(const std::string& cas, int32_t oid) {
     auto it = first.find(cas);
@@ -100,24 +108,41 @@ struct SqliteLibrary::Impl {
         const char* v = getenv("SDCORE_TRACE_JOB");
         return v && *v && strcmp(v, "0") != 0;
       }();
-      // SDCORE_INDEX_SORT=file: the sorter's spill in SQLite's default temp
-      // store instead of memory (A/B)
-      static const bool mem_sort = [] {
-        const char* v = getenv("SDCORE_INDEX_SORT");
-        return !(v && strcmp(v, "file") == 0);
-      }();
+      // (PRAGMA temp_store = MEMORY for the sort measured no faster, 31-34 ms
+      // either way, and changing temp_store drops the connection's TEMP
+      // tables — want_cas)
       const auto t0 = std::chrono::steady_clock::now();
       // the sorter may use helper threads for the one big sort (PRAGMA threads)
       exec("PRAGMA threads = 4");
-      if (mem_sort) exec("PRAGMA temp_store = MEMORY");
       if (const char* f = getenv("SDCORE_FAULT"); f && !strcmp(f, "index_restore"))  // tests: a failing rebuild
         exec("CREATE INDEX file_path_cas_id_idx_fault ON no_such_table (x)");
       exec("CREATE INDEX IF NOT EXISTS file_path_cas_id_idx ON file_path (cas_id)");
       exec("PRAGMA threads = 0");
-      if (mem_sort) exec("PRAGMA temp_store = DEFAULT");
       const auto t1 = std::chrono::steady_clock::now();
-      // the WAL checkpoints the job deferred, once (begin_bulk_identify)
-      exec("PRAGMA wal_checkpoint(PASSIVE)");
+      // the WAL checkpoints the job deferred, once (begin_bulk_identify):
+      // copying the job's pages from the WAL into the database file is
+      // housekeeping no reader waits for (WAL readers see the pages either
+      // way), so a file database runs it on a connection of its own after
+      // the job (SDCORE_CHECKPOINT=sync: here, A/B)
+      static const bool sync_ckpt = [] {
+        const char* v = getenv("SDCORE_CHECKPOINT");
+        return v && strcmp(v, "sync") == 0;
+      }();
+      const bool file_db = !path.empty() && path != ":memory:" && path.rfind("file:", 0) != 0;
+      if (sync_ckpt || !file_db) {
+        exec("PRAGMA wal_checkpoint(PASSIVE)");
+      } else {
+        join_checkpoint();
+        const std::string p = path;
+        checkpointer = std::thread([p] {
+          sqlite3* c = nullptr;
+          if (sqlite3_open_v2(p.c_str(), &c, SQLITE_OPEN_READWRITE | SQLITE_OPEN_NOMUTEX, nullptr) == SQLITE_OK) {
+            sqlite3_busy_timeout(c, 5000);
+            sqlite3_exec(c, "PRAGMA wal_checkpoint(PASSIVE)", nullptr, nullptr, nullptr);
+          }
+          if (c) sqlite3_close(c);
+        });
+      }
       exec("PRAGMA wal_autocheckpoint = 1000");
       if (trace)
         fprintf(stderr, "sqlite index_restore ms: create index %.2f wal checkpoint %.2f\n",
@@ -128,7 +153,6 @@ struct SqliteLibrary::Impl {
       // and stay in bulk mode, so that a later restore (end_bulk_identify)
       // rebuilds the index
       sqlite3_exec(db, "PRAGMA threads = 0", nullptr, nullptr, nullptr);
-      sqlite3_exec(db, "PRAGMA temp_store = DEFAULT", nullptr, nullptr, nullptr);
       if (batch_depth) sqlite3_exec(db, "BEGIN IMMEDIATE", nullptr, nullptr, nullptr);
       throw;
     }
@@ -630,6 +654,7 @@ void SqliteLibrary::connect(int32_t file_path_id, int32_t object_id) {
 bool SqliteLibrary::begin_bulk_identify(size_t orphans) {
   Impl& x = *d_;
   if (!x.cas_index || x.bulk || x.batch_depth) return false;
+  x.join_checkpoint();  // the previous bulk job's deferred checkpoint
   if (sqlite3_step(x.count_cas.s) != SQLITE_ROW) x.fail("count cas_ids");
   const uint64_t with_cas = (uint64_t)sqlite3_column_int64(x.count_cas.s, 0);
   sqlite3_reset(x.count_cas.s);
