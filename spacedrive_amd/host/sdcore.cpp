@@ -626,7 +626,8 @@ using OnGrouped = std::function<void(const sdcas_job_window& done)>;
 static std::pair<size_t, size_t> step_db(Library& db, const std::vector<FilePathRow>& file_paths,
                                          const std::vector<Result<FileMetadata>>& md, const GroupBy& group_by,
                                          sdcas_job_window* window, size_t chunk_size, const OnGrouped* on_grouped,
-                                         const OnGrouped* after_group_by = nullptr);
+                                         const OnGrouped* after_group_by = nullptr,
+                                         const OnGrouped* after_lookup = nullptr);
 
 std::pair<size_t, size_t> identifier_step_db(Library& db, const std::vector<FilePathRow>& file_paths,
                                              const std::vector<Result<FileMetadata>>& md, const GroupBy& group_by,
@@ -637,7 +638,7 @@ std::pair<size_t, size_t> identifier_step_db(Library& db, const std::vector<File
 static std::pair<size_t, size_t> step_db(Library& db, const std::vector<FilePathRow>& file_paths,
                                          const std::vector<Result<FileMetadata>>& md, const GroupBy& group_by,
                                          sdcas_job_window* window, size_t chunk_size, const OnGrouped* on_grouped,
-                                         const OnGrouped* after_group_by) {
+                                         const OnGrouped* after_group_by, const OnGrouped* after_lookup) {
   const size_t n = file_paths.size();
   if (md.size() != n) throw std::invalid_argument("identifier_step_db: one metadata per file_path");
   sdcas_job_window win{};
@@ -694,6 +695,9 @@ static std::pair<size_t, size_t> step_db(Library& db, const std::vector<FilePath
     eobj.push_back(oid);
   }
   trace_lap(JobTrace::kLookup);
+  // (or here: the chunked loop's read-ahead beside the group-by and the
+  // writes, not beside the lookup's index probes)
+  if (after_lookup) (*after_lookup)(win);
   sdcas_job_window gw{};
   gw.max_steps = win.max_steps;
   gw.more = win.more;
@@ -873,16 +877,22 @@ static bool pipeline_enabled() {
   return on;
 }
 
-// SDCORE_AHEAD_AT=groupby: the chunked loop's read-ahead FileMetadata starts
-// after the batch's group-by instead of at its plan (the default: the
-// group-by runs on its own context, Engine::dedup_ctx, so the read-ahead's
-// path call does not hold it up) (A/B)
-static bool ahead_at_plan() {
-  static const bool on = [] {
+// Where the chunked loop's read-ahead FileMetadata starts in a batch
+// (SDCORE_AHEAD_AT): "lookup" (the default) after the existing-Object
+// lookup — beside the group-by (its own context, Engine::dedup_ctx, so the
+// read-ahead's path call does not hold it up) and the writes, but not beside
+// the lookup's index probes, which it slowed (10 000-row batches without bulk
+// identify 316 -> 240-280 K orphans/s at "plan"); "plan" at the plan; "groupby"
+// after the group-by (A/B)
+enum AheadAt { kAheadPlan, kAheadLookup, kAheadGroupBy };
+static AheadAt ahead_at() {
+  static const AheadAt at = [] {
     const char* v = getenv("SDCORE_AHEAD_AT");
-    return !(v && strcmp(v, "groupby") == 0);
+    if (v && strcmp(v, "plan") == 0) return kAheadPlan;
+    if (v && strcmp(v, "groupby") == 0) return kAheadGroupBy;
+    return kAheadLookup;
   }();
-  return on;
+  return at;
 }
 
 // The step loop with the chunk fetcher: each batch is the cursor row when it
@@ -943,8 +953,10 @@ StepLoop run_steps_chunked(Library& db, uint64_t task_count, int32_t cursor, siz
         return a;
       });
     };
-    auto [created, linked] = ahead_at_plan() ? step_db(db, rows, md, group_by, &w, cs, &start_next)
-                                             : step_db(db, rows, md, group_by, &w, cs, nullptr, &start_next);
+    const AheadAt at = ahead_at();
+    auto [created, linked] = step_db(db, rows, md, group_by, &w, cs, at == kAheadPlan ? &start_next : nullptr,
+                                     at == kAheadGroupBy ? &start_next : nullptr,
+                                     at == kAheadLookup ? &start_next : nullptr);
     if (w.steps == 0) break;  // cannot happen: a batch of >= cs rows holds a whole step
     L.created += created;
     L.linked += linked;
