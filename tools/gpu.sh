@@ -5,7 +5,7 @@
 # time limit).
 #
 # usage: tools/gpu.sh OUT STEP [STEP ...]
-#   tests[=EXPR]          pytest -m gpu (EXPR: a -k expression), OUT/pytest_gpu[_EXPR].log
+#   tests[=EXPR]          pytest -m gpu (EXPR: a -k expression, '~' for ' '), OUT/pytest_gpu[_EXPR].log
 #   smoke                 __graft_entry__.smoke()
 #   bench=W[:STEPS:WARM]  bench.py --workload W (c2 c3 c4 c5), OUT/bench_W.json
 #   stats=W               rocprofv3 --kernel-trace --stats of a bench.py W run (20 steps, no baselines), OUT/stats_W/
@@ -33,7 +33,7 @@ step() {
   case $name in
     tests)
       local k=() tag=""
-      [ -n "$arg" ] && k=(-k "$arg") && tag=_$(echo "$arg" | tr -c 'a-zA-Z0-9' '_' | cut -c1-40)
+      [ -n "$arg" ] && k=(-k "${arg//\~/ }") && tag=_$(echo "$arg" | tr -c 'a-zA-Z0-9' '_' | cut -c1-40)
       timeout -k 10 1100 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread "${k[@]}" \
         > "$OUT/pytest_gpu$tag.log" 2>&1
       local rc=$?; tail -2 "$OUT/pytest_gpu$tag.log"; return $rc ;;
