@@ -346,6 +346,10 @@ int sdcas_dedup(sdcas_ctx *ctx, const uint64_t *keys, const uint8_t *has_key, co
  *   max_steps / more as in sdcas_job_window -> d_plan (device u64,
  *   SDCAS_PLAN_WORDS(n_stays)): word 2 the steps run, 3 rows and 8 rereads
  *   (as in sdcas_job_window); the rest is the plan's own (dist_dedup.h).
+ *   Word 9 stamps the building context's coarse index of the plan's re-read
+ *   list (64 or more re-reads; 0: none): an apply on that context uses it
+ *   until the context builds another plan, any other apply searches the
+ *   whole list — the links are the same either way.
  * combine: d_ids[n] ascending; d_has_key / d_status may be NULL (all
  *   present / all ok). Writes exactly one record d_rec[2*u], d_rec[2*u+1] =
  *   (cas key, min id over the files carrying it) per distinct key (capacity

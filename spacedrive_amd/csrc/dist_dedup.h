@@ -54,6 +54,7 @@ struct DistWs {
   bool shard_dirty = false;       // a failed call may have left partial sums in `shard`: zero before use
   Buf<uint64_t> plan, stay_sorted;
   Buf<uint32_t> bitmap;           // dd_plan: the stays ordinals of a long gathered list
+  Buf<uint64_t> ridx;             // the coarse index of a plan's re-read list (k_rr_index), stamped
   void release();
 };
 
@@ -80,6 +81,7 @@ enum : uint32_t {
   kPlanLoop = 6,       // a row every remaining step reads again (all-ones: none); rows after it are not reached
   kPlanLoopReads = 7,  // how many steps read it
   kPlanRereadsRun = 8, // rows two steps the job runs read (sdcas_job_window.rereads)
+  kPlanIndex = 9,      // the stamp of the re-read list's coarse index built for this plan (0: none)
 };
 struct StepWindow {
   uint64_t n_total = 0;    // the job's orphans are ordinals [0, n_total)

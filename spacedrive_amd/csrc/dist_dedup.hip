@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 
@@ -36,20 +37,49 @@ constexpr uint32_t kCountShards = 64;  // the apply's count pairs (a workgroup a
 
 // ---- the steps' positions (see dist_dedup.h, "the job's steps") -------------------
 
+// The re-read list's coarse index (round 6): every keyed file counts the
+// re-reads below two ordinals (its own and its key's first), a binary search
+// of log2(re-reads) dependent loads each — with C5's 0.2 % I/O errors over 50 M
+// files, ~20 per file, the apply 0.80 -> 1.35 ms. k_rr_index counts the
+// re-reads below each of kRrBuckets ordinals b << s (s: the least shift that
+// puts the last re-read below kRrBuckets << s), so a search covers one
+// bucket's entries. ridx: [0] the stamp of the plan it was built for (the
+// plan's word kPlanIndex holds the same; an apply uses the index only when
+// the two agree and are nonzero, so a plan rebuilt elsewhere or never indexed
+// falls back to the full search), [1] s, then kRrBuckets + 1 u32 counts.
+constexpr uint32_t kRrBuckets = 4096;
+constexpr uint32_t kRrWords = 2 + (kRrBuckets + 2) / 2;
+constexpr uint32_t kRrMin = 64;  // shorter lists: the plain search is as short
+
 struct PlanView {
   const uint64_t* rr;  // re-read ordinals, ascending (null: none)
   uint64_t nrr, limit;
   uint64_t loop, loop_reads;  // a row read by every step left (~0: none)
+  const uint32_t* ri;         // the coarse index's counts (null: none)
+  uint32_t rs;                // its shift
 };
 
-__device__ __forceinline__ PlanView plan_view(const uint64_t* plan) {
-  if (!plan) return PlanView{nullptr, 0, ~0ull, ~0ull, 0};
-  return PlanView{plan + kPlanHeader, plan[kPlanRereads], plan[kPlanLimit], plan[kPlanLoop], plan[kPlanLoopReads]};
+__device__ __forceinline__ PlanView plan_view(const uint64_t* plan, const uint64_t* ridx = nullptr) {
+  if (!plan) return PlanView{nullptr, 0, ~0ull, ~0ull, 0, nullptr, 0};
+  PlanView v{plan + kPlanHeader, plan[kPlanRereads], plan[kPlanLimit], plan[kPlanLoop], plan[kPlanLoopReads],
+             nullptr, 0};
+  const uint64_t stamp = plan[kPlanIndex];
+  if (ridx && stamp != 0 && ridx[0] == stamp) {
+    v.ri = reinterpret_cast<const uint32_t*>(ridx + 2);
+    v.rs = (uint32_t)ridx[1];
+  }
+  return v;
 }
 
 // re-read ordinals below x
 __device__ __forceinline__ uint64_t rr_below(const PlanView& pv, uint64_t x) {
   uint64_t lo = 0, hi = pv.nrr;
+  if (pv.ri) {
+    const uint64_t b = x >> pv.rs;
+    if (b >= kRrBuckets) return pv.nrr;  // x >= kRrBuckets << s > the last re-read
+    lo = pv.ri[b];
+    hi = pv.ri[b + 1];
+  }
   while (lo < hi) {
     const uint64_t mid = (lo + hi) >> 1;
     if (pv.rr[mid] < x) lo = mid + 1;
@@ -145,11 +175,12 @@ __global__ void __launch_bounds__(TB) k_dd_apply_r(const uint64_t* __restrict__ 
                                                    const uint32_t* __restrict__ slot, uint32_t n,
                                                    const int64_t* __restrict__ result, uint64_t cs,
                                                    const uint64_t* __restrict__ plan, int64_t* __restrict__ link,
-                                                   unsigned long long* __restrict__ shard) {
+                                                   unsigned long long* __restrict__ shard,
+                                                   const uint64_t* __restrict__ ridx) {
   __shared__ unsigned long long sc[2];
   if (threadIdx.x < 2) sc[threadIdx.x] = 0;
   __syncthreads();
-  const PlanView pv = plan_view(plan);
+  const PlanView pv = plan_view(plan, ridx);
   const uint64_t i0 = (uint64_t)blockIdx.x * TB * R + threadIdx.x;
   uint32_t s[R];
   int64_t me[R], r[R];
@@ -422,8 +453,55 @@ __global__ __launch_bounds__(64) void k_plan_walk(const uint64_t* __restrict__ s
       run = lo;
     }
     plan[kPlanRereadsRun] = run + (loop != ~0ull ? reads - 1 : 0);
-    plan[9] = plan[10] = plan[11] = 0;
+    plan[kPlanIndex] = plan[10] = plan[11] = 0;
   }
+}
+
+// the coarse index of plan's re-read list (above), one thread per count;
+// lists shorter than kRrMin are left unindexed (the plan's stamp stays 0)
+__global__ void k_rr_index(uint64_t* __restrict__ plan, uint64_t* __restrict__ ridx, uint64_t stamp) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t nrr = plan[kPlanRereads];
+  if (nrr < kRrMin || b > kRrBuckets) return;
+  const uint64_t* rr = plan + kPlanHeader;
+  const uint64_t top = rr[nrr - 1];
+  uint32_t s = 0;
+  while ((top >> s) >= kRrBuckets) ++s;
+  auto* cnt = reinterpret_cast<uint32_t*>(ridx + 2);
+  if (b == kRrBuckets) {
+    cnt[b] = (uint32_t)nrr;
+  } else {
+    const uint64_t x = (uint64_t)b << s;  // b < 2^12, s <= 52: no overflow
+    uint64_t lo = 0, hi = nrr;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (rr[mid] < x) lo = mid + 1;
+      else hi = mid;
+    }
+    cnt[b] = (uint32_t)lo;
+  }
+  if (b == 0) {
+    ridx[0] = stamp;
+    ridx[1] = s;
+    plan[kPlanIndex] = stamp;
+  }
+}
+
+// SDCAS_RR_INDEX=0: the applies search the whole re-read list (A/B), read per call
+static bool rr_index_enabled() {
+  const char* v = getenv("SDCAS_RR_INDEX");
+  return !(v && strcmp(v, "0") == 0);
+}
+
+// index plan's re-read list for the applies of this workspace (after the
+// walk that wrote it, on the same stream)
+static hipError_t rr_index(DistWs& w, uint64_t* plan, hipStream_t st) {
+  if (!rr_index_enabled()) return hipSuccess;
+  static std::atomic<uint64_t> stamps{0};
+  hipError_t e;
+  if ((e = w.ridx.ensure(kRrWords))) return e;
+  hipLaunchKernelGGL(k_rr_index, dim3((kRrBuckets + TB) / TB), dim3(TB), 0, st, plan, w.ridx.p, ++stamps);
+  return hipGetLastError();
 }
 
 }  // namespace
@@ -431,7 +509,7 @@ __global__ __launch_bounds__(64) void k_plan_walk(const uint64_t* __restrict__ s
 void DistWs::release() {
   idx_a.release(); idx_b.release(); starts.release(); ocnt.release(); tkey.release(); tmin.release();
   tpos.release(); stay_idx.release(); nstay.release(); stay_cnt.release(); plan.release(); stay_sorted.release();
-  bitmap.release(); flag.release(); shard.release();
+  bitmap.release(); flag.release(); shard.release(); ridx.release();
   shard_dirty = false;
 }
 
@@ -1471,11 +1549,12 @@ __global__ void __launch_bounds__(TB) k_solo_apply_r(const uint64_t* __restrict_
                                                      const uint64_t* __restrict__ emin, uint64_t cs,
                                                      const uint64_t* __restrict__ plan, int64_t* __restrict__ link,
                                                      unsigned long long* __restrict__ shard,
-                                                     const uint32_t* __restrict__ noncontig, uint32_t ebase) {
+                                                     const uint32_t* __restrict__ noncontig, uint32_t ebase,
+                                                     const uint64_t* __restrict__ ridx) {
   __shared__ unsigned long long sc[2];
   if (threadIdx.x < 2) sc[threadIdx.x] = 0;
   __syncthreads();
-  const PlanView pv = plan_view(plan);
+  const PlanView pv = plan_view(plan, ridx);
   // ordinals eids[0] + index (the insert found no other): a key's first
   // ordinal follows from its first file's index, no read
   const bool contig = noncontig && *noncontig == 0;
@@ -1704,11 +1783,13 @@ static hipError_t local_fused(DistWs& w, const uint64_t* keys, const uint8_t* ha
                      ids, stays ? n : 0u, (const uint32_t*)nullptr, win.n_total ? win.n_total : (uint64_t)n, cs,
                      win.max_steps, win.more, w.plan.p, stays ? w.stay_cnt.p + nt : (const uint32_t*)nullptr,
                      stay_groups(nt));
+  if (stays && n >= kRrMin && (e = rr_index(w, w.plan.p, st))) return e;
   const uint64_t* emp = ne ? w.tkey.p : nullptr;
   auto apply = [&](auto kern, uint32_t r) {
     const uint32_t g = (uint32_t)(((uint64_t)n + (uint64_t)TB * r - 1) / ((uint64_t)TB * r));
     if (g) hipLaunchKernelGGL(kern, dim3(g), dim3(TB), 0, st, ids, w.tpos.p, n, tab, emp, cs, w.plan.p, link,
-                              sharded ? w.shard.p : nullptr, contig ? (const uint32_t*)w.flag.p : nullptr, sticky);
+                              sharded ? w.shard.p : nullptr, contig ? (const uint32_t*)w.flag.p : nullptr, sticky,
+                              (const uint64_t*)w.ridx.p);
   };
   switch (ar) {
     case 1: apply(k_solo_apply_r<1>, 1); break;
@@ -1869,6 +1950,7 @@ hipError_t dd_plan(DistWs& w, const uint64_t* stays, uint32_t n_stays, uint64_t 
   hipLaunchKernelGGL(k_plan_walk, dim3(1), dim3(64), 0, st, sorted, (const uint32_t*)nullptr,
                      (const uint64_t*)nullptr, n_stays, (const uint32_t*)nullptr, win.n_total, cs, win.max_steps,
                      win.more, plan, tcnt, ntiles);
+  if (n_stays >= kRrMin && (e = rr_index(w, plan, st))) return e;
   return hipGetLastError();
 }
 
@@ -1948,7 +2030,8 @@ hipError_t dd_apply(DistWs& w, const uint64_t* ids, const uint32_t* slot, uint32
   unsigned long long* sh = ar && counts ? w.shard.p : nullptr;
   auto apply = [&](auto kern, uint32_t r) {
     const uint32_t g = (uint32_t)(((uint64_t)n + (uint64_t)TB * r - 1) / ((uint64_t)TB * r));
-    hipLaunchKernelGGL(kern, dim3(g), dim3(TB), 0, st, ids, slot, n, result, cs, plan, link, sh);
+    hipLaunchKernelGGL(kern, dim3(g), dim3(TB), 0, st, ids, slot, n, result, cs, plan, link, sh,
+                       (const uint64_t*)w.ridx.p);
   };
   switch (ar) {
     case 1: apply(k_dd_apply_r<1>, 1); break;

@@ -325,6 +325,50 @@ def test_combine_contract_one_record_per_key(eng, corpus):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("chunk_size", [100, 7, 2])
+def test_device_reread_index(eng, oracle, chunk_size, monkeypatch):
+    """round 6: the applies count the re-reads below an ordinal through a
+    coarse index of the plan's re-read list (k_rr_index, built for lists of
+    64 or more and stamped with its plan). 8 % stays rows over 200 K files
+    (hundreds to thousands of re-reads; at chunk size 1 the first stays row
+    would be read by every later step, a loop, not re-reads): every link and both counts
+    against the oracle with the index and without it (SDCAS_RR_INDEX=0), on
+    the world-of-one path and on the staged path (combine, resolve, stays,
+    plan, apply); and a plan whose index was replaced by a later plan's on
+    the same stages (stamps differ) falls back to the full search"""
+    from spacedrive_amd.dist_dedup import DeviceStages
+    n = 200_000
+    keys, has, status, existing = make_corpus(4242 + chunk_size, n, pool=n // 4, p_none=0.04, p_err=0.04)
+    want, wc, wl = oracle.identifier_dedup(keys, has, status, chunk_size, existing)
+    (k, h, s, ids), = shard(keys, has, status, existing, 1, device="cuda")[0]
+    ek = torch.from_numpy(np.ascontiguousarray(existing).view(np.int64)).cuda()
+    eids = torch.arange(existing.size, dtype=torch.int64, device="cuda")
+    keys2, has2, status2, _ = make_corpus(99 + chunk_size, n, pool=n // 4, p_none=0.2, p_err=0.0)
+    (_, h2, s2, ids2), = shard(keys2, has2, status2, existing, 1, device="cuda")[0]
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SDCAS_RR_INDEX", flag)
+        st = DeviceStages(eng)
+        link, cnt = st.local(k, h, s, ids, chunk_size, ek, eids)
+        assert np.array_equal(link.cpu().numpy(), want), flag
+        assert tuple(cnt.tolist()) == (wc, wl), flag
+        rec, slot, _ = st.combine(k, h, s, ids, 1)
+        erec, _, _ = st.combine(ek, None, None, eids, 1)
+        ans = st.resolve(rec, erec)
+        stays, _ = st.stays(h, s, ids, n)
+        plan = st.plan(stays, n, chunk_size)
+        if flag == "1":
+            assert int(plan[1]) >= 64 and int(plan[9]) != 0  # indexed
+            stays2, _ = st.stays(h2, s2, ids2, n)
+            plan2 = st.plan(stays2, n, chunk_size)  # the workspace's index is plan2's now
+            assert int(plan2[9]) not in (0, int(plan[9]))
+        else:
+            assert int(plan[9]) == 0
+        link, cnt = st.apply(ids, slot, ans, chunk_size, plan)
+        assert np.array_equal(link.cpu().numpy(), want), flag
+        assert tuple(cnt.tolist()) == (wc, wl), flag
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n", [1024 * 7 + 1, 1024 * 7 + 63, 1024 * 7 + 65, 1024 * 29 + 1000, 1024 * 300 + 17])
 @pytest.mark.parametrize("chunk_size", [100, 7])
 def test_device_local_stays_in_partial_last_tile(eng, oracle, n, chunk_size):
@@ -641,6 +685,9 @@ def test_device_plan_sorts_gathered_stays(eng, oracle, m):
                       max_steps, more).cpu().numpy()
         h = N.SDCAS_PLAN_HEADER_WORDS
         nr = int(got[1])
+        # word 9: the stamp of the re-read list's coarse index, one per plan built (0: none)
+        assert (got[9] != 0) == (nr >= 64) and (ref[9] != 0) == (nr >= 64)
+        got[9] = ref[9] = 0
         assert np.array_equal(got[:h], ref[:h]) and np.array_equal(got[h:h + nr], ref[h:h + nr]), (cs, max_steps)
         # the oracle: rows without a cas_id at exactly those ordinals
         has = np.ones(n_total, np.uint8)
