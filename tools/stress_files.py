@@ -4,8 +4,11 @@ is the checker). For --rounds rounds: a fresh directory of random files —
 sizes from empty to several MiB, around the 100 KiB whole-file / sampled
 cut and the 1 MiB piece, random bytes — then sdcas_cas_ids with each file's
 size (and, for a few, a size recorded larger or smaller than the file: the
-reference's UnexpectedEof and grown-file cases) and sdcas_checksums, every
-key, digest and status against the oracle's cas.rs / hash.rs restatements.
+reference's UnexpectedEof and grown-file cases), sdcas_file_metadata with
+those recorded sizes as its staging hints (FileMetadata::new: the size from
+the read's own descriptor, a cas_id for every non-empty file; round 6) and
+sdcas_checksums, every key, size, flag, digest and status against the
+oracle's cas.rs / hash.rs restatements.
 Prints one JSON line.
 
 usage: stress_files.py [--rounds 4] [--files 3000] [--dir $TMPDIR/sdcas_stress]"""
@@ -66,6 +69,16 @@ def main():
             if (wst == 0) != got_ok or (got_ok and key_to_hex(keys[j]) != want):
                 bad.append({"round": rnd, "file": i, "size": sizes[i], "recorded": rec[i], "call": "cas_ids",
                             "status": int(st[j]), "oracle_status": wst})
+        # FileMetadata::new (mod.rs:48-96) over every file, planned from the
+        # recorded sizes: actual sizes, keys of the non-empty files
+        ms, mk, mst, mfl = eng.file_metadata(paths, rec)
+        for i in range(a.files):
+            ok = int(mst[i]) == 0 and int(ms[i]) == sizes[i] and int(mfl[i]) == (1 if sizes[i] else 0)
+            if ok and sizes[i]:
+                ok = key_to_hex(mk[i]) == oracle.generate_cas_id(paths[i], sizes[i])
+            if not ok:
+                bad.append({"round": rnd, "file": i, "size": sizes[i], "recorded": rec[i], "call": "file_metadata",
+                            "status": int(mst[i]), "got_size": int(ms[i]), "flags": int(mfl[i])})
         dig, st2 = eng.file_checksums(paths)
         for i in range(a.files):
             if int(st2[i]) != 0 or bytes(dig[i]).hex() != oracle.file_checksum(paths[i]):
