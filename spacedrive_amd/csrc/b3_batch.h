@@ -14,10 +14,12 @@ constexpr uint32_t kWG = 512;     // threads per workgroup: 2 slots per lane
 // running a few 1 MiB tiles one CU each (leaf variant kSmallVariant: since
 // round 4 variant 73, a quad of lanes per slot — sdcas_cas_ids of 1 / 10 /
 // 100 / 300 files 68.3 / 124.8 / 291.9 / 545.7 us -> 53.1 / 112.0 / 280.1 /
-// 521.6 us against 71, profiles/r04_small_quad.json).
+// 521.6 us against 71, profiles/r04_small_quad.json; since round 6 variant
+// 84, 73 with four blocks of each chunk in flight and each quad's block
+// staged in LDS, profiles/r06_latency_small.json).
 constexpr uint32_t kSmallTile = 128;
 constexpr uint64_t kSmallSlots = 1ull << 14;
-constexpr int kSmallVariant = 73;
+constexpr int kSmallVariant = 84;
 // The shape sort's workspace: the 256 bin totals, then each scatter
 // workgroup's (kSortPerWG messages) count per bin, bin-major.
 constexpr uint32_t kSortTotalsWords = 256;

@@ -398,6 +398,129 @@ __device__ __forceinline__ void hash_chunk_quad(const uint8_t* __restrict__ p, u
   }
 }
 
+// The same chain with four blocks in flight (round 6): a lone chunk's loop
+// above waits for each block's load before its compression, so a one-file
+// call's kernel was the sum of 16 load latencies (the blocks arrive from L2
+// or HBM right after their upload) and 16 compressions. Here block b + 4 is
+// requested as soon as block b has been compressed, from a ring of four
+// register sets (64 VGPRs: the quad kernel holds few waves), so a load has
+// four compressions (~2 us) to land.
+__device__ __forceinline__ void quad_block(const uint32_t (&m)[16], uint32_t b, uint32_t lb, uint32_t lblen,
+                                           uint32_t endf, uint64_t j, uint32_t (&cv)[8]) {
+  uint32_t mm[16], o[8];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) mm[i] = m[i];
+  const bool last = b == lb;
+  if (last && lblen < BLOCK_LEN) mask_tail_table(mm, lblen);
+  compress_quad(cv, mm, j, last ? lblen : BLOCK_LEN, (b == 0 ? CHUNK_START : 0u) | (last ? endf : 0u), o);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) cv[i] = o[i];
+}
+
+__device__ __forceinline__ void hash_chunk_quad4(const uint8_t* __restrict__ p, uint32_t clen, uint64_t j, bool root,
+                                                 uint32_t (&cv)[8]) {
+  set_iv(cv);
+  const uint32_t lb = clen <= BLOCK_LEN ? 0u : (clen - 1) / BLOCK_LEN;  // last block index
+  const uint32_t lblen = clen - lb * BLOCK_LEN;
+  const uint32_t endf = CHUNK_END | (root ? ROOT : 0u);
+  uint32_t r0[16], r1[16], r2[16], r3[16];
+  // blocks past the last are not loaded: their registers are "whatever is
+  // there" (an empty asm defines them, as in hash_chunk_pl) and never read
+#pragma unroll
+  for (int w = 0; w < 16; ++w) asm volatile("" : "=v"(r1[w]), "=v"(r2[w]), "=v"(r3[w]));
+  load_full_block(p, r0);
+  if (lb >= 1) load_full_block(p + BLOCK_LEN, r1);
+  if (lb >= 2) load_full_block(p + 2 * BLOCK_LEN, r2);
+  if (lb >= 3) load_full_block(p + 3 * BLOCK_LEN, r3);
+  const uint8_t* q = p + 4 * BLOCK_LEN;
+#pragma unroll 1
+  for (uint32_t b = 0;; b += 4, q += 4 * BLOCK_LEN) {
+    quad_block(r0, b, lb, lblen, endf, j, cv);
+    if (b + 4 <= lb) load_full_block(q, r0);
+    if (b + 1 > lb) break;
+    quad_block(r1, b + 1, lb, lblen, endf, j, cv);
+    if (b + 5 <= lb) load_full_block(q + BLOCK_LEN, r1);
+    if (b + 2 > lb) break;
+    quad_block(r2, b + 2, lb, lblen, endf, j, cv);
+    if (b + 6 <= lb) load_full_block(q + 2 * BLOCK_LEN, r2);
+    if (b + 3 > lb) break;
+    quad_block(r3, b + 3, lb, lblen, endf, j, cv);
+    if (b + 7 <= lb) load_full_block(q + 3 * BLOCK_LEN, r3);
+    if (b + 4 > lb) break;
+  }
+}
+
+// QD 3 (round 6): a quad's block staged in LDS. Lane q loads only its
+// quarter of each block (one dwordx4, four blocks in flight), writes it to the
+// quad's 64-byte LDS buffer (qbuf[qslot..qslot+16)), and reads back the 28
+// words its rounds take (word indices wi: kQuadWord for its q, with qslot
+// added) for compress_quad_w — a lone quad's chain without the 84 selects per
+// compression. The quad's lanes are one wave, whose LDS operations run in
+// issue order, so a lane reads its quad's block after the write that holds it
+// and the next block's write lands after these reads; the empty asm keeps the
+// compiler from moving them across each other.
+__device__ __forceinline__ void quad_lds_words(uint32_t* __restrict__ qbuf, uint32_t qslot, uint4 v,
+                                               const uint32_t (&wi)[28], uint32_t (&w)[28]) {
+  const uint32_t q = __lane_id() & 3u;
+  asm volatile("" ::: "memory");
+  *reinterpret_cast<uint4*>(&qbuf[qslot + 4 * q]) = v;
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int k = 0; k < 28; ++k) w[k] = qbuf[wi[k]];
+}
+
+__device__ __forceinline__ void quad_lds_block(uint4 v, uint32_t b, uint32_t lb, uint32_t lblen, uint32_t endf,
+                                               uint64_t j, uint32_t* __restrict__ qbuf, uint32_t qslot,
+                                               const uint32_t (&wi)[28], uint32_t (&cv)[8]) {
+  const bool last = b == lb;
+  if (last && lblen < BLOCK_LEN) {
+    const uint4 mk = reinterpret_cast<const uint4*>(kTailMasks.w[lblen])[__lane_id() & 3u];
+    v.x &= mk.x;
+    v.y &= mk.y;
+    v.z &= mk.z;
+    v.w &= mk.w;
+  }
+  uint32_t w[28], o[8];
+  quad_lds_words(qbuf, qslot, v, wi, w);
+  compress_quad_w(cv, w, j, last ? lblen : BLOCK_LEN, (b == 0 ? CHUNK_START : 0u) | (last ? endf : 0u), o);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) cv[i] = o[i];
+}
+
+__device__ __forceinline__ void hash_chunk_quad_lds(const uint8_t* __restrict__ p, uint32_t clen, uint64_t j,
+                                                    bool root, uint32_t* __restrict__ qbuf, uint32_t qslot,
+                                                    const uint32_t (&wi)[28], uint32_t (&cv)[8]) {
+  set_iv(cv);
+  const uint32_t lb = clen <= BLOCK_LEN ? 0u : (clen - 1) / BLOCK_LEN;  // last block index
+  const uint32_t lblen = clen - lb * BLOCK_LEN;
+  const uint32_t endf = CHUNK_END | (root ? ROOT : 0u);
+  const uint4* src = reinterpret_cast<const uint4*>(p) + (__lane_id() & 3u);  // this lane's quarter of block 0
+  uint4 g0, g1, g2, g3;
+  // quarters of blocks past the last are not loaded (never read)
+  asm volatile("" : "=v"(g1.x), "=v"(g1.y), "=v"(g1.z), "=v"(g1.w));
+  asm volatile("" : "=v"(g2.x), "=v"(g2.y), "=v"(g2.z), "=v"(g2.w));
+  asm volatile("" : "=v"(g3.x), "=v"(g3.y), "=v"(g3.z), "=v"(g3.w));
+  g0 = src[0];
+  if (lb >= 1) g1 = src[4];
+  if (lb >= 2) g2 = src[8];
+  if (lb >= 3) g3 = src[12];
+#pragma unroll 1
+  for (uint32_t b = 0;; b += 4) {
+    quad_lds_block(g0, b, lb, lblen, endf, j, qbuf, qslot, wi, cv);
+    if (b + 4 <= lb) g0 = src[4 * (b + 4)];
+    if (b + 1 > lb) break;
+    quad_lds_block(g1, b + 1, lb, lblen, endf, j, qbuf, qslot, wi, cv);
+    if (b + 5 <= lb) g1 = src[4 * (b + 5)];
+    if (b + 2 > lb) break;
+    quad_lds_block(g2, b + 2, lb, lblen, endf, j, qbuf, qslot, wi, cv);
+    if (b + 6 <= lb) g2 = src[4 * (b + 6)];
+    if (b + 3 > lb) break;
+    quad_lds_block(g3, b + 3, lb, lblen, endf, j, qbuf, qslot, wi, cv);
+    if (b + 7 <= lb) g3 = src[4 * (b + 7)];
+    if (b + 4 > lb) break;
+  }
+}
+
 // Block loop of a leaf chunk: PF 8 = hash_chunk_ps, 9 = hash_chunk_pl, 4 =
 // hash_chunk_pp, 59 = hash_chunk_full for a whole non-root chunk (per lane)
 // else hash_chunk_ps, 69 = hash_chunk_full when every active lane of the wave
@@ -548,7 +671,9 @@ __device__ __forceinline__ void leaf_order(uint32_t tid, const uint32_t (&bin)[T
 // QD: a quad of lanes per slot (WG = 4 x the slots a pass covers): each
 // chunk and each tree node by compress_quad; the quad's lead lane alone
 // writes shared state (task lists, chaining values, digests). Needs ORD 0 and
-// CA 0.
+// CA 0. QD 2 (round 6): the same with four blocks of a chunk in flight
+// (hash_chunk_quad4); QD 3: and each quad's block staged in LDS, every lane
+// reading its rounds' words (hash_chunk_quad_lds, the tree's parents too).
 // XT (round 5), bit 1: a tree level of at most 32 tasks — levels 5-10 in C2's
 // tiles (30, 14, 7 ... tasks), each one wave of mostly idle lanes — runs its
 // parents by quads of lanes (parent_quad: ~310 instructions per lane for a
@@ -574,6 +699,7 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
   __shared__ uint16_t order[ORD ? TL : 1];  // leaf loop position -> slot
   __shared__ uint32_t sexp[(XT & 2) ? TL / 32 : 1];  // XT 2: slots whose node goes to HBM (phase 4)
   __shared__ uint64_t next_tile;
+  __shared__ uint32_t qbuf[QD == 3 ? 16 * (WG / 4) : 1];  // QD 3: each quad's 64-byte block buffer
 
   // XT bits 3-5 (ablation): that many s_nop at the entry, shifting the
   // kernel's code by 4-byte steps (code placement A/B, cdna_hip_programming.md
@@ -587,6 +713,17 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
   constexpr uint32_t SW = QD ? WG / 4 : WG;  // slot workers: lanes, or quads of lanes
   const uint32_t sid = QD ? tid >> 2 : tid;
   const bool lead = !QD || (tid & 3u) == 0;
+  // QD 3: the LDS word indices of this lane's 28 round inputs in its quad's
+  // block buffer (kQuadWord for lane q, fixed for the kernel)
+  const uint32_t qslot = 16 * sid;
+  uint32_t wi[QD == 3 ? 28 : 1];
+  if constexpr (QD == 3) {
+    const uint32_t q = tid & 3u;
+    const bool q1 = q & 1u, q2 = q & 2u;
+#pragma unroll
+    for (int k = 0; k < 28; ++k)
+      wi[k] = qslot + qsel(q1, q2, kQuadWord.w[0][k], kQuadWord.w[1][k], kQuadWord.w[2][k], kQuadWord.w[3][k]);
+  }
   // DYN 1: tiles after the first are handed out by a global counter
   // (total_p[2], zeroed by k_tile_first) instead of round-robin, so a
   // workgroup that drew cheap tiles takes more and the grid drains within
@@ -768,7 +905,9 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
       const uint32_t clen = len == 0 ? 0u : (uint32_t)min<uint64_t>(CHUNK_LEN, len - j * CHUNK_LEN);
       const bool root = (C == 1);
       uint32_t cv[8];
-      if constexpr (QD) hash_chunk_quad(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
+      if constexpr (QD == 3) hash_chunk_quad_lds(blob + offs[m] + j * CHUNK_LEN, clen, j, root, qbuf, qslot, wi, cv);
+      else if constexpr (QD == 2) hash_chunk_quad4(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
+      else if constexpr (QD) hash_chunk_quad(blob + offs[m] + j * CHUNK_LEN, clen, j, root, cv);
       else leaf_hash<PF>(leaf_ptr<PF>(blob, blob + offs[m] + j * CHUNK_LEN), clen, j, root, cv);
       if (!lead) continue;
       if (root) {
@@ -827,14 +966,26 @@ __global__ void __launch_bounds__(WG, MINW ? MINW : (ORD ? 6 : 1)) k_leaf_tree(c
         const uint32_t e = task[task_base<TL>(k) + (TR == 2 ? min(t, T - 1) : t)];
         const uint32_t l = e & 1023u, r = (e >> 10) & 1023u;
         const bool root = e >> 31;
-        uint32_t a[8], b[8], o[8];
+        uint32_t o[8];
+        if constexpr (QD == 3) {
+          // lane q's quarter of the parent block: words 4q..4q+3 of l's CV
+          // (q < 2) or of r's (q >= 2), staged as a leaf block is
+          const uint32_t q = tid & 3u;
+          const uint32_t* src = q < 2 ? &cvs[l][4 * q] : &cvs[r][4 * (q - 2)];
+          uint32_t w[28], iv[8];
+          quad_lds_words(qbuf, qslot, make_uint4(src[0], src[1], src[2], src[3]), wi, w);
+          set_iv(iv);
+          compress_quad_w(iv, w, 0, BLOCK_LEN, PARENT | (root ? ROOT : 0u), o);
+        } else {
+          uint32_t a[8], b[8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          a[q] = cvs[l][q];
-          b[q] = cvs[r][q];
+          for (int q = 0; q < 8; ++q) {
+            a[q] = cvs[l][q];
+            b[q] = cvs[r][q];
+          }
+          if constexpr (QD) parent_quad(a, b, root, o);
+          else parent<kGA<PF>>(a, b, root, o);
         }
-        if constexpr (QD) parent_quad(a, b, root, o);
-        else parent<kGA<PF>>(a, b, root, o);
         if ((TR == 2 && t >= T) || !lead) continue;
         if (root) {
           const uint32_t mm = m0 + ((e >> 20) & 2047u);
@@ -1869,6 +2020,14 @@ static const LeafVariant kLeafVariants[] = {
     ABL1(512, k_leaf_tree<512, 279, 1, 1, 2, 2, 0, kTile, 0, 16>),  //   (s_nop at the entry: code placement A/B)
     ABL1(512, k_leaf_tree<512, 279, 1, 1, 2, 2, 0, kTile, 0, 24>),
     ABL1(512, k_leaf_tree<512, 279, 1, 1, 2, 2, 0, kTile, 0, 32>),
+    // 83 (round 6): 73 with four blocks of each chunk in flight
+    // (hash_chunk_quad4): a one-file call's kernel -4 %, superseded by 84
+    ABLS(4 * kSmallTile, k_leaf_tree<4 * kSmallTile, 79, 1, 0, 2, 0, 0, kSmallTile, 2>),
+    // 84 (product, the small-batch default since round 6): 83 with each
+    // quad's block staged in LDS and every lane reading its rounds' 28 words
+    // from it (hash_chunk_quad_lds, compress_quad_w: no per-round word
+    // selects, 453 -> 141 v_cndmask in the kernel)
+    PRODS(4 * kSmallTile, k_leaf_tree<4 * kSmallTile, 79, 1, 0, 2, 0, 0, kSmallTile, 3>),
 };
 #undef PROD
 #undef PROD1

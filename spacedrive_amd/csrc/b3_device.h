@@ -236,6 +236,75 @@ __device__ __forceinline__ void compress_quad(const uint32_t (&cv)[8], const uin
   out[7] = qperm<0xFF>(hi);
 }
 
+// The same compression with each lane's message words already picked (round
+// 6, the small-batch kernel's QD 3): w[4r..4r+3] are the words lane q's G
+// steps take in round r — m[s(2q)], m[s(2q+1)], m[s(8+2q)], m[s(9+2q)] for
+// round r's schedule s (kQuadWord) — read from the block staged in LDS, so no
+// lane selects them from the whole block (compress_quad's 84 v_cndmask per
+// compression, more than a quarter of its instructions).
+#define B3_QROUND_W(r)                  \
+  do {                                  \
+    B3_G(a, b, c, d, w[4 * (r)], w[4 * (r) + 1]);         \
+    b = qperm<kQ1>(b);                  \
+    c = qperm<kQ2>(c);                  \
+    d = qperm<kQ3>(d);                  \
+    B3_G(a, b, c, d, w[4 * (r) + 2], w[4 * (r) + 3]);     \
+    b = qperm<kQ3>(b);                  \
+    c = qperm<kQ2>(c);                  \
+    d = qperm<kQ1>(d);                  \
+  } while (0)
+
+__device__ __forceinline__ void compress_quad_w(const uint32_t (&cv)[8], const uint32_t (&w)[28], uint64_t counter,
+                                                uint32_t block_len, uint32_t flags, uint32_t (&out)[8]) {
+  const uint32_t q = __lane_id() & 3u;
+  const bool q1 = q & 1u, q2 = q & 2u;
+  uint32_t a = qsel(q1, q2, cv[0], cv[1], cv[2], cv[3]);
+  uint32_t b = qsel(q1, q2, cv[4], cv[5], cv[6], cv[7]);
+  uint32_t c = qsel(q1, q2, IV0, IV1, IV2, IV3);
+  uint32_t d = qsel(q1, q2, (uint32_t)counter, (uint32_t)(counter >> 32), block_len, flags);
+  B3_QROUND_W(0);
+  B3_QROUND_W(1);
+  B3_QROUND_W(2);
+  B3_QROUND_W(3);
+  B3_QROUND_W(4);
+  B3_QROUND_W(5);
+  B3_QROUND_W(6);
+  const uint32_t lo = a ^ c, hi = b ^ d;
+  out[0] = qperm<0x00>(lo);
+  out[1] = qperm<0x55>(lo);
+  out[2] = qperm<0xAA>(lo);
+  out[3] = qperm<0xFF>(lo);
+  out[4] = qperm<0x00>(hi);
+  out[5] = qperm<0x55>(hi);
+  out[6] = qperm<0xAA>(hi);
+  out[7] = qperm<0xFF>(hi);
+}
+
+// kQuadWord[q][4r + k]: the message word lane q's k-th G input of round r
+// takes (the schedules of compress_quad's seven B3_QROUNDs)
+struct QuadWords {
+  uint8_t w[4][28];
+};
+constexpr QuadWords make_quad_words() {
+  constexpr uint8_t s[7][16] = {{0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+                                {2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8},
+                                {3, 4, 10, 12, 13, 2, 7, 14, 6, 5, 9, 0, 11, 15, 8, 1},
+                                {10, 7, 12, 9, 14, 3, 13, 15, 4, 0, 11, 2, 5, 8, 1, 6},
+                                {12, 13, 9, 11, 15, 10, 14, 8, 7, 2, 5, 3, 0, 1, 6, 4},
+                                {9, 14, 11, 5, 8, 12, 15, 1, 13, 3, 0, 10, 2, 6, 4, 7},
+                                {11, 15, 5, 0, 1, 9, 8, 6, 14, 10, 2, 12, 3, 4, 7, 13}};
+  QuadWords t{};
+  for (int q = 0; q < 4; ++q)
+    for (int r = 0; r < 7; ++r) {
+      t.w[q][4 * r] = s[r][2 * q];
+      t.w[q][4 * r + 1] = s[r][2 * q + 1];
+      t.w[q][4 * r + 2] = s[r][8 + 2 * q];
+      t.w[q][4 * r + 3] = s[r][9 + 2 * q];
+    }
+  return t;
+}
+constexpr QuadWords kQuadWord = make_quad_words();
+
 __device__ __forceinline__ void parent_quad(const uint32_t (&l)[8], const uint32_t (&r)[8], bool root,
                                             uint32_t (&out)[8]) {
   uint32_t m[16], iv[8];

@@ -216,6 +216,7 @@ struct sdcas_ctx {
   }
   uint32_t upload_parts = 4;  // sdcas_cas_ids: a lone slot's reads and upload overlapped in this many parts (0/1: off)
   bool plan_small = true;      // small batches planned on the host (SDCAS_PLAN_SMALL=0: on the device)
+  bool small_direct = true;    // such a batch: metadata behind its bytes, results written to pinned memory (slot_submit)
 
   // progress / cancellation of the path APIs (sdcas_options, sdcas_set_progress)
   sdcas_progress_fn progress = nullptr;
@@ -498,29 +499,43 @@ int slot_submit(sdcas_ctx* c, Slot& s, bool res32) {
   // offsets when they fit there (each small copy is a blit kernel of its own)
   const bool packed = 2 * s.n <= s.cap_n;
   if (packed) memcpy(s.hm + s.n, s.lens(), 8 * s.n);
-  const uint64_t* d_lens = s.d_meta.p + (packed ? s.n : s.cap_n);
   // A batch for the small kernel in caller order is planned here and its
   // plan goes up behind the lengths in the same copy: the scan, k_tile_first
   // and (when no message crosses a tile) k_finish_t are not launched.
   uint64_t meta_words = packed ? 2 * s.n : s.n;
-  BatchPlan plan;
   const uint64_t plan_tiles = s.chunks / kSmallTile + 2;
   const uint64_t plan_words = s.n + (plan_tiles + 1) / 2 + 4;
   const bool use_plan = c->plan_small && packed && s.n < kSortMinMsgs && s.chunks <= c->ws.small_slots &&
                         2 * s.n + plan_words <= s.cap_n;
+  if (use_plan) meta_words = 2 * s.n + plan_words;
+  // Round 6, a small planned batch read into the slot (the latency-bound
+  // calls: a lone file of the watcher or of browse): its metadata words go up
+  // behind its bytes in the SAME copy (at a 256-byte offset past them, inside
+  // the slot's capacity), and the kernels write the results straight into the
+  // slot's pinned result words (device-visible host memory) instead of a
+  // device buffer and a download. Two copies (and their API calls) fewer;
+  // the event the host waits on follows the kernels, so their writes to
+  // host memory are visible when it fires. SDCAS_SMALL_DIRECT=0: off (A/B).
+  const uint64_t moff = (s.used + 255) & ~uint64_t(255);
+  const bool direct = c->small_direct && use_plan && !uploaded && !s.src &&
+                      moff + 8 * meta_words + kSlack <= std::min<uint64_t>(s.h_cap, s.d_blob.cap);
+  uint64_t* dm = direct ? reinterpret_cast<uint64_t*>(s.d_blob.p + moff) : s.d_meta.p;
+  const uint64_t* d_lens = dm + (packed ? s.n : s.cap_n);
+  BatchPlan plan;
   if (use_plan) {
     uint64_t* hS = s.hm + 2 * s.n;
     uint32_t* htf = reinterpret_cast<uint32_t*>(hS + s.n);
     uint64_t* htot = hS + s.n + (plan_tiles + 1) / 2;
     batch_plan_host(s.lens(), (uint32_t)s.n, kSmallTile, c->ws.cap_slots, hS, htf, htot, &plan.crossing);
-    plan.S = s.d_meta.p + 2 * s.n;
+    plan.S = dm + 2 * s.n;
     plan.tile_first = reinterpret_cast<const uint32_t*>(plan.S + s.n);
-    plan.total = s.d_meta.p + 2 * s.n + s.n + (plan_tiles + 1) / 2;
+    plan.total = dm + 2 * s.n + s.n + (plan_tiles + 1) / 2;
     plan.tile = kSmallTile;
-    meta_words = 2 * s.n + plan_words;
   }
+  if (direct) memcpy(s.h + moff, s.hm, 8 * meta_words);
   if ((e = slot_upload(c, s, [&](hipStream_t cs) {
          hipError_t r;
+         if (direct) return hipMemcpyAsync(s.d_blob.p, s.h, moff + 8 * meta_words, hipMemcpyHostToDevice, cs);
          if ((!uploaded && (r = hipMemcpyAsync(s.d_blob.p, s.src ? s.src : s.h, s.used, hipMemcpyHostToDevice, cs))) ||
              (r = hipMemcpyAsync(s.d_meta.p, s.hm, 8 * meta_words, hipMemcpyHostToDevice, cs)))
            return r;
@@ -528,11 +543,12 @@ int slot_submit(sdcas_ctx* c, Slot& s, bool res32) {
                        : hipMemcpyAsync(s.d_meta.p + s.cap_n, s.hm + s.cap_n, 8 * s.n, hipMemcpyHostToDevice, cs);
        })))
     return c->hip_fail(e, "H2D");
-  if ((rc = launch_batch(c, s.d_blob.p, s.d_meta.p, d_lens, (uint32_t)s.n, res32 ? s.d_res.p : nullptr,
-                         res32 ? nullptr : reinterpret_cast<uint64_t*>(s.d_res.p), st, s.chunks,
+  uint8_t* res = direct ? s.res() : s.d_res.p;
+  if ((rc = launch_batch(c, s.d_blob.p, dm, d_lens, (uint32_t)s.n, res32 ? res : nullptr,
+                         res32 ? nullptr : reinterpret_cast<uint64_t*>(res), st, s.chunks,
                          use_plan ? &plan : nullptr)))
     return rc;
-  if ((e = hipMemcpyAsync(s.res(), s.d_res.p, (res32 ? 32 : 8) * s.n, hipMemcpyDeviceToHost, st)) ||
+  if ((!direct && (e = hipMemcpyAsync(s.res(), s.d_res.p, (res32 ? 32 : 8) * s.n, hipMemcpyDeviceToHost, st))) ||
       (e = hipEventRecord(s.ev, st)))
     return c->hip_fail(e, "D2H");
   s.busy = true;
@@ -749,6 +765,7 @@ int sdcas_init(const sdcas_options* opts, sdcas_ctx** out) {
   if (const char* e = getenv("SDCAS_SMALL_VARIANT")) c->ws.small_variant = atoi(e);
   if (const char* e = getenv("SDCAS_UPLOAD_PARTS")) c->upload_parts = (uint32_t)std::min(atoi(e) > 0 ? atoi(e) : 0, 16);
   if (const char* e = getenv("SDCAS_PLAN_SMALL")) c->plan_small = atoi(e) != 0;
+  if (const char* e = getenv("SDCAS_SMALL_DIRECT")) c->small_direct = atoi(e) != 0;
   // pinned staging per slot in MiB, over the caller's choice (A/B runs)
   if (const char* e = getenv("SDCAS_STAGING_MB"); e && atoi(e) > 0) c->staging_bytes = (uint64_t)atoi(e) << 20;
   c->device = dev;

@@ -80,8 +80,9 @@ def _kernel_stubs(path):
 
 def test_product_library_holds_only_product_kernels():
     """libsdcas.so carries only the product kernels — leaf 67 (default), 52
-    and the small-batch kernels 73 (default, a quad of lanes per slot) and
-    71, piece 19 (default: k_piece_l4 + k_piece_top) and 17, all bit-exact
+    and the small-batch kernels 84 (default since round 6, a quad of lanes
+    per slot with four blocks in flight staged in LDS), 73 (a quad of lanes
+    per slot) and 71, piece 19 (default: k_piece_l4 + k_piece_top) and 17, all bit-exact
     and GPU-tested — and no ablation or DIAGNOSTIC variant (those produce
     wrong digests and live only in libsdcas_ablate.so)"""
     stubs = _kernel_stubs(N.LIB_PATH)
@@ -89,7 +90,8 @@ def test_product_library_holds_only_product_kernels():
     assert leaf == ["k_leaf_tree<128, 79, 1, 1, 2, 2, 0, 128u, 0, 0>",
                     "k_leaf_tree<512, 209, 1, 1, 2, 2, 0, 1024u, 0, 0>",
                     "k_leaf_tree<512, 279, 1, 1, 2, 2, 0, 1024u, 0, 0>",
-                    "k_leaf_tree<512, 79, 1, 0, 2, 0, 0, 128u, 1, 0>"], leaf
+                    "k_leaf_tree<512, 79, 1, 0, 2, 0, 0, 128u, 1, 0>",
+                    "k_leaf_tree<512, 79, 1, 0, 2, 0, 0, 128u, 3, 0>"], leaf
     finish = [s for s in stubs if s.startswith("k_finish")]
     assert finish == ["k_finish_q<1024u>", "k_finish_q<128u>", "k_finish_t<1024u>", "k_finish_t<128u>"], finish
     assert not [s for s in stubs if "slim" in s or "quad" in s]

@@ -279,12 +279,13 @@ def test_tile_straddles_vs_oracle(eng, oracle):
         assert bytes(d).hex() == oracle.hash(m), len(m)
 
 
-@pytest.mark.parametrize("variant,finish", [(52, "quad"), (67, "quad"), (71, "quad"), (73, "quad"), (67, "lane"),
-                                            (73, "lane")])
+@pytest.mark.parametrize("variant,finish", [(52, "quad"), (67, "quad"), (71, "quad"), (73, "quad"), (84, "quad"),
+                                            (67, "lane"), (73, "lane"), (84, "lane")])
 def test_tile_straddles_per_variant(oracle, variant, finish, monkeypatch):
     """the straddle corpus through each product leaf variant, in caller
-    order (shape sort off) so messages straddle tiles at every level (71 and
-    73, the small-batch kernels — a lane / a quad of lanes per slot — selected
+    order (shape sort off) so messages straddle tiles at every level (71, 73
+    and 84, the small-batch kernels — a lane / a quad of lanes per slot / a
+    quad with four blocks in flight staged in LDS — selected
     explicitly: their 128-slot tiles for the whole batch, so messages of up to
     2049 chunks cross dozens of them), the crossing messages finished by
     k_finish_q (default) or k_finish_t (SDCAS_FINISH=lane)"""
@@ -310,15 +311,16 @@ def test_tile_straddles_per_variant(oracle, variant, finish, monkeypatch):
     assert not bad, [len(msgs[i]) for i in bad[:10]]
 
 
-@pytest.mark.parametrize("variant", [52, 67, 71, 73])
+@pytest.mark.parametrize("variant", [52, 67, 71, 73, 84])
 def test_many_short_multichunk_messages(oracle, variant):
     """C5-shaped batches — mostly 2..5-chunk messages, so tiles hold far more
     partial last chunks than a wave has lanes and the leaf kernel's block-count
     order is taken — next to runs of single-chunk messages and a few long
     ones; every digest against the oracle, for every product kernel (52:
     one tile per workgroup, the last-block-index loop, the first chunk kept
-    from phase 1; 67, the default: 52 with the tail masks from a table; 71 and
-    73: the small-batch kernels, 128-slot tiles, a lane / a quad per slot)"""
+    from phase 1; 67, the default: 52 with the tail masks from a table; 71,
+    73 and 84: the small-batch kernels, 128-slot tiles, a lane / a quad per
+    slot / a quad with four blocks in flight staged in LDS)"""
     from spacedrive_amd import Engine
     rng = np.random.default_rng(55 + variant)
     lens = np.concatenate([rng.integers(1025, 5 * 1024 + 1, 12000), rng.integers(0, 1025, 3000),
@@ -639,3 +641,48 @@ def test_small_calls_and_metadata_layouts(oracle):
         out = e.hash_messages(*e.pack(msgs))
     bad = [i for i, (m, d) in enumerate(zip(msgs, out)) if bytes(d).hex() != oracle.hash(m)]
     assert not bad, bad[:10]
+
+
+@pytest.mark.parametrize("direct", ["1", "0"])
+def test_small_path_calls_direct_results(oracle, tmp_path, monkeypatch, direct):
+    """round 6: a small planned batch read into the slot goes up as ONE copy
+    (its metadata behind its bytes) and the kernels write its cas keys or
+    digests straight into the slot's pinned result words
+    (SDCAS_SMALL_DIRECT, default on; 0: the device buffer and a download).
+    Path calls of 1-20 files (whole-file and sampled, empty and missing ones
+    among them), checksums of small files, and a 600-file call between them on
+    the same context: every cas_id, checksum and status equals the oracle's"""
+    from spacedrive_amd import Engine
+    monkeypatch.setenv("SDCAS_SMALL_DIRECT", direct)
+    rng = np.random.default_rng(84)
+    paths, sizes = [], []
+    for i in range(700):
+        n = int(rng.choice([0, 1, 63, 1024, 1025, 102400, 102401, 300_000])) if i % 7 == 0 else \
+            int(rng.integers(1, 140_000))
+        p = tmp_path / f"s{i}"
+        p.write_bytes(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+        paths.append(str(p))
+        sizes.append(n)
+    paths[5] = str(tmp_path / "missing")
+
+    def check(e, lo, hi):
+        keys, st = e.generate_cas_ids(paths[lo:hi], sizes[lo:hi])
+        for k, i in enumerate(range(lo, hi)):
+            if i == 5:
+                assert st[k] != 0
+                continue
+            assert st[k] == 0, (i, st[k])
+            assert f"{int(keys[k]):016x}" == oracle.generate_cas_id(paths[i], sizes[i]), (direct, i, sizes[i])
+
+    with Engine() as e:
+        lo = 0
+        for n in [1, 1, 2, 3, 5, 8, 13, 20, 1, 7]:
+            check(e, lo, lo + n)
+            lo += n
+        check(e, 100, 700)  # a big call on the same context, then small ones again
+        for n in [1, 4, 20]:
+            check(e, lo, lo + n)
+            lo += n
+        for i in (0, 1, 2, 3):
+            d32, st = e.file_checksums([paths[10 + i]])
+            assert st[0] == 0 and bytes(d32[0]).hex() == oracle.file_checksum(paths[10 + i])
