@@ -568,7 +568,7 @@ __global__ void k_solo_insert_idx(const uint64_t* __restrict__ keys, const uint6
                                   const uint64_t* __restrict__ eids, uint32_t count, uint32_t base,
                                   uint32_t* __restrict__ tab, unsigned long long* __restrict__ emin, uint32_t mask,
                                   uint32_t shift, uint32_t* __restrict__ pos, uint32_t* __restrict__ stay_cnt,
-                                  uint32_t* __restrict__ noncontig, uint32_t sticky);
+                                  uint32_t* __restrict__ noncontig, uint32_t sticky, uint32_t plain = 0);
 
 // ---- the combine through a hash table ----------------------------------------------
 //
@@ -1421,7 +1421,7 @@ __global__ void k_solo_insert_idx(const uint64_t* __restrict__ keys, const uint6
                                   const uint64_t* __restrict__ eids, uint32_t count, uint32_t base,
                                   uint32_t* __restrict__ tab, unsigned long long* __restrict__ emin, uint32_t mask,
                                   uint32_t shift, uint32_t* __restrict__ pos, uint32_t* __restrict__ stay_cnt,
-                                  uint32_t* __restrict__ noncontig, uint32_t sticky) {
+                                  uint32_t* __restrict__ noncontig, uint32_t sticky, uint32_t plain) {
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= count) return;
   const uint32_t x = base + q;
@@ -1451,7 +1451,11 @@ __global__ void k_solo_insert_idx(const uint64_t* __restrict__ keys, const uint6
   uint32_t h = (uint32_t)(key >> shift) & mask;
   uint32_t x_claim = x;
   for (;;) {
-    uint32_t cur = __hip_atomic_load(&tab[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // plain: the probe as an ordinary load, which may hit a stale line in
+    // this XCD's L2 — safe, as a slot only ever goes from empty to an index of
+    // ONE key and then to lower indices of that key: a stale empty is
+    // corrected by the CAS's answer, a stale index names the same key
+    uint32_t cur = plain ? tab[h] : __hip_atomic_load(&tab[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (cur == kIdxEmpty) {
       const uint32_t prev = atomicCAS(&tab[h], kIdxEmpty, x);
       if (prev == kIdxEmpty) break;
@@ -1737,6 +1741,13 @@ static bool exist_min_by_entry() {
   return !(v && strcmp(v, "slot") == 0);
 }
 
+// SDCAS_PROBE=plain: the files' insert probes with ordinary loads instead of
+// agent-scope atomic loads (k_solo_insert_idx), read per call (A/B)
+static bool plain_probe() {
+  const char* v = getenv("SDCAS_PROBE");
+  return v && strcmp(v, "plain") == 0;
+}
+
 static hipError_t local_fused(DistWs& w, const uint64_t* keys, const uint8_t* has_key, const int32_t* status,
                               const uint64_t* ids, uint32_t n, const uint64_t* ekeys, const uint64_t* eids,
                               uint32_t ne, uint64_t cs, const StepWindow& win, int64_t* link,
@@ -1773,7 +1784,7 @@ static hipError_t local_fused(DistWs& w, const uint64_t* keys, const uint8_t* ha
   hipLaunchKernelGGL(k_solo_insert_idx, dim3(blocks(n)), dim3(TB), 0, st, keys, ekeys, n, has_key, status,
                      contig ? ids : (const uint64_t*)nullptr, n, 0u, tab, (unsigned long long*)nullptr, mask, shift,
                      w.tpos.p, stays ? w.stay_cnt.p : (uint32_t*)nullptr, contig ? w.flag.p : (uint32_t*)nullptr,
-                     sticky);
+                     sticky, plain_probe() ? 1u : 0u);
   // the stays rows' ordinals, dense, for the walk (stay_sorted: dd_plan's
   // buffer, free in a world of one); the walk's count is the groups' sum
   if (stays)
