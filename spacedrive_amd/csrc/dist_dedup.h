@@ -55,8 +55,6 @@ struct DistWs {
   Buf<uint64_t> plan, stay_sorted;
   Buf<uint32_t> bitmap;           // dd_plan: the stays ordinals of a long gathered list
   Buf<uint64_t> ridx;             // the coarse index of a plan's re-read list (k_rr_index), stamped
-  Buf<uint32_t> pcnt, psrc;       // the partitioned resolve: per-tile partition counts / offsets, record sources
-  Buf<uint64_t> pkv;              // the partitioned resolve: records in partition order
   void release();
 };
 

@@ -509,8 +509,7 @@ static hipError_t rr_index(DistWs& w, uint64_t* plan, hipStream_t st) {
 void DistWs::release() {
   idx_a.release(); idx_b.release(); starts.release(); ocnt.release(); tkey.release(); tmin.release();
   tpos.release(); stay_idx.release(); nstay.release(); stay_cnt.release(); plan.release(); stay_sorted.release();
-  bitmap.release(); flag.release(); shard.release(); ridx.release(); pcnt.release(); psrc.release();
-  pkv.release();
+  bitmap.release(); flag.release(); shard.release(); ridx.release();
   shard_dirty = false;
 }
 
@@ -1194,260 +1193,12 @@ __global__ void k_rb_clear_idx(uint32_t* __restrict__ tab, unsigned long long* _
   }
 }
 
-// ---- round 6: the owner's resolve by key partitions in LDS ------------------------
-//
-// SDCAS_RESOLVE=part. The table resolve (k_rb_insert_rec / k_rb_answer_rec)
-// makes ~4 random requests per received record at the chip's random-request
-// rate (claims by global CAS at ~24 G/s, key read-backs, folds, answers).
-// Here the received records are first put in key-partition order — a count
-// pass (per-tile LDS histograms), a scan, a scatter — so that one workgroup
-// resolves one partition (~1 K records) in an LDS table: each key's minimum
-// file value and minimum existing value by LDS atomics, then each file
-// record's answer written to its bucket slot. The rank-side tile combine
-// already collapsed the Zipf head to one record per key per tile, so no
-// partition holds more than a few thousand of one key. A partition whose
-// distinct keys overflow the LDS table (adversarial keys) is resolved in
-// 2, 4, ... rounds, each taking the keys of one residue of a second hash.
-constexpr uint32_t kPartTile = 8192;    // record slots per count / scatter workgroup
-constexpr uint32_t kPartSlots = 2048;   // LDS table entries per partition (+1: the all-ones key's own)
-constexpr uint32_t kPartMax = 16384;    // partitions at most (LDS counters per tile)
-constexpr uint32_t kPartWave = 16;      // waves of the scan workgroup
-constexpr uint32_t kPartExisting = 0x80000000u;  // psrc: an existing Object's record
-constexpr uint32_t kPartRoundsMax = 64;           // k_part_resolve's rounds before its exact scan
-
-__device__ __forceinline__ uint64_t part_mix(uint64_t z) {  // a bijection (splitmix64's finaliser)
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
-
-// slot x of the received buckets: (key, value, valid, existing)
-__device__ __forceinline__ bool part_rec(const uint64_t* __restrict__ frec, uint32_t fcap,
-                                         const int64_t* __restrict__ fcounts, const uint64_t* __restrict__ erec,
-                                         uint32_t ecap, const int64_t* __restrict__ ecounts, uint32_t nf, uint32_t x,
-                                         uint64_t* key, uint64_t* val) {
-  const uint64_t* r;
-  if (x < nf) {
-    const uint32_t b = x / fcap;
-    if ((int64_t)(x - b * fcap) >= fcounts[b]) return false;
-    r = frec + 2ull * x;
-  } else {
-    const uint32_t y = x - nf, b = y / ecap;
-    if ((int64_t)(y - b * ecap) >= ecounts[b]) return false;
-    r = erec + 2ull * y;
-  }
-  *key = r[0];
-  *val = r[1];
-  return true;
-}
-
-// per tile: how many of its valid records fall in each partition (tile-major)
-__global__ void __launch_bounds__(TB) k_part_count(const uint64_t* __restrict__ frec, uint32_t fcap,
-                                                   const int64_t* __restrict__ fcounts,
-                                                   const uint64_t* __restrict__ erec, uint32_t ecap,
-                                                   const int64_t* __restrict__ ecounts, uint32_t nf, uint32_t nslots,
-                                                   uint32_t pbits, uint32_t* __restrict__ cnt) {
-  __shared__ uint32_t hist[kPartMax];
-  const uint32_t P = 1u << pbits, t = blockIdx.x;
-  for (uint32_t p = threadIdx.x; p < P; p += TB) hist[p] = 0;
-  __syncthreads();
-  const uint32_t x1 = min(nslots, (t + 1) * kPartTile);
-  for (uint32_t x = t * kPartTile + threadIdx.x; x < x1; x += TB) {
-    uint64_t key, val;
-    if (part_rec(frec, fcap, fcounts, erec, ecap, ecounts, nf, x, &key, &val))
-      atomicAdd(&hist[pbits ? (uint32_t)(part_mix(key) >> (64 - pbits)) : 0u], 1u);
-  }
-  __syncthreads();
-  for (uint32_t p = threadIdx.x; p < P; p += TB) cnt[(uint64_t)t * P + p] = hist[p];
-}
-
-// each partition's counts over the tiles -> exclusive offsets in place, and
-// its total: 64 partitions per workgroup (a lane each), the tiles split over
-// kPartWave waves (partial sums through LDS)
-__global__ void __launch_bounds__(64 * kPartWave) k_part_scan_tiles(uint32_t* __restrict__ cnt, uint32_t nt,
-                                                                   uint32_t pbits, uint32_t* __restrict__ total) {
-  __shared__ uint32_t part[kPartWave][64];
-  const uint32_t P = 1u << pbits, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t p = blockIdx.x * 64 + lane;
-  const uint32_t per = (nt + kPartWave - 1) / kPartWave, t0 = wave * per, t1 = min(nt, t0 + per);
-  uint32_t sum = 0;
-  if (p < P) {
-#pragma unroll 8
-    for (uint32_t t = t0; t < t1; ++t) sum += cnt[(uint64_t)t * P + p];
-  }
-  part[wave][lane] = sum;
-  __syncthreads();
-  uint32_t run = 0;
-  for (uint32_t w = 0; w < wave; ++w) run += part[w][lane];
-  if (p < P) {
-#pragma unroll 8
-    for (uint32_t t = t0; t < t1; ++t) {
-      const uint32_t c = cnt[(uint64_t)t * P + p];
-      cnt[(uint64_t)t * P + p] = run;
-      run += c;
-    }
-  }
-  if (wave == kPartWave - 1 && p < P) total[p] = run;
-}
-
-// base[0..P]: the exclusive prefix of the partitions' totals (one workgroup)
-__global__ void __launch_bounds__(1024) k_part_scan_totals(uint32_t* __restrict__ total, uint32_t pbits) {
-  __shared__ uint32_t ws[16];
-  __shared__ uint32_t carry;
-  const uint32_t P = 1u << pbits, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid == 0) carry = 0;
-  __syncthreads();
-  for (uint32_t c0 = 0; c0 < P; c0 += 1024) {
-    const uint32_t i = c0 + tid;
-    const uint32_t v = i < P ? total[i] : 0u;
-    uint32_t inc = v;
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-      const uint32_t u = __shfl_up(inc, d);
-      if (lane >= d) inc += u;
-    }
-    if (lane == 63) ws[wave] = inc;
-    __syncthreads();
-    uint32_t before = carry;
-    for (uint32_t w = 0; w < wave; ++w) before += ws[w];
-    if (i < P) total[i] = before + inc - v;
-    __syncthreads();
-    if (tid == 1023) carry = before + inc;
-    __syncthreads();
-  }
-  if (tid == 0) total[P] = carry;
-}
-
-// the records of each tile into partition order: (key, value) and the
-// record's bucket slot (kPartExisting: an existing Object's)
-__global__ void __launch_bounds__(TB) k_part_scatter(const uint64_t* __restrict__ frec, uint32_t fcap,
-                                                     const int64_t* __restrict__ fcounts,
-                                                     const uint64_t* __restrict__ erec, uint32_t ecap,
-                                                     const int64_t* __restrict__ ecounts, uint32_t nf,
-                                                     uint32_t nslots, uint32_t pbits,
-                                                     const uint32_t* __restrict__ cnt,
-                                                     const uint32_t* __restrict__ base, uint64_t* __restrict__ pkv,
-                                                     uint32_t* __restrict__ psrc) {
-  __shared__ uint32_t off[kPartMax];
-  const uint32_t P = 1u << pbits, t = blockIdx.x;
-  for (uint32_t p = threadIdx.x; p < P; p += TB) off[p] = base[p] + cnt[(uint64_t)t * P + p];
-  __syncthreads();
-  const uint32_t x1 = min(nslots, (t + 1) * kPartTile);
-  for (uint32_t x = t * kPartTile + threadIdx.x; x < x1; x += TB) {
-    uint64_t key, val;
-    if (!part_rec(frec, fcap, fcounts, erec, ecap, ecounts, nf, x, &key, &val)) continue;
-    const uint32_t q = atomicAdd(&off[pbits ? (uint32_t)(part_mix(key) >> (64 - pbits)) : 0u], 1u);
-    pkv[2ull * q] = key;
-    pkv[2ull * q + 1] = val;
-    psrc[q] = x < nf ? x : kPartExisting;
-  }
-}
-
-// the key's LDS entry (insert: claim it if absent); kPartSlots for the
-// all-ones key, ~0u when the table is too full (the round is redone)
-template <bool INSERT>
-__device__ __forceinline__ uint32_t part_slot(unsigned long long* skey, uint32_t* fill, uint32_t* over, uint64_t key,
-                                              uint64_t z, uint32_t pbits) {
-  if (key == kEmptyKey) return kPartSlots;
-  uint32_t h = (uint32_t)((z << pbits) >> (64 - 11)) & (kPartSlots - 1);
-  static_assert(kPartSlots == 1u << 11, "part_slot takes 11 bits");
-  for (uint32_t k = 0; k < kPartSlots; ++k) {
-    const unsigned long long cur = skey[h];
-    if (cur == key) return h;
-    if (cur == kEmptyKey) {
-      if (!INSERT) return ~0u;
-      const unsigned long long prev = atomicCAS(&skey[h], (unsigned long long)kEmptyKey, (unsigned long long)key);
-      if (prev == kEmptyKey) {
-        if (atomicAdd(fill, 1u) >= kPartSlots * 3 / 4) *over = 1;
-        return h;
-      }
-      if (prev == key) return h;
-    }
-    h = (h + 1) & (kPartSlots - 1);
-  }
-  *over = 1;
-  return ~0u;
-}
-
-// one workgroup per partition: each key's minimum file value and minimum
-// existing value in LDS, then every file record's answer at its bucket slot
-// (mod.rs:202-238: the first existing Object; else mod.rs:246-254: the key's
-// first file)
-__global__ void __launch_bounds__(TB) k_part_resolve(const uint64_t* __restrict__ pkv,
-                                                     const uint32_t* __restrict__ psrc,
-                                                     const uint32_t* __restrict__ base, uint32_t pbits,
-                                                     int64_t* __restrict__ result) {
-  __shared__ unsigned long long skey[kPartSlots + 1], svmin[kPartSlots + 1], semin[kPartSlots + 1];
-  __shared__ uint32_t fill, over;
-  const uint32_t p = blockIdx.x, tid = threadIdx.x;
-  const uint32_t lo = base[p], hi = base[p + 1];
-  if (lo == hi) return;
-  for (uint32_t R = 1;; R <<= 1) {
-    bool ok = true;
-    for (uint32_t round = 0; round < R; ++round) {
-      for (uint32_t s = tid; s <= kPartSlots; s += TB) {
-        skey[s] = kEmptyKey;
-        svmin[s] = ~0ull;
-        semin[s] = ~0ull;
-      }
-      if (tid == 0) fill = over = 0;
-      __syncthreads();
-      for (uint32_t i = lo + tid; i < hi; i += TB) {
-        const uint64_t key = pkv[2ull * i], z = part_mix(key);
-        if ((z & (R - 1)) != round) continue;
-        const uint32_t h = part_slot<true>(skey, &fill, &over, key, z, pbits);
-        if (h == ~0u) continue;
-        atomicMin(psrc[i] == kPartExisting ? &semin[h] : &svmin[h], (unsigned long long)pkv[2ull * i + 1]);
-      }
-      __syncthreads();
-      const bool o = over != 0;
-      __syncthreads();  // every thread has read `over` before the next round clears it
-      if (o) {
-        ok = false;
-        break;
-      }
-      for (uint32_t i = lo + tid; i < hi; i += TB) {
-        const uint32_t src = psrc[i];
-        if (src == kPartExisting) continue;
-        const uint64_t key = pkv[2ull * i], z = part_mix(key);
-        if ((z & (R - 1)) != round) continue;
-        const uint32_t h = part_slot<false>(skey, &fill, &over, key, z, pbits);
-        const unsigned long long e = semin[h];
-        result[src] = e != ~0ull ? -(int64_t)e - 1 : (int64_t)svmin[h];
-      }
-      __syncthreads();
-    }
-    if (ok) return;
-    if (R >= kPartRoundsMax) break;
-  }
-  // more than kPartRoundsMax x 1536 distinct keys agreeing in their hash's
-  // partition bits and low bits: crafted keys (no BLAKE3 output set does
-  // this). Each file record's answer by a scan of its partition: slow,
-  // and exact.
-  for (uint32_t i = lo + tid; i < hi; i += TB) {
-    const uint32_t src = psrc[i];
-    if (src == kPartExisting) continue;
-    const uint64_t key = pkv[2ull * i];
-    unsigned long long e = ~0ull, v = ~0ull;
-    for (uint32_t j = lo; j < hi; ++j) {
-      if (pkv[2ull * j] != key) continue;
-      const unsigned long long x = pkv[2ull * j + 1];
-      if (psrc[j] == kPartExisting) e = min(e, x);
-      else v = min(v, x);
-    }
-    result[src] = e != ~0ull ? -(int64_t)e - 1 : (int64_t)v;
-  }
-}
-
-// SDCAS_RESOLVE: "rec" (the default) = the u32 claim table, each key's
-// minimum folded into its claiming record's value word; "part" = the key
-// partitions in LDS (above); "idx" = the claim table with side minima;
-// "kv" = round 5's 16-byte (key, files' minimum) entries sized on the device;
-// "split" = round 4's key array + minima pairs sized from the buckets'
-// capacity (A/B)
-enum ResolveTable { kResolveIdx = 0, kResolveKv = 1, kResolveSplit = 2, kResolveRec = 3, kResolvePart = 4 };
+// SDCAS_RESOLVE: "idx" (the default, above), "kv" = round 5's 16-byte (key,
+// files' minimum) entries sized on the device, "split" = round 4's key array
+// + minima pairs sized from the buckets' capacity (A/B)
+enum ResolveTable { kResolveIdx = 0, kResolveKv = 1, kResolveSplit = 2, kResolveRec = 3 };
 static ResolveTable resolve_table() {
   const char* v = getenv("SDCAS_RESOLVE");
-  if (v && strcmp(v, "part") == 0) return kResolvePart;
   if (v && strcmp(v, "split") == 0) return kResolveSplit;
   if (v && strcmp(v, "kv") == 0) return kResolveKv;
   if (v && strcmp(v, "idx") == 0) return kResolveIdx;
@@ -1465,27 +1216,6 @@ hipError_t dd_resolve_buckets(DistWs& w, const uint64_t* frec, uint32_t fcap, co
   if (cap > (1ull << 31)) return hipErrorInvalidValue;
   ResolveTable rt = resolve_table();
   if ((rt == kResolveIdx || rt == kResolveRec) && cap > (1ull << 30)) rt = kResolveKv;  // tpos' claimed bit: slots < 2^31
-  if (rt == kResolvePart && (uint64_t)nf + ne < kPartExisting) {
-    const uint32_t nslots = nf + ne;
-    uint32_t pbits = 0;
-    while (pbits < 14 && ((uint64_t)nslots >> pbits) > 1024) ++pbits;  // ~1 K record slots per partition
-    const uint32_t P = 1u << pbits, nt = (nslots + kPartTile - 1) / kPartTile;
-    if ((e = w.pcnt.ensure((uint64_t)nt * P + P + 1)) || (e = w.pkv.ensure(2ull * nslots)) ||
-        (e = w.psrc.ensure(nslots)))
-      return e;
-    uint32_t* base = w.pcnt.p + (uint64_t)nt * P;
-    const int64_t* ec = ne ? ecounts : fcounts;  // (unread when ne == 0)
-    hipLaunchKernelGGL(k_part_count, dim3(nt), dim3(TB), 0, st, frec, fcap, fcounts, erec, ecap, ec, nf, nslots, pbits,
-                       w.pcnt.p);
-    hipLaunchKernelGGL(k_part_scan_tiles, dim3((P + 63) / 64), dim3(64 * kPartWave), 0, st, w.pcnt.p, nt, pbits, base);
-    hipLaunchKernelGGL(k_part_scan_totals, dim3(1), dim3(1024), 0, st, base, pbits);
-    hipLaunchKernelGGL(k_part_scatter, dim3(nt), dim3(TB), 0, st, frec, fcap, fcounts, erec, ecap, ec, nf, nslots,
-                       pbits, (const uint32_t*)w.pcnt.p, (const uint32_t*)base, w.pkv.p, w.psrc.p);
-    hipLaunchKernelGGL(k_part_resolve, dim3(P), dim3(TB), 0, st, (const uint64_t*)w.pkv.p, (const uint32_t*)w.psrc.p,
-                       (const uint32_t*)base, pbits, result);
-    return hipGetLastError();
-  }
-  if (rt == kResolvePart) rt = kResolveRec;
   if (rt == kResolveRec) {
     // the received buckets' value fields take the minima (sdcas.h: resolve_buckets)
     if ((e = w.tmin.ensure(cap / 2 + 1)) || (e = w.tpos.ensure(nf)) || (e = w.starts.ensure(2))) return e;

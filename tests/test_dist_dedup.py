@@ -815,8 +815,8 @@ def test_meta_group_of_a_subgroup():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("combine", ["tile", "tile-part", "tile-idx", "tile-kv", "tile-split", "tile-r0", "tile-r1",
-                                     "hash", "hash-idx", "hash-part"])
+@pytest.mark.parametrize("combine", ["tile", "tile-idx", "tile-kv", "tile-split", "tile-r0", "tile-r1", "hash",
+                                     "hash-idx"])
 @pytest.mark.parametrize("R,chunk_size", [(2, 100), (8, 100), (5, 7)])
 def test_device_bucket_protocol_vs_oracle(eng, oracle, R, chunk_size, combine, monkeypatch):
     """the bucket protocol's device stages (combine_buckets -> equal-split
@@ -825,8 +825,7 @@ def test_device_bucket_protocol_vs_oracle(eng, oracle, R, chunk_size, combine, m
     default: a key may take one record per 2048-file tile) and round 5's
     global hash table (SDCAS_COMBINE=hash, one record per key) — and every
     resolve: the owner's u32 claim table folding the other records' values
-    into the claiming record (the default), round 6's key partitions resolved
-    in LDS (SDCAS_RESOLVE=part), the same table with per-slot side
+    into the claiming record (the default), the same table with per-slot side
     minima (SDCAS_RESOLVE=idx), round 5's 16-byte (key, minimum) entries
     (SDCAS_RESOLVE=kv) and round 4's tables sized from the buckets' capacity
     (SDCAS_RESOLVE=split); the
@@ -838,7 +837,7 @@ def test_device_bucket_protocol_vs_oracle(eng, oracle, R, chunk_size, combine, m
     from tests._dist_stages import dedup_virtual_buckets
     comb, _, knob = combine.partition("-")
     monkeypatch.setenv("SDCAS_COMBINE", comb)
-    if knob in ("split", "kv", "idx", "part"):
+    if knob in ("split", "kv", "idx"):
         monkeypatch.setenv("SDCAS_RESOLVE", knob)
     elif knob.startswith("r"):
         monkeypatch.setenv("SDCAS_APPLY_R", knob[1:])
@@ -864,67 +863,3 @@ def test_device_bucket_protocol_vs_oracle(eng, oracle, R, chunk_size, combine, m
         fills.append(int(cnt.max()))
     _, _, _, over = dedup_virtual_buckets(lambda r: st, shards, chunk_size, ex, (max(fills) - 1, caps[1]))
     assert over
-
-
-_SM1, _SM2 = 0xBF58476D1CE4E5B9, 0x94D049BB133111EB
-_M64 = (1 << 64) - 1
-
-
-def _unxorshift(z, k):
-    x = z
-    for _ in range(64 // k + 1):
-        x = z ^ (x >> k)
-    return x
-
-
-def _part_mix(k):
-    """csrc/dist_dedup.hip part_mix (splitmix64's finaliser)"""
-    z = ((k ^ (k >> 30)) * _SM1) & _M64
-    z = ((z ^ (z >> 27)) * _SM2) & _M64
-    return z ^ (z >> 31)
-
-
-def _part_unmix(z):
-    z = _unxorshift(z, 31)
-    z = (z * pow(_SM2, -1, 1 << 64)) & _M64
-    z = _unxorshift(z, 27)
-    z = (z * pow(_SM1, -1, 1 << 64)) & _M64
-    return _unxorshift(z, 30)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("low_bits", [0, 6])
-def test_partitioned_resolve_crafted_keys(eng, oracle, low_bits, monkeypatch):
-    """SDCAS_RESOLVE=part with keys crafted (through the inverse of its hash,
-    part_mix) so that 2 000 distinct keys share one partition — more than its
-    LDS table takes: with random low hash bits the partition is resolved in 2
-    or 4 rounds; with the low 6 bits equal no round count up to 64 splits
-    them and the partition falls to the exact scan. Every link and both
-    counts against the oracle, existing Objects among the crafted keys."""
-    from spacedrive_amd.dist_dedup import DeviceStages
-    from tests._dist_stages import dedup_virtual_buckets
-    monkeypatch.setenv("SDCAS_RESOLVE", "part")
-    rng = np.random.default_rng(600 + low_bits)
-    mids = rng.choice(1 << 40, 2000, replace=False).astype(np.uint64)
-    crafted = []
-    for m in mids:
-        z = (0x2A5 << 50) | (int(m) << 10)
-        z |= int(rng.integers(0, 1 << 10)) & ~((1 << low_bits) - 1)
-        k = _part_unmix(z)
-        assert _part_mix(k) == z
-        crafted.append(k)
-    crafted = np.array(crafted, np.uint64)
-    keys, has, status, existing = make_corpus(810 + low_bits, 24000, pool=3000, p_none=0.03, p_err=0.03)
-    pos = rng.choice(keys.size, 6000, replace=False)
-    keys[pos] = crafted[rng.integers(0, crafted.size, pos.size)]
-    existing = np.concatenate([existing, crafted[:150]])
-    want, wc, wl = oracle.identifier_dedup(keys, has, status, 100, existing)
-    R = 4
-    shards, ex = shard(keys, has, status, existing, R, device="cuda")
-    st = DeviceStages(eng)
-    n = max(int(s[3].numel()) for s in shards)
-    caps = (n + 1, max(int(e[0].numel()) for e in ex) + 1)
-    links, c, l, over = dedup_virtual_buckets(lambda r: st, shards, 100, ex, caps)
-    assert not over
-    assert np.array_equal(np.concatenate([x.cpu().numpy() for x in links]), want)
-    assert (c, l) == (wc, wl)
