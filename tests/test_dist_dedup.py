@@ -506,7 +506,8 @@ def test_rccl_world1(eng, oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("table", ["idx", "idx-r0", "idx-r1", "idx-r8", "idx-c0", "idx-xslot", "idx4", "kv"])
+@pytest.mark.parametrize("table", ["idx", "idx-r0", "idx-r1", "idx-r8", "idx-c0", "idx-xslot", "idx-pplain", "idx4",
+                                   "kv"])
 @pytest.mark.parametrize("corpus,chunk_size", [("default", 100), ("default", 7), ("default", 1),
                                                ("collisions", 100), ("clustered", 100)])
 def test_device_local_vs_oracle(eng, oracle, corpus, chunk_size, table, monkeypatch):
@@ -519,7 +520,8 @@ def test_device_local_vs_oracle(eng, oracle, corpus, chunk_size, table, monkeypa
     files per thread beside the default 4 (`idx-rN`, SDCAS_APPLY_R), every
     first ordinal read instead of taken from the index (`idx-c0`), the
     existing Objects' minima by table slot instead of by claiming Object
-    (`idx-xslot`, round 5's form); and the
+    (`idx-xslot`, round 5's form), the files' insert probing with ordinary
+    loads (`idx-pplain`, SDCAS_PROBE=plain, round 6's A/B); and the
     existing Objects passed in DB order and shuffled (their DB indices then
     not ascending: the first Object is the lowest DB index, not the first
     entry)"""
@@ -527,7 +529,8 @@ def test_device_local_vs_oracle(eng, oracle, corpus, chunk_size, table, monkeypa
     table, _, knob = table.partition("-")
     monkeypatch.setenv("SDCAS_DEDUP_TABLE", table)
     if knob:
-        monkeypatch.setenv({"r": "SDCAS_APPLY_R", "c": "SDCAS_CONTIG", "x": "SDCAS_EXIST_MIN"}[knob[0]], knob[1:])
+        monkeypatch.setenv({"r": "SDCAS_APPLY_R", "c": "SDCAS_CONTIG", "x": "SDCAS_EXIST_MIN",
+                            "p": "SDCAS_PROBE"}[knob[0]], knob[1:])
     if corpus == "default":
         keys, has, status, existing = make_corpus(91, 40000, pool=6000)
         keys[:2] = np.uint64(2**64 - 1)  # the table's empty marker is a legal key
