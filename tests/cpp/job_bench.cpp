@@ -189,7 +189,11 @@ int main(int argc, char** argv) {
   const size_t sample = argc > 2 ? (size_t)std::atoll(argv[2]) : SIZE_MAX;  // file_path rows
   std::unique_ptr<Engine> engine;
   try {
-    engine = Engine::open();
+    // JOB_IO_THREADS: the library's reader threads (A/B: the readers and
+    // SQLite's one writer share the box's CPU quota)
+    Engine::Options o;
+    if (const char* v = std::getenv("JOB_IO_THREADS")) o.io_threads = (uint32_t)std::atoi(v);
+    engine = Engine::open(o);
   } catch (const LibraryError& e) {
     std::fprintf(stderr, "job_bench: %s\n", e.what());
     return 2;
