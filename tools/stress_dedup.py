@@ -11,7 +11,7 @@ virtual world sizes drawn per seed — every link and both counts of
 against tests/_oracle.py's identifier_dedup. Prints one JSON line: cases
 run, mismatching cases (seed and path), wall time.
 
-usage: stress_dedup.py [--seeds 60] [--max-files 200000]"""
+usage: stress_dedup.py [--seeds 60] [--first-seed 0] [--max-files 200000]"""
 import argparse
 import json
 import os
@@ -27,6 +27,7 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seeds", type=int, default=60)
+    ap.add_argument("--first-seed", type=int, default=0, help="seeds first-seed .. first-seed + seeds - 1")
     ap.add_argument("--max-files", type=int, default=200_000)
     a = ap.parse_args()
     import torch
@@ -41,7 +42,7 @@ def main():
     st = DeviceStages(eng)
     bad, cases = [], 0
     t0 = time.perf_counter()
-    for seed in range(a.seeds):
+    for seed in range(a.first_seed, a.first_seed + a.seeds):
         rng = np.random.default_rng(1000 + seed)
         n = int(rng.integers(1, a.max_files))
         pool = int(rng.integers(1, max(2, n)))
