@@ -116,3 +116,24 @@ def test_ablation_build_is_separate():
     for f in os.listdir(pkg):
         if f.endswith(".py") and f != "_native.py":
             assert "ablat" not in open(os.path.join(pkg, f)).read(), f
+
+
+def test_quad_message_schedules_are_blake3s():
+    """the quad compressions' message schedules in csrc/b3_device.h — the
+    seven B3_QROUND lists of compress_quad and the table make_quad_words
+    builds kQuadWord from (the small-batch kernel 84 reads each lane's 28
+    words by it) — are BLAKE3's: round r applies the message permutation r
+    times (Appendix A of SURVEY.md)"""
+    src = open(os.path.join(ROOT, "spacedrive_amd", "csrc", "b3_device.h")).read()
+    perm = [2, 6, 3, 10, 7, 0, 4, 13, 1, 11, 12, 5, 9, 14, 15, 8]
+    want, s = [], list(range(16))
+    for _ in range(7):
+        want.append(s)
+        s = [s[p] for p in perm]
+    qround = [[int(x) for x in m.split(",")]
+              for m in re.findall(r"^\s*B3_QROUND\(([\d,\s]+)\);", src, re.M)]
+    assert qround == want
+    body = src[src.index("constexpr QuadWords make_quad_words()"):]
+    body = body[:body.index("QuadWords t{}")]
+    table = [[int(x) for x in row.split(",")] for row in re.findall(r"\{([\d,\s]+)\}", body)]
+    assert table == want
